@@ -1,0 +1,203 @@
+"""ctypes binding of the C-ABI in include/avr.h (libavr_hip.so, built in-tree).
+
+This is the same binding a pbrt-side Python tool (or the ctypes stub in
+INTEGRATION.md) would use. There is no fallback: if the HIP library is missing or
+fails to load, importing the product raises.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libavr_hip.so")
+
+c_float_p = ctypes.POINTER(ctypes.c_float)
+c_double_p = ctypes.POINTER(ctypes.c_double)
+c_int_p = ctypes.POINTER(ctypes.c_int)
+
+
+class AvrStats(ctypes.Structure):
+    _fields_ = [
+        ("medium_lookups", ctypes.c_ulonglong),
+        ("medium_items_in", ctypes.c_ulonglong),
+        ("medium_items_out", ctypes.c_ulonglong),
+        ("shadow_lookups", ctypes.c_ulonglong),
+        ("shadow_items", ctypes.c_ulonglong),
+        ("medium_dda_steps", ctypes.c_ulonglong),
+        ("shadow_dda_steps", ctypes.c_ulonglong),
+        ("medium_launches", ctypes.c_ulonglong),
+        ("ms_camera", ctypes.c_double),
+        ("ms_medium", ctypes.c_double),
+        ("ms_shadow", ctypes.c_double),
+        ("ms_film", ctypes.c_double),
+        ("ms_total", ctypes.c_double),
+    ]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+# name -> (restype, argtypes); every symbol include/avr.h declares
+SIGNATURES = {
+    "avr_last_error": (ctypes.c_char_p, []),
+    "avr_context_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_longlong, ctypes.POINTER(ctypes.c_void_p)]),
+    "avr_context_destroy": (ctypes.c_int, [ctypes.c_void_p]),
+    "avr_set_stream": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "avr_medium_grid": (ctypes.c_int, [ctypes.c_void_p, c_float_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                       c_float_p, c_float_p, c_float_p, c_float_p, c_float_p, ctypes.c_float,
+                                       c_float_p, c_float_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_int_p]),
+    "avr_medium_grid_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                              ctypes.c_int, c_float_p, c_float_p, c_float_p, c_float_p, c_float_p,
+                                              ctypes.c_float, c_float_p, c_float_p, ctypes.c_int, ctypes.c_int,
+                                              ctypes.c_int, c_int_p]),
+    "avr_generate_cloud": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_longlong,
+                                          ctypes.c_longlong, ctypes.c_float, ctypes.c_float, ctypes.c_float]),
+    "avr_read_majorant": (ctypes.c_int, [ctypes.c_void_p, c_float_p]),
+    "avr_lights": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, c_int_p, c_float_p, c_float_p, c_float_p,
+                                  ctypes.c_float]),
+    "avr_camera": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, c_float_p, c_float_p]),
+    "avr_film": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, c_float_p, c_float_p, ctypes.c_float,
+                                ctypes.c_float]),
+    "avr_film_clear": (ctypes.c_int, [ctypes.c_void_p]),
+    "avr_render": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
+    "avr_sync": (ctypes.c_int, [ctypes.c_void_p]),
+    "avr_get_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(AvrStats)]),
+    "avr_film_read": (ctypes.c_int, [ctypes.c_void_p, c_double_p, c_double_p]),
+    "avr_film_device_ptrs": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p),
+                                            ctypes.POINTER(ctypes.c_void_p)]),
+    "avr_film_export_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "avr_last_pass_samples": (ctypes.c_int, [ctypes.c_void_p, c_float_p, c_float_p, c_float_p, ctypes.c_longlong,
+                                             c_int_p, c_int_p]),
+}
+
+_lib = None
+
+
+def load():
+    """Load libavr_hip.so (no GPU is touched). Raises if it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"{LIB_PATH} not built: run __graft_entry__.build() (hipcc --offload-arch=gfx950)")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def _fp(a):
+    return a.ctypes.data_as(c_float_p) if a is not None else None
+
+
+def _check(rc):
+    if rc != 0:
+        raise RuntimeError(f"avr error {rc}: {_lib.avr_last_error().decode()}")
+
+
+class Context:
+    """One HIP device context of the integrator (avr_context_create)."""
+
+    def __init__(self, device=0, max_paths=0):
+        self.lib = load()
+        h = ctypes.c_void_p()
+        _check(self.lib.avr_context_create(int(device), int(max_paths), ctypes.byref(h)))
+        self.h = h
+        self._keep = []
+
+    def close(self):
+        if self.h:
+            self.lib.avr_context_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_stream(self, stream_ptr):
+        _check(self.lib.avr_set_stream(self.h, ctypes.c_void_p(stream_ptr)))
+
+    def set_scene(self, scene):
+        med = scene.medium
+        mres = np.asarray(med.majorant_res, np.int32)
+        f32 = lambda a: np.ascontiguousarray(np.asarray(a, np.float32))
+        args = [f32(med.bounds), f32(scene.render_from_medium), f32(scene.medium_from_render), f32(med.sigma_a),
+                f32(med.sigma_s)]
+        Le = f32(med.Le) if med.Le is not None else None
+        ls = f32(med.Lescale)
+        self._keep = args + [Le, ls, mres]
+        if med.device_density is not None:
+            _check(self.lib.avr_medium_grid_device(
+                self.h, ctypes.c_void_p(med.device_density.data_ptr()), med.nx, med.ny, med.nz, _fp(args[0]),
+                _fp(args[1]), _fp(args[2]), _fp(args[3]), _fp(args[4]), float(med.g), _fp(Le), _fp(ls),
+                ls.shape[2], ls.shape[1], ls.shape[0], mres.ctypes.data_as(c_int_p)))
+        else:
+            _check(self.lib.avr_medium_grid(
+                self.h, _fp(med.density), med.nx, med.ny, med.nz, _fp(args[0]), _fp(args[1]), _fp(args[2]),
+                _fp(args[3]), _fp(args[4]), float(med.g), _fp(Le), _fp(ls), ls.shape[2], ls.shape[1], ls.shape[0],
+                mres.ctypes.data_as(c_int_p)))
+        types = np.ascontiguousarray(scene.light_types, np.int32)
+        w = f32(scene.light_w.reshape(-1))
+        L = f32(scene.light_L.reshape(-1))
+        sc = f32(scene.light_scale)
+        _check(self.lib.avr_lights(self.h, len(scene.lights), types.ctypes.data_as(c_int_p), _fp(w), _fp(L), _fp(sc),
+                                   float(scene.scene_radius)))
+        _check(self.lib.avr_camera(self.h, int(scene.camera.type_id), _fp(f32(scene.camera_from_raster)),
+                                   _fp(f32(scene.render_from_camera))))
+        film = scene.film
+        _check(self.lib.avr_film(self.h, film.width, film.height, _fp(f32(film.filter_radius)), _fp(f32(film.sensor)),
+                                 float(film.imaging_ratio), float(film.max_component_value)))
+
+    def generate_cloud(self, d_out_ptr, n, first, count, density=1.0, wispiness=1.0, frequency=5.0):
+        _check(self.lib.avr_generate_cloud(self.h, ctypes.c_void_p(d_out_ptr), int(n), int(first), int(count),
+                                           float(density), float(wispiness), float(frequency)))
+
+    def majorant(self, n):
+        out = np.empty(n, np.float32)
+        _check(self.lib.avr_read_majorant(self.h, _fp(out)))
+        return out
+
+    def film_clear(self):
+        _check(self.lib.avr_film_clear(self.h))
+
+    def render(self, spp_begin, spp_end, seed, max_depth):
+        _check(self.lib.avr_render(self.h, int(spp_begin), int(spp_end), int(seed), int(max_depth)))
+
+    def sync(self):
+        _check(self.lib.avr_sync(self.h))
+
+    def stats(self):
+        s = AvrStats()
+        _check(self.lib.avr_get_stats(self.h, ctypes.byref(s)))
+        return s.as_dict()
+
+    def film_read(self, npix):
+        rgb = np.zeros(3 * npix, np.float64)
+        w = np.zeros(npix, np.float64)
+        _check(self.lib.avr_film_read(self.h, rgb.ctypes.data_as(c_double_p), w.ctypes.data_as(c_double_p)))
+        return rgb, w
+
+    def last_pass_samples(self, npix, max_samples):
+        n = npix * max_samples
+        L = np.zeros((n, 4), np.float32)
+        lam = np.zeros((n, 4), np.float32)
+        pdf = np.zeros((n, 4), np.float32)
+        first, ns = ctypes.c_int(), ctypes.c_int()
+        _check(self.lib.avr_last_pass_samples(self.h, _fp(L), _fp(lam), _fp(pdf), n, ctypes.byref(first),
+                                              ctypes.byref(ns)))
+        m = npix * ns.value
+        return first.value, ns.value, L[:m], lam[:m], pdf[:m]
+
+    def film_export_device(self, d_dst_ptr):
+        _check(self.lib.avr_film_export_device(self.h, ctypes.c_void_p(d_dst_ptr)))
+
+    def film_device_ptrs(self):
+        a, b = ctypes.c_void_p(), ctypes.c_void_p()
+        _check(self.lib.avr_film_device_ptrs(self.h, ctypes.byref(a), ctypes.byref(b)))
+        return a.value, b.value

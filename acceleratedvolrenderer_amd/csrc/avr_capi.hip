@@ -1,0 +1,476 @@
+// avr_capi.hip — host side of libavr_hip.so: the C-ABI (include/avr.h) and the
+// wavefront scheduler that replaces pbrt's ImageTileIntegrator::Render /
+// WavefrontPathIntegrator::Render loops (cpu/integrators.cpp:72-232,
+// wavefront/integrator.cpp:290-493) for the volumetric path.
+//
+// Scheduling: the requested sample range is cut into passes of S sample indices
+// over all P pixels (P*S <= max_paths, default 16M paths in flight — HBM is 288 GB,
+// pbrt's GPU path caps at 1M). Each pass: k_camera, then depth iterations of
+// {k_medium, k_shadow} over compacted queues until no path survives, then k_film.
+// Everything is enqueued on one HIP stream; the host reads back one int (the
+// survivor count) per depth iteration to size the next launch and stop early.
+#include "avr_kernels.hip"
+#include "../../include/avr.h"
+
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+#include <algorithm>
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string &msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                          \
+    do {                                                                                       \
+        hipError_t e_ = (expr);                                                                \
+        if (e_ != hipSuccess)                                                                  \
+            return fail(AVR_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));       \
+    } while (0)
+
+template <typename T>
+hipError_t dalloc(T **p, size_t n) { return hipMalloc((void **)p, std::max<size_t>(n, 1) * sizeof(T)); }
+
+}  // namespace
+
+struct avr_context {
+    int device = 0;
+    long long max_paths = 16ll << 20;
+    hipStream_t own_stream = nullptr, stream = nullptr;
+    // medium
+    avr::DevMedium med{};
+    float *d_density_owned = nullptr;
+    float *d_sigma_a = nullptr, *d_sigma_s = nullptr, *d_Le = nullptr, *d_lescale = nullptr, *d_majorant = nullptr;
+    bool has_medium = false;
+    // lights / camera / film
+    avr::DevLights lights{};
+    float *d_lightL = nullptr;
+    avr::DevCamera cam{};
+    bool has_camera = false;
+    avr::DevFilm film{};
+    float *d_xyz = nullptr;
+    bool has_film = false;
+    // path state
+    long long cap = 0;
+    avr::PathSoA ps{};
+    avr::ShadowSoA sh{};
+    int *d_queue[2] = {nullptr, nullptr};
+    int *d_counts = nullptr;  // [0],[1] queue counts, [2] shadow count
+    unsigned long long *d_stats = nullptr;
+    int *h_count = nullptr;   // pinned
+    avr_stats stats{};
+    std::vector<hipEvent_t> evpool;
+    int last_base = 0, last_S = 0;
+};
+
+namespace {
+
+void free_paths(avr_context *c) {
+    float4 *f4[] = {c->ps.o, c->ps.d, c->ps.lambda, c->ps.pdf, c->ps.beta, c->ps.r_u, c->ps.r_l, c->ps.L,
+                    c->sh.o, c->sh.d, c->sh.bf, c->sh.Ls, c->sh.rp_pl};
+    for (auto p : f4) if (p) (void)hipFree(p);
+    if (c->ps.smp_state) (void)hipFree(c->ps.smp_state);
+    if (c->ps.smp_inc) (void)hipFree(c->ps.smp_inc);
+    if (c->ps.depth) (void)hipFree(c->ps.depth);
+    if (c->sh.path) (void)hipFree(c->sh.path);
+    for (auto &q : c->d_queue) if (q) (void)hipFree(q), q = nullptr;
+    c->ps = {};
+    c->sh = {};
+    c->cap = 0;
+}
+
+int ensure_paths(avr_context *c, long long n) {
+    if (n <= c->cap) return AVR_OK;
+    free_paths(c);
+    const size_t N = (size_t)n;
+    HIP_TRY(dalloc(&c->ps.o, N)); HIP_TRY(dalloc(&c->ps.d, N)); HIP_TRY(dalloc(&c->ps.lambda, N));
+    HIP_TRY(dalloc(&c->ps.pdf, N)); HIP_TRY(dalloc(&c->ps.beta, N)); HIP_TRY(dalloc(&c->ps.r_u, N));
+    HIP_TRY(dalloc(&c->ps.r_l, N)); HIP_TRY(dalloc(&c->ps.L, N));
+    HIP_TRY(dalloc(&c->ps.smp_state, N)); HIP_TRY(dalloc(&c->ps.smp_inc, N)); HIP_TRY(dalloc(&c->ps.depth, N));
+    HIP_TRY(dalloc(&c->sh.path, N)); HIP_TRY(dalloc(&c->sh.o, N)); HIP_TRY(dalloc(&c->sh.d, N));
+    HIP_TRY(dalloc(&c->sh.bf, N)); HIP_TRY(dalloc(&c->sh.Ls, N)); HIP_TRY(dalloc(&c->sh.rp_pl, N));
+    HIP_TRY(dalloc(&c->d_queue[0], N)); HIP_TRY(dalloc(&c->d_queue[1], N));
+    c->cap = n;
+    return AVR_OK;
+}
+
+void copy_xf(avr::Xf &x, const float m[16]) {
+    for (int i = 0; i < 12; ++i) x.m[i] = m[i];
+}
+
+int upload_table(float **dst, const float *src, size_t n, hipStream_t s) {
+    if (*dst) { (void)hipFree(*dst); *dst = nullptr; }
+    if (!src) return AVR_OK;
+    HIP_TRY(dalloc(dst, n));
+    HIP_TRY(hipMemcpyAsync(*dst, src, n * sizeof(float), hipMemcpyHostToDevice, s));
+    return AVR_OK;
+}
+
+int blocks_for(long long n, int per = 256, int cap = 256 * 16) {
+    long long b = (n + per - 1) / per;
+    if (b < 1) b = 1;
+    return (int)std::min<long long>(b, cap);
+}
+
+bool affine(const float m[16]) { return m[12] == 0 && m[13] == 0 && m[14] == 0 && m[15] == 1; }
+
+int medium_common(avr_context *c, const float *d_density, int nx, int ny, int nz, const float bounds[6],
+                  const float rfm[16], const float mfr[16], const float *sigma_a, const float *sigma_s, float g,
+                  const float *Le, const float *Lescale, int lnx, int lny, int lnz, const int mres[3]) {
+    if (!affine(rfm) || !affine(mfr)) return fail(AVR_ERR_ARG, "medium transforms must be affine");
+    if (!sigma_a || !sigma_s) return fail(AVR_ERR_ARG, "sigma_a/sigma_s tables required");
+    if (mres[0] < 1 || mres[1] < 1 || mres[2] < 1) return fail(AVR_ERR_ARG, "bad majorant resolution");
+    if (Le && (!Lescale || lnx < 1 || lny < 1 || lnz < 1)) return fail(AVR_ERR_ARG, "Le needs a Lescale grid");
+    int rc;
+    if ((rc = upload_table(&c->d_sigma_a, sigma_a, avr::kNTable, c->stream))) return rc;
+    if ((rc = upload_table(&c->d_sigma_s, sigma_s, avr::kNTable, c->stream))) return rc;
+    if ((rc = upload_table(&c->d_Le, Le, avr::kNTable, c->stream))) return rc;
+    if ((rc = upload_table(&c->d_lescale, Le ? Lescale : nullptr, (size_t)lnx * lny * lnz, c->stream))) return rc;
+    avr::DevMedium &m = c->med;
+    m.density = d_density;
+    m.nx = nx; m.ny = ny; m.nz = nz;
+    for (int i = 0; i < 3; ++i) { m.bmin[i] = bounds[i]; m.bmax[i] = bounds[3 + i]; m.mres[i] = mres[i]; }
+    copy_xf(m.render_from_medium, rfm);
+    copy_xf(m.medium_from_render, mfr);
+    m.sigma_a = c->d_sigma_a;
+    m.sigma_s = c->d_sigma_s;
+    m.g = g;
+    // isEmissive = Le_spec.MaxValue() > 0 (media.cpp:238)
+    bool emissive = false;
+    if (Le) for (int i = 0; i < avr::kNTable; ++i) emissive |= Le[i] > 0;
+    m.emissive = emissive ? 1 : 0;
+    m.Le = c->d_Le;
+    m.lescale = c->d_lescale;
+    m.lnx = Le ? lnx : 1; m.lny = Le ? lny : 1; m.lnz = Le ? lnz : 1;
+    if (c->d_majorant) (void)hipFree(c->d_majorant);
+    const int nm = mres[0] * mres[1] * mres[2];
+    HIP_TRY(dalloc(&c->d_majorant, (size_t)nm));
+    hipLaunchKernelGGL(avr::k_majorant, dim3(nm), dim3(256), 0, c->stream, d_density, nx, ny, nz, mres[0], mres[1],
+                       mres[2], c->d_majorant);
+    HIP_TRY(hipGetLastError());
+    m.majorant = c->d_majorant;
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    c->has_medium = true;
+    return AVR_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *avr_last_error(void) { return g_err.c_str(); }
+
+int avr_context_create(int device, long long max_paths, avr_context **out) {
+    if (!out) return fail(AVR_ERR_ARG, "null out");
+    int ndev = 0;
+    HIP_TRY(hipGetDeviceCount(&ndev));
+    if (device < 0 || device >= ndev) return fail(AVR_ERR_ARG, "device index out of range");
+    HIP_TRY(hipSetDevice(device));
+    auto *c = new avr_context();
+    c->device = device;
+    if (max_paths > 0) c->max_paths = max_paths;
+    hipError_t e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
+    if (e != hipSuccess) { delete c; return fail(AVR_ERR_HIP, hipGetErrorString(e)); }
+    c->stream = c->own_stream;
+    if (dalloc(&c->d_counts, 4) != hipSuccess || dalloc(&c->d_stats, avr::kNumStats) != hipSuccess ||
+        hipHostMalloc((void **)&c->h_count, sizeof(int) * 4) != hipSuccess) {
+        delete c;
+        return fail(AVR_ERR_HIP, "context allocation failed");
+    }
+    *out = c;
+    return AVR_OK;
+}
+
+int avr_context_destroy(avr_context *c) {
+    if (!c) return AVR_OK;
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    free_paths(c);
+    float *fs[] = {c->d_density_owned, c->d_sigma_a, c->d_sigma_s, c->d_Le, c->d_lescale, c->d_majorant,
+                   c->d_lightL, c->d_xyz};
+    for (auto p : fs) if (p) (void)hipFree(p);
+    if (c->film.rgb_sum) (void)hipFree(c->film.rgb_sum);
+    if (c->film.w_sum) (void)hipFree(c->film.w_sum);
+    if (c->d_counts) (void)hipFree(c->d_counts);
+    if (c->d_stats) (void)hipFree(c->d_stats);
+    if (c->h_count) (void)hipHostFree(c->h_count);
+    for (auto e : c->evpool) (void)hipEventDestroy(e);
+    if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+    delete c;
+    return AVR_OK;
+}
+
+int avr_set_stream(avr_context *c, void *s) {
+    if (!c) return fail(AVR_ERR_ARG, "null context");
+    c->stream = s ? (hipStream_t)s : c->own_stream;
+    return AVR_OK;
+}
+
+int avr_medium_grid(avr_context *c, const float *density, int nx, int ny, int nz, const float bounds[6],
+                    const float rfm[16], const float mfr[16], const float *sigma_a, const float *sigma_s, float g,
+                    const float *Le, const float *Lescale, int lnx, int lny, int lnz, const int mres[3]) {
+    if (!c || !density || nx < 1 || ny < 1 || nz < 1) return fail(AVR_ERR_ARG, "bad grid");
+    HIP_TRY(hipSetDevice(c->device));
+    if (c->d_density_owned) { (void)hipFree(c->d_density_owned); c->d_density_owned = nullptr; }
+    const size_t n = (size_t)nx * ny * nz;
+    if (n > (size_t)INT32_MAX) return fail(AVR_ERR_ARG, "grid too large for int32 indexing (containers.h:834)");
+    HIP_TRY(dalloc(&c->d_density_owned, n));
+    HIP_TRY(hipMemcpyAsync(c->d_density_owned, density, n * sizeof(float), hipMemcpyHostToDevice, c->stream));
+    return medium_common(c, c->d_density_owned, nx, ny, nz, bounds, rfm, mfr, sigma_a, sigma_s, g, Le, Lescale, lnx,
+                         lny, lnz, mres);
+}
+
+int avr_medium_grid_device(avr_context *c, const float *d_density, int nx, int ny, int nz, const float bounds[6],
+                           const float rfm[16], const float mfr[16], const float *sigma_a, const float *sigma_s,
+                           float g, const float *Le, const float *Lescale, int lnx, int lny, int lnz,
+                           const int mres[3]) {
+    if (!c || !d_density || nx < 1 || ny < 1 || nz < 1) return fail(AVR_ERR_ARG, "bad grid");
+    if ((size_t)nx * ny * nz > (size_t)INT32_MAX) return fail(AVR_ERR_ARG, "grid too large for int32 indexing");
+    HIP_TRY(hipSetDevice(c->device));
+    if (c->d_density_owned) { (void)hipFree(c->d_density_owned); c->d_density_owned = nullptr; }
+    return medium_common(c, d_density, nx, ny, nz, bounds, rfm, mfr, sigma_a, sigma_s, g, Le, Lescale, lnx, lny, lnz,
+                         mres);
+}
+
+int avr_generate_cloud(avr_context *c, float *d_out, int n, long long first, long long count, float density,
+                       float wispiness, float frequency) {
+    if (!c || !d_out || n < 1 || count < 0) return fail(AVR_ERR_ARG, "bad cloud args");
+    HIP_TRY(hipSetDevice(c->device));
+    hipLaunchKernelGGL(avr::k_cloud, dim3(blocks_for(count, 256, 256 * 32)), dim3(256), 0, c->stream, d_out, n, first,
+                       count, density, wispiness, frequency);
+    HIP_TRY(hipGetLastError());
+    return AVR_OK;
+}
+
+int avr_read_majorant(avr_context *c, float *out) {
+    if (!c || !c->has_medium || !out) return fail(AVR_ERR_STATE, "no medium");
+    const int nm = c->med.mres[0] * c->med.mres[1] * c->med.mres[2];
+    HIP_TRY(hipMemcpyAsync(out, c->d_majorant, nm * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return AVR_OK;
+}
+
+int avr_lights(avr_context *c, int n, const int *types, const float *w3, const float *L, const float *scale,
+               float scene_radius) {
+    if (!c || n < 0 || n > avr::kMaxLights) return fail(AVR_ERR_ARG, "0..8 lights supported");
+    if (n > 0 && (!types || !w3 || !L || !scale)) return fail(AVR_ERR_ARG, "null light arrays");
+    HIP_TRY(hipSetDevice(c->device));
+    int rc = upload_table(&c->d_lightL, n ? L : nullptr, (size_t)n * avr::kNTable, c->stream);
+    if (rc) return rc;
+    c->lights = {};
+    c->lights.n = n;
+    for (int i = 0; i < n; ++i) {
+        if (types[i] != 0 && types[i] != 1) return fail(AVR_ERR_ARG, "light type must be 0 (distant) or 1 (uniform infinite)");
+        c->lights.type[i] = types[i];
+        for (int k = 0; k < 3; ++k) c->lights.w[i][k] = w3[3 * i + k];
+        c->lights.L[i] = c->d_lightL + (size_t)i * avr::kNTable;
+        c->lights.scale[i] = scale[i];
+    }
+    c->lights.scene_radius = scene_radius;
+    return AVR_OK;
+}
+
+int avr_camera(avr_context *c, int type, const float cfr[16], const float rfc[16]) {
+    if (!c || (type != 0 && type != 1) || !cfr || !rfc) return fail(AVR_ERR_ARG, "bad camera");
+    if (!affine(rfc)) return fail(AVR_ERR_ARG, "render_from_camera must be affine");
+    c->cam.type = type;
+    for (int i = 0; i < 16; ++i) c->cam.raster[i] = cfr[i];
+    copy_xf(c->cam.render_from_camera, rfc);
+    c->has_camera = true;
+    return AVR_OK;
+}
+
+int avr_film(avr_context *c, int width, int height, const float fr[2], const float *sensor, float imaging_ratio,
+             float max_component_value) {
+    if (!c || width < 1 || height < 1 || !fr || !sensor) return fail(AVR_ERR_ARG, "bad film");
+    HIP_TRY(hipSetDevice(c->device));
+    int rc = upload_table(&c->d_xyz, sensor, 3 * (size_t)avr::kNTable, c->stream);
+    if (rc) return rc;
+    if (c->film.rgb_sum) (void)hipFree(c->film.rgb_sum);
+    if (c->film.w_sum) (void)hipFree(c->film.w_sum);
+    c->film = {};
+    c->film.width = width;
+    c->film.height = height;
+    c->film.filter_rx = fr[0];
+    c->film.filter_ry = fr[1];
+    c->film.xyz = c->d_xyz;
+    c->film.imaging_ratio = imaging_ratio;
+    c->film.max_component = max_component_value;
+    const size_t np = (size_t)width * height;
+    HIP_TRY(dalloc(&c->film.rgb_sum, 3 * np));
+    HIP_TRY(dalloc(&c->film.w_sum, np));
+    c->has_film = true;
+    return avr_film_clear(c);
+}
+
+int avr_film_clear(avr_context *c) {
+    if (!c || !c->has_film) return fail(AVR_ERR_STATE, "no film");
+    const size_t np = (size_t)c->film.width * c->film.height;
+    HIP_TRY(hipMemsetAsync(c->film.rgb_sum, 0, 3 * np * sizeof(double), c->stream));
+    HIP_TRY(hipMemsetAsync(c->film.w_sum, 0, np * sizeof(double), c->stream));
+    return AVR_OK;
+}
+
+int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_depth) {
+    if (!c) return fail(AVR_ERR_ARG, "null context");
+    if (!c->has_medium || !c->has_camera || !c->has_film) return fail(AVR_ERR_STATE, "medium, camera and film required");
+    if (spp_begin < 0 || spp_end < spp_begin || max_depth < 0) return fail(AVR_ERR_ARG, "bad sample range");
+    HIP_TRY(hipSetDevice(c->device));
+    const long long P = (long long)c->film.width * c->film.height;
+    if (P > (1ll << 30)) return fail(AVR_ERR_ARG, "film too large");
+    const long long Smax = std::max<long long>(1, c->max_paths / P);
+    const long long need = P * std::min<long long>(Smax, std::max(1, spp_end - spp_begin));
+    int rc = ensure_paths(c, need);
+    if (rc) return rc;
+    if (c->evpool.empty()) {
+        c->evpool.resize(10);
+        for (auto &e : c->evpool) HIP_TRY(hipEventCreate(&e));
+    }
+    hipEvent_t evStart = c->evpool[0], evEnd = c->evpool[1];
+    hipEvent_t e0 = c->evpool[2], e1 = c->evpool[3], e2 = c->evpool[4], e3 = c->evpool[5];
+    c->stats = {};
+    HIP_TRY(hipMemsetAsync(c->d_stats, 0, sizeof(unsigned long long) * avr::kNumStats, c->stream));
+    HIP_TRY(hipEventRecord(evStart, c->stream));
+    float ms = 0;
+    for (long long base = spp_begin; base < spp_end; base += Smax) {
+        const int S = (int)std::min<long long>(Smax, spp_end - base);
+        avr::Params p{};
+        p.med = c->med;
+        p.lights = c->lights;
+        p.cam = c->cam;
+        p.film = c->film;
+        p.ps = c->ps;
+        p.sh = c->sh;
+        p.max_depth = max_depth;
+        p.seed = seed;
+        p.pass_pixels = (int)P;
+        p.pass_samples = S;
+        p.sample_base = (int)base;
+        p.stats = c->d_stats;
+        const long long n0 = P * S;
+        HIP_TRY(hipEventRecord(e0, c->stream));
+        hipLaunchKernelGGL(avr::k_camera, dim3(blocks_for(n0)), dim3(256), 0, c->stream, p);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipEventRecord(e1, c->stream));
+        HIP_TRY(hipEventSynchronize(e1));
+        HIP_TRY(hipEventElapsedTime(&ms, e0, e1));
+        c->stats.ms_camera += ms;
+        c->h_count[0] = (int)n0;
+        HIP_TRY(hipMemcpyAsync(c->d_counts, c->h_count, sizeof(int), hipMemcpyHostToDevice, c->stream));
+        int cur = 0;
+        long long count = n0;
+        bool first = true;
+        while (count > 0) {
+            const int nxt = cur ^ 1;
+            HIP_TRY(hipMemsetAsync(c->d_counts + nxt, 0, sizeof(int), c->stream));
+            HIP_TRY(hipMemsetAsync(c->d_counts + 2, 0, sizeof(int), c->stream));
+            p.queue_in = first ? nullptr : c->d_queue[cur];
+            p.count_in = c->d_counts + cur;
+            p.queue_out = c->d_queue[nxt];
+            p.count_out = c->d_counts + nxt;
+            p.shadow_count = c->d_counts + 2;
+            const int nb = blocks_for(count);
+            HIP_TRY(hipEventRecord(e0, c->stream));
+            hipLaunchKernelGGL(avr::k_medium, dim3(nb), dim3(256), 0, c->stream, p);
+            HIP_TRY(hipGetLastError());
+            HIP_TRY(hipEventRecord(e1, c->stream));
+            hipLaunchKernelGGL(avr::k_shadow, dim3(nb), dim3(256), 0, c->stream, p);
+            HIP_TRY(hipGetLastError());
+            HIP_TRY(hipEventRecord(e2, c->stream));
+            HIP_TRY(hipMemcpyAsync(c->h_count, c->d_counts + nxt, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+            HIP_TRY(hipStreamSynchronize(c->stream));
+            HIP_TRY(hipEventElapsedTime(&ms, e0, e1));
+            c->stats.ms_medium += ms;
+            HIP_TRY(hipEventElapsedTime(&ms, e1, e2));
+            c->stats.ms_shadow += ms;
+            c->stats.medium_launches++;
+            count = c->h_count[0];
+            cur = nxt;
+            first = false;
+        }
+        HIP_TRY(hipEventRecord(e2, c->stream));
+        hipLaunchKernelGGL(avr::k_film, dim3(blocks_for(P)), dim3(256), 0, c->stream, p);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipEventRecord(e3, c->stream));
+        HIP_TRY(hipEventSynchronize(e3));
+        HIP_TRY(hipEventElapsedTime(&ms, e2, e3));
+        c->stats.ms_film += ms;
+        c->last_base = (int)base;
+        c->last_S = S;
+    }
+    HIP_TRY(hipEventRecord(evEnd, c->stream));
+    HIP_TRY(hipEventSynchronize(evEnd));
+    HIP_TRY(hipEventElapsedTime(&ms, evStart, evEnd));
+    c->stats.ms_total = ms;
+    unsigned long long h[avr::kNumStats];
+    HIP_TRY(hipMemcpy(h, c->d_stats, sizeof(h), hipMemcpyDeviceToHost));
+    c->stats.medium_lookups = h[0];
+    c->stats.medium_items_in = h[1];
+    c->stats.medium_items_out = h[2];
+    c->stats.shadow_lookups = h[3];
+    c->stats.shadow_items = h[4];
+    c->stats.medium_dda_steps = h[5];
+    c->stats.shadow_dda_steps = h[6];
+    return AVR_OK;
+}
+
+int avr_sync(avr_context *c) {
+    if (!c) return fail(AVR_ERR_ARG, "null context");
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return AVR_OK;
+}
+
+int avr_get_stats(avr_context *c, avr_stats *out) {
+    if (!c || !out) return fail(AVR_ERR_ARG, "null arg");
+    *out = c->stats;
+    return AVR_OK;
+}
+
+int avr_film_read(avr_context *c, double *rgb, double *w) {
+    if (!c || !c->has_film || !rgb || !w) return fail(AVR_ERR_STATE, "no film");
+    const size_t np = (size_t)c->film.width * c->film.height;
+    HIP_TRY(hipMemcpyAsync(rgb, c->film.rgb_sum, 3 * np * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(w, c->film.w_sum, np * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return AVR_OK;
+}
+
+int avr_film_device_ptrs(avr_context *c, void **rgb, void **w) {
+    if (!c || !c->has_film || !rgb || !w) return fail(AVR_ERR_STATE, "no film");
+    *rgb = c->film.rgb_sum;
+    *w = c->film.w_sum;
+    return AVR_OK;
+}
+
+int avr_last_pass_samples(avr_context *c, float *L, float *lambda, float *pdf, long long n_max, int *first,
+                          int *ns) {
+    if (!c || !c->has_film || !L || !lambda || !pdf || !first || !ns) return fail(AVR_ERR_ARG, "null arg");
+    const long long n = (long long)c->film.width * c->film.height * c->last_S;
+    if (n_max < n) return fail(AVR_ERR_ARG, "buffer too small for the last pass");
+    if (n > 0) {
+        HIP_TRY(hipMemcpy(L, c->ps.L, n * sizeof(float4), hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(lambda, c->ps.lambda, n * sizeof(float4), hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(pdf, c->ps.pdf, n * sizeof(float4), hipMemcpyDeviceToHost));
+    }
+    *first = c->last_base;
+    *ns = c->last_S;
+    return AVR_OK;
+}
+
+int avr_film_export_device(avr_context *c, void *dst) {
+    if (!c || !c->has_film || !dst) return fail(AVR_ERR_STATE, "no film");
+    const size_t np = (size_t)c->film.width * c->film.height;
+    double *d = (double *)dst;
+    HIP_TRY(hipMemcpyAsync(d, c->film.rgb_sum, 3 * np * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(d + 3 * np, c->film.w_sum, np * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return AVR_OK;
+}
+
+}  // extern "C"

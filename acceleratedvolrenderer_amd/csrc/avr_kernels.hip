@@ -1,0 +1,729 @@
+// avr_kernels.hip — MI355X (gfx950) wavefront kernels of the volumetric path integrator.
+//
+// Replaces, for the GPU, pbrt-v4's VolPathIntegrator::Li/SampleLd
+// (cpu/integrators.cpp:962-1399), SampleT_maj + DDAMajorantIterator (media.h:136-214,
+// 730-806), GridMedium sampling (media.h:265-352), the wavefront work queues
+// (wavefront/workqueue.h:41-172) and RGBFilm accumulation (film.h:232-316).
+// Paths relative to /root/reference/src/pbrt.
+//
+// Decomposition (one pass = P pixels x S sample indices, path id = s*P + pixel):
+//   k_camera   : sampler start, wavelengths, box-filter camera sample, camera ray
+//   k_medium   : delta tracking over the majorant DDA (majorant grid staged in LDS),
+//                absorption / real / null events, medium emission, NEE light pick +
+//                shadow-ray spawn, HG phase sampling, escaped-ray infinite lights.
+//                Survivors and shadow rays are pushed with one atomic per wave
+//                (__ballot + __popcll + mbcnt prefix) — stream compaction between events.
+//   k_shadow   : ratio-tracking transmittance with Russian roulette along shadow rays
+//   k_film     : per pixel, samples added in sampleIndex order into fp64 sums
+//                (bit-identical order to ImageTileIntegrator::Render's per-pixel loop).
+#include "avr_numerics.h"
+
+namespace avr {
+
+struct DevMedium {
+    const float *density;
+    int nx, ny, nz;
+    float bmin[3], bmax[3];
+    Xf render_from_medium, medium_from_render;
+    const float *sigma_a, *sigma_s;   // 471-entry densely sampled tables (sigmaScale folded in)
+    float g;
+    int emissive;
+    const float *Le;                  // 471
+    const float *lescale;
+    int lnx, lny, lnz;
+    const float *majorant;
+    int mres[3];
+};
+
+constexpr int kMaxLights = 8;
+struct DevLights {
+    int n;
+    int type[kMaxLights];             // 0 distant (delta), 1 uniform infinite
+    float w[kMaxLights][3];
+    const float *L[kMaxLights];
+    float scale[kMaxLights];
+    float scene_radius;
+};
+
+struct DevCamera {
+    int type;                         // 0 orthographic, 1 perspective
+    float raster[16];                 // cameraFromRaster (full 4x4; perspective is projective)
+    Xf render_from_camera;
+};
+
+struct DevFilm {
+    int width, height;
+    float filter_rx, filter_ry;
+    const float *xyz;                 // 3 x 471
+    float imaging_ratio;
+    float max_component;
+    double *rgb_sum;                  // W*H*3
+    double *w_sum;                    // W*H
+};
+
+struct PathSoA {
+    float4 *o, *d, *lambda, *pdf, *beta, *r_u, *r_l, *L;
+    uint64_t *smp_state, *smp_inc;
+    int *depth;
+};
+struct ShadowSoA {
+    int *path;
+    float4 *o, *d, *bf, *Ls, *rp_pl;
+};
+
+// Per-launch work counters (u64): [0] lookups k_medium, [1] items in k_medium,
+// [2] items out k_medium (survivors + shadow pushes), [3] lookups k_shadow, [4] items k_shadow,
+// [5] DDA steps k_medium, [6] DDA steps k_shadow
+constexpr int kNumStats = 8;
+
+struct Params {
+    DevMedium med;
+    DevLights lights;
+    DevCamera cam;
+    DevFilm film;
+    PathSoA ps;
+    ShadowSoA sh;
+    int max_depth;
+    int seed;
+    int pass_pixels;                  // P
+    int pass_samples;                 // S
+    int sample_base;                  // first sampleIndex of the pass
+    const int *queue_in;              // nullptr: identity (first depth)
+    const int *count_in;
+    int *queue_out;
+    int *count_out;
+    int *shadow_count;
+    unsigned long long *stats;
+};
+
+__device__ __forceinline__ int lane_id() { return __lane_id(); }
+
+// Wave-aggregated queue push: one atomic per wave, lane offset from the ballot prefix.
+__device__ __forceinline__ int wave_push(int *counter, bool pred) {
+    const uint64_t mask = __ballot(pred);
+    if (mask == 0) return -1;
+    const int leader = __ffsll((long long)mask) - 1;
+    int base = 0;
+    if (lane_id() == leader) base = atomicAdd(counter, __popcll(mask));
+    base = __shfl(base, leader);
+    const uint64_t lt = (lane_id() == 0) ? 0ull : (mask & ((~0ull) >> (64 - lane_id())));
+    return pred ? base + __popcll(lt) : -1;
+}
+
+__device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    return v;
+}
+__device__ __forceinline__ void flush_stat(unsigned long long *stats, int idx, unsigned long long v) {
+    v = wave_sum_u64(v);
+    if (lane_id() == 0 && v) atomicAdd(stats + idx, v);
+}
+
+// ---------------------------------------------------------------------------
+// GridMedium density fetch — SampledGrid<float>::Lookup (util/containers.h:804-835)
+__device__ __forceinline__ float grid_at(const float *__restrict__ v, int nx, int ny, int nz, int x, int y, int z) {
+    if (x < 0 || x >= nx || y < 0 || y >= ny || z < 0 || z >= nz) return 0.f;
+    return v[(z * ny + y) * nx + x];
+}
+__device__ __forceinline__ float grid_lookup(const float *__restrict__ v, int nx, int ny, int nz, V3 p) {
+    float psx = p.x * nx - .5f, psy = p.y * ny - .5f, psz = p.z * nz - .5f;
+    int ix = (int)__builtin_floorf(psx), iy = (int)__builtin_floorf(psy), iz = (int)__builtin_floorf(psz);
+    float dx = psx - (float)ix, dy = psy - (float)iy, dz = psz - (float)iz;
+    float d00 = lerp(dx, grid_at(v, nx, ny, nz, ix, iy, iz), grid_at(v, nx, ny, nz, ix + 1, iy, iz));
+    float d10 = lerp(dx, grid_at(v, nx, ny, nz, ix, iy + 1, iz), grid_at(v, nx, ny, nz, ix + 1, iy + 1, iz));
+    float d01 = lerp(dx, grid_at(v, nx, ny, nz, ix, iy, iz + 1), grid_at(v, nx, ny, nz, ix + 1, iy, iz + 1));
+    float d11 = lerp(dx, grid_at(v, nx, ny, nz, ix, iy + 1, iz + 1), grid_at(v, nx, ny, nz, ix + 1, iy + 1, iz + 1));
+    return lerp(dz, lerp(dy, d00, d10), lerp(dy, d01, d11));
+}
+
+struct MediumSample { Spec sigma_a, sigma_s, Le; };
+
+// GridMedium::SamplePoint — media.h:287-319 (no temperature grid); sig_a/sig_s pre-sampled at lambda
+__device__ __forceinline__ MediumSample sample_point(const DevMedium &m, V3 p, const Spec &sig_a, const Spec &sig_s,
+                                                     const Spec &Le_l) {
+    MediumSample ms;
+    p = xf_point_pair(m.medium_from_render, p);
+    p = box_offset(m.bmin, m.bmax, p);
+    float d = grid_lookup(m.density, m.nx, m.ny, m.nz, p);
+    ms.sigma_a = sig_a * d;
+    ms.sigma_s = sig_s * d;
+    ms.Le = Spec::c(0.f);
+    if (m.emissive) {
+        float scale = grid_lookup(m.lescale, m.lnx, m.lny, m.lnz, p);
+        if (scale > 0) ms.Le = Le_l * scale;
+    }
+    return ms;
+}
+
+// DDAMajorantIterator — media.h:136-214
+struct Dda {
+    float tMin, tMax;
+    float next[3], delta[3];
+    int step[3], limit[3], voxel[3];
+};
+__device__ __forceinline__ bool dda_init(Dda &it, const DevMedium &m, Ray ray, float raytMax) {
+    // GridMedium::SampleRay — media.h:322-337
+    ray = xf_ray(m.medium_from_render, ray, &raytMax, /*forward=*/false);
+    float tMin, tMax;
+    if (!intersect_box(m.bmin, m.bmax, ray.o, ray.d, raytMax, &tMin, &tMax)) {
+        it.tMin = kInf; it.tMax = -kInf;
+        return false;
+    }
+    it.tMin = tMin; it.tMax = tMax;
+    float diag[3] = {m.bmax[0] - m.bmin[0], m.bmax[1] - m.bmin[1], m.bmax[2] - m.bmin[2]};
+    V3 go = box_offset(m.bmin, m.bmax, ray.o);
+    V3 gd = {ray.d.x / diag[0], ray.d.y / diag[1], ray.d.z / diag[2]};
+    V3 gi = go + gd * tMin;
+    for (int a = 0; a < 3; ++a) {
+        const int res = m.mres[a];
+        const float gia = comp(gi, a);
+        float gda = comp(gd, a);
+        it.voxel[a] = (int)clampf(gia * res, 0.f, (float)(res - 1));
+        it.delta[a] = 1 / (__builtin_fabsf(gda) * res);
+        if (gda == -0.f) gda = 0.f;
+        if (gda >= 0) {
+            float nextPos = float(it.voxel[a] + 1) / res;
+            it.next[a] = tMin + (nextPos - gia) / gda;
+            it.step[a] = 1;
+            it.limit[a] = res;
+        } else {
+            float nextPos = float(it.voxel[a]) / res;
+            it.next[a] = tMin + (nextPos - gia) / gda;
+            it.step[a] = -1;
+            it.limit[a] = -1;
+        }
+    }
+    return true;
+}
+// Returns false when exhausted; majorant values read through `maj` (LDS-staged when it fits)
+__device__ __forceinline__ bool dda_next(Dda &it, const float *maj, int rx, int ry, float *s0, float *s1, float *mval) {
+    if (it.tMin >= it.tMax) return false;
+    int bits = ((it.next[0] < it.next[1]) << 2) + ((it.next[0] < it.next[2]) << 1) + ((it.next[1] < it.next[2]));
+    // cmpToAxis = {2, 1, 2, 1, 2, 2, 0, 0}
+    int ax = (bits >= 6) ? 0 : ((bits == 1 || bits == 3) ? 1 : 2);
+    float nextA = ax == 0 ? it.next[0] : (ax == 1 ? it.next[1] : it.next[2]);
+    float tExit = fminf_(it.tMax, nextA);
+    *mval = maj[it.voxel[0] + rx * (it.voxel[1] + ry * it.voxel[2])];
+    *s0 = it.tMin;
+    *s1 = tExit;
+    it.tMin = tExit;
+    if (nextA > it.tMax) it.tMin = it.tMax;
+    int vox = (ax == 0 ? it.voxel[0] : (ax == 1 ? it.voxel[1] : it.voxel[2])) + (ax == 0 ? it.step[0] : (ax == 1 ? it.step[1] : it.step[2]));
+    int lim = ax == 0 ? it.limit[0] : (ax == 1 ? it.limit[1] : it.limit[2]);
+    if (vox == lim) it.tMin = it.tMax;
+    float dl = ax == 0 ? it.delta[0] : (ax == 1 ? it.delta[1] : it.delta[2]);
+    if (ax == 0) { it.voxel[0] = vox; it.next[0] += dl; }
+    else if (ax == 1) { it.voxel[1] = vox; it.next[1] += dl; }
+    else { it.voxel[2] = vox; it.next[2] += dl; }
+    return true;
+}
+
+// SampleT_maj<GridMedium> — media.h:741-806. `cb(p, ms, sigma_maj, T_maj)` returns false to stop.
+template <typename F>
+__device__ __forceinline__ Spec sample_t_maj(const DevMedium &m, const float *maj, Ray ray, float tMax, float u,
+                                            Pcg32 &rng, const Spec &sig_a, const Spec &sig_s, const Spec &Le_l,
+                                            unsigned long long &nLookup, unsigned long long &nSteps, F &&cb) {
+    tMax *= length(ray.d);
+    ray.d = normalize(ray.d);
+    Dda it;
+    dda_init(it, m, ray, tMax);
+    const Spec sigma_t = sig_a + sig_s;
+    Spec T_maj = Spec::c(1.f);
+    while (true) {
+        float segMin, segMax, mv;
+        if (!dda_next(it, maj, m.mres[0], m.mres[1], &segMin, &segMax, &mv)) return T_maj;
+        ++nSteps;
+        const Spec sigma_maj = sigma_t * mv;
+        if (sigma_maj.v0 == 0) {
+            float dt = segMax - segMin;
+            if (__builtin_isinf(dt)) dt = kFloatMax;
+            T_maj = T_maj * fast_exp(-(sigma_maj * dt));
+            continue;
+        }
+        float tMin = segMin;
+        while (true) {
+            float t = tMin + sample_exponential(u, sigma_maj.v0);
+            u = rng.uniform();
+            if (t < segMax) {
+                T_maj = T_maj * fast_exp(-(sigma_maj * (t - tMin)));
+                V3 p = ray.o + ray.d * t;
+                ++nLookup;
+                MediumSample ms = sample_point(m, p, sig_a, sig_s, Le_l);
+                if (!cb(p, ms, sigma_maj, T_maj)) return Spec::c(1.f);
+                T_maj = Spec::c(1.f);
+                tMin = t;
+            } else {
+                float dt = segMax - tMin;
+                if (__builtin_isinf(dt)) dt = kFloatMax;
+                T_maj = T_maj * fast_exp(-(sigma_maj * dt));
+                break;
+            }
+        }
+    }
+}
+
+// IndependentSampler — samplers.h:457-466 (state carried per path)
+struct Sampler {
+    Pcg32 rng;
+    __device__ __forceinline__ float get1d() { return rng.uniform(); }
+};
+
+__device__ __forceinline__ float4 to4(V3 v) { return make_float4(v.x, v.y, v.z, 0.f); }
+__device__ __forceinline__ V3 from4(float4 v) { return {v.x, v.y, v.z}; }
+__device__ __forceinline__ float4 to4(Spec s) { return make_float4(s.v0, s.v1, s.v2, s.v3); }
+__device__ __forceinline__ Spec spec4(float4 v) { return {v.x, v.y, v.z, v.w}; }
+
+__device__ __forceinline__ const float *stage_majorant(const DevMedium &m, float *lds) {
+    const int n = m.mres[0] * m.mres[1] * m.mres[2];
+    if (n > 4096) return m.majorant;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) lds[i] = m.majorant[i];
+    __syncthreads();
+    return lds;
+}
+
+// ---------------------------------------------------------------------------
+// Camera rays — RayIntegrator::EvaluatePixelSample (cpu/integrators.cpp:235-268),
+// GetCameraSample (samplers.h:797-815), BoxFilter::Sample (filters.h:67-70),
+// Orthographic/PerspectiveCamera::GenerateRay (cameras.cpp:284-306, 404-427)
+__global__ void __launch_bounds__(256) k_camera(Params P) {
+    const int n = P.pass_pixels * P.pass_samples;
+    for (int id = blockIdx.x * blockDim.x + threadIdx.x; id < n; id += gridDim.x * blockDim.x) {
+        const int pix = id % P.pass_pixels, s = id / P.pass_pixels;
+        const int px = pix % P.film.width, py = pix / P.film.width;
+        const int sampleIndex = P.sample_base + s;
+        Sampler smp;
+        // IndependentSampler::StartPixelSample: rng.SetSequence(Hash(p, seed)) — the one-argument
+        // SetSequence seeds with MixBits(seq) (rng.h:43-45) — then Advance(sampleIndex * 65536).
+        {
+            const uint64_t seq = hash_3u32((uint32_t)px, (uint32_t)py, (uint32_t)P.seed);
+            smp.rng.set_sequence(seq, mix_bits(seq));
+        }
+        smp.rng.advance((uint64_t)sampleIndex * 65536ull);
+        const float lu = smp.get1d();
+        Lambda lam = sample_visible(lu);
+        const float fu0 = smp.get1d(), fu1 = smp.get1d();
+        const float fpx = lerp(fu0, -P.film.filter_rx, P.film.filter_rx);
+        const float fpy = lerp(fu1, -P.film.filter_ry, P.film.filter_ry);
+        const float pFilmX = ((float)px + fpx) + 0.5f, pFilmY = ((float)py + fpy) + 0.5f;
+        smp.get1d();                 // time
+        smp.get1d(); smp.get1d();    // lens
+        const float *r = P.cam.raster;
+        float xp = r[0] * pFilmX + r[1] * pFilmY + r[2] * 0.f + r[3];
+        float yp = r[4] * pFilmX + r[5] * pFilmY + r[6] * 0.f + r[7];
+        float zp = r[8] * pFilmX + r[9] * pFilmY + r[10] * 0.f + r[11];
+        float wp = r[12] * pFilmX + r[13] * pFilmY + r[14] * 0.f + r[15];
+        V3 pCam = {xp, yp, zp};
+        if (wp != 1) pCam = pCam / wp;
+        Ray ray;
+        if (P.cam.type == 0) ray = {pCam, {0.f, 0.f, 1.f}};
+        else ray = {{0.f, 0.f, 0.f}, normalize(pCam)};
+        ray = xf_ray(P.cam.render_from_camera, ray, nullptr, /*forward=*/true);
+        P.ps.o[id] = to4(ray.o);
+        P.ps.d[id] = to4(ray.d);
+        P.ps.lambda[id] = to4(lam.l);
+        P.ps.pdf[id] = to4(lam.pdf);
+        P.ps.beta[id] = make_float4(1.f, 1.f, 1.f, 1.f);
+        P.ps.r_u[id] = make_float4(1.f, 1.f, 1.f, 1.f);
+        P.ps.r_l[id] = make_float4(1.f, 1.f, 1.f, 1.f);
+        P.ps.L[id] = make_float4(0.f, 0.f, 0.f, 0.f);
+        P.ps.smp_state[id] = smp.rng.state;
+        P.ps.smp_inc[id] = smp.rng.inc;
+        P.ps.depth[id] = 0;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Delta tracking — VolPathIntegrator::Li's medium branch (cpu/integrators.cpp:981-1088),
+// SampleLd's light pick and shadow-ray spawn (1282-1338), escaped rays (1090-1107).
+__global__ void __launch_bounds__(256) k_medium(Params P) {
+    __shared__ float s_maj[4096];
+    const float *maj = stage_majorant(P.med, s_maj);
+    const int count = *P.count_in;
+    unsigned long long nLookup = 0, nIn = 0, nOut = 0, nSteps = 0;
+    const int stride = gridDim.x * blockDim.x;
+    // Every lane of a wave runs the same number of outer iterations so the wave-wide
+    // queue pushes below see all 64 lanes.
+    const int nIter = (count + stride - 1) / stride;
+    for (int it = 0; it < nIter; ++it) {
+        const int i = it * stride + blockIdx.x * blockDim.x + threadIdx.x;
+        const bool valid = i < count;
+        bool pushActive = false, pushShadow = false;
+        int path = 0;
+        V3 newO{}, newD{};
+        float4 shO{}, shD{}, shBF{}, shLs{}, shRP{};
+        if (valid) {
+            ++nIn;
+            path = P.queue_in ? P.queue_in[i] : i;
+            const V3 o = from4(P.ps.o[path]);
+            const V3 d = from4(P.ps.d[path]);
+            const Spec lamv = spec4(P.ps.lambda[path]);
+            Spec beta = spec4(P.ps.beta[path]), r_u = spec4(P.ps.r_u[path]), r_l = spec4(P.ps.r_l[path]);
+            Spec L = spec4(P.ps.L[path]);
+            Sampler smp;
+            smp.rng.state = P.ps.smp_state[path];
+            smp.rng.inc = P.ps.smp_inc[path];
+            int depth = P.ps.depth[path];
+            const LambdaIdx li = lambda_index(lamv);
+            const Spec sig_a = sample_table(P.med.sigma_a, li);
+            const Spec sig_s = sample_table(P.med.sigma_s, li);
+            const Spec Le_l = P.med.emissive ? sample_table(P.med.Le, li) : Spec::c(0.f);
+            const int maxDepth = P.max_depth;
+            bool scattered = false, terminated = false;
+            const float h0 = smp.get1d();
+            const float h1 = smp.get1d();
+            Pcg32 rng;
+            rng.set_sequence(hash_u32(f2u(h0)), hash_u32(f2u(h1)));
+            const float u0 = smp.get1d();
+            V3 pScatter{};
+            auto cb = [&](V3 p, const MediumSample &ms, const Spec &sigma_maj, const Spec &T_maj) -> bool {
+                if (!beta.nonzero()) { terminated = true; return false; }
+                if (depth < maxDepth && ms.Le.nonzero()) {
+                    float pdf = sigma_maj.v0 * T_maj.v0;
+                    Spec betap = beta * T_maj / pdf;
+                    Spec r_e = r_u * sigma_maj * T_maj / pdf;
+                    if (r_e.nonzero()) L = L + betap * ms.sigma_a * ms.Le / r_e.avg();
+                }
+                float pAbsorb = ms.sigma_a.v0 / sigma_maj.v0;
+                float pScat = ms.sigma_s.v0 / sigma_maj.v0;
+                float pNull = fmaxf_(0.f, 1 - pAbsorb - pScat);
+                float um = rng.uniform();
+                int mode = sample_discrete3(pAbsorb, pScat, pNull, um);
+                if (mode == 0) { terminated = true; return false; }
+                if (mode == 1) {
+                    if (depth++ >= maxDepth) { terminated = true; return false; }
+                    float pdf = T_maj.v0 * ms.sigma_s.v0;
+                    beta = beta * (T_maj * ms.sigma_s / pdf);
+                    r_u = r_u * (T_maj * ms.sigma_s / pdf);
+                    if (beta.nonzero() && r_u.nonzero()) {
+                        scattered = true;   // resolved below (NEE + phase sampling)
+                        pScatter = p;
+                    }
+                    return false;
+                }
+                Spec sigma_n = clamp_zero(sigma_maj - ms.sigma_a - ms.sigma_s);
+                float pdf = T_maj.v0 * sigma_n.v0;
+                beta = beta * (T_maj * sigma_n / pdf);
+                if (pdf == 0) beta = Spec::c(0.f);
+                r_u = r_u * (T_maj * sigma_n / pdf);
+                r_l = r_l * (T_maj * sigma_maj / pdf);
+                return beta.nonzero() && r_u.nonzero();
+            };
+            Spec T_maj = sample_t_maj(P.med, maj, Ray{o, d}, kInf, u0, rng, sig_a, sig_s, Le_l, nLookup, nSteps, cb);
+
+            if (scattered) {
+                // ---- SampleLd for the medium interaction (integrators.cpp:1282-1338) ----
+                const V3 wo = -d;
+                const float ul = smp.get1d();
+                smp.get1d(); smp.get1d();   // uLight (unused by distant lights)
+                bool shadowSpawned = false;
+                const int nl = P.lights.n;
+                if (nl > 0) {
+                    float pInf = float(nl) / float(nl + 0);
+                    if (ul < pInf) {
+                        float uu = ul / pInf;
+                        int idx = (int)(uu * nl);
+                        idx = idx < nl - 1 ? idx : nl - 1;
+                        float pmf = pInf / nl;
+                        if (P.lights.type[idx] == 0) {
+                            const V3 wi = {P.lights.w[idx][0], P.lights.w[idx][1], P.lights.w[idx][2]};
+                            const V3 pOut = pScatter + wi * (2 * P.lights.scene_radius);
+                            const Spec Ls = sample_table(P.lights.L[idx], li) * P.lights.scale[idx];
+                            if (Ls.nonzero()) {
+                                const float p_l = pmf * 1.f;
+                                const float fval = hg_eval(dot(wo, wi), P.med.g);
+                                const Spec f_hat = Spec::c(fval);
+                                if (f_hat.nonzero()) {
+                                    shO = to4(pScatter);
+                                    shD = to4(pOut - pScatter);
+                                    shBF = to4(beta * f_hat);
+                                    shLs = to4(Ls);
+                                    shRP = to4(r_u * p_l);
+                                    shadowSpawned = true;
+                                }
+                            }
+                        }
+                    }
+                }
+                if (!shadowSpawned) L = L + Spec::c(0.f);   // L += SampleLd(...) == 0
+                pushShadow = shadowSpawned;
+                // ---- phase-function sampling (integrators.cpp:1046-1061) ----
+                const float up0 = smp.get1d(), up1 = smp.get1d();
+                float phPdf;
+                const V3 wi = hg_sample(wo, P.med.g, up0, up1, &phPdf);
+                if (phPdf == 0) {
+                    terminated = true;
+                } else {
+                    beta = beta * (phPdf / phPdf);
+                    r_l = r_u / phPdf;
+                    newO = pScatter;
+                    newD = wi;
+                    pushActive = true;
+                }
+            } else if (!terminated && beta.nonzero() && r_u.nonzero()) {
+                beta = beta * (T_maj / T_maj.v0);
+                r_u = r_u * (T_maj / T_maj.v0);
+                r_l = r_l * (T_maj / T_maj.v0);
+                // escaped: infinite lights (integrators.cpp:1090-1107)
+                for (int k = 0; k < P.lights.n; ++k) {
+                    if (P.lights.type[k] != 1) continue;
+                    const Spec Le = sample_table(P.lights.L[k], li) * P.lights.scale[k];
+                    if (!Le.nonzero()) continue;
+                    if (depth == 0) L = L + beta * Le / r_u.avg();
+                    else {
+                        float p_l = (1.f / (P.lights.n + 0)) * 0.f;
+                        r_l = r_l * p_l;
+                        L = L + beta * Le / (r_u + r_l).avg();
+                    }
+                }
+            }
+            P.ps.L[path] = to4(L);
+            if (pushActive) {
+                P.ps.o[path] = to4(newO);
+                P.ps.d[path] = to4(newD);
+                P.ps.beta[path] = to4(beta);
+                P.ps.r_u[path] = to4(r_u);
+                P.ps.r_l[path] = to4(r_l);
+                P.ps.smp_state[path] = smp.rng.state;
+                P.ps.depth[path] = depth;
+            }
+        }
+        const int slot = wave_push(P.count_out, pushActive);
+        if (pushActive) { P.queue_out[slot] = path; ++nOut; }
+        const int sslot = wave_push(P.shadow_count, pushShadow);
+        if (pushShadow) {
+            ++nOut;
+            P.sh.path[sslot] = path;
+            P.sh.o[sslot] = shO;
+            P.sh.d[sslot] = shD;
+            P.sh.bf[sslot] = shBF;
+            P.sh.Ls[sslot] = shLs;
+            P.sh.rp_pl[sslot] = shRP;
+        }
+    }
+    flush_stat(P.stats, 0, nLookup);
+    flush_stat(P.stats, 1, nIn);
+    flush_stat(P.stats, 2, nOut);
+    flush_stat(P.stats, 5, nSteps);
+}
+
+// ---------------------------------------------------------------------------
+// Ratio tracking along shadow rays — SampleLd's transmittance loop
+// (cpu/integrators.cpp:1339-1398), incl. Russian roulette at Tr < 0.05, q = 0.75.
+__global__ void __launch_bounds__(256) k_shadow(Params P) {
+    __shared__ float s_maj[4096];
+    const float *maj = stage_majorant(P.med, s_maj);
+    const int count = *P.shadow_count;
+    unsigned long long nLookup = 0, nIn = 0, nSteps = 0;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < count; i += gridDim.x * blockDim.x) {
+        ++nIn;
+        const int path = P.sh.path[i];
+        const V3 o = from4(P.sh.o[i]);
+        const V3 d = from4(P.sh.d[i]);
+        const Spec lamv = spec4(P.ps.lambda[path]);
+        const LambdaIdx li = lambda_index(lamv);
+        const Spec sig_a = sample_table(P.med.sigma_a, li);
+        const Spec sig_s = sample_table(P.med.sigma_s, li);
+        const Spec Le_l = P.med.emissive ? sample_table(P.med.Le, li) : Spec::c(0.f);
+        Spec T_ray = Spec::c(1.f), r_l = Spec::c(1.f), r_u = Spec::c(1.f);
+        Pcg32 rng;
+        rng.set_sequence(hash_3u32(f2u(o.x), f2u(o.y), f2u(o.z)), hash_3u32(f2u(d.x), f2u(d.y), f2u(d.z)));
+        const float u = rng.uniform();
+        auto cb = [&](V3, const MediumSample &ms, const Spec &sigma_maj, const Spec &T_maj) -> bool {
+            Spec sigma_n = clamp_zero(sigma_maj - ms.sigma_a - ms.sigma_s);
+            float pdf = T_maj.v0 * sigma_maj.v0;
+            T_ray = T_ray * (T_maj * sigma_n / pdf);
+            r_l = r_l * (T_maj * sigma_maj / pdf);
+            r_u = r_u * (T_maj * sigma_n / pdf);
+            Spec Tr = T_ray / (r_l + r_u).avg();
+            if (Tr.maxc() < 0.05f) {
+                float q = 0.75f;
+                if (rng.uniform() < q) T_ray = Spec::c(0.f);
+                else T_ray = T_ray / (1 - q);
+            }
+            return T_ray.nonzero();
+        };
+        Spec T_maj = sample_t_maj(P.med, maj, Ray{o, d}, 1 - kShadowEpsilon, u, rng, sig_a, sig_s, Le_l, nLookup,
+                                  nSteps, cb);
+        T_ray = T_ray * (T_maj / T_maj.v0);
+        r_l = r_l * (T_maj / T_maj.v0);
+        r_u = r_u * (T_maj / T_maj.v0);
+        Spec contrib = Spec::c(0.f);
+        if (T_ray.nonzero()) {
+            r_l = r_l * spec4(P.sh.rp_pl[i]);
+            contrib = spec4(P.sh.bf[i]) * T_ray * spec4(P.sh.Ls[i]) / r_l.avg();
+        }
+        P.ps.L[path] = to4(spec4(P.ps.L[path]) + contrib);
+    }
+    flush_stat(P.stats, 3, nLookup);
+    flush_stat(P.stats, 4, nIn);
+    flush_stat(P.stats, 6, nSteps);
+}
+
+// ---------------------------------------------------------------------------
+// Film — NaN/Inf guard (integrators.cpp:272-282), PixelSensor::ToSensorRGB (film.h:95-100),
+// RGBFilm::AddSample (film.h:239-255): per pixel, the pass's samples in sampleIndex order.
+__global__ void __launch_bounds__(256) k_film(Params P) {
+    const int npix = P.pass_pixels;
+    for (int pix = blockIdx.x * blockDim.x + threadIdx.x; pix < npix; pix += gridDim.x * blockDim.x) {
+        double s0 = P.film.rgb_sum[3 * (size_t)pix], s1 = P.film.rgb_sum[3 * (size_t)pix + 1],
+               s2 = P.film.rgb_sum[3 * (size_t)pix + 2], ws = P.film.w_sum[pix];
+        for (int s = 0; s < P.pass_samples; ++s) {
+            const int id = s * npix + pix;
+            Spec L = spec4(P.ps.L[id]);
+            const Spec lam = spec4(P.ps.lambda[id]);
+            const Spec pdf = spec4(P.ps.pdf[id]);
+            const LambdaIdx li = lambda_index(lam);
+            bool bad = __builtin_isnan(L.v0) || __builtin_isnan(L.v1) || __builtin_isnan(L.v2) || __builtin_isnan(L.v3);
+            if (!bad) {
+                const Spec Ys = sample_table(P.film.xyz + kNTable, li);
+                float y = safe_div(Ys * L, pdf).avg() / 106.856895f;
+                bad = __builtin_isinf(y);
+            }
+            if (bad) L = Spec::c(0.f);
+            const Spec Ld = safe_div(L, pdf);
+            float rgb[3];
+            for (int c = 0; c < 3; ++c) rgb[c] = (sample_table(P.film.xyz + kNTable * c, li) * Ld).avg() * P.film.imaging_ratio;
+            float mx = fmaxf_(fmaxf_(rgb[0], rgb[1]), rgb[2]);
+            if (mx > P.film.max_component)
+                for (int c = 0; c < 3; ++c) rgb[c] *= P.film.max_component / mx;
+            const float w = 1.f;
+            s0 += (double)(w * rgb[0]);
+            s1 += (double)(w * rgb[1]);
+            s2 += (double)(w * rgb[2]);
+            ws += (double)w;
+        }
+        P.film.rgb_sum[3 * (size_t)pix] = s0;
+        P.film.rgb_sum[3 * (size_t)pix + 1] = s1;
+        P.film.rgb_sum[3 * (size_t)pix + 2] = s2;
+        P.film.w_sum[pix] = ws;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// MajorantGrid build — GridMedium ctor (media.cpp:229, 241-246): each cell is
+// SampledGrid::MaxValue over MajorantGrid::VoxelBounds (containers.h:838-857).
+// One workgroup per majorant cell; wave max-reduction, then LDS.
+__global__ void __launch_bounds__(256) k_majorant(const float *__restrict__ density, int nx, int ny, int nz, int rx,
+                                                  int ry, int rz, float *out) {
+    const int cell = blockIdx.x;
+    const int x = cell % rx, y = (cell / rx) % ry, z = cell / (rx * ry);
+    const float b0[3] = {float(x) / rx, float(y) / ry, float(z) / rz};
+    const float b1[3] = {float(x + 1) / rx, float(y + 1) / ry, float(z + 1) / rz};
+    const int n[3] = {nx, ny, nz};
+    int lo[3], hi[3];
+    for (int a = 0; a < 3; ++a) {
+        float ps0 = b0[a] * n[a] - .5f, ps1 = b1[a] * n[a] - .5f;
+        int l = (int)__builtin_floorf(ps0);
+        lo[a] = l > 0 ? l : 0;
+        int h = (int)__builtin_floorf(ps1) + 1;
+        hi[a] = h < n[a] - 1 ? h : n[a] - 1;
+    }
+    float m = grid_at(density, nx, ny, nz, lo[0], lo[1], lo[2]);
+    const int ex = hi[0] - lo[0] + 1, ey = hi[1] - lo[1] + 1, ez = hi[2] - lo[2] + 1;
+    const long long total = (long long)ex * ey * ez;
+    for (long long k = threadIdx.x; k < total; k += blockDim.x) {
+        const int kx = (int)(k % ex), ky = (int)((k / ex) % ey), kz = (int)(k / ((long long)ex * ey));
+        m = fmaxf_(m, grid_at(density, nx, ny, nz, lo[0] + kx, lo[1] + ky, lo[2] + kz));
+    }
+    for (int off = 32; off > 0; off >>= 1) m = fmaxf_(m, __shfl_xor(m, off));
+    __shared__ float red[4];
+    if (lane_id() == 0) red[threadIdx.x / 64] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float r = red[0];
+        for (int w = 1; w < (int)(blockDim.x / 64); ++w) r = fmaxf_(r, red[w]);
+        out[cell] = r;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Synthetic heterogeneous grid (BASELINE.md S-cloud): CloudMedium::Density
+// (media.h:496-520; density 1, wispiness 1, frequency 5) at voxel centres, with
+// pbrt's Perlin Noise/DNoise (util/noise.cpp). Only +,-,*,floor,fmod: bit-exact vs CPU.
+__constant__ int c_perm[512] = {
+    151, 160, 137, 91, 90, 15, 131, 13, 201, 95, 96, 53, 194, 233, 7, 225, 140, 36, 103, 30, 69, 142,
+    8, 99, 37, 240, 21, 10, 23, 190, 6, 148, 247, 120, 234, 75, 0, 26, 197, 62, 94, 252, 219, 203, 117,
+    35, 11, 32, 57, 177, 33, 88, 237, 149, 56, 87, 174, 20, 125, 136, 171, 168, 68, 175, 74, 165, 71,
+    134, 139, 48, 27, 166, 77, 146, 158, 231, 83, 111, 229, 122, 60, 211, 133, 230, 220, 105, 92, 41,
+    55, 46, 245, 40, 244, 102, 143, 54, 65, 25, 63, 161, 1, 216, 80, 73, 209, 76, 132, 187, 208, 89,
+    18, 169, 200, 196, 135, 130, 116, 188, 159, 86, 164, 100, 109, 198, 173, 186, 3, 64, 52, 217, 226,
+    250, 124, 123, 5, 202, 38, 147, 118, 126, 255, 82, 85, 212, 207, 206, 59, 227, 47, 16, 58, 17, 182,
+    189, 28, 42, 223, 183, 170, 213, 119, 248, 152, 2, 44, 154, 163, 70, 221, 153, 101, 155, 167, 43,
+    172, 9, 129, 22, 39, 253, 19, 98, 108, 110, 79, 113, 224, 232, 178, 185, 112, 104, 218, 246, 97,
+    228, 251, 34, 242, 193, 238, 210, 144, 12, 191, 179, 162, 241, 81, 51, 145, 235, 249, 14, 239,
+    107, 49, 192, 214, 31, 181, 199, 106, 157, 184, 84, 204, 176, 115, 121, 50, 45, 127, 4, 150, 254,
+    138, 236, 205, 93, 222, 114, 67, 29, 24, 72, 243, 141, 128, 195, 78, 66, 215, 61, 156, 180,
+    151, 160, 137, 91, 90, 15, 131, 13, 201, 95, 96, 53, 194, 233, 7, 225, 140, 36, 103, 30, 69, 142,
+    8, 99, 37, 240, 21, 10, 23, 190, 6, 148, 247, 120, 234, 75, 0, 26, 197, 62, 94, 252, 219, 203, 117,
+    35, 11, 32, 57, 177, 33, 88, 237, 149, 56, 87, 174, 20, 125, 136, 171, 168, 68, 175, 74, 165, 71,
+    134, 139, 48, 27, 166, 77, 146, 158, 231, 83, 111, 229, 122, 60, 211, 133, 230, 220, 105, 92, 41,
+    55, 46, 245, 40, 244, 102, 143, 54, 65, 25, 63, 161, 1, 216, 80, 73, 209, 76, 132, 187, 208, 89,
+    18, 169, 200, 196, 135, 130, 116, 188, 159, 86, 164, 100, 109, 198, 173, 186, 3, 64, 52, 217, 226,
+    250, 124, 123, 5, 202, 38, 147, 118, 126, 255, 82, 85, 212, 207, 206, 59, 227, 47, 16, 58, 17, 182,
+    189, 28, 42, 223, 183, 170, 213, 119, 248, 152, 2, 44, 154, 163, 70, 221, 153, 101, 155, 167, 43,
+    172, 9, 129, 22, 39, 253, 19, 98, 108, 110, 79, 113, 224, 232, 178, 185, 112, 104, 218, 246, 97,
+    228, 251, 34, 242, 193, 238, 210, 144, 12, 191, 179, 162, 241, 81, 51, 145, 235, 249, 14, 239,
+    107, 49, 192, 214, 31, 181, 199, 106, 157, 184, 84, 204, 176, 115, 121, 50, 45, 127, 4, 150, 254,
+    138, 236, 205, 93, 222, 114, 67, 29, 24, 72, 243, 141, 128, 195, 78, 66, 215, 61, 156, 180};
+
+__device__ __forceinline__ float noise_grad(int x, int y, int z, float dx, float dy, float dz) {
+    int h = c_perm[c_perm[c_perm[x] + y] + z] & 15;
+    float u = h < 8 || h == 12 || h == 13 ? dx : dy;
+    float v = h < 4 || h == 12 || h == 13 ? dy : dz;
+    return ((h & 1) ? -u : u) + ((h & 2) ? -v : v);
+}
+__device__ __forceinline__ float noise_weight(float t) {
+    float t2 = t * t;
+    return 6 * ((t2 * t2) * t) - 15 * (t2 * t2) + 10 * (t2 * t);
+}
+__device__ float perlin(float x, float y, float z) {
+    x = fmodf(x, float(1 << 30)); y = fmodf(y, float(1 << 30)); z = fmodf(z, float(1 << 30));
+    int ix = (int)__builtin_floorf(x), iy = (int)__builtin_floorf(y), iz = (int)__builtin_floorf(z);
+    float dx = x - ix, dy = y - iy, dz = z - iz;
+    ix &= 255; iy &= 255; iz &= 255;
+    float w000 = noise_grad(ix, iy, iz, dx, dy, dz), w100 = noise_grad(ix + 1, iy, iz, dx - 1, dy, dz);
+    float w010 = noise_grad(ix, iy + 1, iz, dx, dy - 1, dz), w110 = noise_grad(ix + 1, iy + 1, iz, dx - 1, dy - 1, dz);
+    float w001 = noise_grad(ix, iy, iz + 1, dx, dy, dz - 1), w101 = noise_grad(ix + 1, iy, iz + 1, dx - 1, dy, dz - 1);
+    float w011 = noise_grad(ix, iy + 1, iz + 1, dx, dy - 1, dz - 1);
+    float w111 = noise_grad(ix + 1, iy + 1, iz + 1, dx - 1, dy - 1, dz - 1);
+    float wx = noise_weight(dx), wy = noise_weight(dy), wz = noise_weight(dz);
+    float x00 = lerp(wx, w000, w100), x10 = lerp(wx, w010, w110), x01 = lerp(wx, w001, w101), x11 = lerp(wx, w011, w111);
+    return lerp(wz, lerp(wy, x00, x10), lerp(wy, x01, x11));
+}
+__device__ float cloud_density(V3 p, float density, float wispiness, float frequency) {
+    V3 pp = frequency * p;
+    if (wispiness > 0) {
+        float vomega = 0.05f * wispiness, vlambda = 10.f;
+        for (int i = 0; i < 2; ++i) {
+            V3 q = vlambda * pp;
+            const float delta = .01f;
+            float n = perlin(q.x, q.y, q.z);
+            V3 nd = {perlin(q.x + delta, q.y + 0.f, q.z + 0.f), perlin(q.x + 0.f, q.y + delta, q.z + 0.f),
+                     perlin(q.x + 0.f, q.y + 0.f, q.z + delta)};
+            V3 dn = (nd - V3{n, n, n}) / delta;
+            pp = pp + vomega * dn;
+            vomega *= 0.5f;
+            vlambda *= 1.99f;
+        }
+    }
+    float d = 0, omega = 0.5f, lam = 1.f;
+    for (int i = 0; i < 5; ++i) {
+        V3 q = lam * pp;
+        d += omega * perlin(q.x, q.y, q.z);
+        omega *= 0.5f;
+        lam *= 1.99f;
+    }
+    d = clampf((1 - p.y) * 4.5f * density * d, 0, 1);
+    d += 2 * fmaxf_(0.f, 0.5f - p.y);
+    return clampf(d, 0, 1);
+}
+__global__ void __launch_bounds__(256) k_cloud(float *out, int n, long long first, long long count, float density,
+                                               float wispiness, float frequency) {
+    for (long long k = blockIdx.x * (long long)blockDim.x + threadIdx.x; k < count; k += (long long)gridDim.x * blockDim.x) {
+        const long long idx = first + k;
+        const int x = (int)(idx % n), y = (int)((idx / n) % n), z = (int)(idx / ((long long)n * n));
+        out[k] = cloud_density(V3{(x + 0.5f) / n, (y + 0.5f) / n, (z + 0.5f) / n}, density, wispiness, frequency);
+    }
+}
+
+}  // namespace avr

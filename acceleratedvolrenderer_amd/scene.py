@@ -1,0 +1,223 @@
+"""Scene description for the volumetric path: the subset of pbrt-v4 scene objects
+the MI355X integrator consumes, with pbrt's parameter names and defaults.
+
+    GridMedium            media.h:265-352, GridMedium::Create media.cpp:249-330
+    DistantLight          lights.h:244-305, DistantLight::Create lights.cpp:246-276
+    UniformInfiniteLight  lights.cpp:950-972, creation lights.cpp:1529-1566
+    Orthographic/PerspectiveCamera  cameras.h:245-273, cameras.cpp:284-306, 404-427, 365-400, 490-520
+    RGBFilm + PixelSensor film.h:95-100, 232-316; film.cpp:212-250, 484-497, 567-585
+    CameraTransform       cameras.cpp:27-57 (default rendering space: CameraWorld)
+
+The medium's box `[p0, p1]` doubles as the scene's only geometry: an "interface"
+boundary (no BSDF; rays cross it without scattering, interaction.cpp:91-97).
+See DESIGN.md "Scene model" for why that is exact for VolPath's sampling.
+"""
+import math
+
+import numpy as np
+
+from . import spectra
+from . import transform as xf
+
+
+class GridMedium:
+    """pbrt "uniformgrid" medium (GridMedium::Create, media.cpp:249-330).
+
+    density: float32 array shaped (nz, ny, nx) (x fastest, containers.h:834), or a
+    device tensor with `.data_ptr()` (kept alive by the caller) plus `shape`.
+    """
+
+    def __init__(self, density, p0=(0.0, 0.0, 0.0), p1=(1.0, 1.0, 1.0), world_from_medium=None, sigma_a=None,
+                 sigma_s=None, scale=1.0, g=0.0, Le=None, Lescale=None, majorant_res=(16, 16, 16)):
+        if hasattr(density, "data_ptr"):
+            self.device_density = density
+            self.density = None
+            nz, ny, nx = (int(s) for s in density.shape)
+        else:
+            d = np.ascontiguousarray(np.asarray(density, np.float32))
+            if d.ndim != 3:
+                raise ValueError("density must be (nz, ny, nx)")
+            self.device_density = None
+            self.density = d
+            nz, ny, nx = d.shape
+        self.nx, self.ny, self.nz = nx, ny, nz
+        self.p0 = np.asarray(p0, np.float32)
+        self.p1 = np.asarray(p1, np.float32)
+        self.world_from_medium = np.eye(4) if world_from_medium is None else np.asarray(world_from_medium, np.float64)
+        self.g = np.float32(g)
+        # DenselySampledSpectrum(sigma).Scale(sigmaScale) (media.cpp:229-231), defaults 1 (media.cpp:313-320)
+        self.sigma_a = spectra.scaled(spectra.as_table(sigma_a, 1.0), scale)
+        self.sigma_s = spectra.scaled(spectra.as_table(sigma_s, 1.0), scale)
+        # Le / LeScale (media.cpp:283-305)
+        le_norm = np.float32(1.0)
+        if Le is None or float(np.max(spectra.as_table(Le, 0.0))) == 0.0:
+            self.Le = None
+        else:
+            self.Le = spectra.as_table(Le, 0.0)
+            le_norm = np.float32(1.0) / spectra.spectrum_to_photometric(self.Le)
+        if Lescale is None:
+            self.Lescale = np.array([[[le_norm]]], np.float32)
+        else:
+            ls = np.asarray(Lescale, np.float32)
+            if ls.shape != (nz, ny, nx):
+                raise ValueError("Lescale must match the density grid shape")
+            self.Lescale = (ls * le_norm).astype(np.float32)
+        self.majorant_res = tuple(int(r) for r in majorant_res)
+
+    @property
+    def bounds(self):
+        return np.concatenate([self.p0, self.p1]).astype(np.float32)
+
+
+class DistantLight:
+    """DistantLight::Create (lights.cpp:246-276). L defaults to the color space illuminant."""
+    type_id = 0
+
+    def __init__(self, from_=(0.0, 0.0, 0.0), to=(0.0, 0.0, 1.0), L=None, scale=1.0, illuminance=None,
+                 world_from_light=None):
+        self.L = spectra.TABLES["D65"].copy() if L is None else spectra.as_table(L, 1.0)
+        sc = np.float32(scale) / spectra.spectrum_to_photometric(self.L)
+        if illuminance is not None and illuminance > 0:
+            sc = np.float32(sc * np.float32(illuminance))
+        self.scale = np.float32(sc)
+        w = np.asarray(from_, np.float64) - np.asarray(to, np.float64)
+        self.w_light = w / np.linalg.norm(w)
+        self.world_from_light = np.eye(4) if world_from_light is None else np.asarray(world_from_light, np.float64)
+
+    def render_direction(self, render_from_world):
+        """Normalize(renderFromLight(Vector3f(0, 0, 1))) (lights.h:287)."""
+        v = (render_from_world @ self.world_from_light)[:3, :3] @ self.w_light
+        return (v / np.linalg.norm(v)).astype(np.float32)
+
+
+class UniformInfiniteLight:
+    """"infinite" light with constant L (lights.cpp:1529-1566); scale /= SpectrumToPhotometric."""
+    type_id = 1
+
+    def __init__(self, L=None, scale=1.0):
+        self.L = spectra.TABLES["D65"].copy() if L is None else spectra.as_table(L, 1.0)
+        self.scale = np.float32(np.float32(scale) / spectra.spectrum_to_photometric(self.L))
+
+    def render_direction(self, render_from_world):
+        return np.zeros(3, np.float32)
+
+
+class _ProjectiveCamera:
+    type_id = -1
+
+    def __init__(self, pos=(0, 0, 0), look=(0, 0, 1), up=(0, 1, 0), screenwindow=None, frameaspectratio=None,
+                 camera_from_world=None):
+        self.camera_from_world = (xf.look_at(pos, look, up) if camera_from_world is None
+                                  else np.asarray(camera_from_world, np.float64))
+        self.screenwindow = screenwindow
+        self.frameaspectratio = frameaspectratio
+
+    def _screen(self, xres, yres):
+        frame = self.frameaspectratio if self.frameaspectratio is not None else xres / yres
+        if frame > 1:
+            s = [-frame, frame, -1.0, 1.0]
+        else:
+            s = [-1.0, 1.0, -1.0 / frame, 1.0 / frame]
+        if self.screenwindow is not None:
+            s = list(self.screenwindow)
+        return s
+
+    def camera_from_raster(self, xres, yres):
+        """ProjectiveCamera ctor (cameras.h:254-273)."""
+        x0, x1, y0, y1 = self._screen(xres, yres)
+        ndc_from_screen = xf.scale(1 / (x1 - x0), 1 / (y1 - y0), 1) @ xf.translate([-x0, -y1, 0])
+        raster_from_ndc = xf.scale(xres, -yres, 1)
+        screen_from_raster = np.linalg.inv(raster_from_ndc @ ndc_from_screen)
+        return np.linalg.inv(self.screen_from_camera()) @ screen_from_raster
+
+    def world_from_camera(self):
+        return np.linalg.inv(self.camera_from_world)
+
+
+class OrthographicCamera(_ProjectiveCamera):
+    """OrthographicCamera (cameras.h:280-300): screenFromCamera = Orthographic(0, 1)."""
+    type_id = 0
+
+    def screen_from_camera(self):
+        return xf.orthographic(0.0, 1.0)
+
+
+class PerspectiveCamera(_ProjectiveCamera):
+    """PerspectiveCamera (cameras.h:340-350): screenFromCamera = Perspective(fov, 1e-2, 1000)."""
+    type_id = 1
+
+    def __init__(self, fov=90.0, **kw):
+        super().__init__(**kw)
+        self.fov = float(fov)
+
+    def screen_from_camera(self):
+        return xf.perspective(self.fov, 1e-2, 1000.0)
+
+
+class RGBFilm:
+    """RGBFilm (film.h:232-316) with a box filter and the cie1931 PixelSensor (film.cpp:212-250)."""
+
+    def __init__(self, xresolution=1280, yresolution=720, filter_radius=(0.5, 0.5), iso=100.0, exposure_time=1.0,
+                 maxcomponentvalue=math.inf):
+        self.width = int(xresolution)
+        self.height = int(yresolution)
+        self.filter_radius = np.asarray(filter_radius, np.float32)
+        self.imaging_ratio = np.float32(np.float32(exposure_time) * np.float32(iso) / np.float32(100))
+        self.max_component_value = np.float32(maxcomponentvalue)
+        self.sensor = spectra.sensor_cie1931()
+        # outputRGBFromSensorRGB = colorSpace->RGBFromXYZ * XYZFromSensorRGB (film.cpp:496), cie1931: I
+        self.output_from_sensor = spectra.TABLES["srgb_rgb_from_xyz"].astype(np.float32)
+
+
+def _bounding_sphere_radius(pmin, pmax):
+    """Bounds3::BoundingSphere (vecmath.h:1335-1338) in float32."""
+    pmin = pmin.astype(np.float32)
+    pmax = pmax.astype(np.float32)
+    center = ((pmin + pmax) / np.float32(2)).astype(np.float32)
+    inside = bool(np.all(center >= pmin) and np.all(center <= pmax))
+    if not inside:
+        return np.float32(0)
+    d = (pmax - center).astype(np.float32)
+    return np.float32(np.sqrt(np.float32(np.float32(d[0] * d[0] + d[1] * d[1]) + d[2] * d[2])))
+
+
+class Scene:
+    """Resolved render-space scene (CameraWorld rendering space, cameras.cpp:35-41)."""
+
+    def __init__(self, camera, film, medium, lights):
+        self.camera, self.film, self.medium, self.lights = camera, film, medium, list(lights)
+        if len(self.lights) > 8:
+            raise ValueError("at most 8 lights")
+        wfc = camera.world_from_camera()
+        cam_pos = wfc @ np.array([0, 0, 0, 1.0])
+        self.render_from_world = xf.translate(-cam_pos[:3])
+        self.render_from_camera = xf.f32(self.render_from_world @ wfc)
+        self.camera_from_raster = xf.f32(camera.camera_from_raster(film.width, film.height))
+        rfm = self.render_from_world @ medium.world_from_medium
+        self.render_from_medium = xf.f32(rfm)
+        self.medium_from_render = xf.f32(np.linalg.inv(rfm))
+        # scene bounds = render-space bounds of the interface box (the only shape)
+        c = np.array([[x, y, z, 1.0] for x in (medium.p0[0], medium.p1[0]) for y in (medium.p0[1], medium.p1[1])
+                      for z in (medium.p0[2], medium.p1[2])])
+        rc = (rfm @ c.T).T[:, :3]
+        self.scene_radius = _bounding_sphere_radius(rc.min(axis=0), rc.max(axis=0))
+        self.light_types = np.array([l.type_id for l in self.lights], np.int32)
+        self.light_w = np.stack([l.render_direction(self.render_from_world) for l in self.lights]).astype(
+            np.float32) if self.lights else np.zeros((0, 3), np.float32)
+        self.light_L = np.stack([l.L for l in self.lights]).astype(np.float32) if self.lights else np.zeros(
+            (0, spectra.N), np.float32)
+        self.light_scale = np.array([l.scale for l in self.lights], np.float32)
+
+
+def film_rgb(film, rgb_sum, w_sum):
+    """RGBFilm::GetPixelRGB (film.h:258-274) in float32, no splats: returns (H, W, 3)."""
+    rgb = np.asarray(rgb_sum, np.float64).reshape(-1, 3).astype(np.float32)
+    w = np.asarray(w_sum, np.float64).reshape(-1).astype(np.float32)
+    nz = w != 0
+    rgb[nz] = (rgb[nz] / w[nz, None]).astype(np.float32)
+    m = film.output_from_sensor.astype(np.float32)
+    out = np.empty_like(rgb)
+    for r in range(3):
+        out[:, r] = ((m[r, 0] * rgb[:, 0] + m[r, 1] * rgb[:, 1]).astype(np.float32) + m[r, 2] * rgb[:, 2]).astype(
+            np.float32)
+    return out.reshape(film.height, film.width, 3)

@@ -1,0 +1,54 @@
+"""The synthetic inputs of BASELINE.md §2 (the disney-cloud assets are not available offline).
+
+S-uniform  (config C2): GridMedium n^3 of 1.0 on [0,1]^3, orthographic camera looking down +z
+           at the z=0 face through a screen window equal to that face, 512x512.
+           variants: "absorber" (sigma_a=1, sigma_s=0, uniform infinite light Le=1 -> analytic
+           Beer-Lambert), "furnace" (sigma_a=0, sigma_s=4, uniform infinite Le=1, maxdepth 1000
+           -> L = Le), "scatter" (sigma_a=0.5, sigma_s=2, distant light + sky).
+S-cloud    (metric input): GridMedium n^3 filled with CloudMedium::Density (media.h:496-520,
+           density 1, wispiness 1, frequency 5) at voxel centres; sigma_a=0, sigma_s=1,
+           scale 4 (albedo 1), g 0.877, distant light + dim sky, perspective 1280x720, maxdepth 100.
+"""
+import numpy as np
+
+from . import spectra
+from .scene import (GridMedium, DistantLight, UniformInfiniteLight, OrthographicCamera, PerspectiveCamera, RGBFilm,
+                    Scene)
+
+CLOUD_G = 0.877
+CLOUD_MAXDEPTH = 100
+
+
+def s_uniform(n=256, width=512, height=512, variant="absorber", density=None):
+    if density is None:
+        density = np.ones((n, n, n), np.float32)
+    if variant == "absorber":
+        med = GridMedium(density, sigma_a=1.0, sigma_s=0.0, g=0.0)
+        lights = [UniformInfiniteLight(L=1.0, scale=float(spectra.spectrum_to_photometric(spectra.constant(1.0))))]
+    elif variant == "furnace":
+        med = GridMedium(density, sigma_a=0.0, sigma_s=4.0, g=0.0)
+        lights = [UniformInfiniteLight(L=1.0, scale=float(spectra.spectrum_to_photometric(spectra.constant(1.0))))]
+    elif variant == "scatter":
+        med = GridMedium(density, sigma_a=0.5, sigma_s=2.0, g=0.3)
+        lights = [DistantLight(from_=(-1.0, 1.0, -1.0), to=(0.0, 0.0, 0.0), scale=2.0),
+                  UniformInfiniteLight(scale=0.25)]
+    else:
+        raise ValueError(variant)
+    cam = OrthographicCamera(pos=(0.5, 0.5, -1.0), look=(0.5, 0.5, 0.0), up=(0.0, 1.0, 0.0),
+                             screenwindow=(-0.5, 0.5, -0.5, 0.5))
+    film = RGBFilm(width, height)
+    return Scene(cam, film, med, lights)
+
+
+def cloud_medium(density):
+    return GridMedium(density, sigma_a=0.0, sigma_s=1.0, scale=4.0, g=CLOUD_G)
+
+
+def s_cloud(density, width=1280, height=720, fov=45.0):
+    med = cloud_medium(density)
+    # key light from upper right behind the cloud (silver lining with g = 0.877) plus a dim sky
+    lights = [DistantLight(from_=(0.7, 1.0, 0.6), to=(0.0, 0.0, 0.0), scale=3.0), UniformInfiniteLight(scale=0.15)]
+    # framed so the 16:9 view is filled by the [0,1]^3 medium box
+    cam = PerspectiveCamera(fov=fov, pos=(0.5, 0.42, -0.75), look=(0.5, 0.38, 0.5), up=(0.0, 1.0, 0.0))
+    film = RGBFilm(width, height)
+    return Scene(cam, film, med, lights)

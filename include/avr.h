@@ -1,0 +1,129 @@
+/* avr.h — C-ABI of the MI355X-native volumetric path integrator (libavr_hip.so).
+ *
+ * Drop-in boundary for pbrt-v4's volumetric path in tsvdh/AcceleratedVolRenderer
+ * (paths relative to /root/reference/src/pbrt). Plain C types only: opaque
+ * handles, host pointers + sizes, int status codes (0 = ok), a thread-local
+ * error string. No exceptions cross the ABI; buffers passed in are copied
+ * during the call. One context per GPU; calls on one context are serialised
+ * by the caller (pbrt drives Render() from one thread: cpu/render.cpp:159).
+ *
+ * Replaces:
+ *   VolPathIntegrator::Render/Li/SampleLd   cpu/integrators.cpp:72-298, 962-1399
+ *   SampleT_maj + DDAMajorantIterator        media.h:136-214, 730-806
+ *   GridMedium SamplePoint/SampleRay/ctor    media.h:265-352, media.cpp:212-330
+ *   WorkQueue push / ForAllQueued            wavefront/workqueue.h:41-172
+ *   RGBFilm::AddSample / GetPixelRGB         film.h:232-316
+ */
+#ifndef AVR_H
+#define AVR_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AVR_OK 0
+#define AVR_ERR_ARG 1
+#define AVR_ERR_HIP 2
+#define AVR_ERR_STATE 3
+
+#define AVR_TABLE_SIZE 471 /* DenselySampledSpectrum over 360..830 nm (spectrum.h:374-420) */
+
+typedef struct avr_context avr_context;
+
+/* Work counters and kernel times of the last avr_render call (pbrt's
+ * ReportKernelStats analogue, wavefront/wavefront.cpp:47-56). */
+typedef struct avr_stats {
+    unsigned long long medium_lookups;  /* SamplePoint density fetches in k_medium   */
+    unsigned long long medium_items_in; /* work items consumed by k_medium           */
+    unsigned long long medium_items_out;/* survivors + shadow rays pushed by k_medium */
+    unsigned long long shadow_lookups;  /* density fetches in k_shadow               */
+    unsigned long long shadow_items;    /* shadow rays traced                        */
+    unsigned long long medium_dda_steps;
+    unsigned long long shadow_dda_steps;
+    unsigned long long medium_launches;
+    double ms_camera, ms_medium, ms_shadow, ms_film; /* summed hipEvent times      */
+    double ms_total;                                  /* first launch .. film done  */
+} avr_stats;
+
+/* Last error message of the calling thread ("" if none). */
+const char *avr_last_error(void);
+
+/* Context on HIP device `device` (one process per GPU; no implicit peer access).
+ * `max_paths` bounds the paths in flight per wavefront pass (0 = default 16M). */
+int avr_context_create(int device, long long max_paths, avr_context **out);
+int avr_context_destroy(avr_context *ctx);
+/* Run all work of this context on `hip_stream` (a hipStream_t; NULL = the context's own stream). */
+int avr_set_stream(avr_context *ctx, void *hip_stream);
+
+/* GridMedium (media.h:271-275, media.cpp:249-330). density is nx*ny*nz floats,
+ * x fastest ((z*ny + y)*nx + x, util/containers.h:830-835). sigma_a/sigma_s/Le are
+ * DenselySampled tables already scaled (sigmaScale / LeNorm folded in, as the ctor's
+ * Scale() calls do). Le may be NULL (non-emissive). Lescale is the LeScale grid
+ * (lnx*lny*lnz, LeNorm folded in) and may be NULL when Le is NULL.
+ * Transforms are row-major 4x4 (renderFromMedium and its inverse).
+ * The majorant grid (majorant_res, pbrt uses 16^3, media.cpp:229) is built on device. */
+int avr_medium_grid(avr_context *ctx, const float *density, int nx, int ny, int nz, const float bounds[6],
+                    const float render_from_medium[16], const float medium_from_render[16],
+                    const float *sigma_a, const float *sigma_s, float g, const float *Le, const float *Lescale,
+                    int lnx, int lny, int lnz, const int majorant_res[3]);
+/* Same, but the density already lives in device memory of this context's GPU
+ * (e.g. a 4 GiB grid generated on device). The caller keeps ownership and must keep
+ * it alive while the context renders. */
+int avr_medium_grid_device(avr_context *ctx, const float *d_density, int nx, int ny, int nz, const float bounds[6],
+                           const float render_from_medium[16], const float medium_from_render[16],
+                           const float *sigma_a, const float *sigma_s, float g, const float *Le,
+                           const float *Lescale, int lnx, int lny, int lnz, const int majorant_res[3]);
+/* Fill d_out[first .. first+count) of an n^3 grid with CloudMedium::Density
+ * (media.h:496-520) at voxel centres (i+0.5)/n — the synthetic S-cloud input. */
+int avr_generate_cloud(avr_context *ctx, float *d_out, int n, long long first, long long count, float density,
+                       float wispiness, float frequency);
+/* Copy the device majorant grid to host (mres product floats). */
+int avr_read_majorant(avr_context *ctx, float *out);
+
+/* Lights (lights.h:244-305 DistantLight, lights.cpp:950-972 UniformInfiniteLight).
+ * type 0 = distant: w = render-space unit vector towards the light
+ *          (Normalize(renderFromLight(0,0,1)), lights.h:287); type 1 = uniform infinite.
+ * L = n tables of 471 floats; scale = final light scale (1/SpectrumToPhotometric folded in).
+ * scene_radius = Bounds3::BoundingSphere radius of the scene bounds (lights.h:280). */
+int avr_lights(avr_context *ctx, int n, const int *types, const float *w3, const float *L, const float *scale,
+               float scene_radius);
+
+/* Camera: type 0 orthographic, 1 perspective (cameras.cpp:284-306, 404-427).
+ * camera_from_raster: full 4x4 (projective for perspective); render_from_camera: affine 4x4. */
+int avr_camera(avr_context *ctx, int type, const float camera_from_raster[16], const float render_from_camera[16]);
+
+/* RGBFilm with a box filter and a PixelSensor (film.h:95-100, 232-316): sensor_rgb is the
+ * 3 x 471 r̄ḡb̄ (cie1931: X, Y, Z) tables, imaging_ratio = exposureTime*ISO/100.
+ * Allocates and zeroes the fp64 film sums (3 + 1 doubles per pixel). */
+int avr_film(avr_context *ctx, int width, int height, const float filter_radius[2], const float *sensor_rgb,
+             float imaging_ratio, float max_component_value);
+int avr_film_clear(avr_context *ctx);
+
+/* Render sample indices [spp_begin, spp_end) of every pixel (IndependentSampler, seed),
+ * VolPathIntegrator maxdepth. Asynchronous on the context stream. */
+int avr_render(avr_context *ctx, int spp_begin, int spp_end, int seed, int max_depth);
+int avr_sync(avr_context *ctx);
+int avr_get_stats(avr_context *ctx, avr_stats *out);
+
+/* Film readback: rgb_sum[W*H*3] and w_sum[W*H] (fp64 RGBFilm::Pixel sums). */
+int avr_film_read(avr_context *ctx, double *rgb_sum, double *w_sum);
+/* Device pointers of the film sums (for an RCCL reduce across GPUs). */
+int avr_film_device_ptrs(avr_context *ctx, void **d_rgb_sum, void **d_w_sum);
+/* Device-to-device copy of the film sums into caller memory on the same GPU, laid out
+ * [rgb_sum (W*H*3) | w_sum (W*H)] as doubles — the buffer handed to the RCCL reduce. */
+int avr_film_export_device(avr_context *ctx, void *d_dst);
+
+/* Per-sample radiance of the LAST wavefront pass of the last avr_render (replay checks;
+ * pbrt's --debugstart analogue, integrators.cpp:74-102). Element id = s*W*H + pixel,
+ * s = sampleIndex - first sample of that pass. Writes n_max*4 floats into each of
+ * L, lambda, pdf and returns the pass's first sample index and sample count. */
+int avr_last_pass_samples(avr_context *ctx, float *L, float *lambda, float *pdf, long long n_max,
+                          int *first_sample, int *n_samples);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* AVR_H */

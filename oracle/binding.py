@@ -1,0 +1,237 @@
+"""ctypes binding of the CPU oracle (oracle/volpath_oracle.cpp) — TEST INFRASTRUCTURE.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this
+module, and only as the checker / CPU baseline; the product never does.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+SRC = os.path.join(HERE, "volpath_oracle.cpp")
+LIB = os.path.join(HERE, "_build", "liboracle.so")
+
+c_float_p = ctypes.POINTER(ctypes.c_float)
+c_double_p = ctypes.POINTER(ctypes.c_double)
+c_u32_p = ctypes.POINTER(ctypes.c_uint32)
+
+
+def build(force=False):
+    """g++ -O2 -ffp-contract=off (pbrt's CMakeLists.txt:134-137 float semantics)."""
+    os.makedirs(os.path.dirname(LIB), exist_ok=True)
+    if not force and os.path.exists(LIB) and os.path.getmtime(LIB) >= os.path.getmtime(SRC):
+        return LIB
+    cmd = ["g++", "-std=c++17", "-O2", "-ffp-contract=off", "-fPIC", "-shared", "-Wall", SRC, "-o", LIB,
+           "-lpthread"]
+    subprocess.check_call(cmd)
+    return LIB
+
+
+class OracleScene(ctypes.Structure):
+    _fields_ = [
+        ("density", c_float_p), ("nx", ctypes.c_int), ("ny", ctypes.c_int), ("nz", ctypes.c_int),
+        ("bounds", ctypes.c_float * 6),
+        ("render_from_medium", ctypes.c_float * 16),
+        ("medium_from_render", ctypes.c_float * 16),
+        ("sigma_a", c_float_p), ("sigma_s", c_float_p),
+        ("g", ctypes.c_float),
+        ("emissive", ctypes.c_int),
+        ("Le", c_float_p),
+        ("Lescale", c_float_p), ("lnx", ctypes.c_int), ("lny", ctypes.c_int), ("lnz", ctypes.c_int),
+        ("majorant", c_float_p), ("mres", ctypes.c_int * 3),
+        ("nlights", ctypes.c_int),
+        ("light_type", ctypes.c_int * 8),
+        ("light_w", (ctypes.c_float * 3) * 8),
+        ("light_L", c_float_p * 8),
+        ("light_scale", ctypes.c_float * 8),
+        ("scene_radius", ctypes.c_float),
+        ("camera_type", ctypes.c_int),
+        ("camera_from_raster", ctypes.c_float * 16),
+        ("render_from_camera", ctypes.c_float * 16),
+        ("width", ctypes.c_int), ("height", ctypes.c_int),
+        ("filter_radius", ctypes.c_float * 2),
+        ("sensor_xyz", c_float_p),
+        ("imaging_ratio", ctypes.c_float),
+        ("output_from_sensor", ctypes.c_float * 9),
+        ("max_component_value", ctypes.c_float),
+        ("max_depth", ctypes.c_int),
+        ("seed", ctypes.c_int),
+    ]
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        _lib = ctypes.CDLL(build())
+        L = _lib
+        L.oracle_pixel_sample.restype = ctypes.c_int
+        L.oracle_pixel_sample.argtypes = [ctypes.POINTER(OracleScene), ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                          c_float_p, c_float_p, c_float_p]
+        L.oracle_render.restype = ctypes.c_longlong
+        L.oracle_render.argtypes = [ctypes.POINTER(OracleScene), ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                    c_double_p, c_double_p]
+        L.oracle_render_list.restype = ctypes.c_longlong
+        L.oracle_render_list.argtypes = [ctypes.POINTER(OracleScene), ctypes.POINTER(ctypes.c_int), ctypes.c_int,
+                                         ctypes.c_int, ctypes.c_int, ctypes.c_int, c_double_p, c_double_p]
+        L.oracle_film_resolve.argtypes = [ctypes.POINTER(OracleScene), c_double_p, c_double_p, c_float_p]
+        L.oracle_transmittance.argtypes = [ctypes.POINTER(OracleScene), ctypes.c_int, c_float_p, c_float_p,
+                                           ctypes.c_float, c_float_p]
+        L.oracle_dda_segments.restype = ctypes.c_int
+        L.oracle_dda_segments.argtypes = [ctypes.POINTER(OracleScene), c_float_p, c_float_p, ctypes.c_float,
+                                          ctypes.c_float, ctypes.c_int, c_float_p]
+        L.oracle_build_majorant.argtypes = [c_float_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                            ctypes.c_int, ctypes.c_int, c_float_p]
+        L.oracle_rng.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int, c_u32_p, ctypes.c_int64, c_u32_p,
+                                 ctypes.c_int]
+        L.oracle_rng_uniform.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int, ctypes.c_int, c_float_p]
+        L.oracle_rng_single.argtypes = [ctypes.c_uint64, ctypes.c_int, c_u32_p]
+        for name, args in (("oracle_hash_float", [ctypes.c_float]),
+                           ("oracle_hash_pixel_seed", [ctypes.c_int, ctypes.c_int, ctypes.c_int]),
+                           ("oracle_hash_point3f", [ctypes.c_float, ctypes.c_float, ctypes.c_float]),
+                           ("oracle_mixbits", [ctypes.c_uint64])):
+            getattr(L, name).restype = ctypes.c_uint64
+            getattr(L, name).argtypes = args
+        for name, args in (("oracle_fastexp", [ctypes.c_float]),
+                           ("oracle_sample_exponential", [ctypes.c_float, ctypes.c_float]),
+                           ("oracle_hg_eval", [ctypes.c_float, ctypes.c_float]),
+                           ("oracle_grid_lookup", [c_float_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                   ctypes.c_float, ctypes.c_float, ctypes.c_float]),
+                           ("oracle_grid_maxvalue", [c_float_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                     c_float_p]),
+                           ("oracle_noise", [ctypes.c_float, ctypes.c_float, ctypes.c_float, c_float_p]),
+                           ("oracle_blackbody", [ctypes.c_float, ctypes.c_float]),
+                           ("oracle_cloud_density", [ctypes.c_float] * 6)):
+            getattr(L, name).restype = ctypes.c_float
+            getattr(L, name).argtypes = args
+        L.oracle_sample_discrete3.restype = ctypes.c_int
+        L.oracle_sample_discrete3.argtypes = [c_float_p, ctypes.c_float]
+        L.oracle_sample_visible.argtypes = [ctypes.c_float, c_float_p, c_float_p]
+        L.oracle_hg_sample.argtypes = [c_float_p, ctypes.c_float, ctypes.c_float, ctypes.c_float, c_float_p,
+                                       c_float_p]
+        L.oracle_intersectp.restype = ctypes.c_int
+        L.oracle_intersectp.argtypes = [c_float_p, c_float_p, c_float_p, ctypes.c_float, c_float_p]
+        L.oracle_transform_ray.argtypes = [c_float_p, c_float_p, c_float_p, c_float_p, ctypes.c_int, c_float_p]
+        L.oracle_independent_sampler.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                 ctypes.c_int, ctypes.c_int, c_float_p]
+        L.oracle_cloud_grid.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, c_float_p]
+    return _lib
+
+
+def fp(a):
+    return a.ctypes.data_as(c_float_p)
+
+
+def build_majorant(density, res=(16, 16, 16)):
+    d = np.ascontiguousarray(density, np.float32)
+    nz, ny, nx = d.shape
+    out = np.empty(res[0] * res[1] * res[2], np.float32)
+    lib().oracle_build_majorant(fp(d), nx, ny, nz, res[0], res[1], res[2], fp(out))
+    return out
+
+
+def cloud_grid(n, z0=0, z1=None):
+    z1 = n if z1 is None else z1
+    out = np.empty((z1 - z0, n, n), np.float32)
+    lib().oracle_cloud_grid(n, z0, z1, fp(out))
+    return out
+
+
+class OracleRun:
+    """Holds an OracleScene and the numpy buffers it points into."""
+
+    def __init__(self, scene, max_depth=5, seed=0):
+        med = scene.medium
+        if med.density is None:
+            raise ValueError("oracle needs a host density grid")
+        s = OracleScene()
+        keep = []
+
+        def arr(a):
+            a = np.ascontiguousarray(np.asarray(a, np.float32))
+            keep.append(a)
+            return fp(a)
+
+        s.density = arr(med.density)
+        s.nx, s.ny, s.nz = med.nx, med.ny, med.nz
+        s.bounds[:] = [float(v) for v in med.bounds]
+        s.render_from_medium[:] = [float(v) for v in scene.render_from_medium.reshape(-1)]
+        s.medium_from_render[:] = [float(v) for v in scene.medium_from_render.reshape(-1)]
+        s.sigma_a = arr(med.sigma_a)
+        s.sigma_s = arr(med.sigma_s)
+        s.g = float(med.g)
+        s.emissive = 1 if (med.Le is not None and float(np.max(med.Le)) > 0) else 0
+        s.Le = arr(med.Le if med.Le is not None else np.zeros(471, np.float32))
+        ls = np.ascontiguousarray(med.Lescale, np.float32)
+        s.Lescale = arr(ls)
+        s.lnz, s.lny, s.lnx = ls.shape
+        self.majorant = build_majorant(med.density, med.majorant_res)
+        s.majorant = arr(self.majorant)
+        s.mres[:] = list(med.majorant_res)
+        s.nlights = len(scene.lights)
+        for i in range(s.nlights):
+            s.light_type[i] = int(scene.light_types[i])
+            for k in range(3):
+                s.light_w[i][k] = float(scene.light_w[i][k])
+            s.light_L[i] = arr(scene.light_L[i])
+            s.light_scale[i] = float(scene.light_scale[i])
+        s.scene_radius = float(scene.scene_radius)
+        s.camera_type = int(scene.camera.type_id)
+        s.camera_from_raster[:] = [float(v) for v in scene.camera_from_raster.reshape(-1)]
+        s.render_from_camera[:] = [float(v) for v in scene.render_from_camera.reshape(-1)]
+        f = scene.film
+        s.width, s.height = f.width, f.height
+        s.filter_radius[:] = [float(v) for v in f.filter_radius]
+        s.sensor_xyz = arr(f.sensor.reshape(-1))
+        s.imaging_ratio = float(f.imaging_ratio)
+        s.output_from_sensor[:] = [float(v) for v in f.output_from_sensor.reshape(-1)]
+        s.max_component_value = float(f.max_component_value)
+        s.max_depth = int(max_depth)
+        s.seed = int(seed)
+        self.s = s
+        self.keep = keep
+        self.scene = scene
+
+    def pixel_sample(self, px, py, sample_index):
+        L = np.zeros(4, np.float32)
+        lam = np.zeros(4, np.float32)
+        pdf = np.zeros(4, np.float32)
+        n = lib().oracle_pixel_sample(ctypes.byref(self.s), px, py, sample_index, fp(L), fp(lam), fp(pdf))
+        return L, lam, pdf, n
+
+    def render(self, spp0, spp1, nthreads=1):
+        f = self.scene.film
+        npix = f.width * f.height
+        rgb = np.zeros(3 * npix, np.float64)
+        w = np.zeros(npix, np.float64)
+        events = lib().oracle_render(ctypes.byref(self.s), spp0, spp1, nthreads, rgb.ctypes.data_as(c_double_p),
+                                     w.ctypes.data_as(c_double_p))
+        self.last_events = events
+        return rgb, w
+
+    def render_list(self, pixels, spp0, spp1, nthreads=1):
+        pixels = np.ascontiguousarray(pixels, np.int32)
+        rgb = np.zeros(3 * len(pixels), np.float64)
+        w = np.zeros(len(pixels), np.float64)
+        events = lib().oracle_render_list(ctypes.byref(self.s), pixels.ctypes.data_as(ctypes.POINTER(ctypes.c_int)),
+                                          len(pixels), spp0, spp1, nthreads, rgb.ctypes.data_as(c_double_p),
+                                          w.ctypes.data_as(c_double_p))
+        return rgb, w, events
+
+    def transmittance(self, p0, p1, lambda_u=0.5):
+        p0 = np.ascontiguousarray(p0, np.float32)
+        p1 = np.ascontiguousarray(p1, np.float32)
+        out = np.zeros(len(p0), np.float32)
+        lib().oracle_transmittance(ctypes.byref(self.s), len(p0), fp(p0), fp(p1), lambda_u, fp(out))
+        return out
+
+    def dda_segments(self, o, d, tmax=np.inf, lambda_u=0.5, max_segs=256):
+        o = np.ascontiguousarray(o, np.float32)
+        d = np.ascontiguousarray(d, np.float32)
+        out = np.zeros(3 * max_segs, np.float32)
+        n = lib().oracle_dda_segments(ctypes.byref(self.s), fp(o), fp(d), float(tmax), lambda_u, max_segs, fp(out))
+        return out[:3 * n].reshape(n, 3)

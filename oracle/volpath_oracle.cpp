@@ -1,0 +1,1137 @@
+// volpath_oracle.cpp — ORACLE / TEST INFRASTRUCTURE. Never on the product path.
+//
+// A plain scalar C++ restatement of pbrt-v4's null-scattering volumetric path
+// integrator (the AcceleratedVolRenderer reference, /root/reference) for the
+// scene subset the MI355X path supports. Only tests/, __graft_entry__.smoke()
+// and bench.py's cpu_baseline leg load it, as the checker / CPU baseline.
+//
+// Every function cites the reference file:line it restates (paths relative to
+// /root/reference/src/pbrt). Float order of operations follows the reference
+// exactly (compile with -ffp-contract=off, as pbrt's CMakeLists.txt:134-137 does),
+// so per-sample radiance is reproducible bit for bit on the same libm.
+// Pinned by tests/golden/ref_vectors.json, produced by the REAL reference code
+// (oracle/ref/ref_harness.cpp built from the unmodified sources).
+//
+// Scene subset (see DESIGN.md "Scene model"):
+//  * one GridMedium (media.h:265-352) whose bounds are also the scene's only
+//    boundary (an "interface" box: rays enter/leave it without scattering,
+//    interaction.cpp:91-97); camera outside, lights outside;
+//  * DistantLight (lights.h:244-305) and UniformInfiniteLight (lights.cpp:950-972),
+//    picked by the BVH light sampler's infinite-light branch (lightsamplers.h:266-277);
+//  * orthographic / perspective pinhole cameras (cameras.cpp:284-306, 404-427);
+//  * IndependentSampler (samplers.h:442-476), box filter (filters.h:48-77);
+//  * RGBFilm + cie1931 PixelSensor (film.h:95-100, 232-316).
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <limits>
+#include <thread>
+#include <vector>
+
+namespace oracle {
+
+// ---------------------------------------------------------------------------
+// Float helpers — util/float.h:131-300
+static inline uint32_t FloatToBits(float f) { uint32_t u; std::memcpy(&u, &f, 4); return u; }
+static inline float BitsToFloat(uint32_t u) { float f; std::memcpy(&f, &u, 4); return f; }
+static const float Infinity = std::numeric_limits<float>::infinity();
+static const float OneMinusEpsilon = 0x1.fffffep-1f;  // util/math.h
+static const float MachineEpsilon = std::numeric_limits<float>::epsilon() * 0.5f;
+static const float Pi = 3.14159265358979323846f, Inv4Pi = 0.07957747154594766788f;
+static const float ShadowEpsilon = 0.0001f;                    // util/math.h:42
+static inline float gamma(int n) { return (n * MachineEpsilon) / (1 - n * MachineEpsilon); }
+
+// util/float.h:164-193
+static inline float NextFloatUp(float v) {
+    if (std::isinf(v) && v > 0.f) return v;
+    if (v == -0.f) v = 0.f;
+    uint32_t ui = FloatToBits(v);
+    if (v >= 0) ++ui; else --ui;
+    return BitsToFloat(ui);
+}
+static inline float NextFloatDown(float v) {
+    if (std::isinf(v) && v < 0.) return v;
+    if (v == 0.f) v = -0.f;
+    uint32_t ui = FloatToBits(v);
+    if (v > 0) --ui; else ++ui;
+    return BitsToFloat(ui);
+}
+// CPU branches of util/float.h:199-227
+static inline float AddRoundUp(float a, float b) { return NextFloatUp(a + b); }
+static inline float AddRoundDown(float a, float b) { return NextFloatDown(a + b); }
+static inline float SubRoundUp(float a, float b) { return AddRoundUp(a, -b); }
+static inline float SubRoundDown(float a, float b) { return AddRoundDown(a, -b); }
+
+template <typename T, typename U, typename V>
+static inline T Clamp(T val, U low, V high) {  // util/math.h:237-244
+    if (val < low) return T(low);
+    else if (val > high) return T(high);
+    return val;
+}
+static inline float Lerp(float x, float a, float b) { return (1 - x) * a + x * b; }  // math.h:210
+static inline float Sqr(float v) { return v * v; }
+static inline float SafeSqrt(float x) { return std::sqrt(std::max(0.f, x)); }        // math.h:276
+
+// FastExp, CPU branch — util/math.h:450-471 (EvaluatePolynomial uses std::fma, math.h:335)
+static inline float FastExp(float x) {
+    float xp = x * 1.442695041f;
+    float fxp = std::floor(xp), f = xp - fxp;
+    int i = (int)fxp;
+    float twoToF = std::fma(f, std::fma(f, std::fma(f, 0.0781455737f, 0.226173572f), 0.695556856f), 1.f);
+    int exponent = (int)(FloatToBits(twoToF) >> 23) - 127 + i;
+    if (exponent < -126) return 0;
+    if (exponent > 127) return Infinity;
+    uint32_t bits = FloatToBits(twoToF);
+    bits &= 0b10000000011111111111111111111111u;
+    bits |= (uint32_t)(exponent + 127) << 23;
+    return BitsToFloat(bits);
+}
+
+// ---------------------------------------------------------------------------
+// Hash — util/hash.h:19-106
+static inline uint64_t MurmurHash64A(const unsigned char *key, size_t len, uint64_t seed) {
+    const uint64_t m = 0xc6a4a7935bd1e995ull;
+    const int r = 47;
+    uint64_t h = seed ^ (len * m);
+    const unsigned char *end = key + 8 * (len / 8);
+    while (key != end) {
+        uint64_t k;
+        std::memcpy(&k, key, 8);
+        key += 8;
+        k *= m; k ^= k >> r; k *= m;
+        h ^= k; h *= m;
+    }
+    switch (len & 7) {
+    case 7: h ^= uint64_t(key[6]) << 48; [[fallthrough]];
+    case 6: h ^= uint64_t(key[5]) << 40; [[fallthrough]];
+    case 5: h ^= uint64_t(key[4]) << 32; [[fallthrough]];
+    case 4: h ^= uint64_t(key[3]) << 24; [[fallthrough]];
+    case 3: h ^= uint64_t(key[2]) << 16; [[fallthrough]];
+    case 2: h ^= uint64_t(key[1]) << 8; [[fallthrough]];
+    case 1: h ^= uint64_t(key[0]); h *= m;
+    }
+    h ^= h >> r; h *= m; h ^= h >> r;
+    return h;
+}
+static inline uint64_t MixBits(uint64_t v) {
+    v ^= (v >> 31); v *= 0x7fb5d329728ea185; v ^= (v >> 27); v *= 0x81dadef4bc2dd44d; v ^= (v >> 33);
+    return v;
+}
+static inline uint64_t HashBytes(const void *p, size_t n) { return MurmurHash64A((const unsigned char *)p, n, 0); }
+static inline uint64_t HashFloat(float f) { return HashBytes(&f, 4); }
+static inline uint64_t HashPixelSeed(int x, int y, int seed) {
+    int buf[3] = {x, y, seed};
+    return HashBytes(buf, 12);
+}
+
+// ---------------------------------------------------------------------------
+// RNG (PCG32) — util/rng.h:25-160
+struct RNG {
+    uint64_t state = 0x853c49e6748fea9bULL, inc = 0xda3e39cb94b95bdbULL;
+    RNG() = default;
+    RNG(uint64_t seq, uint64_t seed) { SetSequence(seq, seed); }
+    void SetSequence(uint64_t seq, uint64_t seed) {
+        state = 0u;
+        inc = (seq << 1u) | 1u;
+        U32();
+        state += seed;
+        U32();
+    }
+    void SetSequence(uint64_t seq) { SetSequence(seq, MixBits(seq)); }
+    uint32_t U32() {
+        uint64_t oldstate = state;
+        state = oldstate * 0x5851f42d4c957f2dULL + inc;
+        uint32_t xorshifted = (uint32_t)(((oldstate >> 18u) ^ oldstate) >> 27u);
+        uint32_t rot = (uint32_t)(oldstate >> 59u);
+        return (xorshifted >> rot) | (xorshifted << ((~rot + 1u) & 31));
+    }
+    float Uniform() { return std::min<float>(OneMinusEpsilon, U32() * 0x1p-32f); }
+    void Advance(int64_t idelta) {
+        uint64_t curMult = 0x5851f42d4c957f2dULL, curPlus = inc, accMult = 1u, accPlus = 0u;
+        uint64_t delta = (uint64_t)idelta;
+        while (delta > 0) {
+            if (delta & 1) { accMult *= curMult; accPlus = accPlus * curMult + curPlus; }
+            curPlus = (curMult + 1) * curPlus;
+            curMult *= curMult;
+            delta /= 2;
+        }
+        state = accMult * state + accPlus;
+    }
+};
+
+// ---------------------------------------------------------------------------
+// Vectors — util/vecmath.h
+struct V3 { float x, y, z; float operator[](int i) const { return i == 0 ? x : (i == 1 ? y : z); }
+            float &operator[](int i) { return i == 0 ? x : (i == 1 ? y : z); } };
+static inline V3 operator+(V3 a, V3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+static inline V3 operator-(V3 a, V3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+static inline V3 operator*(V3 a, float s) { return {a.x * s, a.y * s, a.z * s}; }
+static inline V3 operator*(float s, V3 a) { return {s * a.x, s * a.y, s * a.z}; }
+static inline V3 operator/(V3 a, float s) { return {a.x / s, a.y / s, a.z / s}; }      // vecmath.h:364-367
+static inline V3 operator-(V3 a) { return {-a.x, -a.y, -a.z}; }
+static inline float Dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }      // vecmath.h:963
+static inline float LengthSquared(V3 v) { return Sqr(v.x) + Sqr(v.y) + Sqr(v.z); }     // vecmath.h:948
+static inline float Length(V3 v) { return std::sqrt(LengthSquared(v)); }
+static inline V3 Normalize(V3 v) { return v / Length(v); }
+static inline V3 Abs(V3 v) { return {std::abs(v.x), std::abs(v.y), std::abs(v.z)}; }
+
+// CoordinateSystem / Frame::FromZ / FromLocal — vecmath.h:1007-1013, 1868-1916
+static inline void CoordinateSystem(V3 v1, V3 *v2, V3 *v3) {
+    float sign = std::copysign(1.f, v1.z);
+    float a = -1 / (sign + v1.z);
+    float b = v1.x * v1.y * a;
+    *v2 = {1 + sign * Sqr(v1.x) * a, sign * b, -sign * v1.x};
+    *v3 = {b, sign + Sqr(v1.y) * a, -v1.y};
+}
+static inline V3 SphericalDirection(float sinTheta, float cosTheta, float phi) {  // vecmath.h:1666
+    return {Clamp(sinTheta, -1, 1) * std::cos(phi), Clamp(sinTheta, -1, 1) * std::sin(phi),
+            Clamp(cosTheta, -1, 1)};
+}
+
+// Interval arithmetic — util/math.h:818-1014 (CPU rounding branch)
+struct Interval {
+    float low, high;
+    static Interval Exact(float v) { return {v, v}; }
+    static Interval FromValueAndError(float v, float err) {
+        if (err == 0) return {v, v};
+        return {SubRoundDown(v, err), AddRoundUp(v, err)};
+    }
+    float Midpoint() const { return (low + high) / 2; }
+    float Width() const { return high - low; }
+};
+static inline Interval IvAdd(Interval a, float f) {  // Interval + Interval(f)
+    float lo = AddRoundDown(a.low, f), hi = AddRoundUp(a.high, f);
+    return {std::min(lo, hi), std::max(lo, hi)};
+}
+
+// ---------------------------------------------------------------------------
+// Transforms (affine, row-major m[4][4]) — util/transform.h / transform.cpp
+struct Xform { float m[4][4], mInv[4][4]; };
+
+// Transform::operator()(Point3<T>) — transform.h:313-322
+static inline V3 XPoint(const float (&m)[4][4], V3 p) {
+    float xp = m[0][0] * p.x + m[0][1] * p.y + m[0][2] * p.z + m[0][3];
+    float yp = m[1][0] * p.x + m[1][1] * p.y + m[1][2] * p.z + m[1][3];
+    float zp = m[2][0] * p.x + m[2][1] * p.y + m[2][2] * p.z + m[2][3];
+    float wp = m[3][0] * p.x + m[3][1] * p.y + m[3][2] * p.z + m[3][3];
+    if (wp == 1) return {xp, yp, zp};
+    return V3{xp, yp, zp} / wp;
+}
+// Transform::operator()(Vector3<T>) / ApplyInverse(Vector3<T>) — transform.h:324-329, 405-410
+static inline V3 XVector(const float (&m)[4][4], V3 v) {
+    return {m[0][0] * v.x + m[0][1] * v.y + m[0][2] * v.z, m[1][0] * v.x + m[1][1] * v.y + m[1][2] * v.z,
+            m[2][0] * v.x + m[2][1] * v.y + m[2][2] * v.z};
+}
+// Transform::ApplyInverse(Point3<T>) — transform.h:391-403 (note the pairwise grouping)
+static inline V3 XInvPoint(const Xform &t, V3 p) {
+    const auto &mi = t.mInv;
+    float xp = (mi[0][0] * p.x + mi[0][1] * p.y) + (mi[0][2] * p.z + mi[0][3]);
+    float yp = (mi[1][0] * p.x + mi[1][1] * p.y) + (mi[1][2] * p.z + mi[1][3]);
+    float zp = (mi[2][0] * p.x + mi[2][1] * p.y) + (mi[2][2] * p.z + mi[2][3]);
+    float wp = (mi[3][0] * p.x + mi[3][1] * p.y) + (mi[3][2] * p.z + mi[3][3]);
+    if (wp == 1) return {xp, yp, zp};
+    return V3{xp, yp, zp} / wp;
+}
+// Point3fi transform of an EXACT point: value + absolute error bound.
+// forward: transform.h:136-179 (error includes |m[i][3]|); inverse: transform.cpp:263-302
+// (error excludes |mInv[i][3]|). Affine transforms only (wp == 1).
+static inline void XPointExactErr(const float (&m)[4][4], V3 p, bool inverse, V3 *v, V3 *err) {
+    for (int i = 0; i < 3; ++i) {
+        (*v)[i] = (m[i][0] * p.x + m[i][1] * p.y) + (m[i][2] * p.z + m[i][3]);
+        float e = std::abs(m[i][0] * p.x) + std::abs(m[i][1] * p.y) + std::abs(m[i][2] * p.z);
+        if (!inverse) e = e + std::abs(m[i][3]);
+        (*err)[i] = gamma(3) * e;
+    }
+}
+struct Ray { V3 o, d; };
+// Transform::operator()(Ray, tMax) — transform.h:340-351 and ApplyInverse(Ray, tMax) — :420-433
+static inline Ray XRay(const Xform &t, Ray r, float *tMax, bool inverse) {
+    const auto &m = inverse ? t.mInv : t.m;
+    V3 v, e;
+    XPointExactErr(m, r.o, inverse, &v, &e);
+    Interval o[3];
+    for (int i = 0; i < 3; ++i) o[i] = Interval::FromValueAndError(v[i], e[i]);
+    V3 d = XVector(m, r.d);
+    float lengthSquared = LengthSquared(d);
+    if (lengthSquared > 0) {
+        V3 oErr = {o[0].Width() / 2, o[1].Width() / 2, o[2].Width() / 2};
+        float dt = Dot(Abs(d), oErr) / lengthSquared;
+        V3 dd = d * dt;
+        for (int i = 0; i < 3; ++i) o[i] = IvAdd(o[i], dd[i]);
+        if (tMax) *tMax -= dt;
+    }
+    return {{o[0].Midpoint(), o[1].Midpoint(), o[2].Midpoint()}, d};
+}
+
+// ---------------------------------------------------------------------------
+// Bounds3f::IntersectP — vecmath.h:1547-1571; Offset — vecmath.h:1323-1332
+struct Bounds { V3 pMin, pMax; };
+static inline bool IntersectP(const Bounds &b, V3 o, V3 d, float tMax, float *hitt0, float *hitt1) {
+    float t0 = 0, t1 = tMax;
+    for (int i = 0; i < 3; ++i) {
+        float invRayDir = 1 / d[i];
+        float tNear = (b.pMin[i] - o[i]) * invRayDir;
+        float tFar = (b.pMax[i] - o[i]) * invRayDir;
+        if (tNear > tFar) std::swap(tNear, tFar);
+        tFar *= 1 + 2 * gamma(3);
+        t0 = tNear > t0 ? tNear : t0;
+        t1 = tFar < t1 ? tFar : t1;
+        if (t0 > t1) return false;
+    }
+    *hitt0 = t0; *hitt1 = t1;
+    return true;
+}
+static inline V3 Offset(const Bounds &b, V3 p) {
+    V3 o = p - b.pMin;
+    if (b.pMax.x > b.pMin.x) o.x /= b.pMax.x - b.pMin.x;
+    if (b.pMax.y > b.pMin.y) o.y /= b.pMax.y - b.pMin.y;
+    if (b.pMax.z > b.pMin.z) o.z /= b.pMax.z - b.pMin.z;
+    return o;
+}
+
+// ---------------------------------------------------------------------------
+// Spectra — util/spectrum.h (NSpectrumSamples = 4)
+static const int NS = 4;
+struct Spec {
+    float v[NS];
+    static Spec Const(float c) { return {{c, c, c, c}}; }
+    float operator[](int i) const { return v[i]; }
+    float &operator[](int i) { return v[i]; }
+    explicit operator bool() const { for (int i = 0; i < NS; ++i) if (v[i] != 0) return true; return false; }
+    float Average() const { float s = v[0]; for (int i = 1; i < NS; ++i) s += v[i]; return s / NS; }
+    float MaxComponentValue() const { float m = v[0]; for (int i = 1; i < NS; ++i) m = std::max(m, v[i]); return m; }
+};
+static inline Spec operator+(Spec a, const Spec &b) { for (int i = 0; i < NS; ++i) a.v[i] += b.v[i]; return a; }
+static inline Spec operator-(Spec a, const Spec &b) { for (int i = 0; i < NS; ++i) a.v[i] -= b.v[i]; return a; }
+static inline Spec operator*(Spec a, const Spec &b) { for (int i = 0; i < NS; ++i) a.v[i] *= b.v[i]; return a; }
+static inline Spec operator/(Spec a, const Spec &b) { for (int i = 0; i < NS; ++i) a.v[i] /= b.v[i]; return a; }
+static inline Spec operator*(Spec a, float s) { for (int i = 0; i < NS; ++i) a.v[i] *= s; return a; }
+static inline Spec operator*(float s, Spec a) { return a * s; }
+static inline Spec operator/(Spec a, float s) { for (int i = 0; i < NS; ++i) a.v[i] /= s; return a; }
+static inline Spec operator-(Spec a) { for (int i = 0; i < NS; ++i) a.v[i] = -a.v[i]; return a; }
+static inline Spec ClampZero(Spec a) { for (int i = 0; i < NS; ++i) a.v[i] = std::max<float>(0, a.v[i]); return a; }
+static inline Spec SafeDiv(Spec a, Spec b) {  // spectrum.h:634-639
+    Spec r; for (int i = 0; i < NS; ++i) r.v[i] = (b.v[i] != 0) ? a.v[i] / b.v[i] : 0.f; return r;
+}
+static inline Spec FastExpSpec(Spec a) { for (int i = 0; i < NS; ++i) a.v[i] = FastExp(a.v[i]); return a; }
+
+struct Lambda { float lambda[NS], pdf[NS]; };
+// SampleVisibleWavelengths / VisibleWavelengthsPDF — sampling.h:163-171;
+// SampledWavelengths::SampleVisible — spectrum.h:334-347
+static inline float SampleVisibleWavelengths(float u) { return 538 - 138.888889f * std::atanh(0.85691062f - 1.82750197f * u); }
+static inline float VisibleWavelengthsPDF(float l) {
+    if (l < 360 || l > 830) return 0;
+    return 0.0039398042f / Sqr(std::cosh(0.0072f * (l - 538)));
+}
+static inline Lambda SampleVisible(float u) {
+    Lambda w;
+    for (int i = 0; i < NS; ++i) {
+        float up = u + float(i) / NS;
+        if (up > 1) up -= 1;
+        w.lambda[i] = SampleVisibleWavelengths(up);
+        w.pdf[i] = VisibleWavelengthsPDF(w.lambda[i]);
+    }
+    return w;
+}
+// DenselySampledSpectrum::Sample — spectrum.h:390-400 (table over 360..830 nm)
+static inline Spec SampleDense(const float *table, const Lambda &l) {
+    Spec s;
+    for (int i = 0; i < NS; ++i) {
+        int offset = (int)std::lround(l.lambda[i]) - 360;
+        s.v[i] = (offset < 0 || offset >= 471) ? 0.f : table[offset];
+    }
+    return s;
+}
+
+// ---------------------------------------------------------------------------
+// Sampling — sampling.h:79-110, 222-225; sampling.cpp:348-372; scattering.h:49-58
+static inline float SampleExponential(float u, float a) { return -std::log(1 - u) / a; }
+static inline int SampleDiscrete3(const float w[3], float u) {
+    float sumWeights = 0;
+    for (int i = 0; i < 3; ++i) sumWeights += w[i];
+    float up = u * sumWeights;
+    if (up == sumWeights) up = NextFloatDown(up);
+    int offset = 0;
+    float sum = 0;
+    while (sum + w[offset] <= up) sum += w[offset++];
+    return offset;
+}
+static inline float HenyeyGreenstein(float cosTheta, float g) {
+    g = Clamp(g, -.99, .99);
+    float denom = 1 + Sqr(g) + 2 * g * cosTheta;
+    return Inv4Pi * (1 - Sqr(g)) / (denom * SafeSqrt(denom));
+}
+static inline V3 SampleHenyeyGreenstein(V3 wo, float g, float u0, float u1, float *pdf) {
+    g = Clamp(g, -.99, .99);
+    float cosTheta;
+    if (std::abs(g) < 1e-3f)
+        cosTheta = 1 - 2 * u0;
+    else
+        cosTheta = -1 / (2 * g) * (1 + Sqr(g) - Sqr((1 - Sqr(g)) / (1 + g - 2 * g * u0)));
+    float sinTheta = SafeSqrt(1 - Sqr(cosTheta));
+    float phi = 2 * Pi * u1;
+    V3 x, y;
+    CoordinateSystem(wo, &x, &y);
+    V3 s = SphericalDirection(sinTheta, cosTheta, phi);
+    V3 wi = s.x * x + s.y * y + s.z * wo;  // Frame::FromLocal, vecmath.h:1916
+    *pdf = HenyeyGreenstein(cosTheta, g);
+    return wi;
+}
+
+// ---------------------------------------------------------------------------
+// SampledGrid<float> — util/containers.h:765-870
+struct Grid {
+    const float *values = nullptr;
+    int nx = 1, ny = 1, nz = 1;
+    float At(int x, int y, int z) const {
+        if (x < 0 || x >= nx || y < 0 || y >= ny || z < 0 || z >= nz) return 0.f;
+        return values[(z * ny + y) * nx + x];
+    }
+    float Lookup(V3 p) const {
+        V3 ps = {p.x * nx - .5f, p.y * ny - .5f, p.z * nz - .5f};
+        int ix = (int)std::floor(ps.x), iy = (int)std::floor(ps.y), iz = (int)std::floor(ps.z);
+        V3 d = {ps.x - (float)ix, ps.y - (float)iy, ps.z - (float)iz};
+        float d00 = Lerp(d.x, At(ix, iy, iz), At(ix + 1, iy, iz));
+        float d10 = Lerp(d.x, At(ix, iy + 1, iz), At(ix + 1, iy + 1, iz));
+        float d01 = Lerp(d.x, At(ix, iy, iz + 1), At(ix + 1, iy, iz + 1));
+        float d11 = Lerp(d.x, At(ix, iy + 1, iz + 1), At(ix + 1, iy + 1, iz + 1));
+        return Lerp(d.z, Lerp(d.y, d00, d10), Lerp(d.y, d01, d11));
+    }
+    float MaxValue(const Bounds &b) const {
+        V3 ps0 = {b.pMin.x * nx - .5f, b.pMin.y * ny - .5f, b.pMin.z * nz - .5f};
+        V3 ps1 = {b.pMax.x * nx - .5f, b.pMax.y * ny - .5f, b.pMax.z * nz - .5f};
+        int lo[3] = {std::max((int)std::floor(ps0.x), 0), std::max((int)std::floor(ps0.y), 0),
+                     std::max((int)std::floor(ps0.z), 0)};
+        int hi[3] = {std::min((int)std::floor(ps1.x) + 1, nx - 1), std::min((int)std::floor(ps1.y) + 1, ny - 1),
+                     std::min((int)std::floor(ps1.z) + 1, nz - 1)};
+        float maxValue = At(lo[0], lo[1], lo[2]);
+        for (int z = lo[2]; z <= hi[2]; ++z)
+            for (int y = lo[1]; y <= hi[1]; ++y)
+                for (int x = lo[0]; x <= hi[0]; ++x) maxValue = std::max(maxValue, At(x, y, z));
+        return maxValue;
+    }
+};
+
+// ---------------------------------------------------------------------------
+// Perlin noise — util/noise.cpp (Ken Perlin's public reference permutation)
+static const int NoisePerm[512] = {
+    151, 160, 137, 91, 90, 15, 131, 13, 201, 95, 96, 53, 194, 233, 7, 225, 140, 36, 103, 30, 69, 142,
+    8, 99, 37, 240, 21, 10, 23, 190, 6, 148, 247, 120, 234, 75, 0, 26, 197, 62, 94, 252, 219, 203, 117,
+    35, 11, 32, 57, 177, 33, 88, 237, 149, 56, 87, 174, 20, 125, 136, 171, 168, 68, 175, 74, 165, 71,
+    134, 139, 48, 27, 166, 77, 146, 158, 231, 83, 111, 229, 122, 60, 211, 133, 230, 220, 105, 92, 41,
+    55, 46, 245, 40, 244, 102, 143, 54, 65, 25, 63, 161, 1, 216, 80, 73, 209, 76, 132, 187, 208, 89,
+    18, 169, 200, 196, 135, 130, 116, 188, 159, 86, 164, 100, 109, 198, 173, 186, 3, 64, 52, 217, 226,
+    250, 124, 123, 5, 202, 38, 147, 118, 126, 255, 82, 85, 212, 207, 206, 59, 227, 47, 16, 58, 17, 182,
+    189, 28, 42, 223, 183, 170, 213, 119, 248, 152, 2, 44, 154, 163, 70, 221, 153, 101, 155, 167, 43,
+    172, 9, 129, 22, 39, 253, 19, 98, 108, 110, 79, 113, 224, 232, 178, 185, 112, 104, 218, 246, 97,
+    228, 251, 34, 242, 193, 238, 210, 144, 12, 191, 179, 162, 241, 81, 51, 145, 235, 249, 14, 239,
+    107, 49, 192, 214, 31, 181, 199, 106, 157, 184, 84, 204, 176, 115, 121, 50, 45, 127, 4, 150, 254,
+    138, 236, 205, 93, 222, 114, 67, 29, 24, 72, 243, 141, 128, 195, 78, 66, 215, 61, 156, 180,
+    151, 160, 137, 91, 90, 15, 131, 13, 201, 95, 96, 53, 194, 233, 7, 225, 140, 36, 103, 30, 69, 142,
+    8, 99, 37, 240, 21, 10, 23, 190, 6, 148, 247, 120, 234, 75, 0, 26, 197, 62, 94, 252, 219, 203, 117,
+    35, 11, 32, 57, 177, 33, 88, 237, 149, 56, 87, 174, 20, 125, 136, 171, 168, 68, 175, 74, 165, 71,
+    134, 139, 48, 27, 166, 77, 146, 158, 231, 83, 111, 229, 122, 60, 211, 133, 230, 220, 105, 92, 41,
+    55, 46, 245, 40, 244, 102, 143, 54, 65, 25, 63, 161, 1, 216, 80, 73, 209, 76, 132, 187, 208, 89,
+    18, 169, 200, 196, 135, 130, 116, 188, 159, 86, 164, 100, 109, 198, 173, 186, 3, 64, 52, 217, 226,
+    250, 124, 123, 5, 202, 38, 147, 118, 126, 255, 82, 85, 212, 207, 206, 59, 227, 47, 16, 58, 17, 182,
+    189, 28, 42, 223, 183, 170, 213, 119, 248, 152, 2, 44, 154, 163, 70, 221, 153, 101, 155, 167, 43,
+    172, 9, 129, 22, 39, 253, 19, 98, 108, 110, 79, 113, 224, 232, 178, 185, 112, 104, 218, 246, 97,
+    228, 251, 34, 242, 193, 238, 210, 144, 12, 191, 179, 162, 241, 81, 51, 145, 235, 249, 14, 239,
+    107, 49, 192, 214, 31, 181, 199, 106, 157, 184, 84, 204, 176, 115, 121, 50, 45, 127, 4, 150, 254,
+    138, 236, 205, 93, 222, 114, 67, 29, 24, 72, 243, 141, 128, 195, 78, 66, 215, 61, 156, 180};
+static inline float Pow3(float v) { return (v * v) * v; }   // math.h:295-309 (Pow<n> by squaring)
+static inline float Pow4(float v) { float n2 = v * v; return n2 * n2; }
+static inline float Pow5(float v) { float n2 = v * v; return (n2 * n2) * v; }
+static inline float Grad(int x, int y, int z, float dx, float dy, float dz) {
+    int h = NoisePerm[NoisePerm[NoisePerm[x] + y] + z];
+    h &= 15;
+    float u = h < 8 || h == 12 || h == 13 ? dx : dy;
+    float v = h < 4 || h == 12 || h == 13 ? dy : dz;
+    return ((h & 1) ? -u : u) + ((h & 2) ? -v : v);
+}
+static inline float NoiseWeight(float t) { return 6 * Pow5(t) - 15 * Pow4(t) + 10 * Pow3(t); }
+static float Noise(float x, float y, float z) {
+    x = std::fmod(x, float(1 << 30)); y = std::fmod(y, float(1 << 30)); z = std::fmod(z, float(1 << 30));
+    int ix = (int)std::floor(x), iy = (int)std::floor(y), iz = (int)std::floor(z);
+    float dx = x - ix, dy = y - iy, dz = z - iz;
+    ix &= 255; iy &= 255; iz &= 255;
+    float w000 = Grad(ix, iy, iz, dx, dy, dz), w100 = Grad(ix + 1, iy, iz, dx - 1, dy, dz);
+    float w010 = Grad(ix, iy + 1, iz, dx, dy - 1, dz), w110 = Grad(ix + 1, iy + 1, iz, dx - 1, dy - 1, dz);
+    float w001 = Grad(ix, iy, iz + 1, dx, dy, dz - 1), w101 = Grad(ix + 1, iy, iz + 1, dx - 1, dy, dz - 1);
+    float w011 = Grad(ix, iy + 1, iz + 1, dx, dy - 1, dz - 1);
+    float w111 = Grad(ix + 1, iy + 1, iz + 1, dx - 1, dy - 1, dz - 1);
+    float wx = NoiseWeight(dx), wy = NoiseWeight(dy), wz = NoiseWeight(dz);
+    float x00 = Lerp(wx, w000, w100), x10 = Lerp(wx, w010, w110);
+    float x01 = Lerp(wx, w001, w101), x11 = Lerp(wx, w011, w111);
+    float y0 = Lerp(wy, x00, x10), y1 = Lerp(wy, x01, x11);
+    return Lerp(wz, y0, y1);
+}
+static inline V3 DNoise(V3 p) {
+    float delta = .01f;
+    float n = Noise(p.x, p.y, p.z);
+    V3 nd = {Noise(p.x + delta, p.y + 0.f, p.z + 0.f), Noise(p.x + 0.f, p.y + delta, p.z + 0.f),
+             Noise(p.x + 0.f, p.y + 0.f, p.z + delta)};
+    return (nd - V3{n, n, n}) / delta;
+}
+// CloudMedium::Density — media.h:496-520 (the synthetic-cloud generator)
+static float CloudDensity(V3 p, float density, float wispiness, float frequency) {
+    V3 pp = frequency * p;
+    if (wispiness > 0) {
+        float vomega = 0.05f * wispiness, vlambda = 10.f;
+        for (int i = 0; i < 2; ++i) {
+            pp = pp + vomega * DNoise(vlambda * pp);
+            vomega *= 0.5f;
+            vlambda *= 1.99f;
+        }
+    }
+    float d = 0, omega = 0.5f, lambda = 1.f;
+    for (int i = 0; i < 5; ++i) {
+        V3 q = lambda * pp;
+        d += omega * Noise(q.x, q.y, q.z);
+        omega *= 0.5f;
+        lambda *= 1.99f;
+    }
+    d = Clamp((1 - p.y) * 4.5f * density * d, 0, 1);
+    d += 2 * std::max<float>(0, 0.5f - p.y);
+    return Clamp(d, 0, 1);
+}
+
+// Blackbody — spectrum.h:69-80, BlackbodySpectrum spectrum.h:500-530
+static inline float Blackbody(float lambda, float T) {
+    if (T <= 0) return 0;
+    const float c = 299792458.f, h = 6.62606957e-34f, kb = 1.3806488e-23f;
+    float l = lambda * 1e-9f;
+    return (2 * h * c * c) / (Pow5(l) * (FastExp((h * c) / (l * kb * T)) - 1));
+}
+
+}  // namespace oracle
+
+// ===========================================================================
+// Scene and integrator
+// ===========================================================================
+using namespace oracle;
+
+extern "C" {
+
+// Must match acceleratedvolrenderer_amd/oracle_binding.py (ctypes) field for field.
+typedef struct OracleScene {
+    // GridMedium (media.h:265-352 / media.cpp:212-330)
+    const float *density; int nx, ny, nz;
+    float bounds[6];                  // p0.xyz, p1.xyz (medium space)
+    float render_from_medium[16];     // row-major m
+    float medium_from_render[16];     // row-major mInv
+    const float *sigma_a;             // 471 (DenselySampled, x sigmaScale)
+    const float *sigma_s;             // 471
+    float g;
+    int emissive;                     // GridMedium::isEmissive
+    const float *Le;                  // 471
+    const float *Lescale; int lnx, lny, lnz;  // LeScale grid (LeNorm folded in)
+    const float *majorant; int mres[3];       // MajorantGrid voxels (x fastest)
+    // lights (BVHLightSampler infinite-light branch; lightsamplers.h:266-277, 323-326)
+    int nlights;
+    int light_type[8];                // 0 = distant (delta), 1 = uniform infinite
+    float light_w[8][3];              // distant: render-space unit vector towards the light
+    const float *light_L[8];          // 471 each
+    float light_scale[8];
+    float scene_radius;               // Bounds3::BoundingSphere of the scene bounds
+    // camera (cameras.cpp:284-306 ortho, 404-427 perspective)
+    int camera_type;                  // 0 ortho, 1 perspective
+    float camera_from_raster[16];
+    float render_from_camera[16];
+    // RGBFilm (film.h:232-316) + cie1931 PixelSensor (film.h:95-100)
+    int width, height;
+    float filter_radius[2];           // box filter
+    const float *sensor_xyz;          // 3 x 471: X, Y, Z matching functions
+    float imaging_ratio;
+    float output_from_sensor[9];      // colorSpace->RGBFromXYZ * XYZFromSensorRGB
+    float max_component_value;
+    // VolPathIntegrator (integrators.cpp:1401-1409) + IndependentSampler seed
+    int max_depth;
+    int seed;
+} OracleScene;
+
+}  // extern "C"
+
+namespace oracle {
+
+struct SceneView {
+    const OracleScene &s;
+    Xform mediumX, cameraX, rasterX;
+    Bounds bounds;
+    Grid density, lescale, majorant;
+    explicit SceneView(const OracleScene &sc) : s(sc) {
+        for (int i = 0; i < 16; ++i) {
+            mediumX.m[i / 4][i % 4] = sc.render_from_medium[i];
+            mediumX.mInv[i / 4][i % 4] = sc.medium_from_render[i];
+            cameraX.m[i / 4][i % 4] = sc.render_from_camera[i];
+            cameraX.mInv[i / 4][i % 4] = 0;
+            rasterX.m[i / 4][i % 4] = sc.camera_from_raster[i];
+            rasterX.mInv[i / 4][i % 4] = 0;
+        }
+        bounds = {{sc.bounds[0], sc.bounds[1], sc.bounds[2]}, {sc.bounds[3], sc.bounds[4], sc.bounds[5]}};
+        density = {sc.density, sc.nx, sc.ny, sc.nz};
+        lescale = {sc.Lescale, sc.lnx, sc.lny, sc.lnz};
+        majorant = {sc.majorant, sc.mres[0], sc.mres[1], sc.mres[2]};
+    }
+};
+
+// MediumProperties for GridMedium::SamplePoint — media.h:287-319 (no temperature grid)
+struct MediumProps { Spec sigma_a, sigma_s, Le; };
+static inline MediumProps SamplePoint(const SceneView &sv, V3 p, const Lambda &l) {
+    MediumProps mp;
+    mp.sigma_a = SampleDense(sv.s.sigma_a, l);
+    mp.sigma_s = SampleDense(sv.s.sigma_s, l);
+    p = XInvPoint(sv.mediumX, p);
+    p = Offset(sv.bounds, p);
+    float d = sv.density.Lookup(p);
+    mp.sigma_a = mp.sigma_a * d;
+    mp.sigma_s = mp.sigma_s * d;
+    mp.Le = Spec::Const(0.f);
+    if (sv.s.emissive) {
+        float scale = sv.lescale.Lookup(p);
+        if (scale > 0) mp.Le = scale * SampleDense(sv.s.Le, l);
+    }
+    return mp;
+}
+
+// DDAMajorantIterator — media.h:136-214
+struct DDA {
+    Spec sigma_t;
+    float tMin = Infinity, tMax = -Infinity;
+    const Grid *grid = nullptr;
+    float nextCrossingT[3], deltaT[3];
+    int step[3], voxelLimit[3], voxel[3];
+    bool valid = false;
+    void Init(Ray ray, float tMin_, float tMax_, const Grid *g, const Bounds &gb, Spec st) {
+        tMin = tMin_; tMax = tMax_; grid = g; sigma_t = st; valid = true;
+        V3 diag = gb.pMax - gb.pMin;
+        Ray rg = {Offset(gb, ray.o), {ray.d.x / diag.x, ray.d.y / diag.y, ray.d.z / diag.z}};
+        V3 gi = rg.o + rg.d * tMin;
+        const int res[3] = {g->nx, g->ny, g->nz};
+        for (int axis = 0; axis < 3; ++axis) {
+            voxel[axis] = (int)Clamp(gi[axis] * res[axis], 0, res[axis] - 1);
+            deltaT[axis] = 1 / (std::abs(rg.d[axis]) * res[axis]);
+            if (rg.d[axis] == -0.f) rg.d[axis] = 0.f;
+            if (rg.d[axis] >= 0) {
+                float nextVoxelPos = float(voxel[axis] + 1) / res[axis];
+                nextCrossingT[axis] = tMin + (nextVoxelPos - gi[axis]) / rg.d[axis];
+                step[axis] = 1;
+                voxelLimit[axis] = res[axis];
+            } else {
+                float nextVoxelPos = float(voxel[axis]) / res[axis];
+                nextCrossingT[axis] = tMin + (nextVoxelPos - gi[axis]) / rg.d[axis];
+                step[axis] = -1;
+                voxelLimit[axis] = -1;
+            }
+        }
+    }
+    // returns false when exhausted
+    bool Next(float *segMin, float *segMax, Spec *sigma_maj) {
+        if (!valid || tMin >= tMax) return false;
+        int bits = ((nextCrossingT[0] < nextCrossingT[1]) << 2) + ((nextCrossingT[0] < nextCrossingT[2]) << 1) +
+                   ((nextCrossingT[1] < nextCrossingT[2]));
+        static const int cmpToAxis[8] = {2, 1, 2, 1, 2, 2, 0, 0};
+        int stepAxis = cmpToAxis[bits];
+        float tVoxelExit = std::min(tMax, nextCrossingT[stepAxis]);
+        *sigma_maj = sigma_t * grid->values[voxel[0] + grid->nx * (voxel[1] + grid->ny * voxel[2])];
+        *segMin = tMin;
+        *segMax = tVoxelExit;
+        tMin = tVoxelExit;
+        if (nextCrossingT[stepAxis] > tMax) tMin = tMax;
+        voxel[stepAxis] += step[stepAxis];
+        if (voxel[stepAxis] == voxelLimit[stepAxis]) tMin = tMax;
+        nextCrossingT[stepAxis] += deltaT[stepAxis];
+        return true;
+    }
+};
+
+// GridMedium::SampleRay — media.h:322-337
+static inline DDA SampleRay(const SceneView &sv, Ray ray, float raytMax, const Lambda &l) {
+    DDA it;
+    ray = XRay(sv.mediumX, ray, &raytMax, /*inverse=*/true);
+    float tMin, tMax;
+    if (!IntersectP(sv.bounds, ray.o, ray.d, raytMax, &tMin, &tMax)) return it;
+    Spec sigma_t = SampleDense(sv.s.sigma_a, l) + SampleDense(sv.s.sigma_s, l);
+    it.Init(ray, tMin, tMax, &sv.majorant, sv.bounds, sigma_t);
+    return it;
+}
+
+// SampleT_maj<GridMedium> — media.h:741-806
+template <typename F>
+static Spec SampleT_maj(const SceneView &sv, Ray ray, float tMax, float u, RNG &rng, const Lambda &l,
+                        F callback) {
+    tMax *= Length(ray.d);
+    ray.d = Normalize(ray.d);
+    DDA iter = SampleRay(sv, ray, tMax, l);
+    Spec T_maj = Spec::Const(1.f);
+    bool done = false;
+    while (!done) {
+        float segMin, segMax;
+        Spec sigma_maj;
+        if (!iter.Next(&segMin, &segMax, &sigma_maj)) return T_maj;
+        if (sigma_maj[0] == 0) {
+            float dt = segMax - segMin;
+            if (std::isinf(dt)) dt = std::numeric_limits<float>::max();
+            T_maj = T_maj * FastExpSpec(-dt * sigma_maj);
+            continue;
+        }
+        float tMin = segMin;
+        while (true) {
+            float t = tMin + SampleExponential(u, sigma_maj[0]);
+            u = rng.Uniform();
+            if (t < segMax) {
+                T_maj = T_maj * FastExpSpec(-(t - tMin) * sigma_maj);
+                V3 p = ray.o + ray.d * t;
+                MediumProps mp = SamplePoint(sv, p, l);
+                if (!callback(p, mp, sigma_maj, T_maj)) { done = true; break; }
+                T_maj = Spec::Const(1.f);
+                tMin = t;
+            } else {
+                float dt = segMax - tMin;
+                if (std::isinf(dt)) dt = std::numeric_limits<float>::max();
+                T_maj = T_maj * FastExpSpec(-dt * sigma_maj);
+                break;
+            }
+        }
+    }
+    return Spec::Const(1.f);
+}
+
+// Per-sample sampler state: IndependentSampler — samplers.h:457-466
+struct Sampler {
+    RNG rng;
+    void Start(int px, int py, int sampleIndex, int seed) {
+        rng.SetSequence(HashPixelSeed(px, py, seed));
+        rng.Advance((int64_t)(sampleIndex * 65536ull + 0));
+    }
+    float Get1D() { return rng.Uniform(); }
+};
+
+// VolPathIntegrator::SampleLd for a medium interaction — integrators.cpp:1282-1399
+static Spec SampleLd(const SceneView &sv, V3 p, V3 wo, const Lambda &l, Sampler &sampler, Spec beta, Spec r_p) {
+    const OracleScene &s = sv.s;
+    // lightSampler.Sample (BVH, infinite lights only) — lightsamplers.h:266-277
+    float u = sampler.Get1D();
+    float uL0 = sampler.Get1D(), uL1 = sampler.Get1D();
+    (void)uL0; (void)uL1;
+    if (s.nlights == 0) return Spec::Const(0.f);
+    float pInfinite = float(s.nlights) / float(s.nlights + 0);
+    if (!(u < pInfinite)) return Spec::Const(0.f);
+    u /= pInfinite;
+    int index = std::min<int>(u * s.nlights, s.nlights - 1);
+    float pmf = pInfinite / s.nlights;
+    if (s.light_type[index] != 0) return Spec::Const(0.f);  // UniformInfiniteLight::SampleLi with allowIncompletePDF
+    // DistantLight::SampleLi — lights.h:284-291
+    V3 wi = {s.light_w[index][0], s.light_w[index][1], s.light_w[index][2]};
+    V3 pOutside = p + wi * (2 * s.scene_radius);
+    Spec Ls = s.light_scale[index] * SampleDense(s.light_L[index], l);
+    if (!Ls) return Spec::Const(0.f);
+    float lsPdf = 1;
+    float p_l = pmf * lsPdf;
+    // phase function
+    float fval = HenyeyGreenstein(Dot(wo, wi), s.g);
+    Spec f_hat = Spec::Const(fval);
+    float scatterPDF = fval;
+    (void)scatterPDF;
+    if (!f_hat) return Spec::Const(0.f);
+    // SpawnRayTo from a medium interaction (ray.h:75-108: zero error, zero normal)
+    Ray lightRay = {p, pOutside - p};
+    Spec T_ray = Spec::Const(1.f), r_l = Spec::Const(1.f), r_u = Spec::Const(1.f);
+    RNG rng(HashBytes(&lightRay.o, 12), HashBytes(&lightRay.d, 12));
+    // The box boundary only toggles the medium; SampleT_maj clips to the same bounds.
+    float tMax = 1 - ShadowEpsilon;
+    float uu = rng.Uniform();
+    Spec T_maj = SampleT_maj(sv, lightRay, tMax, uu, rng, l, [&](V3, const MediumProps &mp, Spec sigma_maj, Spec Tm) {
+        Spec sigma_n = ClampZero(sigma_maj - mp.sigma_a - mp.sigma_s);
+        float pdf = Tm[0] * sigma_maj[0];
+        T_ray = T_ray * (Tm * sigma_n / pdf);
+        r_l = r_l * (Tm * sigma_maj / pdf);
+        r_u = r_u * (Tm * sigma_n / pdf);
+        Spec Tr = T_ray / (r_l + r_u).Average();
+        if (Tr.MaxComponentValue() < 0.05f) {
+            float q = 0.75f;
+            if (rng.Uniform() < q) T_ray = Spec::Const(0.);
+            else T_ray = T_ray / (1 - q);
+        }
+        if (!T_ray) return false;
+        return true;
+    });
+    T_ray = T_ray * (T_maj / T_maj[0]);
+    r_l = r_l * (T_maj / T_maj[0]);
+    r_u = r_u * (T_maj / T_maj[0]);
+    if (!T_ray) return Spec::Const(0.f);
+    r_l = r_l * (r_p * p_l);
+    r_u = r_u * (r_p * scatterPDF);
+    // DistantLight is a delta light
+    return beta * f_hat * T_ray * Ls / r_l.Average();
+}
+
+// VolPathIntegrator::Li — integrators.cpp:962-1280, restricted to the interface-box scene.
+static Spec Li(const SceneView &sv, Ray ray, Lambda &l, Sampler &sampler, int *nEvents) {
+    const OracleScene &s = sv.s;
+    Spec L = Spec::Const(0.f), beta = Spec::Const(1.f), r_u = Spec::Const(1.f), r_l = Spec::Const(1.f);
+    bool specularBounce = false;
+    int depth = 0;
+    const int maxDepth = s.max_depth;
+    while (true) {
+        // ray.medium is the grid medium (see header: the interface box only toggles it)
+        bool scattered = false, terminated = false;
+        float tMax = Infinity;
+        uint64_t hash0 = HashFloat(sampler.Get1D());
+        uint64_t hash1 = HashFloat(sampler.Get1D());
+        RNG rng(hash0, hash1);
+        float u0 = sampler.Get1D();
+        Ray segRay = ray;
+        Spec T_maj = SampleT_maj(sv, segRay, tMax, u0, rng, l,
+            [&](V3 p, const MediumProps &mp, Spec sigma_maj, Spec Tm) -> bool {
+                if (nEvents) ++*nEvents;
+                if (!beta) { terminated = true; return false; }
+                if (depth < maxDepth && mp.Le) {
+                    float pdf = sigma_maj[0] * Tm[0];
+                    Spec betap = beta * Tm / pdf;
+                    Spec r_e = r_u * sigma_maj * Tm / pdf;
+                    if (r_e) L = L + betap * mp.sigma_a * mp.Le / r_e.Average();
+                }
+                float pAbsorb = mp.sigma_a[0] / sigma_maj[0];
+                float pScatter = mp.sigma_s[0] / sigma_maj[0];
+                float pNull = std::max<float>(0, 1 - pAbsorb - pScatter);
+                float um = rng.Uniform();
+                const float w[3] = {pAbsorb, pScatter, pNull};
+                int mode = SampleDiscrete3(w, um);
+                if (mode == 0) { terminated = true; return false; }
+                if (mode == 1) {
+                    if (depth++ >= maxDepth) { terminated = true; return false; }
+                    float pdf = Tm[0] * mp.sigma_s[0];
+                    beta = beta * (Tm * mp.sigma_s / pdf);
+                    r_u = r_u * (Tm * mp.sigma_s / pdf);
+                    if (beta && r_u) {
+                        V3 wo = -ray.d;
+                        L = L + SampleLd(sv, p, wo, l, sampler, beta, r_u);
+                        float uph0 = sampler.Get1D(), uph1 = sampler.Get1D();
+                        float phPdf;
+                        V3 wi = SampleHenyeyGreenstein(wo, s.g, uph0, uph1, &phPdf);
+                        if (phPdf == 0) terminated = true;
+                        else {
+                            beta = beta * (phPdf / phPdf);
+                            r_l = r_u / phPdf;
+                            scattered = true;
+                            ray.o = p;
+                            ray.d = wi;
+                            specularBounce = false;
+                        }
+                    }
+                    return false;
+                }
+                Spec sigma_n = ClampZero(sigma_maj - mp.sigma_a - mp.sigma_s);
+                float pdf = Tm[0] * sigma_n[0];
+                beta = beta * (Tm * sigma_n / pdf);
+                if (pdf == 0) beta = Spec::Const(0.f);
+                r_u = r_u * (Tm * sigma_n / pdf);
+                r_l = r_l * (Tm * sigma_maj / pdf);
+                return (bool)beta && (bool)r_u;
+            });
+        if (terminated || !beta || !r_u) return L;
+        if (scattered) continue;
+        beta = beta * (T_maj / T_maj[0]);
+        r_u = r_u * (T_maj / T_maj[0]);
+        r_l = r_l * (T_maj / T_maj[0]);
+        // Escaped: infinite lights (integrators.cpp:1090-1107)
+        for (int i = 0; i < s.nlights; ++i) {
+            if (s.light_type[i] != 1) continue;
+            Spec Le = s.light_scale[i] * SampleDense(s.light_L[i], l);
+            if (!Le) continue;
+            if (depth == 0 || specularBounce)
+                L = L + beta * Le / r_u.Average();
+            else {
+                float p_l = (1.f / (s.nlights + 0)) * 0.f;  // PMF * PDF_Li(allowIncompletePDF=true) = 0
+                r_l = r_l * p_l;
+                L = L + beta * Le / (r_u + r_l).Average();
+            }
+        }
+        break;
+    }
+    return L;
+}
+
+// RayIntegrator::EvaluatePixelSample — integrators.cpp:235-298 (+ GetCameraSample samplers.h:797-815)
+struct SampleResult { Spec L; Lambda l; };
+static SampleResult EvaluatePixelSample(const SceneView &sv, int px, int py, int sampleIndex, int *nEvents) {
+    const OracleScene &s = sv.s;
+    Sampler sampler;
+    sampler.Start(px, py, sampleIndex, s.seed);
+    float lu = sampler.Get1D();
+    Lambda l = SampleVisible(lu);
+    float fu0 = sampler.Get1D(), fu1 = sampler.Get1D();
+    // BoxFilter::Sample — filters.h:67-70
+    float fpx = Lerp(fu0, -s.filter_radius[0], s.filter_radius[0]);
+    float fpy = Lerp(fu1, -s.filter_radius[1], s.filter_radius[1]);
+    float filterWeight = 1;
+    float pFilmX = ((float)px + fpx) + 0.5f, pFilmY = ((float)py + fpy) + 0.5f;
+    sampler.Get1D();                      // time
+    sampler.Get1D(); sampler.Get1D();     // lens
+    // Camera ray (GenerateRayDifferential main ray, then RenderFromCamera)
+    V3 pCamera = XPoint(sv.rasterX.m, V3{pFilmX, pFilmY, 0.f});
+    Ray ray;
+    if (s.camera_type == 0) ray = {pCamera, {0.f, 0.f, 1.f}};
+    else ray = {{0.f, 0.f, 0.f}, Normalize(pCamera)};
+    ray = XRay(sv.cameraX, ray, nullptr, /*inverse=*/false);
+    Spec L = Spec::Const(1.f) * Li(sv, ray, l, sampler, nEvents);
+    bool bad = false;
+    for (int i = 0; i < NS; ++i) if (std::isnan(L.v[i])) bad = true;
+    if (!bad) {
+        // IsInf(L.y(lambda)) — spectrum.cpp SampledSpectrum::y
+        Spec Ys = SampleDense(s.sensor_xyz + 471, l);
+        Spec pdf; for (int i = 0; i < NS; ++i) pdf.v[i] = l.pdf[i];
+        float y = SafeDiv(Ys * L, pdf).Average() / 106.856895f;
+        if (std::isinf(y)) bad = true;
+    }
+    if (bad) L = Spec::Const(0.f);
+    (void)filterWeight;
+    return {L, l};
+}
+
+// RGBFilm::AddSample — film.h:239-255 with PixelSensor::ToSensorRGB film.h:95-100
+static inline void AddSample(const OracleScene &s, double *rgbSum, double *wSum, const Spec &Lin, const Lambda &l,
+                             float weight) {
+    Spec pdf; for (int i = 0; i < NS; ++i) pdf.v[i] = l.pdf[i];
+    Spec L = SafeDiv(Lin, pdf);
+    float rgb[3];
+    for (int c = 0; c < 3; ++c) rgb[c] = s.imaging_ratio * (SampleDense(s.sensor_xyz + 471 * c, l) * L).Average();
+    float m = std::max({rgb[0], rgb[1], rgb[2]});
+    if (m > s.max_component_value)
+        for (int c = 0; c < 3; ++c) rgb[c] *= s.max_component_value / m;
+    for (int c = 0; c < 3; ++c) rgbSum[c] += weight * rgb[c];
+    *wSum += weight;
+}
+
+}  // namespace oracle
+
+// ===========================================================================
+// C API (ctypes)
+// ===========================================================================
+extern "C" {
+
+// MajorantGrid build — media.cpp:229,241-246 with MajorantGrid::VoxelBounds media.h:123-127
+void oracle_build_majorant(const float *density, int nx, int ny, int nz, int rx, int ry, int rz, float *out) {
+    Grid g{density, nx, ny, nz};
+    for (int z = 0; z < rz; ++z)
+        for (int y = 0; y < ry; ++y)
+            for (int x = 0; x < rx; ++x) {
+                Bounds b{{float(x) / rx, float(y) / ry, float(z) / rz},
+                         {float(x + 1) / rx, float(y + 1) / ry, float(z + 1) / rz}};
+                out[x + rx * (y + ry * z)] = g.MaxValue(b);
+            }
+}
+
+// One pixel sample: L (4), lambda (4), pdf (4); returns number of tentative collisions.
+int oracle_pixel_sample(const OracleScene *s, int px, int py, int sampleIndex, float *L, float *lambda, float *pdf) {
+    SceneView sv(*s);
+    int nEvents = 0;
+    SampleResult r = EvaluatePixelSample(sv, px, py, sampleIndex, &nEvents);
+    for (int i = 0; i < NS; ++i) { L[i] = r.L.v[i]; lambda[i] = r.l.lambda[i]; pdf[i] = r.l.pdf[i]; }
+    return nEvents;
+}
+
+// Film accumulation for samples [spp0, spp1) of every pixel; rgbSum[W*H*3], wSum[W*H] (fp64).
+// Tiles of <=32x32 pixels handed to nthreads workers (util/parallel.cpp:307-328); per pixel
+// the samples are added in sampleIndex order, as ImageTileIntegrator::Render does.
+long long oracle_render(const OracleScene *s, int spp0, int spp1, int nthreads, double *rgbSum, double *wSum) {
+    SceneView sv(*s);
+    const int W = s->width, H = s->height, tile = 32;
+    const int ntx = (W + tile - 1) / tile, nty = (H + tile - 1) / tile;
+    std::atomic<int> next{0};
+    std::atomic<long long> events{0};
+    auto worker = [&]() {
+        long long ev = 0;
+        while (true) {
+            int t = next.fetch_add(1);
+            if (t >= ntx * nty) break;
+            int tx = t % ntx, ty = t / ntx;
+            for (int py = ty * tile; py < std::min(H, (ty + 1) * tile); ++py)
+                for (int px = tx * tile; px < std::min(W, (tx + 1) * tile); ++px)
+                    for (int si = spp0; si < spp1; ++si) {
+                        int ne = 0;
+                        SampleResult r = EvaluatePixelSample(sv, px, py, si, &ne);
+                        ev += ne;
+                        size_t pi = (size_t)py * W + px;
+                        AddSample(*s, rgbSum + 3 * pi, wSum + pi, r.L, r.l, 1.f);
+                    }
+        }
+        events += ev;
+    };
+    if (nthreads <= 1) worker();
+    else {
+        std::vector<std::thread> th;
+        for (int i = 0; i < nthreads; ++i) th.emplace_back(worker);
+        for (auto &t : th) t.join();
+    }
+    return events.load();
+}
+
+// Same, for an explicit pixel list (the bounded CPU-baseline sample of bench.py):
+// pixels[i] = linear pixel index; film sums written per list entry.
+long long oracle_render_list(const OracleScene *s, const int *pixels, int n, int spp0, int spp1, int nthreads,
+                             double *rgbSum, double *wSum) {
+    SceneView sv(*s);
+    std::atomic<int> next{0};
+    std::atomic<long long> events{0};
+    auto worker = [&]() {
+        long long ev = 0;
+        while (true) {
+            int i = next.fetch_add(1);
+            if (i >= n) break;
+            int px = pixels[i] % s->width, py = pixels[i] / s->width;
+            for (int si = spp0; si < spp1; ++si) {
+                int ne = 0;
+                SampleResult r = EvaluatePixelSample(sv, px, py, si, &ne);
+                ev += ne;
+                AddSample(*s, rgbSum + 3 * (size_t)i, wSum + i, r.L, r.l, 1.f);
+            }
+        }
+        events += ev;
+    };
+    if (nthreads <= 1) worker();
+    else {
+        std::vector<std::thread> th;
+        for (int i = 0; i < nthreads; ++i) th.emplace_back(worker);
+        for (auto &t : th) t.join();
+    }
+    return events.load();
+}
+
+// RGBFilm::GetPixelRGB — film.h:258-274 (no splats).
+void oracle_film_resolve(const OracleScene *s, const double *rgbSum, const double *wSum, float *rgbOut) {
+    const size_t n = (size_t)s->width * s->height;
+    for (size_t i = 0; i < n; ++i) {
+        float rgb[3] = {(float)rgbSum[3 * i], (float)rgbSum[3 * i + 1], (float)rgbSum[3 * i + 2]};
+        float w = (float)wSum[i];
+        if (w != 0) for (int c = 0; c < 3; ++c) rgb[c] /= w;
+        const float *m = s->output_from_sensor;
+        for (int r = 0; r < 3; ++r) rgbOut[3 * i + r] = m[3 * r] * rgb[0] + m[3 * r + 1] * rgb[1] + m[3 * r + 2] * rgb[2];
+    }
+}
+
+// Integrator::Tr (integrators.cpp:324-374): ratio-tracking transmittance between
+// medium points p0 -> p1 (no surfaces inside the interface box), n segments; writes Tr[0].
+// Used for the analytic Beer-Lambert known-answer tests.
+void oracle_transmittance(const OracleScene *s, int n, const float *p0, const float *p1, float lambda_u, float *trOut) {
+    SceneView sv(*s);
+    Lambda l = SampleVisible(lambda_u);
+    for (int i = 0; i < n; ++i) {
+        V3 a = {p0[3 * i], p0[3 * i + 1], p0[3 * i + 2]}, b = {p1[3 * i], p1[3 * i + 1], p1[3 * i + 2]};
+        RNG rng(HashBytes(&a, 12), HashBytes(&b, 12));
+        Ray ray = {a, b - a};  // SpawnRayTo from a medium interaction (ray.h:103-108)
+        Spec Tr = Spec::Const(1.f), inv_w = Spec::Const(1.f);
+        if (LengthSquared(ray.d) == 0) { trOut[i] = 1.f; continue; }
+        V3 pExit = ray.o + ray.d * (1 - ShadowEpsilon);
+        ray.d = pExit - ray.o;
+        float u = rng.Uniform();
+        Spec T_maj = SampleT_maj(sv, ray, 1.f, u, rng, l,
+            [&](V3, const MediumProps &mp, Spec sigma_maj, Spec Tm) {
+                Spec sigma_n = ClampZero(sigma_maj - mp.sigma_a - mp.sigma_s);
+                float pr = Tm[0] * sigma_maj[0];
+                Tr = Tr * (Tm * sigma_n / pr);
+                inv_w = inv_w * (Tm * sigma_maj / pr);
+                if (!Tr || !inv_w) return false;
+                return true;
+            });
+        Tr = Tr * (T_maj / T_maj[0]);
+        inv_w = inv_w * (T_maj / T_maj[0]);
+        trOut[i] = (Tr / inv_w.Average())[0];
+    }
+}
+
+// Majorant DDA segments of one ray (for tests): returns count, writes (tMin, tMax, sigma_maj[0]).
+int oracle_dda_segments(const OracleScene *s, const float *o, const float *d, float tMax, float lambda_u, int maxSegs,
+                        float *out) {
+    SceneView sv(*s);
+    Lambda l = SampleVisible(lambda_u);
+    Ray ray = {{o[0], o[1], o[2]}, {d[0], d[1], d[2]}};
+    tMax *= Length(ray.d);
+    ray.d = Normalize(ray.d);
+    DDA it = SampleRay(sv, ray, tMax, l);
+    int n = 0;
+    float a, b; Spec sm;
+    while (n < maxSegs && it.Next(&a, &b, &sm)) { out[3 * n] = a; out[3 * n + 1] = b; out[3 * n + 2] = sm[0]; ++n; }
+    return n;
+}
+
+// ---- primitive exports pinned by tests/golden/ref_vectors.json ------------
+void oracle_rng(uint64_t seq, uint64_t seed, int n, uint32_t *u32, int64_t advance, uint32_t *after, int nAfter) {
+    RNG r(seq, seed);
+    for (int i = 0; i < n; ++i) u32[i] = r.U32();
+    r.Advance(advance);
+    for (int i = 0; i < nAfter; ++i) after[i] = r.U32();
+}
+void oracle_rng_uniform(uint64_t seq, uint64_t seed, int skip, int n, float *out) {
+    RNG r(seq, seed);
+    for (int i = 0; i < skip; ++i) r.U32();
+    for (int i = 0; i < n; ++i) out[i] = r.Uniform();
+}
+void oracle_rng_single(uint64_t seq, int n, uint32_t *out) {
+    RNG r; r.SetSequence(seq);
+    for (int i = 0; i < n; ++i) out[i] = r.U32();
+}
+uint64_t oracle_hash_float(float f) { return HashFloat(f); }
+uint64_t oracle_hash_pixel_seed(int x, int y, int seed) { return HashPixelSeed(x, y, seed); }
+uint64_t oracle_hash_point3f(float x, float y, float z) { float b[3] = {x, y, z}; return HashBytes(b, 12); }
+uint64_t oracle_mixbits(uint64_t v) { return MixBits(v); }
+float oracle_fastexp(float x) { return FastExp(x); }
+float oracle_sample_exponential(float u, float a) { return SampleExponential(u, a); }
+int oracle_sample_discrete3(const float *w, float u) { return SampleDiscrete3(w, u); }
+void oracle_sample_visible(float u, float *lambda, float *pdf) {
+    Lambda l = SampleVisible(u);
+    for (int i = 0; i < NS; ++i) { lambda[i] = l.lambda[i]; pdf[i] = l.pdf[i]; }
+}
+float oracle_hg_eval(float c, float g) { return HenyeyGreenstein(c, g); }
+void oracle_hg_sample(const float *wo, float g, float u0, float u1, float *wi, float *pdf) {
+    V3 w = SampleHenyeyGreenstein(V3{wo[0], wo[1], wo[2]}, g, u0, u1, pdf);
+    wi[0] = w.x; wi[1] = w.y; wi[2] = w.z;
+}
+float oracle_grid_lookup(const float *v, int nx, int ny, int nz, float x, float y, float z) {
+    Grid g{v, nx, ny, nz}; return g.Lookup(V3{x, y, z});
+}
+float oracle_grid_maxvalue(const float *v, int nx, int ny, int nz, const float *b6) {
+    Grid g{v, nx, ny, nz};
+    return g.MaxValue(Bounds{{b6[0], b6[1], b6[2]}, {b6[3], b6[4], b6[5]}});
+}
+int oracle_intersectp(const float *b6, const float *o, const float *d, float tMax, float *t01) {
+    Bounds b{{b6[0], b6[1], b6[2]}, {b6[3], b6[4], b6[5]}};
+    return IntersectP(b, V3{o[0], o[1], o[2]}, V3{d[0], d[1], d[2]}, tMax, &t01[0], &t01[1]) ? 1 : 0;
+}
+void oracle_transform_ray(const float *m16, const float *minv16, const float *o, const float *d, int inverse,
+                          float *out7) {
+    Xform t;
+    for (int i = 0; i < 16; ++i) { t.m[i / 4][i % 4] = m16[i]; t.mInv[i / 4][i % 4] = minv16[i]; }
+    float tMax = 10.f;
+    Ray r = XRay(t, Ray{{o[0], o[1], o[2]}, {d[0], d[1], d[2]}}, &tMax, inverse != 0);
+    out7[0] = r.o.x; out7[1] = r.o.y; out7[2] = r.o.z; out7[3] = r.d.x; out7[4] = r.d.y; out7[5] = r.d.z;
+    out7[6] = tMax;
+}
+void oracle_independent_sampler(int px, int py, int sampleIndex, int seed, int dim0, int n, float *out) {
+    RNG r;
+    r.SetSequence(HashPixelSeed(px, py, seed));
+    r.Advance((int64_t)(sampleIndex * 65536ull + dim0));
+    for (int i = 0; i < n; ++i) out[i] = r.Uniform();
+}
+float oracle_noise(float x, float y, float z, float *dnoise3) {
+    V3 dn = DNoise(V3{x, y, z});
+    dnoise3[0] = dn.x; dnoise3[1] = dn.y; dnoise3[2] = dn.z;
+    return Noise(x, y, z);
+}
+float oracle_blackbody(float lambda, float T) { return Blackbody(lambda, T); }
+float oracle_cloud_density(float x, float y, float z, float density, float wispiness, float frequency) {
+    return CloudDensity(V3{x, y, z}, density, wispiness, frequency);
+}
+// Fill an n^3 grid with CloudMedium::Density at voxel centres (i+0.5)/n (BASELINE.md S-cloud).
+void oracle_cloud_grid(int n, int z0, int z1, float *out) {
+    for (int z = z0; z < z1; ++z)
+        for (int y = 0; y < n; ++y)
+            for (int x = 0; x < n; ++x)
+                out[((size_t)(z - z0) * n + y) * n + x] =
+                    CloudDensity(V3{(x + 0.5f) / n, (y + 0.5f) / n, (z + 0.5f) / n}, 1.f, 1.f, 5.f);
+}
+
+}  // extern "C"
