@@ -10,7 +10,8 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libavr_hip.so")
+# AVR_LIB overrides the library path (A/B experiments with variant builds); default in-tree.
+LIB_PATH = os.environ.get("AVR_LIB", os.path.join(_HERE, "libavr_hip.so"))
 
 c_float_p = ctypes.POINTER(ctypes.c_float)
 c_double_p = ctypes.POINTER(ctypes.c_double)
@@ -27,6 +28,8 @@ class AvrStats(ctypes.Structure):
         ("medium_dda_steps", ctypes.c_ulonglong),
         ("shadow_dda_steps", ctypes.c_ulonglong),
         ("medium_launches", ctypes.c_ulonglong),
+        ("loop_iterations", ctypes.c_ulonglong),
+        ("active_lane_iterations", ctypes.c_ulonglong),
         ("ms_camera", ctypes.c_double),
         ("ms_medium", ctypes.c_double),
         ("ms_shadow", ctypes.c_double),
@@ -44,6 +47,8 @@ SIGNATURES = {
     "avr_context_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_longlong, ctypes.POINTER(ctypes.c_void_p)]),
     "avr_context_destroy": (ctypes.c_int, [ctypes.c_void_p]),
     "avr_set_stream": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "avr_set_kernel_mode": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "avr_set_refill_min": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "avr_medium_grid": (ctypes.c_int, [ctypes.c_void_p, c_float_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                        c_float_p, c_float_p, c_float_p, c_float_p, c_float_p, ctypes.c_float,
                                        c_float_p, c_float_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_int_p]),
@@ -119,6 +124,13 @@ class Context:
             self.close()
         except Exception:
             pass
+
+    def set_kernel_mode(self, mode):
+        """0 = persistent megakernel (default), 1 = wavefront queues."""
+        _check(self.lib.avr_set_kernel_mode(self.h, int(mode)))
+
+    def set_refill_min(self, lanes):
+        _check(self.lib.avr_set_refill_min(self.h, int(lanes)))
 
     def set_stream(self, stream_ptr):
         _check(self.lib.avr_set_stream(self.h, ctypes.c_void_p(stream_ptr)))

@@ -51,6 +51,7 @@ struct avr_context {
     // lights / camera / film
     avr::DevLights lights{};
     float *d_lightL = nullptr;
+    avr::DevLight *d_lights = nullptr;
     avr::DevCamera cam{};
     bool has_camera = false;
     avr::DevFilm film{};
@@ -67,6 +68,13 @@ struct avr_context {
     avr_stats stats{};
     std::vector<hipEvent_t> evpool;
     int last_base = 0, last_S = 0;
+    int kernel_mode = 0;      // 0: persistent k_paths (default), 1: wavefront k_medium/k_shadow
+    int *d_heads = nullptr;   // 8 per-XCD work counters of k_paths
+    int paths_grid = 0;
+    int refill_min = 16;
+    uint64_t *d_advance = nullptr;  // per-pass PCG advance table {A, H}
+    long long advance_cap = 0;
+    std::vector<uint64_t> h_advance;
 };
 
 namespace {
@@ -183,7 +191,36 @@ int avr_context_create(int device, long long max_paths, avr_context **out) {
         delete c;
         return fail(AVR_ERR_HIP, "context allocation failed");
     }
+    if (dalloc(&c->d_heads, 8) != hipSuccess) {
+        delete c;
+        return fail(AVR_ERR_HIP, "context allocation failed");
+    }
+    {
+        hipDeviceProp_t prop;
+        int blocksPerCU = 0;
+        if (hipGetDeviceProperties(&prop, device) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocksPerCU, avr::k_paths<false>, 256, 0) != hipSuccess) {
+            delete c;
+            return fail(AVR_ERR_HIP, "occupancy query failed");
+        }
+        // persistent grid: every admitted block resident (MI355X_MICROARCH.md residency notes);
+        // one block per CU fewer than the API answer would also be safe, none is needed here
+        // because no block ever waits on another (work is pulled from counters).
+        c->paths_grid = prop.multiProcessorCount * std::max(1, blocksPerCU);
+    }
     *out = c;
+    return AVR_OK;
+}
+
+int avr_set_refill_min(avr_context *c, int lanes) {
+    if (!c || lanes < 1 || lanes > 64) return fail(AVR_ERR_ARG, "refill threshold must be 1..64 lanes");
+    c->refill_min = lanes;
+    return AVR_OK;
+}
+
+int avr_set_kernel_mode(avr_context *c, int mode) {
+    if (!c || (mode != 0 && mode != 1)) return fail(AVR_ERR_ARG, "kernel mode must be 0 (persistent) or 1 (wavefront)");
+    c->kernel_mode = mode;
     return AVR_OK;
 }
 
@@ -194,10 +231,13 @@ int avr_context_destroy(avr_context *c) {
     free_paths(c);
     float *fs[] = {c->d_density_owned, c->d_sigma_a, c->d_sigma_s, c->d_Le, c->d_lescale, c->d_majorant,
                    c->d_lightL, c->d_xyz};
+    if (c->d_lights) (void)hipFree(c->d_lights);
     for (auto p : fs) if (p) (void)hipFree(p);
     if (c->film.rgb_sum) (void)hipFree(c->film.rgb_sum);
     if (c->film.w_sum) (void)hipFree(c->film.w_sum);
     if (c->d_counts) (void)hipFree(c->d_counts);
+    if (c->d_heads) (void)hipFree(c->d_heads);
+    if (c->d_advance) (void)hipFree(c->d_advance);
     if (c->d_stats) (void)hipFree(c->d_stats);
     if (c->h_count) (void)hipHostFree(c->h_count);
     for (auto e : c->evpool) (void)hipEventDestroy(e);
@@ -263,15 +303,20 @@ int avr_lights(avr_context *c, int n, const int *types, const float *w3, const f
     HIP_TRY(hipSetDevice(c->device));
     int rc = upload_table(&c->d_lightL, n ? L : nullptr, (size_t)n * avr::kNTable, c->stream);
     if (rc) return rc;
-    c->lights = {};
-    c->lights.n = n;
+    avr::DevLight h[avr::kMaxLights] = {};
     for (int i = 0; i < n; ++i) {
         if (types[i] != 0 && types[i] != 1) return fail(AVR_ERR_ARG, "light type must be 0 (distant) or 1 (uniform infinite)");
-        c->lights.type[i] = types[i];
-        for (int k = 0; k < 3; ++k) c->lights.w[i][k] = w3[3 * i + k];
-        c->lights.L[i] = c->d_lightL + (size_t)i * avr::kNTable;
-        c->lights.scale[i] = scale[i];
+        h[i].type = types[i];
+        for (int k = 0; k < 3; ++k) h[i].w[k] = w3[3 * i + k];
+        h[i].L = c->d_lightL + (size_t)i * avr::kNTable;
+        h[i].scale = scale[i];
     }
+    if (!c->d_lights) HIP_TRY(dalloc(&c->d_lights, avr::kMaxLights));
+    HIP_TRY(hipMemcpyAsync(c->d_lights, h, sizeof(h), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    c->lights = {};
+    c->lights.n = n;
+    c->lights.list = c->d_lights;
     c->lights.scene_radius = scene_radius;
     return AVR_OK;
 }
@@ -354,6 +399,53 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
         p.sample_base = (int)base;
         p.stats = c->d_stats;
         const long long n0 = P * S;
+        if (c->kernel_mode == 0) {
+            // PCG32 Advance(s*65536) as an affine map state' = A*state + inc*H (rng.h:132-146:
+            // every step is linear in inc, so H = accPlus computed with inc = 1).
+            if (S > c->advance_cap) {
+                if (c->d_advance) (void)hipFree(c->d_advance);
+                HIP_TRY(dalloc(&c->d_advance, 2 * (size_t)S));
+                c->advance_cap = S;
+            }
+            c->h_advance.resize(2 * (size_t)S);
+            for (int s = 0; s < S; ++s) {
+                uint64_t delta = (uint64_t)(base + s) * 65536ull;
+                uint64_t curMult = 0x5851f42d4c957f2dULL, curPlus = 1, accMult = 1, accPlus = 0;
+                while (delta > 0) {
+                    if (delta & 1) { accMult *= curMult; accPlus = accPlus * curMult + curPlus; }
+                    curPlus = (curMult + 1) * curPlus;
+                    curMult *= curMult;
+                    delta /= 2;
+                }
+                c->h_advance[2 * s] = accMult;
+                c->h_advance[2 * s + 1] = accPlus;
+            }
+            HIP_TRY(hipMemcpyAsync(c->d_advance, c->h_advance.data(), 2 * (size_t)S * sizeof(uint64_t),
+                                   hipMemcpyHostToDevice, c->stream));
+            p.advance = c->d_advance;
+            p.refill_min = c->refill_min;
+            p.heads = c->d_heads;
+            HIP_TRY(hipMemsetAsync(c->d_heads, 0, 8 * sizeof(int), c->stream));
+            HIP_TRY(hipEventRecord(e0, c->stream));
+            if (c->med.emissive)
+                hipLaunchKernelGGL(avr::k_paths<true>, dim3(c->paths_grid), dim3(256), 0, c->stream, p);
+            else
+                hipLaunchKernelGGL(avr::k_paths<false>, dim3(c->paths_grid), dim3(256), 0, c->stream, p);
+            HIP_TRY(hipGetLastError());
+            HIP_TRY(hipEventRecord(e1, c->stream));
+            hipLaunchKernelGGL(avr::k_film, dim3(blocks_for(P)), dim3(256), 0, c->stream, p);
+            HIP_TRY(hipGetLastError());
+            HIP_TRY(hipEventRecord(e2, c->stream));
+            HIP_TRY(hipEventSynchronize(e2));
+            HIP_TRY(hipEventElapsedTime(&ms, e0, e1));
+            c->stats.ms_medium += ms;
+            c->stats.medium_launches++;
+            HIP_TRY(hipEventElapsedTime(&ms, e1, e2));
+            c->stats.ms_film += ms;
+            c->last_base = (int)base;
+            c->last_S = S;
+            continue;
+        }
         HIP_TRY(hipEventRecord(e0, c->stream));
         hipLaunchKernelGGL(avr::k_camera, dim3(blocks_for(n0)), dim3(256), 0, c->stream, p);
         HIP_TRY(hipGetLastError());
@@ -417,6 +509,8 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
     c->stats.shadow_items = h[4];
     c->stats.medium_dda_steps = h[5];
     c->stats.shadow_dda_steps = h[6];
+    c->stats.loop_iterations = c->kernel_mode == 0 ? h[6] : 0;
+    c->stats.active_lane_iterations = c->kernel_mode == 0 ? h[7] : 0;
     return AVR_OK;
 }
 

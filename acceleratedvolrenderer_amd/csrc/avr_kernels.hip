@@ -36,12 +36,15 @@ struct DevMedium {
 };
 
 constexpr int kMaxLights = 8;
+struct DevLight {
+    int type;                         // 0 distant (delta), 1 uniform infinite
+    float w[3];                       // render-space direction towards a distant light
+    float scale;
+    const float *L;                   // 471-entry table
+};
 struct DevLights {
     int n;
-    int type[kMaxLights];             // 0 distant (delta), 1 uniform infinite
-    float w[kMaxLights][3];
-    const float *L[kMaxLights];
-    float scale[kMaxLights];
+    const DevLight *list;             // device array (indexed by the sampled light)
     float scene_radius;
 };
 
@@ -73,7 +76,8 @@ struct ShadowSoA {
 
 // Per-launch work counters (u64): [0] lookups k_medium, [1] items in k_medium,
 // [2] items out k_medium (survivors + shadow pushes), [3] lookups k_shadow, [4] items k_shadow,
-// [5] DDA steps k_medium, [6] DDA steps k_shadow
+// [5] DDA steps k_medium, [6] DDA steps k_shadow; k_paths: [6] loop iterations (per wave),
+// [7] sum over iterations of active lanes (SIMD utilisation = [7] / (64 * [6]))
 constexpr int kNumStats = 8;
 
 struct Params {
@@ -94,6 +98,10 @@ struct Params {
     int *count_out;
     int *shadow_count;
     unsigned long long *stats;
+    int *heads;                       // k_paths: 8 per-XCD work counters (zeroed per pass)
+    const uint64_t *advance;          // k_paths: per pass sample s, {A, H}: Advance(sIdx*65536) ==
+                                      //   state' = A*state + inc*H (PCG32 advance is linear in inc)
+    int refill_min;                   // k_paths: refill a wave once this many lanes are idle
 };
 
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
@@ -140,7 +148,7 @@ struct MediumSample { Spec sigma_a, sigma_s, Le; };
 
 // GridMedium::SamplePoint — media.h:287-319 (no temperature grid); sig_a/sig_s pre-sampled at lambda
 __device__ __forceinline__ MediumSample sample_point(const DevMedium &m, V3 p, const Spec &sig_a, const Spec &sig_s,
-                                                     const Spec &Le_l) {
+                                                     const Spec &Le_l, bool emissive = true) {
     MediumSample ms;
     p = xf_point_pair(m.medium_from_render, p);
     p = box_offset(m.bmin, m.bmax, p);
@@ -148,19 +156,37 @@ __device__ __forceinline__ MediumSample sample_point(const DevMedium &m, V3 p, c
     ms.sigma_a = sig_a * d;
     ms.sigma_s = sig_s * d;
     ms.Le = Spec::c(0.f);
-    if (m.emissive) {
+    if (emissive && m.emissive) {
         float scale = grid_lookup(m.lescale, m.lnx, m.lny, m.lnz, p);
         if (scale > 0) ms.Le = Le_l * scale;
     }
     return ms;
 }
 
-// DDAMajorantIterator — media.h:136-214
+// DDAMajorantIterator — media.h:136-214. Per-axis state in named scalars (no arrays),
+// so the iterator lives in VGPRs: an indexed array here is demoted to scratch.
 struct Dda {
     float tMin, tMax;
-    float next[3], delta[3];
-    int step[3], limit[3], voxel[3];
+    float nx, ny, nz;      // nextCrossingT
+    float dx, dy, dz;      // deltaT
+    int vx, vy, vz;        // voxel
+    int sx, sy, sz;        // step (+1/-1); voxelLimit = step > 0 ? res : -1
 };
+__device__ __forceinline__ void dda_axis(float gia, float gda, int res, float tMin, int &voxel, float &next,
+                                         float &delta, int &step) {
+    voxel = (int)clampf(gia * res, 0.f, (float)(res - 1));
+    delta = 1 / (__builtin_fabsf(gda) * res);
+    if (gda == -0.f) gda = 0.f;
+    if (gda >= 0) {
+        float nextPos = float(voxel + 1) / res;
+        next = tMin + (nextPos - gia) / gda;
+        step = 1;
+    } else {
+        float nextPos = float(voxel) / res;
+        next = tMin + (nextPos - gia) / gda;
+        step = -1;
+    }
+}
 __device__ __forceinline__ bool dda_init(Dda &it, const DevMedium &m, Ray ray, float raytMax) {
     // GridMedium::SampleRay — media.h:322-337
     ray = xf_ray(m.medium_from_render, ray, &raytMax, /*forward=*/false);
@@ -170,51 +196,41 @@ __device__ __forceinline__ bool dda_init(Dda &it, const DevMedium &m, Ray ray, f
         return false;
     }
     it.tMin = tMin; it.tMax = tMax;
-    float diag[3] = {m.bmax[0] - m.bmin[0], m.bmax[1] - m.bmin[1], m.bmax[2] - m.bmin[2]};
+    const float diag0 = m.bmax[0] - m.bmin[0], diag1 = m.bmax[1] - m.bmin[1], diag2 = m.bmax[2] - m.bmin[2];
     V3 go = box_offset(m.bmin, m.bmax, ray.o);
-    V3 gd = {ray.d.x / diag[0], ray.d.y / diag[1], ray.d.z / diag[2]};
+    V3 gd = {ray.d.x / diag0, ray.d.y / diag1, ray.d.z / diag2};
     V3 gi = go + gd * tMin;
-    for (int a = 0; a < 3; ++a) {
-        const int res = m.mres[a];
-        const float gia = comp(gi, a);
-        float gda = comp(gd, a);
-        it.voxel[a] = (int)clampf(gia * res, 0.f, (float)(res - 1));
-        it.delta[a] = 1 / (__builtin_fabsf(gda) * res);
-        if (gda == -0.f) gda = 0.f;
-        if (gda >= 0) {
-            float nextPos = float(it.voxel[a] + 1) / res;
-            it.next[a] = tMin + (nextPos - gia) / gda;
-            it.step[a] = 1;
-            it.limit[a] = res;
-        } else {
-            float nextPos = float(it.voxel[a]) / res;
-            it.next[a] = tMin + (nextPos - gia) / gda;
-            it.step[a] = -1;
-            it.limit[a] = -1;
-        }
-    }
+    dda_axis(gi.x, gd.x, m.mres[0], tMin, it.vx, it.nx, it.dx, it.sx);
+    dda_axis(gi.y, gd.y, m.mres[1], tMin, it.vy, it.ny, it.dy, it.sy);
+    dda_axis(gi.z, gd.z, m.mres[2], tMin, it.vz, it.nz, it.dz, it.sz);
     return true;
 }
 // Returns false when exhausted; majorant values read through `maj` (LDS-staged when it fits)
-__device__ __forceinline__ bool dda_next(Dda &it, const float *maj, int rx, int ry, float *s0, float *s1, float *mval) {
+__device__ __forceinline__ bool dda_next(Dda &it, const float *maj, const int *res, float *s0, float *s1, float *mval) {
     if (it.tMin >= it.tMax) return false;
-    int bits = ((it.next[0] < it.next[1]) << 2) + ((it.next[0] < it.next[2]) << 1) + ((it.next[1] < it.next[2]));
+    const int bits = ((it.nx < it.ny) << 2) + ((it.nx < it.nz) << 1) + ((it.ny < it.nz));
     // cmpToAxis = {2, 1, 2, 1, 2, 2, 0, 0}
-    int ax = (bits >= 6) ? 0 : ((bits == 1 || bits == 3) ? 1 : 2);
-    float nextA = ax == 0 ? it.next[0] : (ax == 1 ? it.next[1] : it.next[2]);
-    float tExit = fminf_(it.tMax, nextA);
-    *mval = maj[it.voxel[0] + rx * (it.voxel[1] + ry * it.voxel[2])];
+    const int ax = (bits >= 6) ? 0 : ((bits == 1 || bits == 3) ? 1 : 2);
+    const float nextA = ax == 0 ? it.nx : (ax == 1 ? it.ny : it.nz);
+    const float tExit = fminf_(it.tMax, nextA);
+    *mval = maj[it.vx + res[0] * (it.vy + res[1] * it.vz)];
     *s0 = it.tMin;
     *s1 = tExit;
     it.tMin = tExit;
     if (nextA > it.tMax) it.tMin = it.tMax;
-    int vox = (ax == 0 ? it.voxel[0] : (ax == 1 ? it.voxel[1] : it.voxel[2])) + (ax == 0 ? it.step[0] : (ax == 1 ? it.step[1] : it.step[2]));
-    int lim = ax == 0 ? it.limit[0] : (ax == 1 ? it.limit[1] : it.limit[2]);
-    if (vox == lim) it.tMin = it.tMax;
-    float dl = ax == 0 ? it.delta[0] : (ax == 1 ? it.delta[1] : it.delta[2]);
-    if (ax == 0) { it.voxel[0] = vox; it.next[0] += dl; }
-    else if (ax == 1) { it.voxel[1] = vox; it.next[1] += dl; }
-    else { it.voxel[2] = vox; it.next[2] += dl; }
+    if (ax == 0) {
+        it.vx += it.sx;
+        if (it.vx == (it.sx > 0 ? res[0] : -1)) it.tMin = it.tMax;
+        it.nx += it.dx;
+    } else if (ax == 1) {
+        it.vy += it.sy;
+        if (it.vy == (it.sy > 0 ? res[1] : -1)) it.tMin = it.tMax;
+        it.ny += it.dy;
+    } else {
+        it.vz += it.sz;
+        if (it.vz == (it.sz > 0 ? res[2] : -1)) it.tMin = it.tMax;
+        it.nz += it.dz;
+    }
     return true;
 }
 
@@ -231,7 +247,7 @@ __device__ __forceinline__ Spec sample_t_maj(const DevMedium &m, const float *ma
     Spec T_maj = Spec::c(1.f);
     while (true) {
         float segMin, segMax, mv;
-        if (!dda_next(it, maj, m.mres[0], m.mres[1], &segMin, &segMax, &mv)) return T_maj;
+        if (!dda_next(it, maj, m.mres, &segMin, &segMax, &mv)) return T_maj;
         ++nSteps;
         const Spec sigma_maj = sigma_t * mv;
         if (sigma_maj.v0 == 0) {
@@ -424,10 +440,11 @@ __global__ void __launch_bounds__(256) k_medium(Params P) {
                         int idx = (int)(uu * nl);
                         idx = idx < nl - 1 ? idx : nl - 1;
                         float pmf = pInf / nl;
-                        if (P.lights.type[idx] == 0) {
-                            const V3 wi = {P.lights.w[idx][0], P.lights.w[idx][1], P.lights.w[idx][2]};
+                        const DevLight &lt = P.lights.list[idx];
+                        if (lt.type == 0) {
+                            const V3 wi = {lt.w[0], lt.w[1], lt.w[2]};
                             const V3 pOut = pScatter + wi * (2 * P.lights.scene_radius);
-                            const Spec Ls = sample_table(P.lights.L[idx], li) * P.lights.scale[idx];
+                            const Spec Ls = sample_table(lt.L, li) * lt.scale;
                             if (Ls.nonzero()) {
                                 const float p_l = pmf * 1.f;
                                 const float fval = hg_eval(dot(wo, wi), P.med.g);
@@ -465,8 +482,9 @@ __global__ void __launch_bounds__(256) k_medium(Params P) {
                 r_l = r_l * (T_maj / T_maj.v0);
                 // escaped: infinite lights (integrators.cpp:1090-1107)
                 for (int k = 0; k < P.lights.n; ++k) {
-                    if (P.lights.type[k] != 1) continue;
-                    const Spec Le = sample_table(P.lights.L[k], li) * P.lights.scale[k];
+                    const DevLight &lt = P.lights.list[k];
+                    if (lt.type != 1) continue;
+                    const Spec Le = sample_table(lt.L, li) * lt.scale;
                     if (!Le.nonzero()) continue;
                     if (depth == 0) L = L + beta * Le / r_u.avg();
                     else {
@@ -560,6 +578,389 @@ __global__ void __launch_bounds__(256) k_shadow(Params P) {
 }
 
 // ---------------------------------------------------------------------------
+// k_paths — persistent-wave megakernel (the default path).
+//
+// The same VolPath estimator as k_camera + k_medium + k_shadow, restructured for CDNA4:
+// every lane keeps its whole path state in VGPRs and runs a flat state machine
+// {fetch, medium segment, shadow segment}; one loop iteration advances each lane to its
+// next tentative collision (majorant DDA in LDS), does the density fetch for all lanes
+// that reached one together, and applies that lane's event. Lanes whose path ended are
+// refilled from the pass's sample range with one atomic per wave (__ballot/__popcll/
+// mbcnt prefix) on per-XCD work counters, so waves stay full until the pass drains and no
+// per-bounce state goes through HBM. Per-sample L and lambda are written at path end and
+// k_film adds them to the film in sampleIndex order (deterministic, as before).
+// Float operation order per path is identical to the wavefront kernels and to the CPU
+// oracle (cpu/integrators.cpp:962-1399, media.h:741-806).
+enum : int { M_FETCH = 0, M_MEDIUM = 1, M_SHADOW = 2, M_DONE = 3 };
+
+__device__ __forceinline__ int xcc_id() {
+    unsigned v;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(v));
+    return (int)(v & 7);
+}
+
+// Start SampleT_maj (media.h:744-749): normalise, transform to medium space, clip, DDA.
+__device__ __forceinline__ void seg_begin(const DevMedium &m, V3 o, V3 d, float tMax, V3 &sd, Dda &it,
+                                          Spec &T_maj, bool &needNext) {
+    tMax *= length(d);
+    d = normalize(d);
+    sd = d;
+    dda_init(it, m, Ray{o, d}, tMax);
+    T_maj = Spec::c(1.f);
+    needNext = true;
+}
+
+#ifndef AVR_PATHS_MIN_WAVES
+#define AVR_PATHS_MIN_WAVES 1
+#endif
+template <bool kEmissive>
+__global__ void __launch_bounds__(256, AVR_PATHS_MIN_WAVES) k_paths(Params P) {
+    // LDS: majorant grid (16 KiB at pbrt's 16^3) + the 471-entry spectral tables the path
+    // samples at path start, NEE and escape (sigma_a, sigma_s, up to 4 light spectra).
+    __shared__ float s_maj[4096];
+    __shared__ float s_tab[(2 + 4) * kNTable];
+    const float *maj = stage_majorant(P.med, s_maj);
+    const int nlds = P.lights.n < 4 ? P.lights.n : 4;
+    for (int i = threadIdx.x; i < kNTable; i += blockDim.x) {
+        s_tab[i] = P.med.sigma_a[i];
+        s_tab[kNTable + i] = P.med.sigma_s[i];
+        for (int k = 0; k < nlds; ++k) s_tab[(2 + k) * kNTable + i] = P.lights.list[k].L[i];
+    }
+    __syncthreads();
+    const float *tab_sa = s_tab, *tab_ss = s_tab + kNTable;
+    auto light_table = [&](int k) -> const float * {
+        return k < 4 ? s_tab + (2 + k) * kNTable : P.lights.list[k].L;
+    };
+    const DevMedium &m = P.med;
+    const int npix = P.pass_pixels;
+    const long long N = (long long)npix * P.pass_samples;
+    const int lane = lane_id();
+    const int xcc = xcc_id();
+    unsigned long long nLookup = 0, nSteps = 0, nPaths = 0, nShadow = 0, nShadowLookup = 0;
+    unsigned long long nIter = 0, nActive = 0;
+
+    int mode = M_FETCH;
+    int g = 0;
+    // path state (Li, integrators.cpp:966-971)
+    Spec L{}, beta{}, r_u{}, r_l{}, lam{}, sig_a{}, sig_s{}, Le_l{};
+    Sampler smp{};
+    int depth = 0;
+    V3 po{}, pd{};
+    // segment state (SampleT_maj)
+    Pcg32 rng{};
+    float u = 0, tMin = 0, segMax = 0, mv = 0;
+    Dda it{};
+    V3 sd{};               // normalised segment direction; the segment origin is always po
+    Spec T_maj{};
+    bool needNext = true;
+    // shadow state (SampleLd, integrators.cpp:1339-1391)
+    int light = 0;
+    Spec T_ray{}, sr_l{}, sr_u{};
+
+    while (true) {
+        // ---- refill idle lanes: one atomic per wave on a per-XCD head -------------------
+        const uint64_t needMask = __ballot(mode == M_FETCH);
+        const uint64_t busyMask = __ballot(mode == M_MEDIUM || mode == M_SHADOW);
+        if (needMask && (busyMask == 0 || __popcll(needMask) >= P.refill_min)) {
+            const int cnt = __popcll(needMask);
+            const int leader = __ffsll((long long)needMask) - 1;
+            long long base = 0;
+            int granted = 0, exhausted = 0;
+            if (lane == leader) {
+                exhausted = 1;
+                for (int j = 0; j < 8; ++j) {
+                    const int c = (xcc + j) & 7;
+                    const long long lo = N * c / 8, hi = N * (c + 1) / 8;
+                    if (lo >= hi) continue;
+                    const int old = atomicAdd(P.heads + c, cnt);
+                    if (lo + old < hi) {
+                        base = lo + old;
+                        granted = (int)((hi - base) < cnt ? (hi - base) : cnt);
+                        exhausted = 0;
+                        break;
+                    }
+                }
+            }
+            base = __shfl(base, leader);
+            granted = __shfl(granted, leader);
+            exhausted = __shfl(exhausted, leader);
+            if (mode == M_FETCH) {
+                const uint64_t lt = lane == 0 ? 0ull : (needMask & ((~0ull) >> (64 - lane)));
+                const int k = __popcll(lt);
+                if (k < granted) {
+                    g = (int)(base + k);
+                    ++nPaths;
+                    // ---- camera ray (EvaluatePixelSample, integrators.cpp:235-268) ----
+                    const int pix = g % npix, sIdx = g / npix;
+                    const int px = pix % P.film.width, py = pix / P.film.width;
+                    const uint64_t seq = hash_3u32((uint32_t)px, (uint32_t)py, (uint32_t)P.seed);
+                    smp.rng.set_sequence(seq, mix_bits(seq));
+                    // == smp.rng.advance((sample_base + sIdx) * 65536) (rng.h:132-146), precomputed
+                    smp.rng.state = P.advance[2 * sIdx] * smp.rng.state + smp.rng.inc * P.advance[2 * sIdx + 1];
+                    const Lambda lw = sample_visible(smp.get1d());
+                    lam = lw.l;
+                    const float fu0 = smp.get1d(), fu1 = smp.get1d();
+                    const float fpx = lerp(fu0, -P.film.filter_rx, P.film.filter_rx);
+                    const float fpy = lerp(fu1, -P.film.filter_ry, P.film.filter_ry);
+                    const float pFilmX = ((float)px + fpx) + 0.5f, pFilmY = ((float)py + fpy) + 0.5f;
+                    smp.get1d();
+                    smp.get1d(); smp.get1d();
+                    const float *r = P.cam.raster;
+                    V3 pCam = {r[0] * pFilmX + r[1] * pFilmY + r[2] * 0.f + r[3],
+                               r[4] * pFilmX + r[5] * pFilmY + r[6] * 0.f + r[7],
+                               r[8] * pFilmX + r[9] * pFilmY + r[10] * 0.f + r[11]};
+                    const float wp = r[12] * pFilmX + r[13] * pFilmY + r[14] * 0.f + r[15];
+                    if (wp != 1) pCam = pCam / wp;
+                    Ray ray;
+                    if (P.cam.type == 0) ray = {pCam, {0.f, 0.f, 1.f}};
+                    else ray = {{0.f, 0.f, 0.f}, normalize(pCam)};
+                    ray = xf_ray(P.cam.render_from_camera, ray, nullptr, /*forward=*/true);
+                    po = ray.o;
+                    pd = ray.d;
+                    L = Spec::c(0.f);
+                    beta = r_u = r_l = Spec::c(1.f);
+                    depth = 0;
+                    {
+                        const LambdaIdx li = lambda_index(lam);
+                        sig_a = sample_table(tab_sa, li);
+                        sig_s = sample_table(tab_ss, li);
+                        if (kEmissive) Le_l = sample_table(m.Le, li);
+                    }
+                    mode = M_MEDIUM;
+                } else if (exhausted) {
+                    mode = M_DONE;
+                }
+                if (mode == M_MEDIUM) {
+                    // new medium segment: RNG from two sampler dims, u from a third (1001-1010)
+                    const float h0 = smp.get1d();
+                    const float h1 = smp.get1d();
+                    rng.set_sequence(hash_u32(f2u(h0)), hash_u32(f2u(h1)));
+                    u = smp.get1d();
+                    seg_begin(m, po, pd, kInf, sd, it, T_maj, needNext);
+                }
+            }
+        }
+        const uint64_t liveMask = __ballot(mode != M_DONE);
+        if (liveMask == 0) break;
+        if (lane == 0) {
+            ++nIter;
+            nActive += __popcll(__ballot(mode == M_MEDIUM || mode == M_SHADOW));
+        } else {
+            (void)__ballot(mode == M_MEDIUM || mode == M_SHADOW);
+        }
+
+        // ---- advance to the next tentative collision (media.h:754-802) -----------------
+        bool collide = false, segEnd = false;
+        float t = 0;
+        if (mode == M_MEDIUM || mode == M_SHADOW) {
+            while (true) {
+                if (needNext) {
+                    float s0, s1;
+                    if (!dda_next(it, maj, m.mres, &s0, &s1, &mv)) { segEnd = true; break; }
+                    ++nSteps;
+                    const Spec sigma_maj = (sig_a + sig_s) * mv;
+                    if (sigma_maj.v0 == 0) {
+                        float dt = s1 - s0;
+                        if (__builtin_isinf(dt)) dt = kFloatMax;
+                        T_maj = T_maj * fast_exp(-(sigma_maj * dt));
+                        continue;
+                    }
+                    tMin = s0;
+                    segMax = s1;
+                    needNext = false;
+                }
+                const float sm0 = (sig_a.v0 + sig_s.v0) * mv;
+                t = tMin + sample_exponential(u, sm0);
+                u = rng.uniform();
+                if (t < segMax) { collide = true; break; }
+                float dt = segMax - tMin;
+                if (__builtin_isinf(dt)) dt = kFloatMax;
+                T_maj = T_maj * fast_exp(-(((sig_a + sig_s) * mv) * dt));
+                needNext = true;
+            }
+        }
+
+        // ---- collision: density fetch for every lane that reached one ------------------
+        bool stop = false, scattered = false;
+        V3 pc{};
+        if (collide) {
+            const Spec sigma_maj = (sig_a + sig_s) * mv;
+            T_maj = T_maj * fast_exp(-(sigma_maj * (t - tMin)));
+            pc = po + sd * t;
+            const MediumSample ms = sample_point(m, pc, sig_a, sig_s, kEmissive ? Le_l : Spec::c(0.f), kEmissive);
+            if (mode == M_MEDIUM) {
+                ++nLookup;
+                // delta-tracking callback (integrators.cpp:990-1077)
+                if (!beta.nonzero()) {
+                    stop = true;
+                } else {
+                    if (kEmissive && depth < P.max_depth && ms.Le.nonzero()) {
+                        float pdf = sigma_maj.v0 * T_maj.v0;
+                        Spec betap = beta * T_maj / pdf;
+                        Spec r_e = r_u * sigma_maj * T_maj / pdf;
+                        if (r_e.nonzero()) L = L + betap * ms.sigma_a * ms.Le / r_e.avg();
+                    }
+                    const float pAbsorb = ms.sigma_a.v0 / sigma_maj.v0;
+                    const float pScat = ms.sigma_s.v0 / sigma_maj.v0;
+                    const float pNull = fmaxf_(0.f, 1 - pAbsorb - pScat);
+                    const int ev = sample_discrete3(pAbsorb, pScat, pNull, rng.uniform());
+                    if (ev == 0) {
+                        stop = true;
+                    } else if (ev == 1) {
+                        stop = true;
+                        if (depth++ < P.max_depth) {
+                            const float pdf = T_maj.v0 * ms.sigma_s.v0;
+                            beta = beta * (T_maj * ms.sigma_s / pdf);
+                            r_u = r_u * (T_maj * ms.sigma_s / pdf);
+                            scattered = beta.nonzero() && r_u.nonzero();
+                        }
+                    } else {
+                        const Spec sigma_n = clamp_zero(sigma_maj - ms.sigma_a - ms.sigma_s);
+                        const float pdf = T_maj.v0 * sigma_n.v0;
+                        beta = beta * (T_maj * sigma_n / pdf);
+                        if (pdf == 0) beta = Spec::c(0.f);
+                        r_u = r_u * (T_maj * sigma_n / pdf);
+                        r_l = r_l * (T_maj * sigma_maj / pdf);
+                        stop = !(beta.nonzero() && r_u.nonzero());
+                    }
+                }
+            } else {
+                ++nShadowLookup;
+                // ratio-tracking callback with Russian roulette (integrators.cpp:1351-1378)
+                const Spec sigma_n = clamp_zero(sigma_maj - ms.sigma_a - ms.sigma_s);
+                const float pdf = T_maj.v0 * sigma_maj.v0;
+                T_ray = T_ray * (T_maj * sigma_n / pdf);
+                sr_l = sr_l * (T_maj * sigma_maj / pdf);
+                sr_u = sr_u * (T_maj * sigma_n / pdf);
+                const Spec Tr = T_ray / (sr_l + sr_u).avg();
+                if (Tr.maxc() < 0.05f) {
+                    if (rng.uniform() < 0.75f) T_ray = Spec::c(0.f);
+                    else T_ray = T_ray / (1 - 0.75f);
+                }
+                stop = !T_ray.nonzero();
+            }
+            if (!stop) {
+                T_maj = Spec::c(1.f);
+                tMin = t;
+            }
+        }
+
+        // ---- events --------------------------------------------------------------------
+        bool pathEnd = false, phase = false;
+        if (mode == M_MEDIUM && (stop || segEnd)) {
+            if (scattered) {
+                // SampleLd: light pick (BVH infinite branch) and shadow-ray spawn (1282-1338)
+                const V3 wo = -pd;
+                const float ul = smp.get1d();
+                smp.get1d(); smp.get1d();
+                bool spawned = false;
+                const int nl = P.lights.n;
+                if (nl > 0) {
+                    const float pInf = float(nl) / float(nl + 0);
+                    if (ul < pInf) {
+                        int idx = (int)(ul / pInf * nl);
+                        idx = idx < nl - 1 ? idx : nl - 1;
+                        const DevLight &lt = P.lights.list[idx];
+                        if (lt.type == 0) {
+                            const V3 wi = {lt.w[0], lt.w[1], lt.w[2]};
+                            const Spec Ls = sample_table(light_table(idx), lambda_index(lam)) * lt.scale;
+                            if (Ls.nonzero() && hg_eval(dot(wo, wi), m.g) != 0) {
+                                const V3 pOut = pc + wi * (2 * P.lights.scene_radius);
+                                const V3 d = pOut - pc;
+                                light = idx;
+                                T_ray = sr_l = sr_u = Spec::c(1.f);
+                                rng.set_sequence(hash_3u32(f2u(pc.x), f2u(pc.y), f2u(pc.z)),
+                                                 hash_3u32(f2u(d.x), f2u(d.y), f2u(d.z)));
+                                u = rng.uniform();
+                                seg_begin(m, pc, d, 1 - kShadowEpsilon, sd, it, T_maj, needNext);
+                                po = pc;
+                                mode = M_SHADOW;
+                                spawned = true;
+                                ++nShadow;
+                            }
+                        }
+                    }
+                }
+                if (!spawned) {
+                    L = L + Spec::c(0.f);
+                    po = pc;
+                    phase = true;
+                }
+            } else if (stop) {
+                pathEnd = true;   // absorbed / terminated / beta or r_u vanished
+            } else {
+                // escaped (integrators.cpp:1078-1107)
+                beta = beta * (T_maj / T_maj.v0);
+                r_u = r_u * (T_maj / T_maj.v0);
+                r_l = r_l * (T_maj / T_maj.v0);
+                for (int k = 0; k < P.lights.n; ++k) {
+                    const DevLight &lt = P.lights.list[k];
+                    if (lt.type != 1) continue;
+                    const Spec Le = sample_table(light_table(k), lambda_index(lam)) * lt.scale;
+                    if (!Le.nonzero()) continue;
+                    if (depth == 0) L = L + beta * Le / r_u.avg();
+                    else {
+                        r_l = r_l * ((1.f / (P.lights.n + 0)) * 0.f);
+                        L = L + beta * Le / (r_u + r_l).avg();
+                    }
+                }
+                pathEnd = true;
+            }
+        } else if (mode == M_SHADOW && (stop || segEnd)) {
+            // finish SampleLd (1379-1398); SampleT_maj returns 1 when the callback stopped
+            const Spec Tm = stop ? Spec::c(1.f) : T_maj;
+            T_ray = T_ray * (Tm / Tm.v0);
+            sr_l = sr_l * (Tm / Tm.v0);
+            sr_u = sr_u * (Tm / Tm.v0);
+            Spec contrib = Spec::c(0.f);
+            if (T_ray.nonzero()) {
+                const DevLight &lt = P.lights.list[light];
+                const V3 wi = {lt.w[0], lt.w[1], lt.w[2]};
+                const float pInf = float(P.lights.n) / float(P.lights.n + 0);
+                const float p_l = pInf / P.lights.n * 1.f;
+                const Spec f_hat = Spec::c(hg_eval(dot(-pd, wi), m.g));
+                const Spec Ls = sample_table(light_table(light), lambda_index(lam)) * lt.scale;
+                sr_l = sr_l * (r_u * p_l);
+                contrib = beta * f_hat * T_ray * Ls / sr_l.avg();
+            }
+            L = L + contrib;
+            phase = true;
+        }
+        if (phase) {
+            // phase-function sampling (integrators.cpp:1046-1061), then the next segment
+            const float up0 = smp.get1d(), up1 = smp.get1d();
+            float phPdf;
+            const V3 wi = hg_sample(-pd, m.g, up0, up1, &phPdf);
+            if (phPdf == 0) {
+                pathEnd = true;
+            } else {
+                beta = beta * (phPdf / phPdf);
+                r_l = r_u / phPdf;
+                pd = wi;
+                const float h0 = smp.get1d();
+                const float h1 = smp.get1d();
+                rng.set_sequence(hash_u32(f2u(h0)), hash_u32(f2u(h1)));
+                u = smp.get1d();
+                seg_begin(m, po, pd, kInf, sd, it, T_maj, needNext);
+                mode = M_MEDIUM;
+            }
+        }
+        if (pathEnd) {
+            P.ps.L[g] = to4(L);
+            P.ps.lambda[g] = to4(lam);
+            mode = M_FETCH;
+        }
+    }
+    flush_stat(P.stats, 0, nLookup);
+    flush_stat(P.stats, 1, nPaths);
+    flush_stat(P.stats, 3, nShadowLookup);
+    flush_stat(P.stats, 4, nShadow);
+    flush_stat(P.stats, 5, nSteps);
+    flush_stat(P.stats, 6, nIter);
+    flush_stat(P.stats, 7, nActive);
+}
+
+// ---------------------------------------------------------------------------
 // Film — NaN/Inf guard (integrators.cpp:272-282), PixelSensor::ToSensorRGB (film.h:95-100),
 // RGBFilm::AddSample (film.h:239-255): per pixel, the pass's samples in sampleIndex order.
 __global__ void __launch_bounds__(256) k_film(Params P) {
@@ -571,7 +972,8 @@ __global__ void __launch_bounds__(256) k_film(Params P) {
             const int id = s * npix + pix;
             Spec L = spec4(P.ps.L[id]);
             const Spec lam = spec4(P.ps.lambda[id]);
-            const Spec pdf = spec4(P.ps.pdf[id]);
+            const Spec pdf = {visible_wavelength_pdf(lam.v0), visible_wavelength_pdf(lam.v1),
+                              visible_wavelength_pdf(lam.v2), visible_wavelength_pdf(lam.v3)};
             const LambdaIdx li = lambda_index(lam);
             bool bad = __builtin_isnan(L.v0) || __builtin_isnan(L.v1) || __builtin_isnan(L.v2) || __builtin_isnan(L.v3);
             if (!bad) {
@@ -611,7 +1013,7 @@ __global__ void __launch_bounds__(256) k_majorant(const float *__restrict__ dens
     const float b1[3] = {float(x + 1) / rx, float(y + 1) / ry, float(z + 1) / rz};
     const int n[3] = {nx, ny, nz};
     int lo[3], hi[3];
-    for (int a = 0; a < 3; ++a) {
+    _Pragma("unroll") for (int a = 0; a < 3; ++a) {
         float ps0 = b0[a] * n[a] - .5f, ps1 = b1[a] * n[a] - .5f;
         int l = (int)__builtin_floorf(ps0);
         lo[a] = l > 0 ? l : 0;

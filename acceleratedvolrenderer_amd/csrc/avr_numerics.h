@@ -170,7 +170,7 @@ AVR_HD float visible_wavelength_pdf(float l) {
 struct Lambda { Spec l, pdf; };
 AVR_HD Lambda sample_visible(float u) {
     float up[4];
-    for (int i = 0; i < 4; ++i) { up[i] = u + float(i) / 4; if (up[i] > 1) up[i] -= 1; }
+    _Pragma("unroll") for (int i = 0; i < 4; ++i) { up[i] = u + float(i) / 4; if (up[i] > 1) up[i] -= 1; }
     Lambda w;
     w.l = {sample_visible_wavelength(up[0]), sample_visible_wavelength(up[1]), sample_visible_wavelength(up[2]),
            sample_visible_wavelength(up[3])};
@@ -248,7 +248,7 @@ struct Ray { V3 o, d; };
 AVR_HD Ray xf_ray(const Xf &t, Ray r, float *tMax, bool forward) {
     float v[3], lo[3], hi[3];
     const float g3 = gamma_n(3);
-    for (int i = 0; i < 3; ++i) {
+    _Pragma("unroll") for (int i = 0; i < 3; ++i) {
         const float *m = &t.m[4 * i];
         v[i] = (m[0] * r.o.x + m[1] * r.o.y) + (m[2] * r.o.z + m[3]);
         float e = __builtin_fabsf(m[0] * r.o.x) + __builtin_fabsf(m[1] * r.o.y) + __builtin_fabsf(m[2] * r.o.z);
@@ -264,7 +264,7 @@ AVR_HD Ray xf_ray(const Xf &t, Ray r, float *tMax, bool forward) {
         float dt = dot({__builtin_fabsf(d.x), __builtin_fabsf(d.y), __builtin_fabsf(d.z)}, oerr) / lsq;
         V3 dd = d * dt;
         float ddv[3] = {dd.x, dd.y, dd.z};
-        for (int i = 0; i < 3; ++i) {
+        _Pragma("unroll") for (int i = 0; i < 3; ++i) {
             float a = next_down(lo[i] + ddv[i]), b = next_up(hi[i] + ddv[i]);
             lo[i] = fminf_(a, b); hi[i] = fmaxf_(a, b);
         }
@@ -277,7 +277,7 @@ AVR_HD Ray xf_ray(const Xf &t, Ray r, float *tMax, bool forward) {
 AVR_HD bool intersect_box(const float bmin[3], const float bmax[3], V3 o, V3 d, float tMax, float *h0, float *h1) {
     float t0 = 0, t1 = tMax;
     const float s = 1 + 2 * gamma_n(3);
-    for (int i = 0; i < 3; ++i) {
+    _Pragma("unroll") for (int i = 0; i < 3; ++i) {
         float inv = 1 / comp(d, i);
         float tNear = (bmin[i] - comp(o, i)) * inv;
         float tFar = (bmax[i] - comp(o, i)) * inv;

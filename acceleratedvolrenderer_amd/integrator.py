@@ -29,7 +29,7 @@ def shard_samples(spp, rank, world_size):
 
 class VolPathIntegrator:
     def __init__(self, scene, maxdepth=5, spp=16, seed=0, device=0, max_paths=0, lightsampler="bvh",
-                 regularize=False, name="volpath"):
+                 regularize=False, name="volpath", kernel="persistent"):
         if name not in INTEGRATOR_NAMES:
             raise ValueError(f"unknown integrator {name!r}")
         if lightsampler not in ("bvh", "uniform", "power"):
@@ -44,6 +44,9 @@ class VolPathIntegrator:
         self.seed = int(seed)
         self.device = int(device)
         self.ctx = capi.Context(device, max_paths)
+        if kernel not in ("persistent", "wavefront"):
+            raise ValueError("kernel must be 'persistent' or 'wavefront'")
+        self.ctx.set_kernel_mode(0 if kernel == "persistent" else 1)
         self.ctx.set_scene(scene)
 
     @classmethod

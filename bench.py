@@ -41,6 +41,8 @@ def parse():
     p.add_argument("--max-paths", type=int, default=0)
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU-baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--kernel", default="persistent", choices=["persistent", "wavefront"])
+    p.add_argument("--refill-min", type=int, default=0, help="k_paths refill threshold (0 = library default)")
     return p.parse_args()
 
 
@@ -108,8 +110,10 @@ def main():
     tgen = time.perf_counter() - tgen
     scene = scenes.s_cloud(density, width=args.width, height=args.height)
     integ = VolPathIntegrator(scene, maxdepth=scenes.CLOUD_MAXDEPTH, spp=args.spp_per_step, seed=0, device=dev,
-                              max_paths=args.max_paths)
+                              max_paths=args.max_paths, kernel=args.kernel)
     S = args.spp_per_step
+    if args.refill_min:
+        integ.ctx.set_refill_min(args.refill_min)
 
     def step(k):
         base = (k * world + rank) * S
@@ -147,11 +151,18 @@ def main():
 
     samples = npix * S * args.steps * world
     value = samples / elapsed / 1e6
-    # roofline of the dominant kernel (k_medium): algorithmic bytes / device time
-    med_bytes = BYTES_PER_LOOKUP * agg["medium_lookups"] + BYTES_PER_ITEM * (agg["medium_items_in"] +
-                                                                            agg["medium_items_out"])
+    # roofline of the dominant kernel: algorithmic bytes / summed device time of its launches
     med_s = agg["ms_medium"] / 1e3
     launches = max(1, agg["medium_launches"])
+    if args.kernel == "persistent":
+        # k_paths fuses delta tracking and ratio tracking: 32 B per trilinear lookup (both kinds)
+        # + the 32 B per-sample record (L, lambda) it writes; path state never leaves VGPRs.
+        kname = "k_paths (persistent: delta + ratio tracking, density fetch)"
+        med_bytes = BYTES_PER_LOOKUP * (agg["medium_lookups"] + agg["shadow_lookups"]) + 32 * agg["medium_items_in"]
+    else:
+        kname = "k_medium (wavefront delta tracking + density fetch)"
+        med_bytes = BYTES_PER_LOOKUP * agg["medium_lookups"] + BYTES_PER_ITEM * (agg["medium_items_in"] +
+                                                                                agg["medium_items_out"])
     achieved = med_bytes / med_s / 1e9 if med_s > 0 else 0.0
     out = None
     if rank == 0:
@@ -177,7 +188,7 @@ def main():
                                    f"{S} spp/step/GPU, maxdepth {scenes.CLOUD_MAXDEPTH}, independent sampler",
                        "global_batch": samples // args.steps, "parallelism": f"sample-shard x{world}"},
             "roofline": {
-                "kernel": "k_medium (delta tracking + density fetch)",
+                "kernel": kname,
                 "bound": "hbm",
                 "achieved": round(achieved, 2),
                 "peak": HBM_PEAK_GBPS,
@@ -188,12 +199,15 @@ def main():
                 "avg_launch_ms": agg["ms_medium"] / launches,
                 "launches": launches,
             },
+            "simd_utilisation": (agg["active_lane_iterations"] / (64.0 * agg["loop_iterations"])
+                                 if agg.get("loop_iterations") else None),
             "cpu_baseline": cpu,
             "detail": {
                 "grid_gen_s": round(tgen, 3),
                 "ms_camera": agg["ms_camera"], "ms_medium": agg["ms_medium"], "ms_shadow": agg["ms_shadow"],
                 "ms_film": agg["ms_film"], "medium_lookups": agg["medium_lookups"],
                 "shadow_lookups": agg["shadow_lookups"], "medium_items_in": agg["medium_items_in"],
+                "loop_iterations": agg.get("loop_iterations"), "medium_dda_steps": agg["medium_dda_steps"],
                 "medium_items_out": agg["medium_items_out"], "shadow_items": agg["shadow_items"],
                 "shadow_achieved_GBps": round((BYTES_PER_LOOKUP * agg["shadow_lookups"] + BYTES_PER_ITEM *
                                                agg["shadow_items"]) / max(1e-9, agg["ms_shadow"] / 1e3) / 1e9, 2),

@@ -44,6 +44,8 @@ typedef struct avr_stats {
     unsigned long long medium_dda_steps;
     unsigned long long shadow_dda_steps;
     unsigned long long medium_launches;
+    unsigned long long loop_iterations;        /* k_paths: wave loop iterations           */
+    unsigned long long active_lane_iterations; /* k_paths: sum of busy lanes per iteration */
     double ms_camera, ms_medium, ms_shadow, ms_film; /* summed hipEvent times      */
     double ms_total;                                  /* first launch .. film done  */
 } avr_stats;
@@ -55,6 +57,13 @@ const char *avr_last_error(void);
  * `max_paths` bounds the paths in flight per wavefront pass (0 = default 16M). */
 int avr_context_create(int device, long long max_paths, avr_context **out);
 int avr_context_destroy(avr_context *ctx);
+/* Kernel organisation: 0 = persistent-wave megakernel k_paths (default: path state in
+ * VGPRs, ballot-based lane refill), 1 = wavefront kernels k_camera/k_medium/k_shadow with
+ * compacted SoA queues between events (pbrt wavefront decomposition). Same estimator. */
+int avr_set_kernel_mode(avr_context *ctx, int mode);
+/* k_paths: refill a wave's idle lanes with new samples once at least `lanes` (1..64)
+ * are idle (or none is busy); larger values batch the camera-ray setup across lanes. */
+int avr_set_refill_min(avr_context *ctx, int lanes);
 /* Run all work of this context on `hip_stream` (a hipStream_t; NULL = the context's own stream). */
 int avr_set_stream(avr_context *ctx, void *hip_stream);
 

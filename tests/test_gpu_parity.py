@@ -94,15 +94,16 @@ def test_cloud_generator_bit_exact():
     ctx.close()
 
 
+@pytest.mark.parametrize("kernel", ["persistent", "wavefront"])
 @pytest.mark.parametrize("variant", ["scatter", "absorber"])
-def test_uniform_box_film_parity(variant):
+def test_uniform_box_film_parity(variant, kernel):
     from acceleratedvolrenderer_amd import scenes
     from oracle import binding
     n, W, H, spp = 16, 32, 32, 8
     rng = np.random.default_rng(5)
     dens = (0.25 + rng.random((n, n, n), dtype=np.float32)).astype(np.float32)
     scene = scenes.s_uniform(n=n, width=W, height=H, variant=variant, density=dens)
-    integ = _integrator(scene, maxdepth=5, spp=spp)
+    integ = _integrator(scene, maxdepth=5, spp=spp, kernel=kernel)
     rgb, w = integ.render()
     ref = binding.OracleRun(scene, max_depth=5, seed=0)
     rgb_o, w_o = ref.render(0, spp, nthreads=8)
@@ -110,7 +111,7 @@ def test_uniform_box_film_parity(variant):
     err = _rel_rms(integ.image(rgb, w), integ.image(rgb_o, w_o))
     noise = _oracle_noise(scene, 5, spp, integ, rgb_o, w_o)
     frac, worst_lambda = _compare_samples(integ, ref, 0, spp)
-    print(f"{variant}: film rel RMS {err:.3e} (MC noise {noise:.3e}), bit-exact samples {frac:.4f}, "
+    print(f"{variant}/{kernel}: film rel RMS {err:.3e} (MC noise {noise:.3e}), bit-exact samples {frac:.4f}, "
           f"max |dlambda| {worst_lambda:.2e}")
     assert worst_lambda < 1e-3
     assert frac >= 0.90
@@ -118,36 +119,59 @@ def test_uniform_box_film_parity(variant):
     integ.close()
 
 
-def test_cloud_film_parity_perspective():
+@pytest.mark.parametrize("kernel", ["persistent", "wavefront"])
+def test_cloud_film_parity_perspective(kernel):
     from acceleratedvolrenderer_amd import scenes
     from oracle import binding
     n, W, H, spp = 32, 64, 36, 8
     dens = binding.cloud_grid(n)
     scene = scenes.s_cloud(dens, width=W, height=H)
-    integ = _integrator(scene, maxdepth=scenes.CLOUD_MAXDEPTH, spp=spp)
+    integ = _integrator(scene, maxdepth=scenes.CLOUD_MAXDEPTH, spp=spp, kernel=kernel)
     rgb, w = integ.render()
     ref = binding.OracleRun(scene, max_depth=scenes.CLOUD_MAXDEPTH, seed=0)
     rgb_o, w_o = ref.render(0, spp, nthreads=8)
     err = _rel_rms(integ.image(rgb, w), integ.image(rgb_o, w_o))
     noise = _oracle_noise(scene, scenes.CLOUD_MAXDEPTH, spp, integ, rgb_o, w_o)
     frac, _ = _compare_samples(integ, ref, 0, spp)
-    print(f"cloud: film rel RMS {err:.3e} (MC noise {noise:.3e}), bit-exact samples {frac:.4f}")
+    print(f"cloud/{kernel}: film rel RMS {err:.3e} (MC noise {noise:.3e}), bit-exact samples {frac:.4f}")
     assert frac >= 0.90
     assert err <= 0.5 * noise
     integ.close()
 
 
-def test_multipass_equals_single_pass_and_deterministic():
+def test_persistent_and_wavefront_kernels_agree_bit_for_bit():
+    """Both kernel organisations run the same device arithmetic per sample, so the
+    per-sample radiance and the fp64 film sums are identical."""
+    from acceleratedvolrenderer_amd import scenes
+    from oracle import binding
+    dens = binding.cloud_grid(24)
+    scene = scenes.s_cloud(dens, width=40, height=24)
+    a = _integrator(scene, maxdepth=scenes.CLOUD_MAXDEPTH, spp=6, kernel="persistent")
+    b = _integrator(scene, maxdepth=scenes.CLOUD_MAXDEPTH, spp=6, kernel="wavefront")
+    ra, wa = a.render()
+    rb, wb = b.render()
+    npix = 40 * 24
+    La = a.ctx.last_pass_samples(npix, 6)[2]
+    Lb = b.ctx.last_pass_samples(npix, 6)[2]
+    assert np.array_equal(La.view(np.uint32), Lb.view(np.uint32))
+    assert np.array_equal(ra, rb) and np.array_equal(wa, wb)
+    a.close()
+    b.close()
+
+
+@pytest.mark.parametrize("kernel", ["persistent", "wavefront"])
+def test_multipass_equals_single_pass_and_deterministic(kernel):
     """Pass splitting (max_paths) and repeat runs give bit-identical fp64 film sums."""
     from acceleratedvolrenderer_amd import scenes, VolPathIntegrator
     n, W, H, spp = 16, 20, 20, 8
     rng = np.random.default_rng(9)
     dens = rng.random((n, n, n), dtype=np.float32)
     scene = scenes.s_uniform(n=n, width=W, height=H, variant="scatter", density=dens)
-    a = VolPathIntegrator(scene, maxdepth=5, spp=spp, device=0)
+    a = VolPathIntegrator(scene, maxdepth=5, spp=spp, device=0, kernel=kernel)
     rgb1, w1 = a.render()
     rgb2, w2 = a.render()
-    b = VolPathIntegrator(scene, maxdepth=5, spp=spp, device=0, max_paths=W * H * 3)  # passes of 3 samples
+    b = VolPathIntegrator(scene, maxdepth=5, spp=spp, device=0, max_paths=W * H * 3,
+                          kernel=kernel)  # passes of 3 samples
     rgb3, w3 = b.render()
     assert np.array_equal(rgb1, rgb2) and np.array_equal(w1, w2)
     assert np.array_equal(rgb1, rgb3) and np.array_equal(w1, w3)
