@@ -49,6 +49,9 @@ SIGNATURES = {
     "avr_set_stream": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "avr_set_kernel_mode": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "avr_set_refill_min": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "avr_set_dda_budget": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "avr_set_grid_layout": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "avr_grid_layout_active": (ctypes.c_int, [ctypes.c_void_p]),
     "avr_medium_grid": (ctypes.c_int, [ctypes.c_void_p, c_float_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                        c_float_p, c_float_p, c_float_p, c_float_p, c_float_p, ctypes.c_float,
                                        c_float_p, c_float_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_int_p]),
@@ -128,6 +131,16 @@ class Context:
     def set_kernel_mode(self, mode):
         """0 = persistent megakernel (default), 1 = wavefront queues."""
         _check(self.lib.avr_set_kernel_mode(self.h, int(mode)))
+
+    def set_grid_layout(self, layout):
+        """1 = fat footprint copy (default), 0 = pbrt's linear layout only; applies to the next set_scene."""
+        _check(self.lib.avr_set_grid_layout(self.h, int(layout)))
+
+    def grid_layout_active(self):
+        return int(self.lib.avr_grid_layout_active(self.h))
+
+    def set_dda_budget(self, cells):
+        _check(self.lib.avr_set_dda_budget(self.h, int(cells)))
 
     def set_refill_min(self, lanes):
         _check(self.lib.avr_set_refill_min(self.h, int(lanes)))

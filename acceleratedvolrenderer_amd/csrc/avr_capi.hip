@@ -72,6 +72,10 @@ struct avr_context {
     int *d_heads = nullptr;   // 8 per-XCD work counters of k_paths
     int paths_grid = 0;
     int refill_min = 16;
+    int dda_budget = 4;
+    int grid_layout = 1;
+    bool gray = false;        // sigma_a and sigma_s constant over 360..830 nm      // 1: build the fat (footprint) copy when memory allows, 0: linear only
+    float4 *d_fat = nullptr;
     uint64_t *d_advance = nullptr;  // per-pass PCG advance table {A, H}
     long long advance_cap = 0;
     std::vector<uint64_t> h_advance;
@@ -144,11 +148,14 @@ int medium_common(avr_context *c, const float *d_density, int nx, int ny, int nz
     m.density = d_density;
     m.nx = nx; m.ny = ny; m.nz = nz;
     for (int i = 0; i < 3; ++i) { m.bmin[i] = bounds[i]; m.bmax[i] = bounds[3 + i]; m.mres[i] = mres[i]; }
+    m.unit_box = (m.bmax[0] - m.bmin[0] == 1.f && m.bmax[1] - m.bmin[1] == 1.f && m.bmax[2] - m.bmin[2] == 1.f) ? 1 : 0;
     copy_xf(m.render_from_medium, rfm);
     copy_xf(m.medium_from_render, mfr);
     m.sigma_a = c->d_sigma_a;
     m.sigma_s = c->d_sigma_s;
     m.g = g;
+    c->gray = true;
+    for (int i = 1; i < avr::kNTable; ++i) c->gray &= sigma_a[i] == sigma_a[0] && sigma_s[i] == sigma_s[0];
     // isEmissive = Le_spec.MaxValue() > 0 (media.cpp:238)
     bool emissive = false;
     if (Le) for (int i = 0; i < avr::kNTable; ++i) emissive |= Le[i] > 0;
@@ -163,6 +170,23 @@ int medium_common(avr_context *c, const float *d_density, int nx, int ny, int nz
                        mres[2], c->d_majorant);
     HIP_TRY(hipGetLastError());
     m.majorant = c->d_majorant;
+    if (c->d_fat) { (void)hipFree(c->d_fat); c->d_fat = nullptr; }
+    m.fat = nullptr;
+    if (c->grid_layout == 1) {
+        const size_t nfat = (size_t)(nx + 1) * (ny + 1) * (nz + 1);
+        size_t freeB = 0, totalB = 0;
+        HIP_TRY(hipMemGetInfo(&freeB, &totalB));
+        // keep >= 8 GiB for path state / film / other ranks' traffic
+        if (nfat * 32 + (8ull << 30) < freeB && hipMalloc((void **)&c->d_fat, nfat * 32) == hipSuccess) {
+            hipLaunchKernelGGL(avr::k_fatten, dim3(blocks_for((long long)nfat, 256, 256 * 64)), dim3(256), 0,
+                               c->stream, d_density, nx, ny, nz, c->d_fat);
+            HIP_TRY(hipGetLastError());
+            m.fat = c->d_fat;
+        } else {
+            (void)hipGetLastError();
+            c->d_fat = nullptr;
+        }
+    }
     HIP_TRY(hipStreamSynchronize(c->stream));
     c->has_medium = true;
     return AVR_OK;
@@ -199,7 +223,7 @@ int avr_context_create(int device, long long max_paths, avr_context **out) {
         hipDeviceProp_t prop;
         int blocksPerCU = 0;
         if (hipGetDeviceProperties(&prop, device) != hipSuccess ||
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocksPerCU, avr::k_paths<false>, 256, 0) != hipSuccess) {
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocksPerCU, (void (*)(avr::Params))avr::k_paths<false, false>, 256, 0) != hipSuccess) {
             delete c;
             return fail(AVR_ERR_HIP, "occupancy query failed");
         }
@@ -209,6 +233,20 @@ int avr_context_create(int device, long long max_paths, avr_context **out) {
         c->paths_grid = prop.multiProcessorCount * std::max(1, blocksPerCU);
     }
     *out = c;
+    return AVR_OK;
+}
+
+int avr_set_grid_layout(avr_context *c, int layout) {
+    if (!c || (layout != 0 && layout != 1)) return fail(AVR_ERR_ARG, "grid layout must be 0 (linear) or 1 (fat)");
+    c->grid_layout = layout;
+    return AVR_OK;
+}
+
+int avr_grid_layout_active(avr_context *c) { return (c && c->d_fat) ? 1 : 0; }
+
+int avr_set_dda_budget(avr_context *c, int cells) {
+    if (!c || cells < 1) return fail(AVR_ERR_ARG, "DDA budget must be >= 1 cell");
+    c->dda_budget = cells;
     return AVR_OK;
 }
 
@@ -238,6 +276,7 @@ int avr_context_destroy(avr_context *c) {
     if (c->d_counts) (void)hipFree(c->d_counts);
     if (c->d_heads) (void)hipFree(c->d_heads);
     if (c->d_advance) (void)hipFree(c->d_advance);
+    if (c->d_fat) (void)hipFree(c->d_fat);
     if (c->d_stats) (void)hipFree(c->d_stats);
     if (c->h_count) (void)hipHostFree(c->h_count);
     for (auto e : c->evpool) (void)hipEventDestroy(e);
@@ -424,13 +463,14 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
                                    hipMemcpyHostToDevice, c->stream));
             p.advance = c->d_advance;
             p.refill_min = c->refill_min;
+            p.dda_budget = c->dda_budget;
             p.heads = c->d_heads;
             HIP_TRY(hipMemsetAsync(c->d_heads, 0, 8 * sizeof(int), c->stream));
             HIP_TRY(hipEventRecord(e0, c->stream));
-            if (c->med.emissive)
-                hipLaunchKernelGGL(avr::k_paths<true>, dim3(c->paths_grid), dim3(256), 0, c->stream, p);
-            else
-                hipLaunchKernelGGL(avr::k_paths<false>, dim3(c->paths_grid), dim3(256), 0, c->stream, p);
+            // gray medium: sigma_a and sigma_s tables constant over all 471 wavelengths
+            void (*kern)(avr::Params) = c->med.emissive ? (c->gray ? avr::k_paths<true, true> : avr::k_paths<true, false>)
+                                                        : (c->gray ? avr::k_paths<false, true> : avr::k_paths<false, false>);
+            hipLaunchKernelGGL(kern, dim3(c->paths_grid), dim3(256), 0, c->stream, p);
             HIP_TRY(hipGetLastError());
             HIP_TRY(hipEventRecord(e1, c->stream));
             hipLaunchKernelGGL(avr::k_film, dim3(blocks_for(P)), dim3(256), 0, c->stream, p);

@@ -18,6 +18,8 @@
 //                (bit-identical order to ImageTileIntegrator::Render's per-pixel loop).
 #include "avr_numerics.h"
 
+#include <type_traits>
+
 namespace avr {
 
 struct DevMedium {
@@ -33,6 +35,13 @@ struct DevMedium {
     int lnx, lny, lnz;
     const float *majorant;
     int mres[3];
+    // "fat" copy of the density grid (the trilinear footprint of every lookup stored
+    // contiguously): entry (ix,iy,iz), ix in [-1, nx-1], holds the 8 taps
+    // v(ix..ix+1, iy..iy+1, iz..iz+1) (zero outside the grid) as two float4 = 32 B, so a
+    // lookup is ONE 32-B-aligned access inside one cache line instead of 8 scattered taps
+    // in 2-4 lines. 8x the grid's memory ((n+1)^3 x 32 B; 34 GB at 1024^3 of the 288 GB).
+    const float4 *fat;
+    int unit_box;          // bounds extent exactly 1 on every axis: Offset's divisions are by 1.0f
 };
 
 constexpr int kMaxLights = 8;
@@ -102,6 +111,8 @@ struct Params {
     const uint64_t *advance;          // k_paths: per pass sample s, {A, H}: Advance(sIdx*65536) ==
                                       //   state' = A*state + inc*H (PCG32 advance is linear in inc)
     int refill_min;                   // k_paths: refill a wave once this many lanes are idle
+    int dda_budget;                   // k_paths: majorant cells a lane may cross per tracking
+                                      //   iteration before yielding (bounds DDA divergence)
 };
 
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
@@ -144,6 +155,35 @@ __device__ __forceinline__ float grid_lookup(const float *__restrict__ v, int nx
     return lerp(dz, lerp(dy, d00, d10), lerp(dy, d01, d11));
 }
 
+// Same value as grid_lookup() bit for bit (same taps, same lerp order) from the fat layout.
+__device__ __forceinline__ float fat_lookup(const float4 *__restrict__ fat, const float *__restrict__ v, int nx, int ny,
+                                            int nz, V3 p) {
+    float psx = p.x * nx - .5f, psy = p.y * ny - .5f, psz = p.z * nz - .5f;
+    int ix = (int)__builtin_floorf(psx), iy = (int)__builtin_floorf(psy), iz = (int)__builtin_floorf(psz);
+    if (ix < -1 || ix >= nx || iy < -1 || iy >= ny || iz < -1 || iz >= nz) return grid_lookup(v, nx, ny, nz, p);
+    float dx = psx - (float)ix, dy = psy - (float)iy, dz = psz - (float)iz;
+    const size_t e = (((size_t)(iz + 1) * (ny + 1) + (iy + 1)) * (nx + 1) + (ix + 1)) * 2;
+    const float4 a = fat[e], b = fat[e + 1];
+    float d00 = lerp(dx, a.x, a.y);
+    float d10 = lerp(dx, a.z, a.w);
+    float d01 = lerp(dx, b.x, b.y);
+    float d11 = lerp(dx, b.z, b.w);
+    return lerp(dz, lerp(dy, d00, d10), lerp(dy, d01, d11));
+}
+
+__global__ void __launch_bounds__(256) k_fatten(const float *__restrict__ v, int nx, int ny, int nz, float4 *fat) {
+    const size_t n = (size_t)(nx + 1) * (ny + 1) * (nz + 1);
+    for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < n; e += (size_t)gridDim.x * blockDim.x) {
+        const int ix = (int)(e % (nx + 1)) - 1, iy = (int)((e / (nx + 1)) % (ny + 1)) - 1,
+                  iz = (int)(e / ((size_t)(nx + 1) * (ny + 1))) - 1;
+        fat[2 * e] = make_float4(grid_at(v, nx, ny, nz, ix, iy, iz), grid_at(v, nx, ny, nz, ix + 1, iy, iz),
+                                 grid_at(v, nx, ny, nz, ix, iy + 1, iz), grid_at(v, nx, ny, nz, ix + 1, iy + 1, iz));
+        fat[2 * e + 1] = make_float4(grid_at(v, nx, ny, nz, ix, iy, iz + 1), grid_at(v, nx, ny, nz, ix + 1, iy, iz + 1),
+                                     grid_at(v, nx, ny, nz, ix, iy + 1, iz + 1),
+                                     grid_at(v, nx, ny, nz, ix + 1, iy + 1, iz + 1));
+    }
+}
+
 struct MediumSample { Spec sigma_a, sigma_s, Le; };
 
 // GridMedium::SamplePoint — media.h:287-319 (no temperature grid); sig_a/sig_s pre-sampled at lambda
@@ -151,8 +191,9 @@ __device__ __forceinline__ MediumSample sample_point(const DevMedium &m, V3 p, c
                                                      const Spec &Le_l, bool emissive = true) {
     MediumSample ms;
     p = xf_point_pair(m.medium_from_render, p);
-    p = box_offset(m.bmin, m.bmax, p);
-    float d = grid_lookup(m.density, m.nx, m.ny, m.nz, p);
+    // Bounds3::Offset (vecmath.h:1323-1332); x / 1.0f == x exactly, so a unit box skips it
+    p = m.unit_box ? V3{p.x - m.bmin[0], p.y - m.bmin[1], p.z - m.bmin[2]} : box_offset(m.bmin, m.bmax, p);
+    float d = m.fat ? fat_lookup(m.fat, m.density, m.nx, m.ny, m.nz, p) : grid_lookup(m.density, m.nx, m.ny, m.nz, p);
     ms.sigma_a = sig_a * d;
     ms.sigma_s = sig_s * d;
     ms.Le = Spec::c(0.f);
@@ -610,11 +651,49 @@ __device__ __forceinline__ void seg_begin(const DevMedium &m, V3 o, V3 d, float 
     needNext = true;
 }
 
-#ifndef AVR_PATHS_MIN_WAVES
-#define AVR_PATHS_MIN_WAVES 1
+#ifndef AVR_PATHS_WAVES_GRAY
+#define AVR_PATHS_WAVES_GRAY 3   // 168 VGPRs, no scratch (4 waves -> 128 VGPRs spills ~100 B/lane)
 #endif
-template <bool kEmissive>
-__global__ void __launch_bounds__(256, AVR_PATHS_MIN_WAVES) k_paths(Params P) {
+#ifndef AVR_PATHS_WAVES_SPEC
+#define AVR_PATHS_WAVES_SPEC 2   // 4-wavelength state: ~220 VGPRs without scratch
+#endif
+// Lane events, deferred and handled in batches: a lane that reaches an event parks until
+// enough lanes of its wave need service, so each event handler runs once per batch
+// instead of once per tracking iteration (SQ_INSTS_VALU showed the per-iteration union
+// of all branches, ~8k wave-instructions, dominating an eager state machine).
+enum : int { EV_NONE = 0, EV_SCATTER = 1, EV_SHADOW_DONE = 2, EV_PHASE = 3, EV_ESCAPE = 4, EV_END = 5 };
+
+// Spectral-state type of k_paths: Spec (4 wavelengths) in general; float for a GRAY medium
+// (sigma_a and sigma_s tables constant over 360..830 nm, decided on the host). In a gray
+// medium beta, r_u, r_l, T_maj and the shadow ratios have four equal components at every
+// step (they start at 1 and only ever multiply/divide by gray factors), so one scalar op
+// yields exactly the bits each component would get: the overloads below restate Spec's
+// operations on one component (Spec::avg of four equal values is (((x+x)+x)+x)/4, NOT x).
+__device__ __forceinline__ float sv0(float x) { return x; }
+__device__ __forceinline__ float sv0(const Spec &x) { return x.v0; }
+__device__ __forceinline__ bool snz(float x) { return x != 0; }
+__device__ __forceinline__ bool snz(const Spec &x) { return x.nonzero(); }
+__device__ __forceinline__ float savg(float x) { return (((x + x) + x) + x) / 4; }
+__device__ __forceinline__ float savg(const Spec &x) { return x.avg(); }
+__device__ __forceinline__ float smaxc(float x) { return x; }
+__device__ __forceinline__ float smaxc(const Spec &x) { return x.maxc(); }
+__device__ __forceinline__ float sclamp0(float x) { return fmaxf_(0.f, x); }
+__device__ __forceinline__ Spec sclamp0(const Spec &x) { return clamp_zero(x); }
+__device__ __forceinline__ float sexp(float x) { return fast_exp(x); }
+__device__ __forceinline__ Spec sexp(const Spec &x) { return fast_exp(x); }
+template <typename S> __device__ __forceinline__ S sconst(float a);
+template <> __device__ __forceinline__ float sconst<float>(float a) { return a; }
+template <> __device__ __forceinline__ Spec sconst<Spec>(float a) { return Spec::c(a); }
+template <typename S> __device__ __forceinline__ S sfrom(const Spec &x);
+template <> __device__ __forceinline__ float sfrom<float>(const Spec &x) { return x.v0; }
+template <> __device__ __forceinline__ Spec sfrom<Spec>(const Spec &x) { return x; }
+// spectrum (light / emission) times path state: component-wise products commute exactly
+__device__ __forceinline__ Spec smul(const Spec &a, float b) { return a * b; }
+__device__ __forceinline__ Spec smul(const Spec &a, const Spec &b) { return a * b; }
+
+template <bool kEmissive, bool kGray>
+__global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_WAVES_SPEC) k_paths(Params P) {
+    using S = typename std::conditional<kGray, float, Spec>::type;
     // LDS: majorant grid (16 KiB at pbrt's 16^3) + the 471-entry spectral tables the path
     // samples at path start, NEE and escape (sigma_a, sigma_s, up to 4 light spectra).
     __shared__ float s_maj[4096];
@@ -639,26 +718,143 @@ __global__ void __launch_bounds__(256, AVR_PATHS_MIN_WAVES) k_paths(Params P) {
     unsigned long long nLookup = 0, nSteps = 0, nPaths = 0, nShadow = 0, nShadowLookup = 0;
     unsigned long long nIter = 0, nActive = 0;
 
-    int mode = M_FETCH;
+    int mode = M_FETCH, ev = EV_NONE;
     int g = 0;
     // path state (Li, integrators.cpp:966-971)
-    Spec L{}, beta{}, r_u{}, r_l{}, lam{}, sig_a{}, sig_s{}, Le_l{};
+    Spec L{}, lam{}, Le_l{};
+    S beta{}, r_u{}, r_l{}, sig_a{}, sig_s{};
     Sampler smp{};
     int depth = 0;
-    V3 po{}, pd{};
+    V3 po{}, pd{};         // segment origin (== the path vertex) and the path's ray direction
     // segment state (SampleT_maj)
     Pcg32 rng{};
     float u = 0, tMin = 0, segMax = 0, mv = 0;
     Dda it{};
-    V3 sd{};               // normalised segment direction; the segment origin is always po
-    Spec T_maj{};
-    bool needNext = true;
+    V3 sd{};               // normalised segment direction
+    S T_maj{};
+    bool needNext = true, shadowStopped = false;
     // shadow state (SampleLd, integrators.cpp:1339-1391)
     int light = 0;
-    Spec T_ray{}, sr_l{}, sr_u{};
+    S T_ray{}, sr_l{}, sr_u{};
+
+    auto seg_start = [&](V3 o, V3 d, float tMax) {
+        Spec tm;
+        seg_begin(m, o, d, tMax, sd, it, tm, needNext);
+        T_maj = sconst<S>(1.f);
+    };
 
     while (true) {
-        // ---- refill idle lanes: one atomic per wave on a per-XCD head -------------------
+        // =================== batched event handlers (each runs once per batch) ===========
+        if (__ballot(ev == EV_SCATTER)) {
+            if (ev == EV_SCATTER) {
+                // SampleLd: light pick (BVH infinite-light branch) + shadow-ray spawn (1282-1338)
+                const V3 wo = -pd;
+                const float ul = smp.get1d();
+                smp.get1d(); smp.get1d();
+                ev = EV_PHASE;                       // unless a shadow ray is spawned
+                L = L + Spec::c(0.f);                // L += SampleLd(...) == 0 if nothing spawns
+                const int nl = P.lights.n;
+                if (nl > 0) {
+                    const float pInf = float(nl) / float(nl + 0);
+                    if (ul < pInf) {
+                        int idx = (int)(ul / pInf * nl);
+                        idx = idx < nl - 1 ? idx : nl - 1;
+                        const DevLight &lt = P.lights.list[idx];
+                        if (lt.type == 0) {
+                            const V3 wi = {lt.w[0], lt.w[1], lt.w[2]};
+                            const Spec Ls = sample_table(light_table(idx), lambda_index(lam)) * lt.scale;
+                            if (Ls.nonzero() && hg_eval(dot(wo, wi), m.g) != 0) {
+                                const V3 pOut = po + wi * (2 * P.lights.scene_radius);
+                                const V3 d = pOut - po;
+                                light = idx;
+                                T_ray = sr_l = sr_u = sconst<S>(1.f);
+                                rng.set_sequence(hash_3u32(f2u(po.x), f2u(po.y), f2u(po.z)),
+                                                 hash_3u32(f2u(d.x), f2u(d.y), f2u(d.z)));
+                                u = rng.uniform();
+                                seg_start(po, d, 1 - kShadowEpsilon);
+                                mode = M_SHADOW;
+                                ev = EV_NONE;
+                                ++nShadow;
+                            }
+                        }
+                    }
+                }
+            }
+        }
+        if (__ballot(ev == EV_SHADOW_DONE)) {
+            if (ev == EV_SHADOW_DONE) {
+                // finish SampleLd (1379-1398); SampleT_maj returned 1 if the callback stopped
+                const S Tm = shadowStopped ? sconst<S>(1.f) : T_maj;
+                T_ray = T_ray * (Tm / sv0(Tm));
+                sr_l = sr_l * (Tm / sv0(Tm));
+                sr_u = sr_u * (Tm / sv0(Tm));
+                Spec contrib = Spec::c(0.f);
+                if (snz(T_ray)) {
+                    const DevLight &lt = P.lights.list[light];
+                    const V3 wi = {lt.w[0], lt.w[1], lt.w[2]};
+                    const float pInf = float(P.lights.n) / float(P.lights.n + 0);
+                    const float p_l = pInf / P.lights.n * 1.f;
+                    const S f_hat = sconst<S>(hg_eval(dot(-pd, wi), m.g));
+                    const Spec Ls = sample_table(light_table(light), lambda_index(lam)) * lt.scale;
+                    sr_l = sr_l * (r_u * p_l);
+                    contrib = smul(Ls, beta * f_hat * T_ray) / savg(sr_l);
+                }
+                L = L + contrib;
+                ev = EV_PHASE;
+            }
+        }
+        if (__ballot(ev == EV_PHASE)) {
+            if (ev == EV_PHASE) {
+                // phase-function sampling (integrators.cpp:1046-1061), then the next segment
+                const float up0 = smp.get1d(), up1 = smp.get1d();
+                float phPdf;
+                const V3 wi = hg_sample(-pd, m.g, up0, up1, &phPdf);
+                if (phPdf == 0) {
+                    ev = EV_END;
+                } else {
+                    beta = beta * (phPdf / phPdf);
+                    r_l = r_u / phPdf;
+                    pd = wi;
+                    const float h0 = smp.get1d();
+                    const float h1 = smp.get1d();
+                    rng.set_sequence(hash_u32(f2u(h0)), hash_u32(f2u(h1)));
+                    u = smp.get1d();
+                    seg_start(po, pd, kInf);
+                    mode = M_MEDIUM;
+                    ev = EV_NONE;
+                }
+            }
+        }
+        if (__ballot(ev == EV_ESCAPE)) {
+            if (ev == EV_ESCAPE) {
+                // escaped (integrators.cpp:1078-1107)
+                beta = beta * (T_maj / sv0(T_maj));
+                r_u = r_u * (T_maj / sv0(T_maj));
+                r_l = r_l * (T_maj / sv0(T_maj));
+                for (int k = 0; k < P.lights.n; ++k) {
+                    const DevLight &lt = P.lights.list[k];
+                    if (lt.type != 1) continue;
+                    const Spec Le = sample_table(light_table(k), lambda_index(lam)) * lt.scale;
+                    if (!Le.nonzero()) continue;
+                    if (depth == 0) L = L + smul(Le, beta) / savg(r_u);
+                    else {
+                        r_l = r_l * ((1.f / (P.lights.n + 0)) * 0.f);
+                        L = L + smul(Le, beta) / savg(r_u + r_l);
+                    }
+                }
+                ev = EV_END;
+            }
+        }
+        if (__ballot(ev == EV_END)) {
+            if (ev == EV_END) {
+                P.ps.L[g] = to4(L);
+                P.ps.lambda[g] = to4(lam);
+                mode = M_FETCH;
+                ev = EV_NONE;
+            }
+        }
+
+        // =================== refill idle lanes: one atomic per wave on a per-XCD head ======
         const uint64_t needMask = __ballot(mode == M_FETCH);
         const uint64_t busyMask = __ballot(mode == M_MEDIUM || mode == M_SHADOW);
         if (needMask && (busyMask == 0 || __popcll(needMask) >= P.refill_min)) {
@@ -718,237 +914,168 @@ __global__ void __launch_bounds__(256, AVR_PATHS_MIN_WAVES) k_paths(Params P) {
                     po = ray.o;
                     pd = ray.d;
                     L = Spec::c(0.f);
-                    beta = r_u = r_l = Spec::c(1.f);
+                    beta = r_u = r_l = sconst<S>(1.f);
                     depth = 0;
                     {
                         const LambdaIdx li = lambda_index(lam);
-                        sig_a = sample_table(tab_sa, li);
-                        sig_s = sample_table(tab_ss, li);
+                        sig_a = sfrom<S>(sample_table(tab_sa, li));
+                        sig_s = sfrom<S>(sample_table(tab_ss, li));
                         if (kEmissive) Le_l = sample_table(m.Le, li);
                     }
-                    mode = M_MEDIUM;
-                } else if (exhausted) {
-                    mode = M_DONE;
-                }
-                if (mode == M_MEDIUM) {
-                    // new medium segment: RNG from two sampler dims, u from a third (1001-1010)
+                    // first medium segment: RNG from two sampler dims, u from a third (984-989)
                     const float h0 = smp.get1d();
                     const float h1 = smp.get1d();
                     rng.set_sequence(hash_u32(f2u(h0)), hash_u32(f2u(h1)));
                     u = smp.get1d();
-                    seg_begin(m, po, pd, kInf, sd, it, T_maj, needNext);
+                    seg_start(po, pd, kInf);
+                    mode = M_MEDIUM;
+                } else if (exhausted) {
+                    mode = M_DONE;
                 }
             }
         }
-        const uint64_t liveMask = __ballot(mode != M_DONE);
-        if (liveMask == 0) break;
-        if (lane == 0) {
-            ++nIter;
-            nActive += __popcll(__ballot(mode == M_MEDIUM || mode == M_SHADOW));
-        } else {
-            (void)__ballot(mode == M_MEDIUM || mode == M_SHADOW);
-        }
+        if (__ballot(mode != M_DONE) == 0) break;
 
-        // ---- advance to the next tentative collision (media.h:754-802) -----------------
-        bool collide = false, segEnd = false;
-        float t = 0;
-        if (mode == M_MEDIUM || mode == M_SHADOW) {
+        // =================== tracking: advance every busy lane collision by collision ======
+        // until a batch of lanes needs service (events or refill) or none is busy.
+        while (true) {
+            const bool busy = (mode == M_MEDIUM || mode == M_SHADOW) && ev == EV_NONE;
+            const uint64_t busyNow = __ballot(busy);
+            const uint64_t service = __ballot(mode != M_DONE && !busy);
+            if (busyNow == 0 || __popcll(service) >= P.refill_min) break;
+            if (lane == 0) { ++nIter; nActive += __popcll(busyNow); }
+            if (!busy) continue;
+            // ---- advance to the next tentative collision (media.h:754-802) ----
+            // Hot loop: on the S-cloud input a path crosses ~20 majorant cells per density
+            // fetch. Bit-exact shortcuts: gray medium -> scalar state; a rejected candidate
+            // (t >= segMax only consumes its RNG draw; its t is never used) is decided from a
+            // v_log_f32 estimate outside a conservative error margin, exactly otherwise and
+            // for every accepted collision; each lane crosses at most P.dda_budget cells per
+            // iteration, bounding how long early lanes wait for the longest walk.
+            bool collide = false, segEnd = false;
+            float t = 0;
+            const S sig_t = sig_a + sig_s;
+            const float st0 = sv0(sig_t);
+            int budget = P.dda_budget;
             while (true) {
                 if (needNext) {
+                    if (budget-- == 0) break;
                     float s0, s1;
                     if (!dda_next(it, maj, m.mres, &s0, &s1, &mv)) { segEnd = true; break; }
                     ++nSteps;
-                    const Spec sigma_maj = (sig_a + sig_s) * mv;
-                    if (sigma_maj.v0 == 0) {
+                    const S sigma_maj = sig_t * mv;
+                    if (sv0(sigma_maj) == 0) {
                         float dt = s1 - s0;
                         if (__builtin_isinf(dt)) dt = kFloatMax;
-                        T_maj = T_maj * fast_exp(-(sigma_maj * dt));
+                        T_maj = T_maj * sexp(-(sigma_maj * dt));
                         continue;
                     }
                     tMin = s0;
                     segMax = s1;
                     needNext = false;
                 }
-                const float sm0 = (sig_a.v0 + sig_s.v0) * mv;
-                t = tMin + sample_exponential(u, sm0);
+                const float sm0 = st0 * mv;
+                const float x = 1 - u;
+                const float eFast = -__logf(x) * __builtin_amdgcn_rcpf(sm0);
+                const float tFast = tMin + eFast;
+                const float margin = 1e-5f * __builtin_fabsf(eFast) + 4.8e-7f * __builtin_fabsf(segMax) + 1e-30f;
+                bool accept;
+                if (tFast > segMax + margin) {
+                    accept = false;
+                } else {
+                    t = tMin + sample_exponential(u, sm0);
+                    accept = t < segMax;
+                }
                 u = rng.uniform();
-                if (t < segMax) { collide = true; break; }
+                if (accept) { collide = true; break; }
                 float dt = segMax - tMin;
                 if (__builtin_isinf(dt)) dt = kFloatMax;
-                T_maj = T_maj * fast_exp(-(((sig_a + sig_s) * mv) * dt));
+                T_maj = T_maj * sexp(-((sig_t * mv) * dt));
                 needNext = true;
             }
-        }
-
-        // ---- collision: density fetch for every lane that reached one ------------------
-        bool stop = false, scattered = false;
-        V3 pc{};
-        if (collide) {
-            const Spec sigma_maj = (sig_a + sig_s) * mv;
-            T_maj = T_maj * fast_exp(-(sigma_maj * (t - tMin)));
-            pc = po + sd * t;
-            const MediumSample ms = sample_point(m, pc, sig_a, sig_s, kEmissive ? Le_l : Spec::c(0.f), kEmissive);
+            if (segEnd) {
+                if (mode == M_MEDIUM) ev = EV_ESCAPE;
+                else { ev = EV_SHADOW_DONE; shadowStopped = false; }
+                continue;
+            }
+            if (!collide) continue;   // walk budget used up: resume the DDA next iteration
+            // ---- collision: density fetch for every lane that reached one ----
+            const S sigma_maj = sig_t * mv;
+            T_maj = T_maj * sexp(-(sigma_maj * (t - tMin)));
+            const V3 pc = po + sd * t;
+            // GridMedium::SamplePoint (media.h:287-319)
+            V3 pm = xf_point_pair(m.medium_from_render, pc);
+            pm = m.unit_box ? V3{pm.x - m.bmin[0], pm.y - m.bmin[1], pm.z - m.bmin[2]} : box_offset(m.bmin, m.bmax, pm);
+            const float dens = m.fat ? fat_lookup(m.fat, m.density, m.nx, m.ny, m.nz, pm)
+                                     : grid_lookup(m.density, m.nx, m.ny, m.nz, pm);
+            const S ms_a = sig_a * dens, ms_s = sig_s * dens;
+            bool stop = false;
             if (mode == M_MEDIUM) {
                 ++nLookup;
                 // delta-tracking callback (integrators.cpp:990-1077)
-                if (!beta.nonzero()) {
+                if (!snz(beta)) {
                     stop = true;
+                    ev = EV_END;
                 } else {
-                    if (kEmissive && depth < P.max_depth && ms.Le.nonzero()) {
-                        float pdf = sigma_maj.v0 * T_maj.v0;
-                        Spec betap = beta * T_maj / pdf;
-                        Spec r_e = r_u * sigma_maj * T_maj / pdf;
-                        if (r_e.nonzero()) L = L + betap * ms.sigma_a * ms.Le / r_e.avg();
+                    if (kEmissive && depth < P.max_depth) {
+                        Spec Le = Spec::c(0.f);
+                        const float sc = grid_lookup(m.lescale, m.lnx, m.lny, m.lnz, pm);
+                        if (sc > 0) Le = Le_l * sc;
+                        if (Le.nonzero()) {
+                            float pdf = sv0(sigma_maj) * sv0(T_maj);
+                            S betap = beta * T_maj / pdf;
+                            S r_e = r_u * sigma_maj * T_maj / pdf;
+                            if (snz(r_e)) L = L + smul(Le, betap * ms_a) / savg(r_e);
+                        }
                     }
-                    const float pAbsorb = ms.sigma_a.v0 / sigma_maj.v0;
-                    const float pScat = ms.sigma_s.v0 / sigma_maj.v0;
+                    const float pAbsorb = sv0(ms_a) / sv0(sigma_maj);
+                    const float pScat = sv0(ms_s) / sv0(sigma_maj);
                     const float pNull = fmaxf_(0.f, 1 - pAbsorb - pScat);
-                    const int ev = sample_discrete3(pAbsorb, pScat, pNull, rng.uniform());
-                    if (ev == 0) {
+                    const int e = sample_discrete3(pAbsorb, pScat, pNull, rng.uniform());
+                    if (e == 0) {
                         stop = true;
-                    } else if (ev == 1) {
+                        ev = EV_END;
+                    } else if (e == 1) {
                         stop = true;
+                        ev = EV_END;
                         if (depth++ < P.max_depth) {
-                            const float pdf = T_maj.v0 * ms.sigma_s.v0;
-                            beta = beta * (T_maj * ms.sigma_s / pdf);
-                            r_u = r_u * (T_maj * ms.sigma_s / pdf);
-                            scattered = beta.nonzero() && r_u.nonzero();
+                            const float pdf = sv0(T_maj) * sv0(ms_s);
+                            beta = beta * (T_maj * ms_s / pdf);
+                            r_u = r_u * (T_maj * ms_s / pdf);
+                            if (snz(beta) && snz(r_u)) {
+                                po = pc;     // the scatter vertex: shadow-ray and next-segment origin
+                                ev = EV_SCATTER;
+                            }
                         }
                     } else {
-                        const Spec sigma_n = clamp_zero(sigma_maj - ms.sigma_a - ms.sigma_s);
-                        const float pdf = T_maj.v0 * sigma_n.v0;
+                        const S sigma_n = sclamp0(sigma_maj - ms_a - ms_s);
+                        const float pdf = sv0(T_maj) * sv0(sigma_n);
                         beta = beta * (T_maj * sigma_n / pdf);
-                        if (pdf == 0) beta = Spec::c(0.f);
+                        if (pdf == 0) beta = sconst<S>(0.f);
                         r_u = r_u * (T_maj * sigma_n / pdf);
                         r_l = r_l * (T_maj * sigma_maj / pdf);
-                        stop = !(beta.nonzero() && r_u.nonzero());
+                        if (!(snz(beta) && snz(r_u))) { stop = true; ev = EV_END; }
                     }
                 }
             } else {
                 ++nShadowLookup;
                 // ratio-tracking callback with Russian roulette (integrators.cpp:1351-1378)
-                const Spec sigma_n = clamp_zero(sigma_maj - ms.sigma_a - ms.sigma_s);
-                const float pdf = T_maj.v0 * sigma_maj.v0;
+                const S sigma_n = sclamp0(sigma_maj - ms_a - ms_s);
+                const float pdf = sv0(T_maj) * sv0(sigma_maj);
                 T_ray = T_ray * (T_maj * sigma_n / pdf);
                 sr_l = sr_l * (T_maj * sigma_maj / pdf);
                 sr_u = sr_u * (T_maj * sigma_n / pdf);
-                const Spec Tr = T_ray / (sr_l + sr_u).avg();
-                if (Tr.maxc() < 0.05f) {
-                    if (rng.uniform() < 0.75f) T_ray = Spec::c(0.f);
+                const S Tr = T_ray / savg(sr_l + sr_u);
+                if (smaxc(Tr) < 0.05f) {
+                    if (rng.uniform() < 0.75f) T_ray = sconst<S>(0.f);
                     else T_ray = T_ray / (1 - 0.75f);
                 }
-                stop = !T_ray.nonzero();
+                if (!snz(T_ray)) { stop = true; ev = EV_SHADOW_DONE; shadowStopped = true; }
             }
             if (!stop) {
-                T_maj = Spec::c(1.f);
+                T_maj = sconst<S>(1.f);
                 tMin = t;
             }
-        }
-
-        // ---- events --------------------------------------------------------------------
-        bool pathEnd = false, phase = false;
-        if (mode == M_MEDIUM && (stop || segEnd)) {
-            if (scattered) {
-                // SampleLd: light pick (BVH infinite branch) and shadow-ray spawn (1282-1338)
-                const V3 wo = -pd;
-                const float ul = smp.get1d();
-                smp.get1d(); smp.get1d();
-                bool spawned = false;
-                const int nl = P.lights.n;
-                if (nl > 0) {
-                    const float pInf = float(nl) / float(nl + 0);
-                    if (ul < pInf) {
-                        int idx = (int)(ul / pInf * nl);
-                        idx = idx < nl - 1 ? idx : nl - 1;
-                        const DevLight &lt = P.lights.list[idx];
-                        if (lt.type == 0) {
-                            const V3 wi = {lt.w[0], lt.w[1], lt.w[2]};
-                            const Spec Ls = sample_table(light_table(idx), lambda_index(lam)) * lt.scale;
-                            if (Ls.nonzero() && hg_eval(dot(wo, wi), m.g) != 0) {
-                                const V3 pOut = pc + wi * (2 * P.lights.scene_radius);
-                                const V3 d = pOut - pc;
-                                light = idx;
-                                T_ray = sr_l = sr_u = Spec::c(1.f);
-                                rng.set_sequence(hash_3u32(f2u(pc.x), f2u(pc.y), f2u(pc.z)),
-                                                 hash_3u32(f2u(d.x), f2u(d.y), f2u(d.z)));
-                                u = rng.uniform();
-                                seg_begin(m, pc, d, 1 - kShadowEpsilon, sd, it, T_maj, needNext);
-                                po = pc;
-                                mode = M_SHADOW;
-                                spawned = true;
-                                ++nShadow;
-                            }
-                        }
-                    }
-                }
-                if (!spawned) {
-                    L = L + Spec::c(0.f);
-                    po = pc;
-                    phase = true;
-                }
-            } else if (stop) {
-                pathEnd = true;   // absorbed / terminated / beta or r_u vanished
-            } else {
-                // escaped (integrators.cpp:1078-1107)
-                beta = beta * (T_maj / T_maj.v0);
-                r_u = r_u * (T_maj / T_maj.v0);
-                r_l = r_l * (T_maj / T_maj.v0);
-                for (int k = 0; k < P.lights.n; ++k) {
-                    const DevLight &lt = P.lights.list[k];
-                    if (lt.type != 1) continue;
-                    const Spec Le = sample_table(light_table(k), lambda_index(lam)) * lt.scale;
-                    if (!Le.nonzero()) continue;
-                    if (depth == 0) L = L + beta * Le / r_u.avg();
-                    else {
-                        r_l = r_l * ((1.f / (P.lights.n + 0)) * 0.f);
-                        L = L + beta * Le / (r_u + r_l).avg();
-                    }
-                }
-                pathEnd = true;
-            }
-        } else if (mode == M_SHADOW && (stop || segEnd)) {
-            // finish SampleLd (1379-1398); SampleT_maj returns 1 when the callback stopped
-            const Spec Tm = stop ? Spec::c(1.f) : T_maj;
-            T_ray = T_ray * (Tm / Tm.v0);
-            sr_l = sr_l * (Tm / Tm.v0);
-            sr_u = sr_u * (Tm / Tm.v0);
-            Spec contrib = Spec::c(0.f);
-            if (T_ray.nonzero()) {
-                const DevLight &lt = P.lights.list[light];
-                const V3 wi = {lt.w[0], lt.w[1], lt.w[2]};
-                const float pInf = float(P.lights.n) / float(P.lights.n + 0);
-                const float p_l = pInf / P.lights.n * 1.f;
-                const Spec f_hat = Spec::c(hg_eval(dot(-pd, wi), m.g));
-                const Spec Ls = sample_table(light_table(light), lambda_index(lam)) * lt.scale;
-                sr_l = sr_l * (r_u * p_l);
-                contrib = beta * f_hat * T_ray * Ls / sr_l.avg();
-            }
-            L = L + contrib;
-            phase = true;
-        }
-        if (phase) {
-            // phase-function sampling (integrators.cpp:1046-1061), then the next segment
-            const float up0 = smp.get1d(), up1 = smp.get1d();
-            float phPdf;
-            const V3 wi = hg_sample(-pd, m.g, up0, up1, &phPdf);
-            if (phPdf == 0) {
-                pathEnd = true;
-            } else {
-                beta = beta * (phPdf / phPdf);
-                r_l = r_u / phPdf;
-                pd = wi;
-                const float h0 = smp.get1d();
-                const float h1 = smp.get1d();
-                rng.set_sequence(hash_u32(f2u(h0)), hash_u32(f2u(h1)));
-                u = smp.get1d();
-                seg_begin(m, po, pd, kInf, sd, it, T_maj, needNext);
-                mode = M_MEDIUM;
-            }
-        }
-        if (pathEnd) {
-            P.ps.L[g] = to4(L);
-            P.ps.lambda[g] = to4(lam);
-            mode = M_FETCH;
         }
     }
     flush_stat(P.stats, 0, nLookup);

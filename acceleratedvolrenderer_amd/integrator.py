@@ -29,7 +29,7 @@ def shard_samples(spp, rank, world_size):
 
 class VolPathIntegrator:
     def __init__(self, scene, maxdepth=5, spp=16, seed=0, device=0, max_paths=0, lightsampler="bvh",
-                 regularize=False, name="volpath", kernel="persistent"):
+                 regularize=False, name="volpath", kernel="persistent", grid_layout="fat"):
         if name not in INTEGRATOR_NAMES:
             raise ValueError(f"unknown integrator {name!r}")
         if lightsampler not in ("bvh", "uniform", "power"):
@@ -47,6 +47,9 @@ class VolPathIntegrator:
         if kernel not in ("persistent", "wavefront"):
             raise ValueError("kernel must be 'persistent' or 'wavefront'")
         self.ctx.set_kernel_mode(0 if kernel == "persistent" else 1)
+        if grid_layout not in ("fat", "linear"):
+            raise ValueError("grid_layout must be 'fat' or 'linear'")
+        self.ctx.set_grid_layout(1 if grid_layout == "fat" else 0)
         self.ctx.set_scene(scene)
 
     @classmethod

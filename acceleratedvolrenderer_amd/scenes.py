@@ -4,7 +4,9 @@ S-uniform  (config C2): GridMedium n^3 of 1.0 on [0,1]^3, orthographic camera lo
            at the z=0 face through a screen window equal to that face, 512x512.
            variants: "absorber" (sigma_a=1, sigma_s=0, uniform infinite light Le=1 -> analytic
            Beer-Lambert), "furnace" (sigma_a=0, sigma_s=4, uniform infinite Le=1, maxdepth 1000
-           -> L = Le), "scatter" (sigma_a=0.5, sigma_s=2, distant light + sky).
+           -> L = Le), "scatter" (sigma_a=0.5, sigma_s=2, distant light + sky), "chromatic"
+           (wavelength-dependent sigma_a/sigma_s ramps, distant light + sky), "emissive" /
+           "emissive_chromatic" (gray / chromatic sigma, Le with a spatially varying Lescale).
 S-cloud    (metric input): GridMedium n^3 filled with CloudMedium::Density (media.h:496-520,
            density 1, wispiness 1, frequency 5) at voxel centres; sigma_a=0, sigma_s=1,
            scale 4 (albedo 1), g 0.877, distant light + dim sky, perspective 1280x720, maxdepth 100.
@@ -32,6 +34,22 @@ def s_uniform(n=256, width=512, height=512, variant="absorber", density=None):
         med = GridMedium(density, sigma_a=0.5, sigma_s=2.0, g=0.3)
         lights = [DistantLight(from_=(-1.0, 1.0, -1.0), to=(0.0, 0.0, 0.0), scale=2.0),
                   UniformInfiniteLight(scale=0.25)]
+    elif variant in ("chromatic", "emissive", "emissive_chromatic"):
+        # sigma tables that vary over 360..830 nm exercise the 4-wavelength (non-gray) path
+        ramp = np.linspace(0.0, 1.0, spectra.N, dtype=np.float32)
+        chrom = variant != "emissive"
+        sa = (0.2 + 1.0 * ramp).astype(np.float32) if chrom else 0.6
+        ss = (2.5 - 2.0 * ramp).astype(np.float32) if chrom else 1.5
+        le = les = None
+        if variant != "chromatic":
+            le = (0.5 + ramp * ramp).astype(np.float32)
+            d = np.asarray(density) if not hasattr(density, "data_ptr") else None
+            shape = d.shape if d is not None else tuple(int(x) for x in density.shape)
+            z, y, x = np.meshgrid(*(np.linspace(0.0, 1.0, k, dtype=np.float32) for k in shape), indexing="ij")
+            les = (2.0 * x * (1.0 - y) + 0.25 * z).astype(np.float32)
+        med = GridMedium(density, sigma_a=sa, sigma_s=ss, g=-0.2, Le=le, Lescale=les)
+        lights = [DistantLight(from_=(1.0, 1.0, -1.0), to=(0.0, 0.0, 0.0), scale=1.5),
+                  UniformInfiniteLight(scale=0.2)]
     else:
         raise ValueError(variant)
     cam = OrthographicCamera(pos=(0.5, 0.5, -1.0), look=(0.5, 0.5, 0.0), up=(0.0, 1.0, 0.0),

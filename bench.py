@@ -37,12 +37,14 @@ def parse():
     p.add_argument("--res", type=int, default=1024, help="density grid resolution (n^3)")
     p.add_argument("--width", type=int, default=1280)
     p.add_argument("--height", type=int, default=720)
-    p.add_argument("--spp-per-step", type=int, default=4)
+    p.add_argument("--spp-per-step", type=int, default=16)
     p.add_argument("--max-paths", type=int, default=0)
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU-baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--kernel", default="persistent", choices=["persistent", "wavefront"])
     p.add_argument("--refill-min", type=int, default=0, help="k_paths refill threshold (0 = library default)")
+    p.add_argument("--grid-layout", default="fat", choices=["fat", "linear"])
+    p.add_argument("--dda-budget", type=int, default=0, help="k_paths DDA cells per iteration (0 = default)")
     return p.parse_args()
 
 
@@ -110,10 +112,12 @@ def main():
     tgen = time.perf_counter() - tgen
     scene = scenes.s_cloud(density, width=args.width, height=args.height)
     integ = VolPathIntegrator(scene, maxdepth=scenes.CLOUD_MAXDEPTH, spp=args.spp_per_step, seed=0, device=dev,
-                              max_paths=args.max_paths, kernel=args.kernel)
+                              max_paths=args.max_paths, kernel=args.kernel, grid_layout=args.grid_layout)
     S = args.spp_per_step
     if args.refill_min:
         integ.ctx.set_refill_min(args.refill_min)
+    if args.dda_budget:
+        integ.ctx.set_dda_budget(args.dda_budget)
 
     def step(k):
         base = (k * world + rank) * S
@@ -199,6 +203,7 @@ def main():
                 "avg_launch_ms": agg["ms_medium"] / launches,
                 "launches": launches,
             },
+            "grid_layout": "fat" if integ.ctx.grid_layout_active() else "linear",
             "simd_utilisation": (agg["active_lane_iterations"] / (64.0 * agg["loop_iterations"])
                                  if agg.get("loop_iterations") else None),
             "cpu_baseline": cpu,

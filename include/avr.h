@@ -64,6 +64,17 @@ int avr_set_kernel_mode(avr_context *ctx, int mode);
 /* k_paths: refill a wave's idle lanes with new samples once at least `lanes` (1..64)
  * are idle (or none is busy); larger values batch the camera-ray setup across lanes. */
 int avr_set_refill_min(avr_context *ctx, int lanes);
+/* k_paths: majorant-grid cells a lane may cross per tracking iteration before yielding to
+ * the wave (default 4); bounds the divergence of the DDA walk. No effect on results. */
+int avr_set_dda_budget(avr_context *ctx, int cells);
+/* Density layout for the NEXT avr_medium_grid* call: 1 (default) also builds a "fat"
+ * footprint copy — entry (ix,iy,iz) holds the 8 trilinear taps as 32 contiguous bytes,
+ * (n+1)^3 x 32 B, built on device if it fits in free HBM with 8 GiB to spare — so a
+ * density fetch is one 32-B access in one cache line; 0 keeps only pbrt's linear layout
+ * (containers.h:834). Results are bit-identical either way. */
+int avr_set_grid_layout(avr_context *ctx, int layout);
+/* 1 if the current medium uses the fat layout, else 0. */
+int avr_grid_layout_active(avr_context *ctx);
 /* Run all work of this context on `hip_stream` (a hipStream_t; NULL = the context's own stream). */
 int avr_set_stream(avr_context *ctx, void *hip_stream);
 

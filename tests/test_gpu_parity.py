@@ -95,7 +95,7 @@ def test_cloud_generator_bit_exact():
 
 
 @pytest.mark.parametrize("kernel", ["persistent", "wavefront"])
-@pytest.mark.parametrize("variant", ["scatter", "absorber"])
+@pytest.mark.parametrize("variant", ["scatter", "absorber", "chromatic", "emissive", "emissive_chromatic"])
 def test_uniform_box_film_parity(variant, kernel):
     from acceleratedvolrenderer_amd import scenes
     from oracle import binding
@@ -154,6 +154,23 @@ def test_persistent_and_wavefront_kernels_agree_bit_for_bit():
     La = a.ctx.last_pass_samples(npix, 6)[2]
     Lb = b.ctx.last_pass_samples(npix, 6)[2]
     assert np.array_equal(La.view(np.uint32), Lb.view(np.uint32))
+    assert np.array_equal(ra, rb) and np.array_equal(wa, wb)
+    a.close()
+    b.close()
+
+
+def test_fat_and_linear_grid_layouts_agree_bit_for_bit():
+    """The fat footprint copy of the density grid changes where the 8 taps are read from,
+    not their values or the lerp order: films are identical."""
+    from acceleratedvolrenderer_amd import scenes
+    from oracle import binding
+    dens = binding.cloud_grid(20)
+    scene = scenes.s_cloud(dens, width=32, height=18)
+    a = _integrator(scene, maxdepth=scenes.CLOUD_MAXDEPTH, spp=4, grid_layout="fat")
+    b = _integrator(scene, maxdepth=scenes.CLOUD_MAXDEPTH, spp=4, grid_layout="linear")
+    assert a.ctx.grid_layout_active() == 1 and b.ctx.grid_layout_active() == 0
+    ra, wa = a.render()
+    rb, wb = b.render()
     assert np.array_equal(ra, rb) and np.array_equal(wa, wb)
     a.close()
     b.close()
