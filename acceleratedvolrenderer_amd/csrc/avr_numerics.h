@@ -161,11 +161,22 @@ AVR_HD Spec safe_div(Spec a, Spec b) {
 }
 AVR_HD Spec fast_exp(Spec a) { return {fast_exp(a.v0), fast_exp(a.v1), fast_exp(a.v2), fast_exp(a.v3)}; }
 
+// Transcendentals: the correctly rounded float (evaluated in f64, rounded once). pbrt's
+// float libm calls are last-ulp platform-specific (glibc FMA/non-FMA variants, MSVC, CUDA);
+// this is the one convention both this path and the oracle's "canonical" mode implement,
+// so a device sample replays the oracle's bit for bit. Used once per path (wavelengths),
+// per scatter (phase direction) and per accepted free-flight candidate (log).
+AVR_HD float cr_log(float x) { return (float)::log((double)x); }
+AVR_HD float cr_sin(float x) { return (float)::sin((double)x); }
+AVR_HD float cr_cos(float x) { return (float)::cos((double)x); }
+AVR_HD float cr_atanh(float x) { return (float)::atanh((double)x); }
+AVR_HD float cr_cosh(float x) { return (float)::cosh((double)x); }
+
 // Wavelength sampling — sampling.h:163-171, spectrum.h:334-347
-AVR_HD float sample_visible_wavelength(float u) { return 538 - 138.888889f * atanhf(0.85691062f - 1.82750197f * u); }
+AVR_HD float sample_visible_wavelength(float u) { return 538 - 138.888889f * cr_atanh(0.85691062f - 1.82750197f * u); }
 AVR_HD float visible_wavelength_pdf(float l) {
     if (l < 360 || l > 830) return 0;
-    return 0.0039398042f / sqr(coshf(0.0072f * (l - 538)));
+    return 0.0039398042f / sqr(cr_cosh(0.0072f * (l - 538)));
 }
 struct Lambda { Spec l, pdf; };
 AVR_HD Lambda sample_visible(float u) {
@@ -190,7 +201,7 @@ AVR_HD Spec sample_table(const float *t, const LambdaIdx &i) {
 }
 
 // sampling.h:222-225, 79-110
-AVR_HD float sample_exponential(float u, float a) { return -logf(1 - u) / a; }
+AVR_HD float sample_exponential(float u, float a) { return -cr_log(1 - u) / a; }
 AVR_HD int sample_discrete3(float w0, float w1, float w2, float u) {
     float sum = ((0.f + w0) + w1) + w2;
     float up = u * sum;
@@ -220,7 +231,7 @@ AVR_HD V3 hg_sample(V3 wo, float g, float u0, float u1, float *pdf) {
     V3 fx = {1 + sign * sqr(wo.x) * a, sign * b, -sign * wo.x};
     V3 fy = {b, sign + sqr(wo.y) * a, -wo.y};
     float st = clampf(sinTheta, -1, 1);
-    V3 s = {st * cosf(phi), st * sinf(phi), clampf(cosTheta, -1, 1)};
+    V3 s = {st * cr_cos(phi), st * cr_sin(phi), clampf(cosTheta, -1, 1)};
     V3 wi = s.x * fx + s.y * fy + s.z * wo;
     *pdf = hg_eval(cosTheta, g);
     return wi;

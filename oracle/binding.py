@@ -119,7 +119,18 @@ def lib():
         L.oracle_independent_sampler.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                                  ctypes.c_int, ctypes.c_int, c_float_p]
         L.oracle_cloud_grid.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, c_float_p]
+        L.oracle_set_libm.argtypes = [ctypes.c_int]
+        L.oracle_get_libm.restype = ctypes.c_int
     return _lib
+
+
+LIBM_MODES = {"platform": 0, "canonical": 1}
+
+
+def set_libm(mode):
+    """'platform': pbrt's float libm calls as built on this host (pinned by the goldens);
+    'canonical': correctly rounded transcendentals, the HIP path's convention."""
+    lib().oracle_set_libm(LIBM_MODES[mode])
 
 
 def fp(a):
@@ -144,7 +155,10 @@ def cloud_grid(n, z0=0, z1=None):
 class OracleRun:
     """Holds an OracleScene and the numpy buffers it points into."""
 
-    def __init__(self, scene, max_depth=5, seed=0):
+    def __init__(self, scene, max_depth=5, seed=0, libm="platform"):
+        if libm not in LIBM_MODES:
+            raise ValueError(f"libm must be one of {sorted(LIBM_MODES)}")
+        self.libm = libm
         med = scene.medium
         if med.density is None:
             raise ValueError("oracle needs a host density grid")
@@ -200,6 +214,7 @@ class OracleRun:
         L = np.zeros(4, np.float32)
         lam = np.zeros(4, np.float32)
         pdf = np.zeros(4, np.float32)
+        set_libm(self.libm)
         n = lib().oracle_pixel_sample(ctypes.byref(self.s), px, py, sample_index, fp(L), fp(lam), fp(pdf))
         return L, lam, pdf, n
 
@@ -208,6 +223,7 @@ class OracleRun:
         npix = f.width * f.height
         rgb = np.zeros(3 * npix, np.float64)
         w = np.zeros(npix, np.float64)
+        set_libm(self.libm)
         events = lib().oracle_render(ctypes.byref(self.s), spp0, spp1, nthreads, rgb.ctypes.data_as(c_double_p),
                                      w.ctypes.data_as(c_double_p))
         self.last_events = events
@@ -217,6 +233,7 @@ class OracleRun:
         pixels = np.ascontiguousarray(pixels, np.int32)
         rgb = np.zeros(3 * len(pixels), np.float64)
         w = np.zeros(len(pixels), np.float64)
+        set_libm(self.libm)
         events = lib().oracle_render_list(ctypes.byref(self.s), pixels.ctypes.data_as(ctypes.POINTER(ctypes.c_int)),
                                           len(pixels), spp0, spp1, nthreads, rgb.ctypes.data_as(c_double_p),
                                           w.ctypes.data_as(c_double_p))
@@ -226,6 +243,7 @@ class OracleRun:
         p0 = np.ascontiguousarray(p0, np.float32)
         p1 = np.ascontiguousarray(p1, np.float32)
         out = np.zeros(len(p0), np.float32)
+        set_libm(self.libm)
         lib().oracle_transmittance(ctypes.byref(self.s), len(p0), fp(p0), fp(p1), lambda_u, fp(out))
         return out
 
@@ -233,5 +251,6 @@ class OracleRun:
         o = np.ascontiguousarray(o, np.float32)
         d = np.ascontiguousarray(d, np.float32)
         out = np.zeros(3 * max_segs, np.float32)
+        set_libm(self.libm)
         n = lib().oracle_dda_segments(ctypes.byref(self.s), fp(o), fp(d), float(tmax), lambda_u, max_segs, fp(out))
         return out[:3 * n].reshape(n, 3)

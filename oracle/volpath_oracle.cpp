@@ -177,6 +177,21 @@ static inline float Length(V3 v) { return std::sqrt(LengthSquared(v)); }
 static inline V3 Normalize(V3 v) { return v / Length(v); }
 static inline V3 Abs(V3 v) { return {std::abs(v.x), std::abs(v.y), std::abs(v.z)}; }
 
+// libm policy. pbrt calls the float overloads of std::log / sin / cos / atanh / cosh, whose
+// last-ulp results are platform-specific: glibc 2.35 picks FMA or non-FMA variants at load
+// time, and MSVC and CUDA's libdevice differ again. So pbrt's own sample streams differ
+// across builds in ~1% of transcendental calls (then a path may take another, equally valid
+// branch). Mode 0 ("platform", the default) calls them exactly as pbrt does; this is what
+// the golden vectors of the reference harness built here pin. Mode 1 ("canonical") returns
+// the correctly rounded float, evaluated in double and rounded once. The HIP path
+// implements that convention, so device and oracle replay each sample bit for bit.
+static int g_libm = 0;
+static inline float LmLog(float x) { return g_libm ? (float)std::log((double)x) : std::log(x); }
+static inline float LmSin(float x) { return g_libm ? (float)std::sin((double)x) : std::sin(x); }
+static inline float LmCos(float x) { return g_libm ? (float)std::cos((double)x) : std::cos(x); }
+static inline float LmAtanh(float x) { return g_libm ? (float)std::atanh((double)x) : std::atanh(x); }
+static inline float LmCosh(float x) { return g_libm ? (float)std::cosh((double)x) : std::cosh(x); }
+
 // CoordinateSystem / Frame::FromZ / FromLocal — vecmath.h:1007-1013, 1868-1916
 static inline void CoordinateSystem(V3 v1, V3 *v2, V3 *v3) {
     float sign = std::copysign(1.f, v1.z);
@@ -186,7 +201,7 @@ static inline void CoordinateSystem(V3 v1, V3 *v2, V3 *v3) {
     *v3 = {b, sign + Sqr(v1.y) * a, -v1.y};
 }
 static inline V3 SphericalDirection(float sinTheta, float cosTheta, float phi) {  // vecmath.h:1666
-    return {Clamp(sinTheta, -1, 1) * std::cos(phi), Clamp(sinTheta, -1, 1) * std::sin(phi),
+    return {Clamp(sinTheta, -1, 1) * LmCos(phi), Clamp(sinTheta, -1, 1) * LmSin(phi),
             Clamp(cosTheta, -1, 1)};
 }
 
@@ -320,10 +335,10 @@ static inline Spec FastExpSpec(Spec a) { for (int i = 0; i < NS; ++i) a.v[i] = F
 struct Lambda { float lambda[NS], pdf[NS]; };
 // SampleVisibleWavelengths / VisibleWavelengthsPDF — sampling.h:163-171;
 // SampledWavelengths::SampleVisible — spectrum.h:334-347
-static inline float SampleVisibleWavelengths(float u) { return 538 - 138.888889f * std::atanh(0.85691062f - 1.82750197f * u); }
+static inline float SampleVisibleWavelengths(float u) { return 538 - 138.888889f * LmAtanh(0.85691062f - 1.82750197f * u); }
 static inline float VisibleWavelengthsPDF(float l) {
     if (l < 360 || l > 830) return 0;
-    return 0.0039398042f / Sqr(std::cosh(0.0072f * (l - 538)));
+    return 0.0039398042f / Sqr(LmCosh(0.0072f * (l - 538)));
 }
 static inline Lambda SampleVisible(float u) {
     Lambda w;
@@ -347,7 +362,7 @@ static inline Spec SampleDense(const float *table, const Lambda &l) {
 
 // ---------------------------------------------------------------------------
 // Sampling — sampling.h:79-110, 222-225; sampling.cpp:348-372; scattering.h:49-58
-static inline float SampleExponential(float u, float a) { return -std::log(1 - u) / a; }
+static inline float SampleExponential(float u, float a) { return -LmLog(1 - u) / a; }
 static inline int SampleDiscrete3(const float w[3], float u) {
     float sumWeights = 0;
     for (int i = 0; i < 3; ++i) sumWeights += w[i];
@@ -912,6 +927,10 @@ static inline void AddSample(const OracleScene &s, double *rgbSum, double *wSum,
 // C API (ctypes)
 // ===========================================================================
 extern "C" {
+// 0 = platform float libm (pbrt as built on this host), 1 = correctly rounded (HIP convention)
+void oracle_set_libm(int mode) { g_libm = mode ? 1 : 0; }
+int oracle_get_libm() { return g_libm; }
+
 
 // MajorantGrid build — media.cpp:229,241-246 with MajorantGrid::VoxelBounds media.h:123-127
 void oracle_build_majorant(const float *density, int nx, int ny, int nz, int rx, int ry, int rz, float *out) {

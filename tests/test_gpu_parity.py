@@ -4,12 +4,14 @@ seeded inputs. Run on an MI355X with `pytest -m gpu`.
 Tolerances (stated per BASELINE.md §3 "Parity"):
   * integer / index work (majorant max, cloud generator, sample counts): bit-exact;
   * per-sample radiance: the device replays the CPU sample stream (same PCG32/Murmur
-    streams, same float operation order, -ffp-contract=off). Only libm results can
-    differ: glibc 2.35's logf/sinf/cosf are not correctly rounded (0.7-1.3% of inputs
-    differ from the correctly rounded value, atanhf/coshf ~20%) and neither is ocml's,
-    so a 1-ulp difference in a free-flight distance or a phase direction can flip a
-    branch and send that one sample down another (equally valid) path.
-    Required: >= 90% of samples bit-identical (typically 95-100%).
+    streams, same float operation order, -ffp-contract=off) with correctly rounded
+    transcendentals (log/sin/cos/atanh/cosh evaluated in f64, rounded once). The oracle's
+    "canonical" libm mode implements the same convention, so replay is compared to it:
+    >= 99.9% of samples bit-identical (a rare f64 double-rounding difference between glibc
+    and ocml may flip one sample). The oracle's default "platform" mode is pbrt as built
+    here (glibc float libm, pinned by the reference goldens); the two modes agree on ~99%
+    of samples (tests/test_oracle_known_answers.py), and the film test below compares the
+    device to the platform mode.
   * film: relative RMS over pixels between the GPU film and the oracle film at the SAME
     seed must be <= 0.5 x the relative RMS between two oracle films at DIFFERENT seeds
     (i.e. the GPU deviates from the CPU reference by well under its own Monte Carlo
@@ -110,12 +112,17 @@ def test_uniform_box_film_parity(variant, kernel):
     assert np.array_equal(w, w_o)
     err = _rel_rms(integ.image(rgb, w), integ.image(rgb_o, w_o))
     noise = _oracle_noise(scene, 5, spp, integ, rgb_o, w_o)
-    frac, worst_lambda = _compare_samples(integ, ref, 0, spp)
-    print(f"{variant}/{kernel}: film rel RMS {err:.3e} (MC noise {noise:.3e}), bit-exact samples {frac:.4f}, "
-          f"max |dlambda| {worst_lambda:.2e}")
+    canon = binding.OracleRun(scene, max_depth=5, seed=0, libm="canonical")
+    frac, worst_lambda = _compare_samples(integ, canon, 0, spp)
+    rgb_c, w_c = canon.render(0, spp, nthreads=8)
+    err_c = _rel_rms(integ.image(rgb, w), integ.image(rgb_c, w_c))
+    print(f"{variant}/{kernel}: film rel RMS {err:.3e} vs platform oracle (MC noise {noise:.3e}), {err_c:.3e} vs "
+          f"canonical; bit-exact samples {frac:.5f}, max |dlambda| {worst_lambda:.2e}")
     assert worst_lambda < 1e-3
-    assert frac >= 0.90
-    assert err <= (1e-6 if frac == 1.0 else 0.5 * noise)
+    assert frac >= 0.999
+    assert err <= 0.5 * noise
+    if frac == 1.0:
+        assert err_c <= 1e-6
     integ.close()
 
 
@@ -132,9 +139,11 @@ def test_cloud_film_parity_perspective(kernel):
     rgb_o, w_o = ref.render(0, spp, nthreads=8)
     err = _rel_rms(integ.image(rgb, w), integ.image(rgb_o, w_o))
     noise = _oracle_noise(scene, scenes.CLOUD_MAXDEPTH, spp, integ, rgb_o, w_o)
-    frac, _ = _compare_samples(integ, ref, 0, spp)
-    print(f"cloud/{kernel}: film rel RMS {err:.3e} (MC noise {noise:.3e}), bit-exact samples {frac:.4f}")
-    assert frac >= 0.90
+    canon = binding.OracleRun(scene, max_depth=scenes.CLOUD_MAXDEPTH, seed=0, libm="canonical")
+    frac, _ = _compare_samples(integ, canon, 0, spp)
+    print(f"cloud/{kernel}: film rel RMS {err:.3e} vs platform oracle (MC noise {noise:.3e}), "
+          f"bit-exact samples vs canonical {frac:.5f}")
+    assert frac >= 0.999
     assert err <= 0.5 * noise
     integ.close()
 
