@@ -69,10 +69,11 @@ struct avr_context {
     std::vector<hipEvent_t> evpool;
     int last_base = 0, last_S = 0;
     int kernel_mode = 0;      // 0: persistent k_paths (default), 1: wavefront k_medium/k_shadow
+    bool last_persistent = false;   // which organisation the last avr_render ran
     int *d_heads = nullptr;   // 8 per-XCD work counters of k_paths
-    int paths_grid = 0;
+    int paths_grid[4] = {0, 0, 0, 0};   // k_paths<emissive, gray> at index 2*emissive + gray
     int refill_min = 16;
-    int dda_budget = 4;
+    int dda_budget = 12;
     int grid_layout = 1;
     bool gray = false;        // sigma_a and sigma_s constant over 360..830 nm      // 1: build the fat (footprint) copy when memory allows, 0: linear only
     float4 *d_fat = nullptr;
@@ -220,17 +221,25 @@ int avr_context_create(int device, long long max_paths, avr_context **out) {
         return fail(AVR_ERR_HIP, "context allocation failed");
     }
     {
+        // persistent grid per k_paths variant: every admitted block resident. No block ever
+        // waits on another (work is pulled from counters), so the API's answer is safe as is.
+        // The variants differ in VGPRs (gray: 3 waves/SIMD, 4-wavelength: 2), so each gets
+        // its own grid.
         hipDeviceProp_t prop;
-        int blocksPerCU = 0;
-        if (hipGetDeviceProperties(&prop, device) != hipSuccess ||
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocksPerCU, (void (*)(avr::Params))avr::k_paths<false, false>, 256, 0) != hipSuccess) {
+        if (hipGetDeviceProperties(&prop, device) != hipSuccess) {
             delete c;
-            return fail(AVR_ERR_HIP, "occupancy query failed");
+            return fail(AVR_ERR_HIP, "device query failed");
         }
-        // persistent grid: every admitted block resident (MI355X_MICROARCH.md residency notes);
-        // one block per CU fewer than the API answer would also be safe, none is needed here
-        // because no block ever waits on another (work is pulled from counters).
-        c->paths_grid = prop.multiProcessorCount * std::max(1, blocksPerCU);
+        void (*kerns[4])(avr::Params) = {avr::k_paths<false, false>, avr::k_paths<false, true>,
+                                         avr::k_paths<true, false>, avr::k_paths<true, true>};
+        for (int k = 0; k < 4; ++k) {
+            int blocksPerCU = 0;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocksPerCU, kerns[k], 256, 0) != hipSuccess) {
+                delete c;
+                return fail(AVR_ERR_HIP, "occupancy query failed");
+            }
+            c->paths_grid[k] = prop.multiProcessorCount * std::max(1, blocksPerCU);
+        }
     }
     *out = c;
     return AVR_OK;
@@ -438,7 +447,13 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
         p.sample_base = (int)base;
         p.stats = c->d_stats;
         const long long n0 = P * S;
-        if (c->kernel_mode == 0) {
+        // k_paths keeps the majorant grid in LDS (4096 cells = pbrt's 16^3); larger grids
+        // take the wavefront kernels, which read it through L2
+        const bool persistent = c->kernel_mode == 0 &&
+                                c->med.mres[0] * c->med.mres[1] * c->med.mres[2] <= 4096 &&
+                                c->med.mres[0] <= 255 && c->med.mres[1] <= 255 && c->med.mres[2] <= 255;
+        c->last_persistent = persistent;
+        if (persistent) {
             // PCG32 Advance(s*65536) as an affine map state' = A*state + inc*H (rng.h:132-146:
             // every step is linear in inc, so H = accPlus computed with inc = 1).
             if (S > c->advance_cap) {
@@ -470,7 +485,8 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
             // gray medium: sigma_a and sigma_s tables constant over all 471 wavelengths
             void (*kern)(avr::Params) = c->med.emissive ? (c->gray ? avr::k_paths<true, true> : avr::k_paths<true, false>)
                                                         : (c->gray ? avr::k_paths<false, true> : avr::k_paths<false, false>);
-            hipLaunchKernelGGL(kern, dim3(c->paths_grid), dim3(256), 0, c->stream, p);
+            const int grid = c->paths_grid[2 * (c->med.emissive ? 1 : 0) + (c->gray ? 1 : 0)];
+            hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, c->stream, p);
             HIP_TRY(hipGetLastError());
             HIP_TRY(hipEventRecord(e1, c->stream));
             hipLaunchKernelGGL(avr::k_film, dim3(blocks_for(P)), dim3(256), 0, c->stream, p);
@@ -549,8 +565,8 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
     c->stats.shadow_items = h[4];
     c->stats.medium_dda_steps = h[5];
     c->stats.shadow_dda_steps = h[6];
-    c->stats.loop_iterations = c->kernel_mode == 0 ? h[6] : 0;
-    c->stats.active_lane_iterations = c->kernel_mode == 0 ? h[7] : 0;
+    c->stats.loop_iterations = c->last_persistent ? h[6] : 0;
+    c->stats.active_lane_iterations = c->last_persistent ? h[7] : 0;
     return AVR_OK;
 }
 

@@ -651,6 +651,67 @@ __device__ __forceinline__ void seg_begin(const DevMedium &m, V3 o, V3 d, float 
     needNext = true;
 }
 
+// k_paths' DDA: DDAMajorantIterator (media.h:141-214) restated for the persistent kernel.
+// Same segments, bit for bit; the state is laid out for a branch-free step:
+//   voxel (x,y,z)           -> one linear index into the LDS majorant (x-fastest, media.h:112-115)
+//   step[] / voxelLimit[]   -> the sign bit of deltaT[] and a packed count of the cells left
+//                              before the exit face (8 bits per axis; majorant res <= 255)
+struct DdaL {
+    float tMin, tMax;
+    float nx, ny, nz;      // nextCrossingT
+    float dx, dy, dz;      // deltaT, negated when the step along that axis is -1
+    int vidx;              // x + rx * (y + ry * z)
+    int rem;               // cells left: x bits 0-7, y 8-15, z 16-23
+};
+__device__ __forceinline__ void ddal_init(DdaL &q, const DevMedium &m, Ray ray, float raytMax) {
+    Dda it;
+    if (!dda_init(it, m, ray, raytMax)) {
+        q.tMin = kInf; q.tMax = -kInf;
+        q.nx = q.ny = q.nz = q.dx = q.dy = q.dz = 0; q.vidx = 0; q.rem = 0;
+        return;
+    }
+    q.tMin = it.tMin; q.tMax = it.tMax;
+    q.nx = it.nx; q.ny = it.ny; q.nz = it.nz;
+    q.dx = it.sx > 0 ? it.dx : -it.dx;
+    q.dy = it.sy > 0 ? it.dy : -it.dy;
+    q.dz = it.sz > 0 ? it.dz : -it.dz;
+    q.vidx = it.vx + m.mres[0] * (it.vy + m.mres[1] * it.vz);
+    const int cx = it.sx > 0 ? m.mres[0] - 1 - it.vx : it.vx;
+    const int cy = it.sy > 0 ? m.mres[1] - 1 - it.vy : it.vy;
+    const int cz = it.sz > 0 ? m.mres[2] - 1 - it.vz : it.vz;
+    q.rem = cx | (cy << 8) | (cz << 16);
+}
+// Next(): false when exhausted. `maj` is the LDS copy; sy/sz the linear strides of y and z.
+__device__ __forceinline__ bool ddal_next(DdaL &q, const float *maj, int sy, int sz, float *s0, float *s1,
+                                          float *mval) {
+    // fields are copied to values first: a select between struct members invites the
+    // compiler to turn the struct into a scratch array indexed by the axis
+    const float tMin = q.tMin, tMax = q.tMax, nx = q.nx, ny = q.ny, nz = q.nz;
+    const float dx = q.dx, dy = q.dy, dz = q.dz;
+    const int rem = q.rem, vidx = q.vidx;
+    if (tMin >= tMax) return false;
+    // cmpToAxis = {2, 1, 2, 1, 2, 2, 0, 0} over bits (nx<ny, nx<nz, ny<nz)
+    const bool xy = nx < ny, xz = nx < nz, yz = ny < nz;
+    const bool ax0 = xy && xz, ax1 = !xy && yz;
+    const float nextA = ax0 ? nx : (ax1 ? ny : nz);
+    const float dA = ax0 ? dx : (ax1 ? dy : dz);
+    const int shift = ax0 ? 0 : (ax1 ? 8 : 16);
+    const int stride = ax0 ? 1 : (ax1 ? sy : sz);
+    *mval = maj[vidx];
+    *s0 = tMin;
+    const float tExit = fminf_(tMax, nextA);
+    *s1 = tExit;
+    const bool last = ((rem >> shift) & 0xff) == 0;   // voxel + step == voxelLimit
+    q.tMin = (nextA > tMax || last) ? tMax : tExit;
+    q.rem = rem - (1 << shift);
+    q.vidx = vidx + (__builtin_signbit(dA) ? -stride : stride);
+    const float nn = nextA + __builtin_fabsf(dA);
+    q.nx = ax0 ? nn : nx;
+    q.ny = ax1 ? nn : ny;
+    q.nz = (!ax0 && !ax1) ? nn : nz;
+    return true;
+}
+
 #ifndef AVR_PATHS_WAVES_GRAY
 #define AVR_PATHS_WAVES_GRAY 3   // 168 VGPRs, no scratch (4 waves -> 128 VGPRs spills ~100 B/lane)
 #endif
@@ -698,7 +759,8 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
     // samples at path start, NEE and escape (sigma_a, sigma_s, up to 4 light spectra).
     __shared__ float s_maj[4096];
     __shared__ float s_tab[(2 + 4) * kNTable];
-    const float *maj = stage_majorant(P.med, s_maj);
+    // the host routes majorant grids of more than 4096 cells to the wavefront kernels
+    stage_majorant(P.med, s_maj);
     const int nlds = P.lights.n < 4 ? P.lights.n : 4;
     for (int i = threadIdx.x; i < kNTable; i += blockDim.x) {
         s_tab[i] = P.med.sigma_a[i];
@@ -720,6 +782,7 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
 
     int mode = M_FETCH, ev = EV_NONE;
     int g = 0;
+    const int maj_sy = m.mres[0], maj_sz = m.mres[0] * m.mres[1];
     // path state (Li, integrators.cpp:966-971)
     Spec L{}, lam{}, Le_l{};
     S beta{}, r_u{}, r_l{}, sig_a{}, sig_s{};
@@ -729,7 +792,7 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
     // segment state (SampleT_maj)
     Pcg32 rng{};
     float u = 0, tMin = 0, segMax = 0, mv = 0;
-    Dda it{};
+    DdaL it{};
     V3 sd{};               // normalised segment direction
     S T_maj{};
     bool needNext = true, shadowStopped = false;
@@ -738,9 +801,13 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
     S T_ray{}, sr_l{}, sr_u{};
 
     auto seg_start = [&](V3 o, V3 d, float tMax) {
-        Spec tm;
-        seg_begin(m, o, d, tMax, sd, it, tm, needNext);
+        // SampleT_maj prologue (media.h:744-749): normalise, medium-space ray, clip, DDA
+        tMax *= length(d);
+        d = normalize(d);
+        sd = d;
+        ddal_init(it, m, Ray{o, d}, tMax);
         T_maj = sconst<S>(1.f);
+        needNext = true;
     };
 
     while (true) {
@@ -952,53 +1019,76 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
             // v_log_f32 estimate outside a conservative error margin, exactly otherwise and
             // for every accepted collision; each lane crosses at most P.dda_budget cells per
             // iteration, bounding how long early lanes wait for the longest walk.
-            bool collide = false, segEnd = false;
             float t = 0;
             const S sig_t = sig_a + sig_s;
             const float st0 = sv0(sig_t);
-            int budget = P.dda_budget;
-            while (true) {
-                if (needNext) {
-                    if (budget-- == 0) break;
+            // walk: 0 walking, 1 candidate pending (accepted or ambiguous), 2 segments exhausted.
+            // Each step crosses at most one majorant cell and tests at most one candidate; the
+            // loop has one wave-uniform exit so the body stays predicated (no per-exit masks).
+            int walk = 0;
+            for (int b = 0; b < P.dda_budget; ++b) {
+                if (walk == 0 && needNext) {
                     float s0, s1;
-                    if (!dda_next(it, maj, m.mres, &s0, &s1, &mv)) { segEnd = true; break; }
-                    ++nSteps;
-                    const S sigma_maj = sig_t * mv;
-                    if (sv0(sigma_maj) == 0) {
-                        float dt = s1 - s0;
-                        if (__builtin_isinf(dt)) dt = kFloatMax;
-                        T_maj = T_maj * sexp(-(sigma_maj * dt));
-                        continue;
+                    if (!ddal_next(it, s_maj, maj_sy, maj_sz, &s0, &s1, &mv)) {
+                        walk = 2;
+                    } else {
+                        ++nSteps;
+                        // zero-majorant cell: T_maj *= FastExp(-0 * dt); for a gray medium that
+                        // factor is exactly 1, so the multiply is skipped
+                        const S sigma_maj = sig_t * mv;
+                        if (sv0(sigma_maj) == 0) {
+                            if (!kGray) {
+                                float dt = s1 - s0;
+                                if (__builtin_isinf(dt)) dt = kFloatMax;
+                                T_maj = T_maj * sexp(-(sigma_maj * dt));
+                            }
+                        } else {
+                            tMin = s0;
+                            segMax = s1;
+                            needNext = false;
+                        }
                     }
-                    tMin = s0;
-                    segMax = s1;
-                    needNext = false;
                 }
-                const float sm0 = st0 * mv;
-                const float x = 1 - u;
-                const float eFast = -__logf(x) * __builtin_amdgcn_rcpf(sm0);
-                const float tFast = tMin + eFast;
-                const float margin = 1e-5f * __builtin_fabsf(eFast) + 4.8e-7f * __builtin_fabsf(segMax) + 1e-30f;
-                bool accept;
-                if (tFast > segMax + margin) {
-                    accept = false;
-                } else {
-                    t = tMin + sample_exponential(u, sm0);
-                    accept = t < segMax;
+                if (walk == 0 && !needNext) {
+                    // Fast reject: the candidate t = tMin - log(1-u)/sigma_maj is decided against
+                    // segMax from the hardware log2 (v_log_f32, ~1 ulp) when it lies outside an
+                    // error margin bounding |tFast - t| (relative terms for the log and the add,
+                    // an absolute one for log2 near 1); accepted and ambiguous candidates stay
+                    // "pending" and are decided exactly, once per wave, after the walk.
+                    const float sm0 = st0 * mv;
+                    const float rs = __builtin_amdgcn_rcpf(sm0);
+                    const float eFast = -__builtin_amdgcn_logf(1 - u) * (kLn2 * rs);
+                    const float tFast = tMin + eFast;
+                    const float margin = 1e-5f * eFast + 4.8e-7f * __builtin_fabsf(segMax) + 1e-6f * rs + 1e-30f;
+                    if (!(tFast > segMax + margin)) {
+                        walk = 1;
+                    } else {
+                        u = rng.uniform();
+                        float dt = segMax - tMin;
+                        if (__builtin_isinf(dt)) dt = kFloatMax;
+                        T_maj = T_maj * sexp(-((sig_t * mv) * dt));
+                        needNext = true;
+                    }
                 }
-                u = rng.uniform();
-                if (accept) { collide = true; break; }
-                float dt = segMax - tMin;
-                if (__builtin_isinf(dt)) dt = kFloatMax;
-                T_maj = T_maj * sexp(-((sig_t * mv) * dt));
-                needNext = true;
+                if (__ballot(walk == 0) == 0) break;
             }
+            const bool segEnd = walk == 2, pend = walk == 1;
             if (segEnd) {
                 if (mode == M_MEDIUM) ev = EV_ESCAPE;
                 else { ev = EV_SHADOW_DONE; shadowStopped = false; }
                 continue;
             }
-            if (!collide) continue;   // walk budget used up: resume the DDA next iteration
+            if (!pend) continue;   // walk budget used up: resume the DDA next iteration
+            // exact candidate (media.h:770-777): t = tMin + SampleExponential(u, sigma_maj[0])
+            t = tMin + sample_exponential(u, st0 * mv);
+            u = rng.uniform();
+            if (!(t < segMax)) {   // rejected after all: close the segment (media.h:790-801)
+                float dt = segMax - tMin;
+                if (__builtin_isinf(dt)) dt = kFloatMax;
+                T_maj = T_maj * sexp(-((sig_t * mv) * dt));
+                needNext = true;
+                continue;
+            }
             // ---- collision: density fetch for every lane that reached one ----
             const S sigma_maj = sig_t * mv;
             T_maj = T_maj * sexp(-(sigma_maj * (t - tMin)));

@@ -23,6 +23,7 @@ constexpr float kInf = __builtin_huge_valf();
 constexpr float kFloatMax = 3.40282346638528859812e+38f;
 constexpr float kPi = 3.14159265358979323846f;
 constexpr float kInv4Pi = 0.07957747154594766788f;
+constexpr float kLn2 = 0.693147180559945309f;
 constexpr float kShadowEpsilon = 0.0001f;
 constexpr float kMachineEpsilon = 5.96046448e-08f;  // FLT_EPSILON/2
 AVR_HD float gamma_n(int n) { return (n * kMachineEpsilon) / (1 - n * kMachineEpsilon); }
@@ -166,11 +167,19 @@ AVR_HD Spec fast_exp(Spec a) { return {fast_exp(a.v0), fast_exp(a.v1), fast_exp(
 // this is the one convention both this path and the oracle's "canonical" mode implement,
 // so a device sample replays the oracle's bit for bit. Used once per path (wavelengths),
 // per scatter (phase direction) and per accepted free-flight candidate (log).
+#ifndef AVR_FLOAT_LIBM
 AVR_HD float cr_log(float x) { return (float)::log((double)x); }
 AVR_HD float cr_sin(float x) { return (float)::sin((double)x); }
 AVR_HD float cr_cos(float x) { return (float)::cos((double)x); }
 AVR_HD float cr_atanh(float x) { return (float)::atanh((double)x); }
 AVR_HD float cr_cosh(float x) { return (float)::cosh((double)x); }
+#else   // measurement-only build (cost of the canonical convention); breaks replay parity
+AVR_HD float cr_log(float x) { return logf(x); }
+AVR_HD float cr_sin(float x) { return sinf(x); }
+AVR_HD float cr_cos(float x) { return cosf(x); }
+AVR_HD float cr_atanh(float x) { return atanhf(x); }
+AVR_HD float cr_cosh(float x) { return coshf(x); }
+#endif
 
 // Wavelength sampling — sampling.h:163-171, spectrum.h:334-347
 AVR_HD float sample_visible_wavelength(float u) { return 538 - 138.888889f * cr_atanh(0.85691062f - 1.82750197f * u); }
