@@ -960,8 +960,7 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
                     smp.rng.set_sequence(seq, mix_bits(seq));
                     // == smp.rng.advance((sample_base + sIdx) * 65536) (rng.h:132-146), precomputed
                     smp.rng.state = P.advance[2 * sIdx] * smp.rng.state + smp.rng.inc * P.advance[2 * sIdx + 1];
-                    const Lambda lw = sample_visible(smp.get1d());
-                    lam = lw.l;
+                    lam = sample_visible_lambda(smp.get1d());   // pdf: recomputed by k_film
                     const float fu0 = smp.get1d(), fu1 = smp.get1d();
                     const float fpx = lerp(fu0, -P.film.filter_rx, P.film.filter_rx);
                     const float fpy = lerp(fu1, -P.film.filter_ry, P.film.filter_ry);

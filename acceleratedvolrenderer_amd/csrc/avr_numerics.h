@@ -15,6 +15,7 @@
 #include <stdint.h>
 
 #define AVR_HD __host__ __device__ __forceinline__
+#include "avr_canon.h"
 
 namespace avr {
 
@@ -162,23 +163,22 @@ AVR_HD Spec safe_div(Spec a, Spec b) {
 }
 AVR_HD Spec fast_exp(Spec a) { return {fast_exp(a.v0), fast_exp(a.v1), fast_exp(a.v2), fast_exp(a.v3)}; }
 
-// Transcendentals: the correctly rounded float (evaluated in f64, rounded once). pbrt's
-// float libm calls are last-ulp platform-specific (glibc FMA/non-FMA variants, MSVC, CUDA);
-// this is the one convention both this path and the oracle's "canonical" mode implement,
-// so a device sample replays the oracle's bit for bit. Used once per path (wavelengths),
-// per scatter (phase direction) and per accepted free-flight candidate (log).
+// Transcendentals: the canonical convention of avr_canon.h (f64 evaluation by a fixed IEEE
+// op sequence, one rounding to float; the correctly rounded float except within ~1e-16 of a
+// midpoint). pbrt's float libm calls are last-ulp platform-specific (glibc FMA/non-FMA
+// variants, MSVC, CUDA); the oracle's "canonical" mode restates the same sequences, so a
+// device sample replays the oracle's bit for bit. Used once per path (wavelengths), per
+// scatter (phase direction) and per accepted free-flight candidate (log).
 #ifndef AVR_FLOAT_LIBM
-AVR_HD float cr_log(float x) { return (float)::log((double)x); }
-AVR_HD float cr_sin(float x) { return (float)::sin((double)x); }
-AVR_HD float cr_cos(float x) { return (float)::cos((double)x); }
-AVR_HD float cr_atanh(float x) { return (float)::atanh((double)x); }
-AVR_HD float cr_cosh(float x) { return (float)::cosh((double)x); }
+AVR_HD float cr_log(float x) { return canon::log_f(x); }
+AVR_HD float cr_atanh(float x) { return canon::atanh_f(x); }
+AVR_HD float cr_cosh(float x) { return canon::cosh_f(x); }
+AVR_HD void cr_sincos(float x, float *s, float *c) { canon::sincos_f(x, s, c); }
 #else   // measurement-only build (cost of the canonical convention); breaks replay parity
 AVR_HD float cr_log(float x) { return logf(x); }
-AVR_HD float cr_sin(float x) { return sinf(x); }
-AVR_HD float cr_cos(float x) { return cosf(x); }
 AVR_HD float cr_atanh(float x) { return atanhf(x); }
 AVR_HD float cr_cosh(float x) { return coshf(x); }
+AVR_HD void cr_sincos(float x, float *s, float *c) { *s = sinf(x); *c = cosf(x); }
 #endif
 
 // Wavelength sampling — sampling.h:163-171, spectrum.h:334-347
@@ -188,12 +188,32 @@ AVR_HD float visible_wavelength_pdf(float l) {
     return 0.0039398042f / sqr(cr_cosh(0.0072f * (l - 538)));
 }
 struct Lambda { Spec l, pdf; };
+// Device: the four f64 evaluations are kept apart (scheduling barriers) so their
+// temporaries are not all live at once in the register-bound path kernel.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define AVR_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
+#else
+#define AVR_SCHED_FENCE() ((void)0)
+#endif
+AVR_HD float visible_up(float u, int i) {
+    float up = u + float(i) / 4;
+    if (up > 1) up -= 1;
+    return up;
+}
+AVR_HD Spec sample_visible_lambda(float u) {
+    Spec l;
+    l.v0 = sample_visible_wavelength(visible_up(u, 0));
+    AVR_SCHED_FENCE();
+    l.v1 = sample_visible_wavelength(visible_up(u, 1));
+    AVR_SCHED_FENCE();
+    l.v2 = sample_visible_wavelength(visible_up(u, 2));
+    AVR_SCHED_FENCE();
+    l.v3 = sample_visible_wavelength(visible_up(u, 3));
+    return l;
+}
 AVR_HD Lambda sample_visible(float u) {
-    float up[4];
-    _Pragma("unroll") for (int i = 0; i < 4; ++i) { up[i] = u + float(i) / 4; if (up[i] > 1) up[i] -= 1; }
     Lambda w;
-    w.l = {sample_visible_wavelength(up[0]), sample_visible_wavelength(up[1]), sample_visible_wavelength(up[2]),
-           sample_visible_wavelength(up[3])};
+    w.l = sample_visible_lambda(u);
     w.pdf = {visible_wavelength_pdf(w.l.v0), visible_wavelength_pdf(w.l.v1), visible_wavelength_pdf(w.l.v2),
              visible_wavelength_pdf(w.l.v3)};
     return w;
@@ -240,7 +260,9 @@ AVR_HD V3 hg_sample(V3 wo, float g, float u0, float u1, float *pdf) {
     V3 fx = {1 + sign * sqr(wo.x) * a, sign * b, -sign * wo.x};
     V3 fy = {b, sign + sqr(wo.y) * a, -wo.y};
     float st = clampf(sinTheta, -1, 1);
-    V3 s = {st * cr_cos(phi), st * cr_sin(phi), clampf(cosTheta, -1, 1)};
+    float sinPhi, cosPhi;
+    cr_sincos(phi, &sinPhi, &cosPhi);
+    V3 s = {st * cosPhi, st * sinPhi, clampf(cosTheta, -1, 1)};
     V3 wi = s.x * fx + s.y * fy + s.z * wo;
     *pdf = hg_eval(cosTheta, g);
     return wi;

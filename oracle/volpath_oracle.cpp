@@ -182,15 +182,103 @@ static inline V3 Abs(V3 v) { return {std::abs(v.x), std::abs(v.y), std::abs(v.z)
 // time, and MSVC and CUDA's libdevice differ again. So pbrt's own sample streams differ
 // across builds in ~1% of transcendental calls (then a path may take another, equally valid
 // branch). Mode 0 ("platform", the default) calls them exactly as pbrt does; this is what
-// the golden vectors of the reference harness built here pin. Mode 1 ("canonical") returns
-// the correctly rounded float, evaluated in double and rounded once. The HIP path
-// implements that convention, so device and oracle replay each sample bit for bit.
+// the golden vectors of the reference harness built here pin. Mode 1 ("canonical") is the
+// HIP path's convention: each function evaluated in f64 by a fixed sequence of IEEE ops
+// (+ - * / fma), then rounded once to float, which is the correctly rounded float except
+// within ~1e-16 of a midpoint. Restated here from the convention's definition (coefficients
+// 1/(2k+1) and 1/k!, two-part Cody-Waite constants) independently of the device header
+// acceleratedvolrenderer_amd/csrc/avr_canon.h; parity tests require the two to agree.
 static int g_libm = 0;
-static inline float LmLog(float x) { return g_libm ? (float)std::log((double)x) : std::log(x); }
-static inline float LmSin(float x) { return g_libm ? (float)std::sin((double)x) : std::sin(x); }
-static inline float LmCos(float x) { return g_libm ? (float)std::cos((double)x) : std::cos(x); }
-static inline float LmAtanh(float x) { return g_libm ? (float)std::atanh((double)x) : std::atanh(x); }
-static inline float LmCosh(float x) { return g_libm ? (float)std::cosh((double)x) : std::cosh(x); }
+namespace canon {
+static const double kLn2Hi = 0x1.62e42fee00000p-1, kLn2Lo = 0x1.a39ef35793c76p-33;
+static const double kPio2Hi = 0x1.921fb54400000p+0, kPio2Lo = 0x1.0b4611a626331p-34;
+static const double kTwoOverPi = 0x1.45f306dc9c883p-1, kInvLn2 = 0x1.71547652b82fep+0;
+static const double kSqrt2 = 0x1.6a09e667f3bcdp+0;
+// 1/k!, k = 0..23, each the nearest double to the exact rational
+static const double kInvFact[24] = {
+    0x1.0000000000000p+0, 0x1.0000000000000p+0, 0x1.0000000000000p-1, 0x1.5555555555555p-3,
+    0x1.5555555555555p-5, 0x1.1111111111111p-7, 0x1.6c16c16c16c17p-10, 0x1.a01a01a01a01ap-13,
+    0x1.a01a01a01a01ap-16, 0x1.71de3a556c734p-19, 0x1.27e4fb7789f5cp-22, 0x1.ae64567f544e4p-26,
+    0x1.1eed8eff8d898p-29, 0x1.6124613a86d09p-33, 0x1.93974a8c07c9dp-37, 0x1.ae7f3e733b81fp-41,
+    0x1.ae7f3e733b81fp-45, 0x1.952c77030ad4ap-49, 0x1.6827863b97d97p-53, 0x1.2f49b46814157p-57,
+    0x1.e542ba4020225p-62, 0x1.71b8ef6dcf572p-66, 0x1.0ce396db7f853p-70, 0x1.761b41316381ap-75,
+};
+static double InvFact(int k) { return kInvFact[k]; }
+// Horner over c[0] (highest power) .. c[n-1] with fma
+static double Horner(const double *c, int n, double z) {
+    double p = c[0];
+    for (int i = 1; i < n; ++i) p = std::fma(p, z, c[i]);
+    return p;
+}
+struct Tables {
+    double atanh[12], sinp[8], cosp[8], expp[18];
+    Tables() {
+        for (int i = 0; i < 12; ++i) atanh[i] = 1.0 / (23 - 2 * i);              // 1/23 .. 1/1
+        for (int i = 0; i < 8; ++i) sinp[i] = ((7 - i) % 2 ? -1 : 1) * InvFact(15 - 2 * i);   // -1/15! .. 1
+        for (int i = 0; i < 8; ++i) cosp[i] = ((7 - i) % 2 ? -1 : 1) * InvFact(16 - 2 * i);   // -1/16! .. 1/2
+        for (int i = 0; i < 18; ++i) expp[i] = InvFact(17 - i);                  // 1/17! .. 1
+    }
+};
+static const Tables T;
+static double Log(double x) {
+    if (!(x > 0)) return x == 0 ? -INFINITY : NAN;
+    if (std::isinf(x)) return x;
+    uint64_t b;
+    std::memcpy(&b, &x, 8);
+    int e = (int)((b >> 52) & 0x7ff) - 1023;
+    uint64_t mb = (b & 0x000fffffffffffffull) | 0x3ff0000000000000ull;
+    double m;
+    std::memcpy(&m, &mb, 8);
+    if (m > kSqrt2) { m = m * 0.5; e += 1; }
+    double s = (m - 1.0) / (m + 1.0);
+    double t = 2.0 * s * Horner(T.atanh, 12, s * s);
+    return std::fma((double)e, kLn2Hi, std::fma((double)e, kLn2Lo, t));
+}
+static double Atanh(double x) {
+    if (std::fabs(x) <= 0.171) return x * Horner(T.atanh, 12, x * x);
+    return 0.5 * Log((1.0 + x) / (1.0 - x));
+}
+static void SinCos(double x, double *sn, double *cs) {
+    double kf = std::rint(x * kTwoOverPi);
+    double r = (x - kf * kPio2Hi) - kf * kPio2Lo;
+    double z = r * r;
+    double sr = r * Horner(T.sinp, 8, z);
+    double cr = std::fma(-z, Horner(T.cosp, 8, z), 1.0);
+    switch ((int)kf & 3) {
+    case 0: *sn = sr; *cs = cr; break;
+    case 1: *sn = cr; *cs = -sr; break;
+    case 2: *sn = -sr; *cs = -cr; break;
+    default: *sn = -cr; *cs = sr; break;
+    }
+}
+static double Exp(double x) {
+    double kf = std::rint(x * kInvLn2);
+    double r = (x - kf * kLn2Hi) - kf * kLn2Lo;
+    double p = Horner(T.expp, 18, r);
+    uint64_t sb = (uint64_t)((int)kf + 1023) << 52;
+    double sc;
+    std::memcpy(&sc, &sb, 8);
+    return p * sc;
+}
+static double Cosh(double x) {
+    double e = Exp(std::fabs(x));
+    return 0.5 * (e + 1.0 / e);
+}
+}  // namespace canon
+static inline float LmLog(float x) { return g_libm ? (float)canon::Log((double)x) : std::log(x); }
+static inline float LmAtanh(float x) { return g_libm ? (float)canon::Atanh((double)x) : std::atanh(x); }
+static inline float LmCosh(float x) { return g_libm ? (float)canon::Cosh((double)x) : std::cosh(x); }
+static inline void LmSinCos(float x, float *s, float *c) {
+    if (g_libm) {
+        double sd, cd;
+        canon::SinCos((double)x, &sd, &cd);
+        *s = (float)sd;
+        *c = (float)cd;
+    } else {
+        *s = std::sin(x);
+        *c = std::cos(x);
+    }
+}
 
 // CoordinateSystem / Frame::FromZ / FromLocal — vecmath.h:1007-1013, 1868-1916
 static inline void CoordinateSystem(V3 v1, V3 *v2, V3 *v3) {
@@ -201,7 +289,9 @@ static inline void CoordinateSystem(V3 v1, V3 *v2, V3 *v3) {
     *v3 = {b, sign + Sqr(v1.y) * a, -v1.y};
 }
 static inline V3 SphericalDirection(float sinTheta, float cosTheta, float phi) {  // vecmath.h:1666
-    return {Clamp(sinTheta, -1, 1) * LmCos(phi), Clamp(sinTheta, -1, 1) * LmSin(phi),
+    float sinPhi, cosPhi;
+    LmSinCos(phi, &sinPhi, &cosPhi);
+    return {Clamp(sinTheta, -1, 1) * cosPhi, Clamp(sinTheta, -1, 1) * sinPhi,
             Clamp(cosTheta, -1, 1)};
 }
 
@@ -930,6 +1020,16 @@ extern "C" {
 // 0 = platform float libm (pbrt as built on this host), 1 = correctly rounded (HIP convention)
 void oracle_set_libm(int mode) { g_libm = mode ? 1 : 0; }
 int oracle_get_libm() { return g_libm; }
+// the canonical convention's float functions (tests)
+float oracle_canon_log(float x) { return (float)canon::Log((double)x); }
+float oracle_canon_atanh(float x) { return (float)canon::Atanh((double)x); }
+float oracle_canon_cosh(float x) { return (float)canon::Cosh((double)x); }
+void oracle_canon_sincos(float x, float *s, float *c) {
+    double sd, cd;
+    canon::SinCos((double)x, &sd, &cd);
+    *s = (float)sd;
+    *c = (float)cd;
+}
 
 
 // MajorantGrid build — media.cpp:229,241-246 with MajorantGrid::VoxelBounds media.h:123-127

@@ -1,0 +1,25 @@
+#!/bin/bash
+# GPU pass l: canonical transcendentals as fixed f64 sequences (no ocml), coefficients
+# materialised at use (no spills) — parity tests, A/B against the previous commit.
+set -u
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/l
+mkdir -p $O
+export PYTHONUNBUFFERED=1
+step() {   # name timeout cmd... ; stops the script on any nonzero status
+  local name=$1 t=$2; shift 2
+  timeout -k 10 $t "$@" > $O/$name.log 2>&1; local rc=$?
+  echo "$name rc=$rc"
+  [ $rc -eq 0 ] || { echo "stop: $name rc=$rc"; tail -20 $O/$name.log; exit $rc; }
+}
+step gpu_tests 900 python -m pytest tests -m gpu -x -q -s -rA
+B="python bench.py --steps 3 --warmup 1 --no-cpu-baseline"
+step ab_base 300 $B
+step ab_prev 300 env AVR_LIB=$R/variants/libavr_prev.so $B
+step ab_g4 300 env AVR_LIB=$R/variants/libavr_g4.so $B
+step ab_fl 300 env AVR_LIB=$R/variants/libavr_fl.so $B
+step ab_b16 300 $B --dda-budget 16
+step ab_r8 300 $B --refill-min 8
+step ab_r24 300 $B --refill-min 24
+step ab_base2 300 $B
+exit 0
