@@ -71,6 +71,7 @@ SIGNATURES = {
     "avr_render": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     "avr_sync": (ctypes.c_int, [ctypes.c_void_p]),
     "avr_get_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(AvrStats)]),
+    "avr_reset_stats": (ctypes.c_int, [ctypes.c_void_p]),
     "avr_film_read": (ctypes.c_int, [ctypes.c_void_p, c_double_p, c_double_p]),
     "avr_film_device_ptrs": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p),
                                             ctypes.POINTER(ctypes.c_void_p)]),
@@ -197,7 +198,11 @@ class Context:
     def sync(self):
         _check(self.lib.avr_sync(self.h))
 
+    def reset_stats(self):
+        _check(self.lib.avr_reset_stats(self.h))
+
     def stats(self):
+        """Counters and kernel times accumulated since creation or reset_stats()."""
         s = AvrStats()
         _check(self.lib.avr_get_stats(self.h, ctypes.byref(s)))
         return s.as_dict()

@@ -66,20 +66,22 @@ struct avr_context {
     unsigned long long *d_stats = nullptr;
     int *h_count = nullptr;   // pinned
     avr_stats stats{};
-    std::vector<hipEvent_t> evpool;
+    std::vector<hipEvent_t> evpool;   // timing events; the first ev_used are recorded, unresolved
+    size_t ev_used = 0;
+    struct Timed { int a, b; double avr_stats::*field; bool launch; };
+    std::vector<Timed> timed;         // pending (event a -> event b) intervals to fold into stats
     int last_base = 0, last_S = 0;
     int kernel_mode = 0;      // 0: persistent k_paths (default), 1: wavefront k_medium/k_shadow
     bool last_persistent = false;   // which organisation the last avr_render ran
     int *d_heads = nullptr;   // 8 per-XCD work counters of k_paths
     int paths_grid[4] = {0, 0, 0, 0};   // k_paths<emissive, gray> at index 2*emissive + gray
-    int refill_min = 16;
+    int refill_min = 32;
     int dda_budget = 12;
     int grid_layout = 1;
     bool gray = false;        // sigma_a and sigma_s constant over 360..830 nm      // 1: build the fat (footprint) copy when memory allows, 0: linear only
     float4 *d_fat = nullptr;
     uint64_t *d_advance = nullptr;  // per-pass PCG advance table {A, H}
     long long advance_cap = 0;
-    std::vector<uint64_t> h_advance;
 };
 
 namespace {
@@ -216,7 +218,8 @@ int avr_context_create(int device, long long max_paths, avr_context **out) {
         delete c;
         return fail(AVR_ERR_HIP, "context allocation failed");
     }
-    if (dalloc(&c->d_heads, 8) != hipSuccess) {
+    if (dalloc(&c->d_heads, 8) != hipSuccess ||
+        hipMemset(c->d_stats, 0, sizeof(unsigned long long) * avr::kNumStats) != hipSuccess) {
         delete c;
         return fail(AVR_ERR_HIP, "context allocation failed");
     }
@@ -410,6 +413,55 @@ int avr_film_clear(avr_context *c) {
     return AVR_OK;
 }
 
+// Stats are resolved lazily so that a render stays asynchronous: every timed interval
+// records two pool events and is folded (one stream sync) when stats are read.
+static int fold_stats(avr_context *c) {
+    if (c->timed.empty()) return AVR_OK;
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    for (const auto &t : c->timed) {
+        float ms = 0;
+        HIP_TRY(hipEventElapsedTime(&ms, c->evpool[t.a], c->evpool[t.b]));
+        c->stats.*(t.field) += ms;
+        if (t.launch) c->stats.medium_launches++;
+    }
+    c->timed.clear();
+    c->ev_used = 0;
+    unsigned long long h[avr::kNumStats];
+    HIP_TRY(hipMemcpy(h, c->d_stats, sizeof(h), hipMemcpyDeviceToHost));
+    c->stats.medium_lookups = h[0];
+    c->stats.medium_items_in = h[1];
+    c->stats.medium_items_out = h[2];
+    c->stats.shadow_lookups = h[3];
+    c->stats.shadow_items = h[4];
+    c->stats.medium_dda_steps = h[5];
+    c->stats.shadow_dda_steps = h[6];
+    c->stats.loop_iterations = h[8];
+    c->stats.active_lane_iterations = h[9];
+    return AVR_OK;
+}
+
+// next free pool event (folds first when the pool is full)
+static int next_event(avr_context *c, int *idx) {
+    if (c->ev_used >= 512) {
+        int rc = fold_stats(c);
+        if (rc) return rc;
+    }
+    if (c->ev_used == c->evpool.size()) {
+        hipEvent_t e;
+        HIP_TRY(hipEventCreate(&e));
+        c->evpool.push_back(e);
+    }
+    *idx = (int)c->ev_used++;
+    HIP_TRY(hipEventRecord(c->evpool[*idx], c->stream));
+    return AVR_OK;
+}
+#define EV_MARK(var)                      \
+    int var;                              \
+    do {                                  \
+        int rc_ = next_event(c, &var);    \
+        if (rc_) return rc_;              \
+    } while (0)
+
 int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_depth) {
     if (!c) return fail(AVR_ERR_ARG, "null context");
     if (!c->has_medium || !c->has_camera || !c->has_film) return fail(AVR_ERR_STATE, "medium, camera and film required");
@@ -421,16 +473,7 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
     const long long need = P * std::min<long long>(Smax, std::max(1, spp_end - spp_begin));
     int rc = ensure_paths(c, need);
     if (rc) return rc;
-    if (c->evpool.empty()) {
-        c->evpool.resize(10);
-        for (auto &e : c->evpool) HIP_TRY(hipEventCreate(&e));
-    }
-    hipEvent_t evStart = c->evpool[0], evEnd = c->evpool[1];
-    hipEvent_t e0 = c->evpool[2], e1 = c->evpool[3], e2 = c->evpool[4], e3 = c->evpool[5];
-    c->stats = {};
-    HIP_TRY(hipMemsetAsync(c->d_stats, 0, sizeof(unsigned long long) * avr::kNumStats, c->stream));
-    HIP_TRY(hipEventRecord(evStart, c->stream));
-    float ms = 0;
+    EV_MARK(evStart);
     for (long long base = spp_begin; base < spp_end; base += Smax) {
         const int S = (int)std::min<long long>(Smax, spp_end - base);
         avr::Params p{};
@@ -461,54 +504,36 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
                 HIP_TRY(dalloc(&c->d_advance, 2 * (size_t)S));
                 c->advance_cap = S;
             }
-            c->h_advance.resize(2 * (size_t)S);
-            for (int s = 0; s < S; ++s) {
-                uint64_t delta = (uint64_t)(base + s) * 65536ull;
-                uint64_t curMult = 0x5851f42d4c957f2dULL, curPlus = 1, accMult = 1, accPlus = 0;
-                while (delta > 0) {
-                    if (delta & 1) { accMult *= curMult; accPlus = accPlus * curMult + curPlus; }
-                    curPlus = (curMult + 1) * curPlus;
-                    curMult *= curMult;
-                    delta /= 2;
-                }
-                c->h_advance[2 * s] = accMult;
-                c->h_advance[2 * s + 1] = accPlus;
-            }
-            HIP_TRY(hipMemcpyAsync(c->d_advance, c->h_advance.data(), 2 * (size_t)S * sizeof(uint64_t),
-                                   hipMemcpyHostToDevice, c->stream));
+            hipLaunchKernelGGL(avr::k_advance, dim3((S + 255) / 256), dim3(256), 0, c->stream, c->d_advance,
+                               (long long)base, S);
+            HIP_TRY(hipGetLastError());
             p.advance = c->d_advance;
             p.refill_min = c->refill_min;
             p.dda_budget = c->dda_budget;
             p.heads = c->d_heads;
             HIP_TRY(hipMemsetAsync(c->d_heads, 0, 8 * sizeof(int), c->stream));
-            HIP_TRY(hipEventRecord(e0, c->stream));
+            EV_MARK(e0);
             // gray medium: sigma_a and sigma_s tables constant over all 471 wavelengths
             void (*kern)(avr::Params) = c->med.emissive ? (c->gray ? avr::k_paths<true, true> : avr::k_paths<true, false>)
                                                         : (c->gray ? avr::k_paths<false, true> : avr::k_paths<false, false>);
             const int grid = c->paths_grid[2 * (c->med.emissive ? 1 : 0) + (c->gray ? 1 : 0)];
             hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, c->stream, p);
             HIP_TRY(hipGetLastError());
-            HIP_TRY(hipEventRecord(e1, c->stream));
+            EV_MARK(e1);
             hipLaunchKernelGGL(avr::k_film, dim3(blocks_for(P)), dim3(256), 0, c->stream, p);
             HIP_TRY(hipGetLastError());
-            HIP_TRY(hipEventRecord(e2, c->stream));
-            HIP_TRY(hipEventSynchronize(e2));
-            HIP_TRY(hipEventElapsedTime(&ms, e0, e1));
-            c->stats.ms_medium += ms;
-            c->stats.medium_launches++;
-            HIP_TRY(hipEventElapsedTime(&ms, e1, e2));
-            c->stats.ms_film += ms;
+            EV_MARK(e2);
+            c->timed.push_back({e0, e1, &avr_stats::ms_medium, true});
+            c->timed.push_back({e1, e2, &avr_stats::ms_film, false});
             c->last_base = (int)base;
             c->last_S = S;
             continue;
         }
-        HIP_TRY(hipEventRecord(e0, c->stream));
+        EV_MARK(c0);
         hipLaunchKernelGGL(avr::k_camera, dim3(blocks_for(n0)), dim3(256), 0, c->stream, p);
         HIP_TRY(hipGetLastError());
-        HIP_TRY(hipEventRecord(e1, c->stream));
-        HIP_TRY(hipEventSynchronize(e1));
-        HIP_TRY(hipEventElapsedTime(&ms, e0, e1));
-        c->stats.ms_camera += ms;
+        EV_MARK(c1);
+        c->timed.push_back({c0, c1, &avr_stats::ms_camera, false});
         c->h_count[0] = (int)n0;
         HIP_TRY(hipMemcpyAsync(c->d_counts, c->h_count, sizeof(int), hipMemcpyHostToDevice, c->stream));
         int cur = 0;
@@ -524,49 +549,32 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
             p.count_out = c->d_counts + nxt;
             p.shadow_count = c->d_counts + 2;
             const int nb = blocks_for(count);
-            HIP_TRY(hipEventRecord(e0, c->stream));
+            EV_MARK(m0);
             hipLaunchKernelGGL(avr::k_medium, dim3(nb), dim3(256), 0, c->stream, p);
             HIP_TRY(hipGetLastError());
-            HIP_TRY(hipEventRecord(e1, c->stream));
+            EV_MARK(m1);
             hipLaunchKernelGGL(avr::k_shadow, dim3(nb), dim3(256), 0, c->stream, p);
             HIP_TRY(hipGetLastError());
-            HIP_TRY(hipEventRecord(e2, c->stream));
+            EV_MARK(m2);
+            c->timed.push_back({m0, m1, &avr_stats::ms_medium, true});
+            c->timed.push_back({m1, m2, &avr_stats::ms_shadow, false});
+            // the queue length decides the next launch: the wavefront organisation syncs here
             HIP_TRY(hipMemcpyAsync(c->h_count, c->d_counts + nxt, sizeof(int), hipMemcpyDeviceToHost, c->stream));
             HIP_TRY(hipStreamSynchronize(c->stream));
-            HIP_TRY(hipEventElapsedTime(&ms, e0, e1));
-            c->stats.ms_medium += ms;
-            HIP_TRY(hipEventElapsedTime(&ms, e1, e2));
-            c->stats.ms_shadow += ms;
-            c->stats.medium_launches++;
             count = c->h_count[0];
             cur = nxt;
             first = false;
         }
-        HIP_TRY(hipEventRecord(e2, c->stream));
+        EV_MARK(f0);
         hipLaunchKernelGGL(avr::k_film, dim3(blocks_for(P)), dim3(256), 0, c->stream, p);
         HIP_TRY(hipGetLastError());
-        HIP_TRY(hipEventRecord(e3, c->stream));
-        HIP_TRY(hipEventSynchronize(e3));
-        HIP_TRY(hipEventElapsedTime(&ms, e2, e3));
-        c->stats.ms_film += ms;
+        EV_MARK(f1);
+        c->timed.push_back({f0, f1, &avr_stats::ms_film, false});
         c->last_base = (int)base;
         c->last_S = S;
     }
-    HIP_TRY(hipEventRecord(evEnd, c->stream));
-    HIP_TRY(hipEventSynchronize(evEnd));
-    HIP_TRY(hipEventElapsedTime(&ms, evStart, evEnd));
-    c->stats.ms_total = ms;
-    unsigned long long h[avr::kNumStats];
-    HIP_TRY(hipMemcpy(h, c->d_stats, sizeof(h), hipMemcpyDeviceToHost));
-    c->stats.medium_lookups = h[0];
-    c->stats.medium_items_in = h[1];
-    c->stats.medium_items_out = h[2];
-    c->stats.shadow_lookups = h[3];
-    c->stats.shadow_items = h[4];
-    c->stats.medium_dda_steps = h[5];
-    c->stats.shadow_dda_steps = h[6];
-    c->stats.loop_iterations = c->last_persistent ? h[6] : 0;
-    c->stats.active_lane_iterations = c->last_persistent ? h[7] : 0;
+    EV_MARK(evEnd);
+    c->timed.push_back({evStart, evEnd, &avr_stats::ms_total, false});
     return AVR_OK;
 }
 
@@ -578,7 +586,21 @@ int avr_sync(avr_context *c) {
 
 int avr_get_stats(avr_context *c, avr_stats *out) {
     if (!c || !out) return fail(AVR_ERR_ARG, "null arg");
+    HIP_TRY(hipSetDevice(c->device));
+    int rc = fold_stats(c);
+    if (rc) return rc;
     *out = c->stats;
+    return AVR_OK;
+}
+
+int avr_reset_stats(avr_context *c) {
+    if (!c) return fail(AVR_ERR_ARG, "null context");
+    HIP_TRY(hipSetDevice(c->device));
+    int rc = fold_stats(c);
+    if (rc) return rc;
+    c->stats = {};
+    HIP_TRY(hipMemsetAsync(c->d_stats, 0, sizeof(unsigned long long) * avr::kNumStats, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
     return AVR_OK;
 }
 

@@ -87,7 +87,7 @@ struct ShadowSoA {
 // [2] items out k_medium (survivors + shadow pushes), [3] lookups k_shadow, [4] items k_shadow,
 // [5] DDA steps k_medium, [6] DDA steps k_shadow; k_paths: [6] loop iterations (per wave),
 // [7] sum over iterations of active lanes (SIMD utilisation = [7] / (64 * [6]))
-constexpr int kNumStats = 8;
+constexpr int kNumStats = 10;   // 0-6 wavefront/shared work counters, 8-9 k_paths wave loop
 
 struct Params {
     DevMedium med;
@@ -712,6 +712,28 @@ __device__ __forceinline__ bool ddal_next(DdaL &q, const float *maj, int sy, int
     return true;
 }
 
+// PCG32 Advance(s * 65536) of sample index s (IndependentSampler::StartPixelSample,
+// samplers.h:457-460; rng.h:132-146) as an affine map state' = A * state + inc * H: every
+// step of the log-time loop is linear in inc, so H is the loop's accPlus run with inc = 1.
+// One entry per sample index of a pass; k_paths applies it to each pixel's stream.
+__global__ void k_advance(uint64_t *adv, long long base, int S) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= S) return;
+    uint64_t delta = (uint64_t)(base + s) * 65536ull;
+    uint64_t curMult = 0x5851f42d4c957f2dULL, curPlus = 1, accMult = 1, accPlus = 0;
+    while (delta > 0) {
+        if (delta & 1) {
+            accMult *= curMult;
+            accPlus = accPlus * curMult + curPlus;
+        }
+        curPlus = (curMult + 1) * curPlus;
+        curMult *= curMult;
+        delta /= 2;
+    }
+    adv[2 * s] = accMult;
+    adv[2 * s + 1] = accPlus;
+}
+
 #ifndef AVR_PATHS_WAVES_GRAY
 #define AVR_PATHS_WAVES_GRAY 3   // 168 VGPRs, no scratch (4 waves -> 128 VGPRs spills ~100 B/lane)
 #endif
@@ -796,6 +818,8 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
     V3 sd{};               // normalised segment direction
     S T_maj{};
     bool needNext = true, shadowStopped = false;
+    bool segPending = false;      // a segment start is queued for the shared block below
+    uint64_t seqA = 0, seqB = 0;  // its RNG SetSequence arguments
     // shadow state (SampleLd, integrators.cpp:1339-1391)
     int light = 0;
     S T_ray{}, sr_l{}, sr_u{};
@@ -835,10 +859,11 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
                                 const V3 d = pOut - po;
                                 light = idx;
                                 T_ray = sr_l = sr_u = sconst<S>(1.f);
-                                rng.set_sequence(hash_3u32(f2u(po.x), f2u(po.y), f2u(po.z)),
-                                                 hash_3u32(f2u(d.x), f2u(d.y), f2u(d.z)));
-                                u = rng.uniform();
-                                seg_start(po, d, 1 - kShadowEpsilon);
+                                // shadow-ray RNG (integrators.cpp:1338); u is its first draw
+                                seqA = hash_3u32(f2u(po.x), f2u(po.y), f2u(po.z));
+                                seqB = hash_3u32(f2u(d.x), f2u(d.y), f2u(d.z));
+                                sd = d;
+                                segPending = true;
                                 mode = M_SHADOW;
                                 ev = EV_NONE;
                                 ++nShadow;
@@ -884,9 +909,11 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
                     pd = wi;
                     const float h0 = smp.get1d();
                     const float h1 = smp.get1d();
-                    rng.set_sequence(hash_u32(f2u(h0)), hash_u32(f2u(h1)));
+                    seqA = hash_u32(f2u(h0));
+                    seqB = hash_u32(f2u(h1));
                     u = smp.get1d();
-                    seg_start(po, pd, kInf);
+                    sd = pd;
+                    segPending = true;
                     mode = M_MEDIUM;
                     ev = EV_NONE;
                 }
@@ -991,13 +1018,26 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
                     // first medium segment: RNG from two sampler dims, u from a third (984-989)
                     const float h0 = smp.get1d();
                     const float h1 = smp.get1d();
-                    rng.set_sequence(hash_u32(f2u(h0)), hash_u32(f2u(h1)));
+                    seqA = hash_u32(f2u(h0));
+                    seqB = hash_u32(f2u(h1));
                     u = smp.get1d();
-                    seg_start(po, pd, kInf);
+                    sd = pd;
+                    segPending = true;
                     mode = M_MEDIUM;
                 } else if (exhausted) {
                     mode = M_DONE;
                 }
+            }
+        }
+        // =================== segment starts, shared by the NEE shadow ray, the phase-sampled
+        // continuation and the camera ray: RNG(seqA, seqB), then SampleT_maj's prologue
+        // (medium-space ray, clip, DDA setup) once per batch for every lane that needs one
+        if (__ballot(segPending)) {
+            if (segPending) {
+                rng.set_sequence(seqA, seqB);
+                if (mode == M_SHADOW) u = rng.uniform();
+                seg_start(po, sd, mode == M_SHADOW ? 1 - kShadowEpsilon : kInf);
+                segPending = false;
             }
         }
         if (__ballot(mode != M_DONE) == 0) break;
@@ -1172,8 +1212,8 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
     flush_stat(P.stats, 3, nShadowLookup);
     flush_stat(P.stats, 4, nShadow);
     flush_stat(P.stats, 5, nSteps);
-    flush_stat(P.stats, 6, nIter);
-    flush_stat(P.stats, 7, nActive);
+    flush_stat(P.stats, 8, nIter);
+    flush_stat(P.stats, 9, nActive);
 }
 
 // ---------------------------------------------------------------------------

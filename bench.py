@@ -8,8 +8,9 @@ camera rays -> delta tracking -> ratio-tracked shadow rays -> film). Each rank r
 its own disjoint sample indices (weak scaling); the fp64 film is SUM-reduced over RCCL
 once at the end of the timed region (T_render ends at the film reduce).
 
-Prints ONE JSON line (rank 0) with roofline (k_medium, the delta-tracking / density-fetch
-kernel) and cpu_baseline (the oracle restatement on a bounded sample of the same workload).
+Prints ONE JSON line (rank 0) with roofline (k_paths, the fused delta-tracking /
+ratio-tracking / density-fetch kernel; HIP-event time of its launches on the context stream)
+and cpu_baseline (the oracle restatement on a bounded sample of the same workload).
 """
 import argparse
 import json
@@ -120,34 +121,34 @@ def main():
         integ.ctx.set_dda_budget(args.dda_budget)
 
     def step(k):
+        # asynchronous on the context stream: steps queue back to back
         base = (k * world + rank) * S
         integ.ctx.render(base, base + S, 0, scenes.CLOUD_MAXDEPTH)
-        return integ.ctx.stats()
 
     for k in range(args.warmup):
         step(k)
     integ.ctx.film_clear()
+    integ.ctx.reset_stats()   # waits for the warmup; counters and kernel times restart
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    agg = {}
     for k in range(args.warmup, args.warmup + args.steps):
-        st = step(k)
-        for key, v in st.items():
-            agg[key] = agg.get(key, 0) + v
+        step(k)
     # final film reduce over RCCL (part of T_render)
     npix = args.width * args.height
     buf = torch.empty(4 * npix, dtype=torch.float64, device=f"cuda:{dev}")
     integ.ctx.film_export_device(buf.data_ptr())
     if world > 1:
         dist.reduce(buf, dst=0, op=dist.ReduceOp.SUM)
+    integ.ctx.sync()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    agg = integ.ctx.stats()   # device counters + per-launch HIP-event times of the timed steps
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{dev}")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -168,6 +169,19 @@ def main():
         med_bytes = BYTES_PER_LOOKUP * agg["medium_lookups"] + BYTES_PER_ITEM * (agg["medium_items_in"] +
                                                                                 agg["medium_items_out"])
     achieved = med_bytes / med_s / 1e9 if med_s > 0 else 0.0
+    # HBM traffic per launch from the committed rocprofv3 PMC passes of this kernel on this
+    # workload (FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md HBM section); bench.py
+    # itself cannot read counters. Null when the profile does not match the run.
+    traffic, traffic_src, valu = None, None, None
+    prof = os.path.join(ROOT, "profiles", "r01_pmc_k_paths.json")
+    if args.kernel == "persistent" and n == 1024 and S == 16 and os.path.exists(prof):
+        pm = json.load(open(prof))
+        traffic = round(pm["hbm_traffic_bytes_per_launch"] / 1e9, 3)
+        traffic_src = "profiles/r01_pmc_k_paths.json (GB per launch, PMC FETCH_SIZE x2 + WRITE_SIZE)"
+        # the bound that is actually close: VALU issue (wave64 op = 2 SIMD cycles)
+        valu = {"wave_instructions_per_launch": pm["valu_wave_instructions_per_launch"],
+                "issue_fraction": round(pm["valu_issue_fraction"], 4),
+                "wave_cycle_split": pm["wave_cycle_split"], "source": "profiles/r01_pmc_k_paths.json"}
     out = None
     if rank == 0:
         cpu = None
@@ -198,11 +212,13 @@ def main():
                 "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBPS, 5),
-                "traffic": None,
+                "traffic": traffic,
+                "traffic_source": traffic_src,
                 "bytes_per_launch": med_bytes / launches,
                 "avg_launch_ms": agg["ms_medium"] / launches,
                 "launches": launches,
             },
+            "valu": valu,
             "grid_layout": "fat" if integ.ctx.grid_layout_active() else "linear",
             "simd_utilisation": (agg["active_lane_iterations"] / (64.0 * agg["loop_iterations"])
                                  if agg.get("loop_iterations") else None),

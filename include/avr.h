@@ -33,8 +33,9 @@ extern "C" {
 
 typedef struct avr_context avr_context;
 
-/* Work counters and kernel times of the last avr_render call (pbrt's
- * ReportKernelStats analogue, wavefront/wavefront.cpp:47-56). */
+/* Work counters and kernel times accumulated over every avr_render call since the context
+ * was created or avr_reset_stats (pbrt's ReportKernelStats analogue,
+ * wavefront/wavefront.cpp:47-56). Resolved when read: rendering never waits for them. */
 typedef struct avr_stats {
     unsigned long long medium_lookups;  /* SamplePoint density fetches in k_medium   */
     unsigned long long medium_items_in; /* work items consumed by k_medium           */
@@ -44,7 +45,7 @@ typedef struct avr_stats {
     unsigned long long medium_dda_steps;
     unsigned long long shadow_dda_steps;
     unsigned long long medium_launches;
-    unsigned long long loop_iterations;        /* k_paths: wave loop iterations           */
+    unsigned long long loop_iterations;        /* k_paths: wave tracking iterations       */
     unsigned long long active_lane_iterations; /* k_paths: sum of busy lanes per iteration */
     double ms_camera, ms_medium, ms_shadow, ms_film; /* summed hipEvent times      */
     double ms_total;                                  /* first launch .. film done  */
@@ -126,7 +127,8 @@ int avr_film_clear(avr_context *ctx);
  * VolPathIntegrator maxdepth. Asynchronous on the context stream. */
 int avr_render(avr_context *ctx, int spp_begin, int spp_end, int seed, int max_depth);
 int avr_sync(avr_context *ctx);
-int avr_get_stats(avr_context *ctx, avr_stats *out);
+int avr_get_stats(avr_context *ctx, avr_stats *out);   /* waits for queued work */
+int avr_reset_stats(avr_context *ctx);
 
 /* Film readback: rgb_sum[W*H*3] and w_sum[W*H] (fp64 RGBFilm::Pixel sums). */
 int avr_film_read(avr_context *ctx, double *rgb_sum, double *w_sum);

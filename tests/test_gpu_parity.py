@@ -230,3 +230,28 @@ def test_white_furnace():
     _, ns, L, _, _ = integ.ctx.last_pass_samples(W * H, spp)
     assert np.all(L == 1.0)
     integ.close()
+
+
+@pytest.mark.parametrize("kernel", ["persistent", "wavefront"])
+def test_stats_accumulate_reset_and_count_every_sample_once(kernel):
+    """avr_get_stats folds asynchronously recorded counters: every (pixel, sample) path is
+    started exactly once, counters accumulate over renders until avr_reset_stats."""
+    from acceleratedvolrenderer_amd import scenes
+    n, W, H = 16, 24, 20
+    dens = (0.25 + np.random.default_rng(2).random((n, n, n), dtype=np.float32)).astype(np.float32)
+    scene = scenes.s_uniform(n=n, width=W, height=H, variant="scatter", density=dens)
+    integ = _integrator(scene, maxdepth=5, spp=6, kernel=kernel, max_paths=W * H * 4)   # 2 passes per render
+    integ.ctx.reset_stats()
+    integ.ctx.render(0, 6, 0, 5)
+    integ.ctx.render(6, 9, 0, 5)
+    st = integ.ctx.stats()
+    if kernel == "persistent":
+        assert st["medium_items_in"] == W * H * 9          # paths started
+    else:
+        assert st["medium_items_in"] >= W * H * 9          # queue items over all launches
+    assert st["medium_lookups"] > 0 and st["ms_medium"] > 0 and st["ms_total"] > 0
+    assert st["medium_launches"] >= (3 if kernel == "persistent" else 4)
+    integ.ctx.reset_stats()
+    st = integ.ctx.stats()
+    assert st["medium_items_in"] == 0 and st["ms_medium"] == 0 and st["medium_launches"] == 0
+    integ.close()
