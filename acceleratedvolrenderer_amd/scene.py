@@ -154,14 +154,61 @@ class PerspectiveCamera(_ProjectiveCamera):
         return xf.perspective(self.fov, 1e-2, 1000.0)
 
 
+class BoxFilter:
+    """BoxFilter (filters.h:48-77; Create filters.cpp: radius default 0.5)."""
+    type_id = 0
+
+    def __init__(self, radius=(0.5, 0.5)):
+        self.radius = np.asarray(radius, np.float32)
+        self.sigma = np.float32(0)
+
+
+class GaussianFilter:
+    """GaussianFilter (filters.h:80-118; Create filters.cpp: radius 1.5, sigma 0.5) — pbrt's
+    default filter (scene.cpp:94). Sampled through FilterSampler's tabulated distribution;
+    samples carry weight f/pdf."""
+    type_id = 1
+
+    def __init__(self, radius=(1.5, 1.5), sigma=0.5):
+        self.radius = np.asarray(radius, np.float32)
+        self.sigma = np.float32(sigma)
+        if not (self.radius > 0).all() or int(32 * self.radius[0]) < 1 or int(32 * self.radius[1]) < 1:
+            raise ValueError("gaussian filter radius too small")
+        if int(32 * self.radius[0]) > 128 or int(32 * self.radius[1]) > 128:
+            raise ValueError("gaussian filter radius above 4 is not supported")
+
+
+class IndependentSampler:
+    """IndependentSampler (samplers.h:442-476): PCG32 stream per (pixel, sampleIndex)."""
+    type_id = 0
+
+    def __init__(self, pixelsamples=16, seed=None):
+        self.pixelsamples = int(pixelsamples)
+        self.seed = seed
+
+
+class ZSobolSampler:
+    """ZSobolSampler (samplers.h:225-330) with FastOwen randomisation — pbrt's default
+    sampler (scene.cpp:93). pixelsamples should be a power of two (Warning otherwise)."""
+    type_id = 1
+
+    def __init__(self, pixelsamples=16, seed=None, randomization="fastowen"):
+        if randomization != "fastowen":
+            raise NotImplementedError("only the default FastOwen randomisation is implemented")
+        self.pixelsamples = int(pixelsamples)
+        self.seed = seed
+
+
 class RGBFilm:
-    """RGBFilm (film.h:232-316) with a box filter and the cie1931 PixelSensor (film.cpp:212-250)."""
+    """RGBFilm (film.h:232-316) with the cie1931 PixelSensor (film.cpp:212-250) and a box
+    (default here) or Gaussian pixel filter."""
 
     def __init__(self, xresolution=1280, yresolution=720, filter_radius=(0.5, 0.5), iso=100.0, exposure_time=1.0,
-                 maxcomponentvalue=math.inf):
+                 maxcomponentvalue=math.inf, filter=None):
         self.width = int(xresolution)
         self.height = int(yresolution)
-        self.filter_radius = np.asarray(filter_radius, np.float32)
+        self.filter = filter if filter is not None else BoxFilter(filter_radius)
+        self.filter_radius = self.filter.radius
         self.imaging_ratio = np.float32(np.float32(exposure_time) * np.float32(iso) / np.float32(100))
         self.max_component_value = np.float32(maxcomponentvalue)
         self.sensor = spectra.sensor_cie1931()
@@ -184,8 +231,9 @@ def _bounding_sphere_radius(pmin, pmax):
 class Scene:
     """Resolved render-space scene (CameraWorld rendering space, cameras.cpp:35-41)."""
 
-    def __init__(self, camera, film, medium, lights):
+    def __init__(self, camera, film, medium, lights, sampler=None):
         self.camera, self.film, self.medium, self.lights = camera, film, medium, list(lights)
+        self.sampler = sampler if sampler is not None else IndependentSampler()
         if len(self.lights) > 8:
             raise ValueError("at most 8 lights")
         wfc = camera.world_from_camera()

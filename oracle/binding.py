@@ -58,6 +58,10 @@ class OracleScene(ctypes.Structure):
         ("max_component_value", ctypes.c_float),
         ("max_depth", ctypes.c_int),
         ("seed", ctypes.c_int),
+        ("sampler_type", ctypes.c_int),
+        ("samples_per_pixel", ctypes.c_int),
+        ("filter_type", ctypes.c_int),
+        ("filter_sigma", ctypes.c_float),
     ]
 
 
@@ -71,7 +75,14 @@ def lib():
         L = _lib
         L.oracle_pixel_sample.restype = ctypes.c_int
         L.oracle_pixel_sample.argtypes = [ctypes.POINTER(OracleScene), ctypes.c_int, ctypes.c_int, ctypes.c_int,
-                                          c_float_p, c_float_p, c_float_p]
+                                          c_float_p, c_float_p, c_float_p, c_float_p]
+        L.oracle_zsobol.argtypes = [ctypes.c_int] * 7 + [ctypes.c_char_p, c_float_p]
+        L.oracle_sobol_fastowen.restype = ctypes.c_float
+        L.oracle_sobol_fastowen.argtypes = [ctypes.c_ulonglong, ctypes.c_int, ctypes.c_uint]
+        L.oracle_sobol_plain.restype = ctypes.c_float
+        L.oracle_sobol_plain.argtypes = [ctypes.c_ulonglong, ctypes.c_int]
+        L.oracle_gaussian_filter_sample.argtypes = [ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_int,
+                                                    c_float_p, c_float_p]
         L.oracle_render.restype = ctypes.c_longlong
         L.oracle_render.argtypes = [ctypes.POINTER(OracleScene), ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                     c_double_p, c_double_p]
@@ -206,16 +217,24 @@ class OracleRun:
         s.max_component_value = float(f.max_component_value)
         s.max_depth = int(max_depth)
         s.seed = int(seed)
+        smp = scene.sampler
+        s.sampler_type = int(smp.type_id)
+        s.samples_per_pixel = int(smp.pixelsamples)
+        s.filter_type = int(f.filter.type_id)
+        s.filter_sigma = float(f.filter.sigma)
         self.s = s
         self.keep = keep
         self.scene = scene
 
-    def pixel_sample(self, px, py, sample_index):
+    def pixel_sample(self, px, py, sample_index, with_weight=False):
         L = np.zeros(4, np.float32)
         lam = np.zeros(4, np.float32)
         pdf = np.zeros(4, np.float32)
+        w = np.zeros(1, np.float32)
         set_libm(self.libm)
-        n = lib().oracle_pixel_sample(ctypes.byref(self.s), px, py, sample_index, fp(L), fp(lam), fp(pdf))
+        n = lib().oracle_pixel_sample(ctypes.byref(self.s), px, py, sample_index, fp(L), fp(lam), fp(pdf), fp(w))
+        if with_weight:
+            return L, lam, pdf, n, w[0]
         return L, lam, pdf, n
 
     def render(self, spp0, spp1, nthreads=1):
@@ -254,3 +273,19 @@ class OracleRun:
         set_libm(self.libm)
         n = lib().oracle_dda_segments(ctypes.byref(self.s), fp(o), fp(d), float(tmax), lambda_u, max_segs, fp(out))
         return out[:3 * n].reshape(n, 3)
+
+
+def zsobol_stream(spp, resx, resy, px, py, sample_index, seed, pattern):
+    """ZSobolSampler outputs for a pattern of '1' (Get1D) / '2' (Get2D) calls."""
+    n = sum(1 if c == "1" else 2 for c in pattern)
+    out = np.zeros(n, np.float32)
+    lib().oracle_zsobol(spp, resx, resy, px, py, sample_index, seed, pattern.encode(), fp(out))
+    return out
+
+
+def gaussian_filter_samples(rx, ry, sigma, u):
+    """GaussianFilter::Sample for u (n x 2): rows (p.x, p.y, weight)."""
+    u = np.ascontiguousarray(u, np.float32)
+    out = np.zeros((len(u), 3), np.float32)
+    lib().oracle_gaussian_filter_sample(rx, ry, sigma, len(u), fp(u), fp(out))
+    return out

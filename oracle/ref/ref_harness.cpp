@@ -11,7 +11,10 @@
 //   SampledGrid::Lookup/MaxValue (util/containers.h:765-870),
 //   Bounds3::IntersectP (util/vecmath.h:1547-1571),
 //   Transform::operator()/ApplyInverse(Ray) (util/transform.h:340-433),
-//   IndependentSampler (samplers.h:442-476), Noise/DNoise (util/noise.cpp),
+//   IndependentSampler (samplers.h:442-476), ZSobolSampler (samplers.h:225-330),
+//   SobolSample + FastOwenScrambler (util/lowdiscrepancy.h:168-237),
+//   GaussianFilter / FilterSampler (filters.h:26-118, filters.cpp:133-147),
+//   Noise/DNoise (util/noise.cpp),
 //   Blackbody (util/spectrum.h:69-80), CIE/D65 tables (util/spectrum.cpp),
 //   sRGB RGBFromXYZ (util/colorspace.cpp).
 // Output: JSON on stdout (golden vectors) and, with --tables <file>, a raw
@@ -28,6 +31,7 @@
 #include <pbrt/util/noise.h>
 #include <pbrt/util/colorspace.h>
 #include <pbrt/samplers.h>
+#include <pbrt/filters.h>
 
 #include <cstdio>
 #include <cstring>
@@ -314,6 +318,72 @@ int main(int argc, char **argv) {
             printf("%s{\"px\":%d,\"py\":%d,\"s\":%d,\"seed\":%d,\"dims\":", c ? "," : "", cases[c][0],
                    cases[c][1], cases[c][2], cases[c][3]);
             arr_u32(v); printf(",\"from_dim6\":"); arr_u32(v6); printf("}");
+        }
+        printf("]");
+    }
+
+    // ---- ZSobolSampler (samplers.h:225-330), FastOwen randomisation ---------
+    // Call pattern per case: the dimension consumption of one VolPath sample (SURVEY
+    // Appendix A): 1D (lambda), pixel 2D (filter), 1D (time), 2D (lens), then 1D x3 per
+    // segment and 1D + 2D + 2D per scatter, repeated.
+    {
+        j.key("zsobol");
+        printf("[");
+        struct Case { int spp, resx, resy, px, py, s, seed; };
+        const Case cases[] = {{16, 1280, 720, 0, 0, 0, 0},     {16, 1280, 720, 17, 5, 3, 0},
+                              {16, 1280, 720, 1279, 719, 15, 0}, {16, 1280, 720, 640, 360, 7, 7},
+                              {1, 1280, 720, 100, 200, 0, 0},    {2, 1280, 720, 100, 200, 1, 0},
+                              {8, 1280, 720, 33, 44, 5, 3},      {64, 1920, 1080, 1919, 1079, 63, 0},
+                              {256, 1280, 720, 321, 123, 200, 0}, {4, 32, 32, 31, 0, 2, 1}};
+        const char *pattern = "1212111111221112211122";
+        int ci = 0;
+        for (const Case &c : cases) {
+            ZSobolSampler zs(c.spp, Point2i(c.resx, c.resy), RandomizeStrategy::FastOwen, c.seed);
+            zs.StartPixelSample(Point2i(c.px, c.py), c.s, 0);
+            std::vector<uint32_t> v;
+            for (const char *q = pattern; *q; ++q) {
+                if (*q == '1') v.push_back(fb(zs.Get1D()));
+                else { Point2f u = (q == pattern + 1) ? zs.GetPixel2D() : zs.Get2D(); v.push_back(fb(u.x)); v.push_back(fb(u.y)); }
+            }
+            printf("%s{\"spp\":%d,\"resx\":%d,\"resy\":%d,\"px\":%d,\"py\":%d,\"s\":%d,\"seed\":%d,\"pattern\":\"%s\",\"u\":",
+                   ci++ ? "," : "", c.spp, c.resx, c.resy, c.px, c.py, c.s, c.seed, pattern);
+            arr_u32(v);
+            printf("}");
+        }
+        printf("]");
+        // SobolSample(a, dim, FastOwenScrambler(seed)) for dims 0, 1 (the two ZSobol uses)
+        j.key("sobol_fastowen");
+        printf("[");
+        RNG rng(5, 9);
+        for (int i = 0; i < 64; ++i) {
+            uint64_t a = i < 8 ? (uint64_t)i : (uint64_t)rng.Uniform<uint32_t>();
+            uint32_t seed = rng.Uniform<uint32_t>();
+            printf("%s[\"%llu\",%u,%u,%u,%u,%u]", i ? "," : "", (unsigned long long)a, seed,
+                   fb(SobolSample(a, 0, FastOwenScrambler(seed))), fb(SobolSample(a, 1, FastOwenScrambler(seed))),
+                   fb(SobolSample(a, 0, NoRandomizer())), fb(SobolSample(a, 1, NoRandomizer())));
+        }
+        printf("]");
+    }
+
+    // ---- GaussianFilter sampling (filters.h:80-118, filters.cpp:133-147) -----
+    {
+        j.key("gaussian_filter");
+        printf("[");
+        const float cfg[][3] = {{1.5f, 1.5f, 0.5f}, {0.5f, 0.5f, 0.5f}, {2.f, 1.f, 0.75f}};
+        RNG rng(11, 3);
+        for (int c = 0; c < 3; ++c) {
+            GaussianFilter gf(Vector2f(cfg[c][0], cfg[c][1]), cfg[c][2]);
+            printf("%s{\"rx\":%u,\"ry\":%u,\"sigma\":%u,\"samples\":[", c ? "," : "", fb(cfg[c][0]), fb(cfg[c][1]),
+                   fb(cfg[c][2]));
+            for (int i = 0; i < 96; ++i) {
+                Point2f u(rng.Uniform<Float>(), rng.Uniform<Float>());
+                if (i == 0) u = Point2f(0.f, 0.f);
+                if (i == 1) u = Point2f(0.99999994f, 0.99999994f);
+                if (i == 2) u = Point2f(0.5f, 0.5f);
+                FilterSample fs = gf.Sample(u);
+                printf("%s[%u,%u,%u,%u,%u]", i ? "," : "", fb(u.x), fb(u.y), fb(fs.p.x), fb(fs.p.y), fb(fs.weight));
+            }
+            printf("]}");
         }
         printf("]");
     }

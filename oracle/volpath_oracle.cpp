@@ -121,6 +121,13 @@ static inline uint64_t MixBits(uint64_t v) {
 }
 static inline uint64_t HashBytes(const void *p, size_t n) { return MurmurHash64A((const unsigned char *)p, n, 0); }
 static inline uint64_t HashFloat(float f) { return HashBytes(&f, 4); }
+// Hash(int, int): the variadic Hash packs its arguments' bytes (util/hash.h:94-106)
+static inline uint64_t HashInts2(int a, int b) {
+    unsigned char buf[8];
+    std::memcpy(buf, &a, 4);
+    std::memcpy(buf + 4, &b, 4);
+    return HashBytes(buf, 8);
+}
 static inline uint64_t HashPixelSeed(int x, int y, int seed) {
     int buf[3] = {x, y, seed};
     return HashBytes(buf, 12);
@@ -647,26 +654,239 @@ typedef struct OracleScene {
     float render_from_camera[16];
     // RGBFilm (film.h:232-316) + cie1931 PixelSensor (film.h:95-100)
     int width, height;
-    float filter_radius[2];           // box filter
+    float filter_radius[2];           // filter radius (box or gaussian)
     const float *sensor_xyz;          // 3 x 471: X, Y, Z matching functions
     float imaging_ratio;
     float output_from_sensor[9];      // colorSpace->RGBFromXYZ * XYZFromSensorRGB
     float max_component_value;
-    // VolPathIntegrator (integrators.cpp:1401-1409) + IndependentSampler seed
+    // VolPathIntegrator (integrators.cpp:1401-1409) + sampler seed
     int max_depth;
     int seed;
+    // sampler (samplers.h): 0 IndependentSampler, 1 ZSobolSampler (FastOwen); its
+    // samplesPerPixel (ZSobol's Morton layout depends on it) — film full resolution = width x height
+    int sampler_type;
+    int samples_per_pixel;
+    // pixel filter (filters.h): 0 BoxFilter, 1 GaussianFilter(radius = filter_radius, sigma)
+    int filter_type;
+    float filter_sigma;
 } OracleScene;
 
 }  // extern "C"
 
 namespace oracle {
 
+// ---------------------------------------------------------------------------
+// Samplers (samplers.h). IndependentSampler — samplers.h:442-476: Get2D = two Get1D.
+// ZSobolSampler — samplers.h:225-330 with RandomizeStrategy::FastOwen (the default): the
+// pixel's Morton index with the sample index appended, each base-4 digit permuted by a
+// hash of the higher digits and the dimension, then a scrambled Sobol' point of
+// dimension 0 (1D) or dimensions 0 and 1 (2D) — lowdiscrepancy.h:168-180, 220-237.
+
+// Sobol' generator matrices of dimensions 0 and 1 (sobolmatrices.cpp, first two rows),
+// from their definition: dimension 0 is the van der Corput radical inverse (column i =
+// bit 31-i); dimension 1 is the Pascal matrix mod 2 (direction numbers of x + 1):
+// column i = column i-1 XOR (column i-1 >> 1). Columns >= 32 do not exist in 32 bits and
+// ZSobol indices stay below 2^32 (checked by the host).
+static uint32_t SobolColumn(int dim, int i) {
+    if (i >= 32) return 0;
+    if (dim == 0) return 1u << (31 - i);
+    uint32_t v = 0x80000000u;
+    for (int k = 1; k <= i; ++k) v ^= v >> 1;
+    return v;
+}
+static uint32_t SobolBits(uint64_t a, int dim) {
+    uint32_t v = 0;
+    for (int i = 0; a != 0; a >>= 1, ++i)
+        if (a & 1) v ^= SobolColumn(dim, i);
+    return v;
+}
+static inline uint32_t ReverseBits32(uint32_t n) {   // util/math.h:56-66
+    n = (n << 16) | (n >> 16);
+    n = ((n & 0x00ff00ffu) << 8) | ((n & 0xff00ff00u) >> 8);
+    n = ((n & 0x0f0f0f0fu) << 4) | ((n & 0xf0f0f0f0u) >> 4);
+    n = ((n & 0x33333333u) << 2) | ((n & 0xccccccccu) >> 2);
+    n = ((n & 0x55555555u) << 1) | ((n & 0xaaaaaaaau) >> 1);
+    return n;
+}
+static inline uint32_t FastOwen(uint32_t v, uint32_t seed) {   // lowdiscrepancy.h:220-237
+    v = ReverseBits32(v);
+    v ^= v * 0x3d20adeau;
+    v += seed;
+    v *= (seed >> 16) | 1;
+    v ^= v * 0x05526c56u;
+    v ^= v * 0x53a22864u;
+    return ReverseBits32(v);
+}
+static inline float SobolSampleFastOwen(uint64_t a, int dim, uint32_t seed) {   // :168-180
+    uint32_t v = FastOwen(SobolBits(a, dim), seed);
+    return std::min(v * 0x1p-32f, 0x1.fffffep-1f);
+}
+static inline uint64_t LeftShift2(uint64_t x) {   // util/math.h:83-91
+    x &= 0xffffffff;
+    x = (x ^ (x << 16)) & 0x0000ffff0000ffffull;
+    x = (x ^ (x << 8)) & 0x00ff00ff00ff00ffull;
+    x = (x ^ (x << 4)) & 0x0f0f0f0f0f0f0f0full;
+    x = (x ^ (x << 2)) & 0x3333333333333333ull;
+    x = (x ^ (x << 1)) & 0x5555555555555555ull;
+    return x;
+}
+static inline uint64_t EncodeMorton2(uint32_t x, uint32_t y) { return (LeftShift2(y) << 1) | LeftShift2(x); }
+static inline int Log2Int(uint32_t v) { return 31 - __builtin_clz(v); }
+static inline uint32_t RoundUpPow2(uint32_t v) {
+    v--; v |= v >> 1; v |= v >> 2; v |= v >> 4; v |= v >> 8; v |= v >> 16; return v + 1;
+}
+// the 24 permutations of a base-4 digit, in ZSobolSampler::GetSampleIndex's order
+static const uint8_t kZPerm[24][4] = {
+    {0, 1, 2, 3}, {0, 1, 3, 2}, {0, 2, 1, 3}, {0, 2, 3, 1}, {0, 3, 2, 1}, {0, 3, 1, 2},
+    {1, 0, 2, 3}, {1, 0, 3, 2}, {1, 2, 0, 3}, {1, 2, 3, 0}, {1, 3, 2, 0}, {1, 3, 0, 2},
+    {2, 1, 0, 3}, {2, 1, 3, 0}, {2, 0, 1, 3}, {2, 0, 3, 1}, {2, 3, 0, 1}, {2, 3, 1, 0},
+    {3, 1, 2, 0}, {3, 1, 0, 2}, {3, 2, 1, 0}, {3, 2, 0, 1}, {3, 0, 2, 1}, {3, 0, 1, 2}};
+
+struct Sampler {
+    // IndependentSampler
+    RNG rng;
+    // ZSobolSampler
+    int type = 0, seed = 0, log2spp = 0, nBase4Digits = 0, dimension = 0;
+    uint64_t mortonIndex = 0;
+
+    void Start(const OracleScene &s, int px, int py, int sampleIndex) {
+        type = s.sampler_type;
+        seed = s.seed;
+        if (type == 0) {   // samplers.h:457-460
+            rng.SetSequence(HashPixelSeed(px, py, s.seed));
+            rng.Advance((int64_t)(sampleIndex * 65536ull + 0));
+            return;
+        }
+        // ZSobolSampler ctor (samplers.h:228-238) + StartPixelSample (:250-254)
+        log2spp = Log2Int((uint32_t)s.samples_per_pixel);
+        int res = (int)RoundUpPow2((uint32_t)std::max(s.width, s.height));
+        int log4spp = (log2spp + 1) / 2;
+        nBase4Digits = Log2Int((uint32_t)res) + log4spp;
+        dimension = 0;
+        mortonIndex = (EncodeMorton2((uint32_t)px, (uint32_t)py) << log2spp) | (uint64_t)sampleIndex;
+    }
+    uint64_t SampleIndex() const {   // samplers.h:296-355
+        uint64_t sampleIndex = 0;
+        bool pow2Samples = log2spp & 1;
+        int lastDigit = pow2Samples ? 1 : 0;
+        for (int i = nBase4Digits - 1; i >= lastDigit; --i) {
+            int digitShift = 2 * i - (pow2Samples ? 1 : 0);
+            int digit = (mortonIndex >> digitShift) & 3;
+            uint64_t higherDigits = mortonIndex >> (digitShift + 2);
+            int p = (MixBits(higherDigits ^ (0x55555555u * (uint32_t)dimension)) >> 24) % 24;
+            digit = kZPerm[p][digit];
+            sampleIndex |= uint64_t(digit) << digitShift;
+        }
+        if (pow2Samples) {
+            int digit = mortonIndex & 1;
+            sampleIndex |= digit ^ (MixBits((mortonIndex >> 1) ^ (0x55555555u * (uint32_t)dimension)) & 1);
+        }
+        return sampleIndex;
+    }
+    float Get1D() {
+        if (type == 0) return rng.Uniform();
+        uint64_t sampleIndex = SampleIndex();
+        ++dimension;
+        uint32_t sampleHash = (uint32_t)HashInts2(dimension, seed);
+        return SobolSampleFastOwen(sampleIndex, 0, sampleHash);
+    }
+    void Get2D(float *u0, float *u1) {
+        if (type == 0) {   // {Uniform, Uniform}, left to right
+            *u0 = rng.Uniform();
+            *u1 = rng.Uniform();
+            return;
+        }
+        uint64_t sampleIndex = SampleIndex();
+        dimension += 2;
+        uint64_t bits = HashInts2(dimension, seed);
+        *u0 = SobolSampleFastOwen(sampleIndex, 0, (uint32_t)bits);
+        *u1 = SobolSampleFastOwen(sampleIndex, 1, (uint32_t)(bits >> 32));
+    }
+};
+
+// ---------------------------------------------------------------------------
+// GaussianFilter sampling — filters.h:80-118 via FilterSampler (filters.h:26-45,
+// filters.cpp:133-147): the filter tabulated at 32 x radius cells per axis over
+// [-radius, radius], sampled with PiecewiseConstant2D (sampling.h:603-770), weight =
+// f[cell] / pdf.
+static inline float GaussianF(float x, float mu, float sigma) {   // util/math.h:477-480
+    return 1 / std::sqrt(2 * Pi * sigma * sigma) * FastExp(-Sqr(x - mu) / (2 * sigma * sigma));
+}
+struct PC1D {   // PiecewiseConstant1D
+    std::vector<float> func, cdf;
+    float min = 0, max = 1, funcInt = 0;
+    void Build(const float *f, int n, float mn, float mx) {
+        func.assign(f, f + n);
+        cdf.assign(n + 1, 0.f);
+        min = mn; max = mx;
+        for (float &v : func) v = std::abs(v);
+        cdf[0] = 0;
+        for (int i = 1; i < n + 1; ++i) cdf[i] = cdf[i - 1] + func[i - 1] * (max - min) / n;
+        funcInt = cdf[n];
+        if (funcInt == 0)
+            for (int i = 1; i < n + 1; ++i) cdf[i] = float(i) / float(n);
+        else
+            for (int i = 1; i < n + 1; ++i) cdf[i] /= funcInt;
+    }
+    float Sample(float u, float *pdf, int *offset) const {
+        // FindInterval (util/math.h:508-519) over cdf[index] <= u
+        long size = (long)cdf.size() - 2, first = 1;
+        while (size > 0) {
+            long half = size >> 1, middle = first + half;
+            bool pr = cdf[middle] <= u;
+            first = pr ? middle + 1 : first;
+            size = pr ? size - (half + 1) : half;
+        }
+        int o = (int)std::clamp<long>(first - 1, 0, (long)cdf.size() - 2);
+        *offset = o;
+        float du = u - cdf[o];
+        if (cdf[o + 1] - cdf[o] > 0) du /= cdf[o + 1] - cdf[o];
+        *pdf = (funcInt > 0) ? func[o] / funcInt : 0;
+        return Lerp((o + du) / (float)func.size(), min, max);
+    }
+};
+struct GaussianSampler {
+    int nx = 0, ny = 0;
+    std::vector<float> f;            // nx * ny, x fastest (Array2D)
+    std::vector<PC1D> cond;          // per row
+    PC1D marginal;
+    void Build(float rx, float ry, float sigma) {
+        float expX = GaussianF(rx, 0, sigma), expY = GaussianF(ry, 0, sigma);
+        nx = int(32 * rx);
+        ny = int(32 * ry);
+        f.assign((size_t)nx * ny, 0.f);
+        for (int y = 0; y < ny; ++y)
+            for (int x = 0; x < nx; ++x) {
+                // Bounds2f::Lerp (vecmath.h:1228-1231) of ((x+0.5)/nx, (y+0.5)/ny) over [-r, r]
+                float px = Lerp((x + 0.5f) / nx, -rx, rx), py = Lerp((y + 0.5f) / ny, -ry, ry);
+                f[(size_t)y * nx + x] = std::max<float>(0, GaussianF(px, 0, sigma) - expX) *
+                                        std::max<float>(0, GaussianF(py, 0, sigma) - expY);
+            }
+        cond.resize(ny);
+        std::vector<float> marg(ny);
+        for (int y = 0; y < ny; ++y) {
+            cond[y].Build(&f[(size_t)y * nx], nx, -rx, rx);
+            marg[y] = cond[y].funcInt;
+        }
+        marginal.Build(marg.data(), ny, -ry, ry);
+    }
+    void Sample(float u0, float u1, float *p0, float *p1, float *weight) const {
+        float pdf1, pdf0;
+        int v, uo;
+        *p1 = marginal.Sample(u1, &pdf1, &v);
+        *p0 = cond[v].Sample(u0, &pdf0, &uo);
+        *weight = f[(size_t)v * nx + uo] / (pdf0 * pdf1);
+    }
+};
+
 struct SceneView {
     const OracleScene &s;
     Xform mediumX, cameraX, rasterX;
     Bounds bounds;
     Grid density, lescale, majorant;
+    GaussianSampler gauss;
     explicit SceneView(const OracleScene &sc) : s(sc) {
+        if (sc.filter_type == 1) gauss.Build(sc.filter_radius[0], sc.filter_radius[1], sc.filter_sigma);
         for (int i = 0; i < 16; ++i) {
             mediumX.m[i / 4][i % 4] = sc.render_from_medium[i];
             mediumX.mInv[i / 4][i % 4] = sc.medium_from_render[i];
@@ -804,22 +1024,13 @@ static Spec SampleT_maj(const SceneView &sv, Ray ray, float tMax, float u, RNG &
     return Spec::Const(1.f);
 }
 
-// Per-sample sampler state: IndependentSampler — samplers.h:457-466
-struct Sampler {
-    RNG rng;
-    void Start(int px, int py, int sampleIndex, int seed) {
-        rng.SetSequence(HashPixelSeed(px, py, seed));
-        rng.Advance((int64_t)(sampleIndex * 65536ull + 0));
-    }
-    float Get1D() { return rng.Uniform(); }
-};
-
 // VolPathIntegrator::SampleLd for a medium interaction — integrators.cpp:1282-1399
 static Spec SampleLd(const SceneView &sv, V3 p, V3 wo, const Lambda &l, Sampler &sampler, Spec beta, Spec r_p) {
     const OracleScene &s = sv.s;
     // lightSampler.Sample (BVH, infinite lights only) — lightsamplers.h:266-277
     float u = sampler.Get1D();
-    float uL0 = sampler.Get1D(), uL1 = sampler.Get1D();
+    float uL0, uL1;
+    sampler.Get2D(&uL0, &uL1);   // uLight (unused by distant lights)
     (void)uL0; (void)uL1;
     if (s.nlights == 0) return Spec::Const(0.f);
     float pInfinite = float(s.nlights) / float(s.nlights + 0);
@@ -914,7 +1125,8 @@ static Spec Li(const SceneView &sv, Ray ray, Lambda &l, Sampler &sampler, int *n
                     if (beta && r_u) {
                         V3 wo = -ray.d;
                         L = L + SampleLd(sv, p, wo, l, sampler, beta, r_u);
-                        float uph0 = sampler.Get1D(), uph1 = sampler.Get1D();
+                        float uph0, uph1;
+                        sampler.Get2D(&uph0, &uph1);
                         float phPdf;
                         V3 wi = SampleHenyeyGreenstein(wo, s.g, uph0, uph1, &phPdf);
                         if (phPdf == 0) terminated = true;
@@ -961,21 +1173,26 @@ static Spec Li(const SceneView &sv, Ray ray, Lambda &l, Sampler &sampler, int *n
 }
 
 // RayIntegrator::EvaluatePixelSample — integrators.cpp:235-298 (+ GetCameraSample samplers.h:797-815)
-struct SampleResult { Spec L; Lambda l; };
+struct SampleResult { Spec L; Lambda l; float weight; };
 static SampleResult EvaluatePixelSample(const SceneView &sv, int px, int py, int sampleIndex, int *nEvents) {
     const OracleScene &s = sv.s;
     Sampler sampler;
-    sampler.Start(px, py, sampleIndex, s.seed);
+    sampler.Start(s, px, py, sampleIndex);
     float lu = sampler.Get1D();
     Lambda l = SampleVisible(lu);
-    float fu0 = sampler.Get1D(), fu1 = sampler.Get1D();
-    // BoxFilter::Sample — filters.h:67-70
-    float fpx = Lerp(fu0, -s.filter_radius[0], s.filter_radius[0]);
-    float fpy = Lerp(fu1, -s.filter_radius[1], s.filter_radius[1]);
-    float filterWeight = 1;
+    float fu0, fu1;
+    sampler.Get2D(&fu0, &fu1);            // GetPixel2D
+    float fpx, fpy, filterWeight = 1;
+    if (s.filter_type == 0) {             // BoxFilter::Sample — filters.h:67-70
+        fpx = Lerp(fu0, -s.filter_radius[0], s.filter_radius[0]);
+        fpy = Lerp(fu1, -s.filter_radius[1], s.filter_radius[1]);
+    } else {
+        sv.gauss.Sample(fu0, fu1, &fpx, &fpy, &filterWeight);
+    }
     float pFilmX = ((float)px + fpx) + 0.5f, pFilmY = ((float)py + fpy) + 0.5f;
     sampler.Get1D();                      // time
-    sampler.Get1D(); sampler.Get1D();     // lens
+    float ul0, ul1;
+    sampler.Get2D(&ul0, &ul1);            // lens
     // Camera ray (GenerateRayDifferential main ray, then RenderFromCamera)
     V3 pCamera = XPoint(sv.rasterX.m, V3{pFilmX, pFilmY, 0.f});
     Ray ray;
@@ -993,8 +1210,7 @@ static SampleResult EvaluatePixelSample(const SceneView &sv, int px, int py, int
         if (std::isinf(y)) bad = true;
     }
     if (bad) L = Spec::Const(0.f);
-    (void)filterWeight;
-    return {L, l};
+    return {L, l, filterWeight};
 }
 
 // RGBFilm::AddSample — film.h:239-255 with PixelSensor::ToSensorRGB film.h:95-100
@@ -1045,11 +1261,13 @@ void oracle_build_majorant(const float *density, int nx, int ny, int nz, int rx,
 }
 
 // One pixel sample: L (4), lambda (4), pdf (4); returns number of tentative collisions.
-int oracle_pixel_sample(const OracleScene *s, int px, int py, int sampleIndex, float *L, float *lambda, float *pdf) {
+int oracle_pixel_sample(const OracleScene *s, int px, int py, int sampleIndex, float *L, float *lambda, float *pdf,
+                        float *weight) {
     SceneView sv(*s);
     int nEvents = 0;
     SampleResult r = EvaluatePixelSample(sv, px, py, sampleIndex, &nEvents);
     for (int i = 0; i < NS; ++i) { L[i] = r.L.v[i]; lambda[i] = r.l.lambda[i]; pdf[i] = r.l.pdf[i]; }
+    if (weight) *weight = r.weight;
     return nEvents;
 }
 
@@ -1075,7 +1293,7 @@ long long oracle_render(const OracleScene *s, int spp0, int spp1, int nthreads, 
                         SampleResult r = EvaluatePixelSample(sv, px, py, si, &ne);
                         ev += ne;
                         size_t pi = (size_t)py * W + px;
-                        AddSample(*s, rgbSum + 3 * pi, wSum + pi, r.L, r.l, 1.f);
+                        AddSample(*s, rgbSum + 3 * pi, wSum + pi, r.L, r.l, r.weight);
                     }
         }
         events += ev;
@@ -1106,7 +1324,7 @@ long long oracle_render_list(const OracleScene *s, const int *pixels, int n, int
                 int ne = 0;
                 SampleResult r = EvaluatePixelSample(sv, px, py, si, &ne);
                 ev += ne;
-                AddSample(*s, rgbSum + 3 * (size_t)i, wSum + i, r.L, r.l, 1.f);
+                AddSample(*s, rgbSum + 3 * (size_t)i, wSum + i, r.L, r.l, r.weight);
             }
         }
         events += ev;
@@ -1234,6 +1452,30 @@ void oracle_independent_sampler(int px, int py, int sampleIndex, int seed, int d
     r.SetSequence(HashPixelSeed(px, py, seed));
     r.Advance((int64_t)(sampleIndex * 65536ull + dim0));
     for (int i = 0; i < n; ++i) out[i] = r.Uniform();
+}
+// ZSobolSampler stream for one (pixel, sample): pattern of '1' (Get1D) / '2' (Get2D) calls
+void oracle_zsobol(int spp, int resx, int resy, int px, int py, int sampleIndex, int seed, const char *pattern,
+                   float *out) {
+    OracleScene sc{};
+    sc.sampler_type = 1;
+    sc.samples_per_pixel = spp;
+    sc.width = resx;
+    sc.height = resy;
+    sc.seed = seed;
+    Sampler smp;
+    smp.Start(sc, px, py, sampleIndex);
+    for (const char *q = pattern; *q; ++q) {
+        if (*q == '1') *out++ = smp.Get1D();
+        else { smp.Get2D(out, out + 1); out += 2; }
+    }
+}
+float oracle_sobol_fastowen(unsigned long long a, int dim, unsigned int seed) { return SobolSampleFastOwen(a, dim, seed); }
+float oracle_sobol_plain(unsigned long long a, int dim) { return std::min(SobolBits(a, dim) * 0x1p-32f, 0x1.fffffep-1f); }
+// GaussianFilter::Sample(u): out = {p.x, p.y, weight}
+void oracle_gaussian_filter_sample(float rx, float ry, float sigma, int n, const float *u, float *out) {
+    GaussianSampler g;
+    g.Build(rx, ry, sigma);
+    for (int i = 0; i < n; ++i) g.Sample(u[2 * i], u[2 * i + 1], out + 3 * i, out + 3 * i + 1, out + 3 * i + 2);
 }
 float oracle_noise(float x, float y, float z, float *dnoise3) {
     V3 dn = DNoise(V3{x, y, z});

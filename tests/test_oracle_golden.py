@@ -172,3 +172,34 @@ def test_spectral_tables_and_light_scale(golden):
     photometric = spectra.spectrum_to_photometric(spectra.TABLES["D65"])
     assert np.float32(photometric).view(np.uint32) == np.uint32(golden["d65_photometric"])
     assert np.float32(np.float32(1) / photometric).view(np.uint32) == np.uint32(golden["d65_scale"])
+
+
+def test_sobol_dims_0_1_and_fastowen(golden):
+    """SobolSample(a, dim, FastOwenScrambler / NoRandomizer) for the two dimensions
+    ZSobolSampler uses (lowdiscrepancy.h:168-237; matrices from their definition)."""
+    L = ob.lib()
+    for a, seed, f0, f1, p0, p1 in golden["sobol_fastowen"]:
+        a = int(a)
+        assert np.float32(L.oracle_sobol_fastowen(a, 0, seed)).view(np.uint32) == f0
+        assert np.float32(L.oracle_sobol_fastowen(a, 1, seed)).view(np.uint32) == f1
+        assert np.float32(L.oracle_sobol_plain(a, 0)).view(np.uint32) == p0
+        assert np.float32(L.oracle_sobol_plain(a, 1)).view(np.uint32) == p1
+
+
+def test_zsobol_sampler_streams(golden):
+    """ZSobolSampler (samplers.h:225-330): Get1D/Get2D streams of pixel samples for several
+    sample counts (powers of 4, of 2 but not 4, and 1), resolutions and seeds."""
+    for c in golden["zsobol"]:
+        got = ob.zsobol_stream(c["spp"], c["resx"], c["resy"], c["px"], c["py"], c["s"], c["seed"], c["pattern"])
+        assert got.view(np.uint32).tolist() == c["u"], c
+
+
+def test_gaussian_filter_sampling(golden):
+    """GaussianFilter::Sample through FilterSampler (filters.h:26-118, filters.cpp:133-147):
+    position and weight f/pdf bit for bit, incl. u = 0, u -> 1 and the centre."""
+    for c in golden["gaussian_filter"]:
+        rx, ry, sigma = (float(f([c[k]])[0]) for k in ("rx", "ry", "sigma"))
+        rows = np.array(c["samples"], np.uint32)
+        u = rows[:, :2].view(np.float32)
+        got = ob.gaussian_filter_samples(rx, ry, sigma, u)
+        assert got.view(np.uint32).tolist() == rows[:, 2:].tolist()
