@@ -65,6 +65,9 @@ SIGNATURES = {
     "avr_lights": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, c_int_p, c_float_p, c_float_p, c_float_p,
                                   ctypes.c_float]),
     "avr_camera": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, c_float_p, c_float_p]),
+    "avr_last_pass_weights": (ctypes.c_int, [ctypes.c_void_p, c_float_p, ctypes.c_longlong]),
+    "avr_set_filter": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, c_float_p, ctypes.c_float]),
+    "avr_set_sampler": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]),
     "avr_film": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, c_float_p, c_float_p, ctypes.c_float,
                                 ctypes.c_float]),
     "avr_film_clear": (ctypes.c_int, [ctypes.c_void_p]),
@@ -179,6 +182,9 @@ class Context:
         film = scene.film
         _check(self.lib.avr_film(self.h, film.width, film.height, _fp(f32(film.filter_radius)), _fp(f32(film.sensor)),
                                  float(film.imaging_ratio), float(film.max_component_value)))
+        flt = film.filter
+        _check(self.lib.avr_set_filter(self.h, int(flt.type_id), _fp(f32(flt.radius)), float(flt.sigma)))
+        _check(self.lib.avr_set_sampler(self.h, int(scene.sampler.type_id), int(scene.sampler.pixelsamples)))
 
     def generate_cloud(self, d_out_ptr, n, first, count, density=1.0, wispiness=1.0, frequency=5.0):
         _check(self.lib.avr_generate_cloud(self.h, ctypes.c_void_p(d_out_ptr), int(n), int(first), int(count),
@@ -223,6 +229,11 @@ class Context:
                                               ctypes.byref(ns)))
         m = npix * ns.value
         return first.value, ns.value, L[:m], lam[:m], pdf[:m]
+
+    def last_pass_weights(self, npix, max_samples):
+        w = np.zeros(npix * max_samples, np.float32)
+        _check(self.lib.avr_last_pass_weights(self.h, _fp(w), len(w)))
+        return w
 
     def film_export_device(self, d_dst_ptr):
         _check(self.lib.avr_film_export_device(self.h, ctypes.c_void_p(d_dst_ptr)))

@@ -74,7 +74,14 @@ struct avr_context {
     int kernel_mode = 0;      // 0: persistent k_paths (default), 1: wavefront k_medium/k_shadow
     bool last_persistent = false;   // which organisation the last avr_render ran
     int *d_heads = nullptr;   // 8 per-XCD work counters of k_paths
-    int paths_grid[4] = {0, 0, 0, 0};   // k_paths<emissive, gray> at index 2*emissive + gray
+    int paths_grid[8] = {};   // k_paths<emissive, gray, zsobol> at index 4*zsobol + 2*emissive + gray
+    void (*kpaths[8])(avr::Params) = {};
+    // pixel sampler (avr_set_sampler) and filter (avr_set_filter)
+    int sampler_kind = 0;     // 0 IndependentSampler, 1 ZSobolSampler
+    int sampler_spp = 16;     // samplesPerPixel of the sampler (ZSobol's Morton layout)
+    int filter_type = 0;      // 0 BoxFilter (radius from avr_film), 1 GaussianFilter
+    float *d_filter = nullptr;
+    avr::smp::FilterTables ftab{};
     int refill_min = 32;
     int dda_budget = 12;
     int grid_layout = 1;
@@ -93,6 +100,7 @@ void free_paths(avr_context *c) {
     if (c->ps.smp_state) (void)hipFree(c->ps.smp_state);
     if (c->ps.smp_inc) (void)hipFree(c->ps.smp_inc);
     if (c->ps.depth) (void)hipFree(c->ps.depth);
+    if (c->ps.weight) (void)hipFree(c->ps.weight);
     if (c->sh.path) (void)hipFree(c->sh.path);
     for (auto &q : c->d_queue) if (q) (void)hipFree(q), q = nullptr;
     c->ps = {};
@@ -108,6 +116,7 @@ int ensure_paths(avr_context *c, long long n) {
     HIP_TRY(dalloc(&c->ps.pdf, N)); HIP_TRY(dalloc(&c->ps.beta, N)); HIP_TRY(dalloc(&c->ps.r_u, N));
     HIP_TRY(dalloc(&c->ps.r_l, N)); HIP_TRY(dalloc(&c->ps.L, N));
     HIP_TRY(dalloc(&c->ps.smp_state, N)); HIP_TRY(dalloc(&c->ps.smp_inc, N)); HIP_TRY(dalloc(&c->ps.depth, N));
+    HIP_TRY(dalloc(&c->ps.weight, N));
     HIP_TRY(dalloc(&c->sh.path, N)); HIP_TRY(dalloc(&c->sh.o, N)); HIP_TRY(dalloc(&c->sh.d, N));
     HIP_TRY(dalloc(&c->sh.bf, N)); HIP_TRY(dalloc(&c->sh.Ls, N)); HIP_TRY(dalloc(&c->sh.rp_pl, N));
     HIP_TRY(dalloc(&c->d_queue[0], N)); HIP_TRY(dalloc(&c->d_queue[1], N));
@@ -233,15 +242,18 @@ int avr_context_create(int device, long long max_paths, avr_context **out) {
             delete c;
             return fail(AVR_ERR_HIP, "device query failed");
         }
-        void (*kerns[4])(avr::Params) = {avr::k_paths<false, false>, avr::k_paths<false, true>,
-                                         avr::k_paths<true, false>, avr::k_paths<true, true>};
-        for (int k = 0; k < 4; ++k) {
+        void (*kerns[8])(avr::Params) = {avr::k_paths<false, false, false>, avr::k_paths<false, true, false>,
+                                         avr::k_paths<true, false, false>,  avr::k_paths<true, true, false>,
+                                         avr::k_paths<false, false, true>,  avr::k_paths<false, true, true>,
+                                         avr::k_paths<true, false, true>,   avr::k_paths<true, true, true>};
+        for (int k = 0; k < 8; ++k) {
             int blocksPerCU = 0;
             if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocksPerCU, kerns[k], 256, 0) != hipSuccess) {
                 delete c;
                 return fail(AVR_ERR_HIP, "occupancy query failed");
             }
             c->paths_grid[k] = prop.multiProcessorCount * std::max(1, blocksPerCU);
+            c->kpaths[k] = kerns[k];
         }
     }
     *out = c;
@@ -288,6 +300,7 @@ int avr_context_destroy(avr_context *c) {
     if (c->d_counts) (void)hipFree(c->d_counts);
     if (c->d_heads) (void)hipFree(c->d_heads);
     if (c->d_advance) (void)hipFree(c->d_advance);
+    if (c->d_filter) (void)hipFree(c->d_filter);
     if (c->d_fat) (void)hipFree(c->d_fat);
     if (c->d_stats) (void)hipFree(c->d_stats);
     if (c->h_count) (void)hipHostFree(c->h_count);
@@ -405,6 +418,72 @@ int avr_film(avr_context *c, int width, int height, const float fr[2], const flo
     return avr_film_clear(c);
 }
 
+// FilterSampler tables of GaussianFilter(radius, sigma) — filters.h:80-118,
+// filters.cpp:133-147, PiecewiseConstant1D/2D sampling.h:603-770 — built on the host in
+// pbrt's float operation order (this file is compiled with -ffp-contract=off).
+static float gaussian_1d(float x, float mu, float sigma) {   // util/math.h:477-480
+    return 1 / std::sqrt(2 * avr::kPi * sigma * sigma) * avr::fast_exp(-avr::sqr(x - mu) / (2 * sigma * sigma));
+}
+static void pc1d_build(const float *f, int n, float mn, float mx, float *cdf, float *funcInt) {
+    cdf[0] = 0;
+    for (int i = 1; i < n + 1; ++i) cdf[i] = cdf[i - 1] + std::abs(f[i - 1]) * (mx - mn) / n;
+    *funcInt = cdf[n];
+    if (*funcInt == 0)
+        for (int i = 1; i < n + 1; ++i) cdf[i] = float(i) / float(n);
+    else
+        for (int i = 1; i < n + 1; ++i) cdf[i] /= *funcInt;
+}
+
+int avr_set_filter(avr_context *c, int type, const float radius[2], float sigma) {
+    if (!c || (type != 0 && type != 1) || !radius || !(radius[0] > 0) || !(radius[1] > 0))
+        return fail(AVR_ERR_ARG, "filter: type 0 (box) or 1 (gaussian) with a positive radius");
+    HIP_TRY(hipSetDevice(c->device));
+    if (type == 0) {
+        c->filter_type = 0;
+        c->film.filter_rx = radius[0];
+        c->film.filter_ry = radius[1];
+        return AVR_OK;
+    }
+    const int nx = int(32 * radius[0]), ny = int(32 * radius[1]);
+    if (nx < 1 || ny < 1 || nx > 128 || ny > 128) return fail(AVR_ERR_ARG, "gaussian filter radius out of range");
+    const float expX = gaussian_1d(radius[0], 0, sigma), expY = gaussian_1d(radius[1], 0, sigma);
+    std::vector<float> t((size_t)avr::smp::filter_table_floats(nx, ny));
+    float *f = t.data(), *ccdf = f + nx * ny, *cint = ccdf + ny * (nx + 1), *mcdf = cint + ny, *mint = mcdf + ny + 1;
+    for (int y = 0; y < ny; ++y)
+        for (int x = 0; x < nx; ++x) {
+            // Bounds2f::Lerp of ((x + 0.5) / nx, (y + 0.5) / ny) over [-r, r]
+            const float tx = (x + 0.5f) / nx, ty = (y + 0.5f) / ny;
+            const float px = (1 - tx) * -radius[0] + tx * radius[0], py = (1 - ty) * -radius[1] + ty * radius[1];
+            f[(size_t)y * nx + x] = std::max<float>(0, gaussian_1d(px, 0, sigma) - expX) *
+                                    std::max<float>(0, gaussian_1d(py, 0, sigma) - expY);
+        }
+    for (int y = 0; y < ny; ++y) pc1d_build(f + (size_t)y * nx, nx, -radius[0], radius[0], ccdf + (size_t)y * (nx + 1), cint + y);
+    pc1d_build(cint, ny, -radius[1], radius[1], mcdf, mint);
+    if (c->d_filter) (void)hipFree(c->d_filter);
+    c->d_filter = nullptr;
+    HIP_TRY(dalloc(&c->d_filter, t.size()));
+    HIP_TRY(hipMemcpy(c->d_filter, t.data(), t.size() * sizeof(float), hipMemcpyHostToDevice));
+    c->ftab.nx = nx;
+    c->ftab.ny = ny;
+    c->ftab.rx = radius[0];
+    c->ftab.ry = radius[1];
+    c->ftab.f = c->d_filter;
+    c->ftab.ccdf = c->d_filter + nx * ny;
+    c->ftab.cint = c->ftab.ccdf + ny * (nx + 1);
+    c->ftab.mcdf = c->ftab.cint + ny;
+    c->ftab.mint = *mint;
+    c->filter_type = 1;
+    return AVR_OK;
+}
+
+int avr_set_sampler(avr_context *c, int kind, int samples_per_pixel) {
+    if (!c || (kind != 0 && kind != 1) || samples_per_pixel < 1)
+        return fail(AVR_ERR_ARG, "sampler: kind 0 (independent) or 1 (zsobol), samples_per_pixel >= 1");
+    c->sampler_kind = kind;
+    c->sampler_spp = samples_per_pixel;
+    return AVR_OK;
+}
+
 int avr_film_clear(avr_context *c) {
     if (!c || !c->has_film) return fail(AVR_ERR_STATE, "no film");
     const size_t np = (size_t)c->film.width * c->film.height;
@@ -466,6 +545,14 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
     if (!c) return fail(AVR_ERR_ARG, "null context");
     if (!c->has_medium || !c->has_camera || !c->has_film) return fail(AVR_ERR_STATE, "medium, camera and film required");
     if (spp_begin < 0 || spp_end < spp_begin || max_depth < 0) return fail(AVR_ERR_ARG, "bad sample range");
+    avr::smp::ZSobolParams zs{};
+    if (c->sampler_kind == 1) {
+        // ZSobolSampler indexes (Morton(pixel) << log2(spp)) | sampleIndex: indices must stay
+        // below the sampler's samplesPerPixel and the Sobol' index below 2^32
+        if (spp_end > c->sampler_spp) return fail(AVR_ERR_ARG, "zsobol: sample index beyond samplesPerPixel");
+        zs = avr::smp::zsobol_params(c->sampler_spp, c->film.width, c->film.height, seed);
+        if (zs.nBase4Digits > 16) return fail(AVR_ERR_ARG, "zsobol: resolution x spp beyond 2^32 sample indices");
+    }
     HIP_TRY(hipSetDevice(c->device));
     const long long P = (long long)c->film.width * c->film.height;
     if (P > (1ll << 30)) return fail(AVR_ERR_ARG, "film too large");
@@ -481,6 +568,10 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
         p.lights = c->lights;
         p.cam = c->cam;
         p.film = c->film;
+        p.film.filter_type = c->filter_type;
+        p.film.gauss = c->ftab;
+        p.sampler_kind = c->sampler_kind;
+        p.zs = zs;
         p.ps = c->ps;
         p.sh = c->sh;
         p.max_depth = max_depth;
@@ -514,10 +605,8 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
             HIP_TRY(hipMemsetAsync(c->d_heads, 0, 8 * sizeof(int), c->stream));
             EV_MARK(e0);
             // gray medium: sigma_a and sigma_s tables constant over all 471 wavelengths
-            void (*kern)(avr::Params) = c->med.emissive ? (c->gray ? avr::k_paths<true, true> : avr::k_paths<true, false>)
-                                                        : (c->gray ? avr::k_paths<false, true> : avr::k_paths<false, false>);
-            const int grid = c->paths_grid[2 * (c->med.emissive ? 1 : 0) + (c->gray ? 1 : 0)];
-            hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, c->stream, p);
+            const int kv = 4 * c->sampler_kind + 2 * (c->med.emissive ? 1 : 0) + (c->gray ? 1 : 0);
+            hipLaunchKernelGGL(c->kpaths[kv], dim3(c->paths_grid[kv]), dim3(256), 0, c->stream, p);
             HIP_TRY(hipGetLastError());
             EV_MARK(e1);
             hipLaunchKernelGGL(avr::k_film, dim3(blocks_for(P)), dim3(256), 0, c->stream, p);
@@ -530,7 +619,8 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
             continue;
         }
         EV_MARK(c0);
-        hipLaunchKernelGGL(avr::k_camera, dim3(blocks_for(n0)), dim3(256), 0, c->stream, p);
+        if (c->sampler_kind) hipLaunchKernelGGL(avr::k_camera<true>, dim3(blocks_for(n0)), dim3(256), 0, c->stream, p);
+        else hipLaunchKernelGGL(avr::k_camera<false>, dim3(blocks_for(n0)), dim3(256), 0, c->stream, p);
         HIP_TRY(hipGetLastError());
         EV_MARK(c1);
         c->timed.push_back({c0, c1, &avr_stats::ms_camera, false});
@@ -550,7 +640,8 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
             p.shadow_count = c->d_counts + 2;
             const int nb = blocks_for(count);
             EV_MARK(m0);
-            hipLaunchKernelGGL(avr::k_medium, dim3(nb), dim3(256), 0, c->stream, p);
+            if (c->sampler_kind) hipLaunchKernelGGL(avr::k_medium<true>, dim3(nb), dim3(256), 0, c->stream, p);
+            else hipLaunchKernelGGL(avr::k_medium<false>, dim3(nb), dim3(256), 0, c->stream, p);
             HIP_TRY(hipGetLastError());
             EV_MARK(m1);
             hipLaunchKernelGGL(avr::k_shadow, dim3(nb), dim3(256), 0, c->stream, p);
@@ -632,6 +723,18 @@ int avr_last_pass_samples(avr_context *c, float *L, float *lambda, float *pdf, l
     }
     *first = c->last_base;
     *ns = c->last_S;
+    return AVR_OK;
+}
+
+int avr_last_pass_weights(avr_context *c, float *w, long long n_max) {
+    if (!c || !c->has_film || !w) return fail(AVR_ERR_ARG, "null arg");
+    const long long n = (long long)c->film.width * c->film.height * c->last_S;
+    if (n_max < n) return fail(AVR_ERR_ARG, "buffer too small for the last pass");
+    if (c->filter_type == 0) {
+        for (long long i = 0; i < n; ++i) w[i] = 1.f;   // BoxFilter::Sample weight
+    } else if (n > 0) {
+        HIP_TRY(hipMemcpy(w, c->ps.weight, n * sizeof(float), hipMemcpyDeviceToHost));
+    }
     return AVR_OK;
 }
 

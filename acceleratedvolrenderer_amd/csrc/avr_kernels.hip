@@ -17,6 +17,7 @@
 //   k_film     : per pixel, samples added in sampleIndex order into fp64 sums
 //                (bit-identical order to ImageTileIntegrator::Render's per-pixel loop).
 #include "avr_numerics.h"
+#include "avr_sampling.h"
 
 #include <type_traits>
 
@@ -66,6 +67,8 @@ struct DevCamera {
 struct DevFilm {
     int width, height;
     float filter_rx, filter_ry;
+    int filter_type;                  // 0 BoxFilter, 1 GaussianFilter (FilterSampler tables below)
+    smp::FilterTables gauss;
     const float *xyz;                 // 3 x 471
     float imaging_ratio;
     float max_component;
@@ -77,6 +80,7 @@ struct PathSoA {
     float4 *o, *d, *lambda, *pdf, *beta, *r_u, *r_l, *L;
     uint64_t *smp_state, *smp_inc;
     int *depth;
+    float *weight;                    // per-sample filter weight (GaussianFilter only)
 };
 struct ShadowSoA {
     int *path;
@@ -110,6 +114,8 @@ struct Params {
     int *heads;                       // k_paths: 8 per-XCD work counters (zeroed per pass)
     const uint64_t *advance;          // k_paths: per pass sample s, {A, H}: Advance(sIdx*65536) ==
                                       //   state' = A*state + inc*H (PCG32 advance is linear in inc)
+    int sampler_kind;                 // 0 IndependentSampler, 1 ZSobolSampler (kernels templated on it)
+    smp::ZSobolParams zs;
     int refill_min;                   // k_paths: refill a wave once this many lanes are idle
     int dda_budget;                   // k_paths: majorant cells a lane may cross per tracking
                                       //   iteration before yielding (bounds DDA divergence)
@@ -319,11 +325,60 @@ __device__ __forceinline__ Spec sample_t_maj(const DevMedium &m, const float *ma
     }
 }
 
-// IndependentSampler — samplers.h:457-466 (state carried per path)
-struct Sampler {
+// Per-path sampler state. IndependentSampler — samplers.h:442-476: PCG32 stream
+// SetSequence(Hash(p, seed)) (the one-argument SetSequence seeds with MixBits(seq),
+// rng.h:43-45) advanced by sampleIndex * 65536; Get2D = two Get1D, left to right.
+// ZSobolSampler — samplers.h:225-330 (avr_sampling.h). In the wavefront SoA the state
+// lives in smp_state / smp_inc (PCG state / increment, or Morton index / dimension).
+template <bool kZSobol> struct PathSampler;
+template <> struct PathSampler<false> {
     Pcg32 rng;
-    __device__ __forceinline__ float get1d() { return rng.uniform(); }
+    __device__ __forceinline__ void start(const Params &P, int px, int py, int sampleIndex) {
+        const uint64_t seq = hash_3u32((uint32_t)px, (uint32_t)py, (uint32_t)P.seed);
+        rng.set_sequence(seq, mix_bits(seq));
+        rng.advance((uint64_t)sampleIndex * 65536ull);
+    }
+    __device__ __forceinline__ float get1d(const Params &) { return rng.uniform(); }
+    __device__ __forceinline__ void get2d(const Params &, float *u0, float *u1) {
+        *u0 = rng.uniform();
+        *u1 = rng.uniform();
+    }
+    __device__ __forceinline__ void load(const Params &P, int i) { rng.state = P.ps.smp_state[i]; rng.inc = P.ps.smp_inc[i]; }
+    __device__ __forceinline__ void save(const Params &P, int i) { P.ps.smp_state[i] = rng.state; P.ps.smp_inc[i] = rng.inc; }
 };
+template <> struct PathSampler<true> {
+    smp::ZSobol z;
+    __device__ __forceinline__ void start(const Params &P, int px, int py, int sampleIndex) {
+        z.start(px, py, sampleIndex, P.zs);
+    }
+    __device__ __forceinline__ float get1d(const Params &P) { return z.get1d(P.zs); }
+    __device__ __forceinline__ void get2d(const Params &P, float *u0, float *u1) { z.get2d(P.zs, u0, u1); }
+    __device__ __forceinline__ void load(const Params &P, int i) { z.morton = P.ps.smp_state[i]; z.dimension = (uint32_t)P.ps.smp_inc[i]; }
+    __device__ __forceinline__ void save(const Params &P, int i) { P.ps.smp_state[i] = z.morton; P.ps.smp_inc[i] = z.dimension; }
+};
+
+// GetCameraSample (samplers.h:797-815) after the wavelength draw: pixel 2D through the
+// film's filter (BoxFilter::Sample filters.h:67-70 or GaussianFilter's FilterSampler),
+// time (1D) and lens (2D); returns pFilm and the filter weight.
+template <typename Smp>
+__device__ __forceinline__ void camera_sample(const Params &P, Smp &smp, int px, int py, float *pFilmX, float *pFilmY,
+                                              float *weight) {
+    float fu0, fu1;
+    smp.get2d(P, &fu0, &fu1);
+    float fpx, fpy;
+    *weight = 1.f;
+    if (P.film.filter_type == 0) {
+        fpx = lerp(fu0, -P.film.filter_rx, P.film.filter_rx);
+        fpy = lerp(fu1, -P.film.filter_ry, P.film.filter_ry);
+    } else {
+        ::avr::smp::gaussian_filter_sample(P.film.gauss, fu0, fu1, &fpx, &fpy, weight);
+    }
+    *pFilmX = ((float)px + fpx) + 0.5f;
+    *pFilmY = ((float)py + fpy) + 0.5f;
+    smp.get1d(P);                 // time
+    float l0, l1;
+    smp.get2d(P, &l0, &l1);       // lens
+}
 
 __device__ __forceinline__ float4 to4(V3 v) { return make_float4(v.x, v.y, v.z, 0.f); }
 __device__ __forceinline__ V3 from4(float4 v) { return {v.x, v.y, v.z}; }
@@ -342,28 +397,20 @@ __device__ __forceinline__ const float *stage_majorant(const DevMedium &m, float
 // Camera rays — RayIntegrator::EvaluatePixelSample (cpu/integrators.cpp:235-268),
 // GetCameraSample (samplers.h:797-815), BoxFilter::Sample (filters.h:67-70),
 // Orthographic/PerspectiveCamera::GenerateRay (cameras.cpp:284-306, 404-427)
+template <bool kZSobol>
 __global__ void __launch_bounds__(256) k_camera(Params P) {
     const int n = P.pass_pixels * P.pass_samples;
     for (int id = blockIdx.x * blockDim.x + threadIdx.x; id < n; id += gridDim.x * blockDim.x) {
         const int pix = id % P.pass_pixels, s = id / P.pass_pixels;
         const int px = pix % P.film.width, py = pix / P.film.width;
         const int sampleIndex = P.sample_base + s;
-        Sampler smp;
-        // IndependentSampler::StartPixelSample: rng.SetSequence(Hash(p, seed)) — the one-argument
-        // SetSequence seeds with MixBits(seq) (rng.h:43-45) — then Advance(sampleIndex * 65536).
-        {
-            const uint64_t seq = hash_3u32((uint32_t)px, (uint32_t)py, (uint32_t)P.seed);
-            smp.rng.set_sequence(seq, mix_bits(seq));
-        }
-        smp.rng.advance((uint64_t)sampleIndex * 65536ull);
-        const float lu = smp.get1d();
+        PathSampler<kZSobol> smp;
+        smp.start(P, px, py, sampleIndex);
+        const float lu = smp.get1d(P);
         Lambda lam = sample_visible(lu);
-        const float fu0 = smp.get1d(), fu1 = smp.get1d();
-        const float fpx = lerp(fu0, -P.film.filter_rx, P.film.filter_rx);
-        const float fpy = lerp(fu1, -P.film.filter_ry, P.film.filter_ry);
-        const float pFilmX = ((float)px + fpx) + 0.5f, pFilmY = ((float)py + fpy) + 0.5f;
-        smp.get1d();                 // time
-        smp.get1d(); smp.get1d();    // lens
+        float pFilmX, pFilmY, fweight;
+        camera_sample(P, smp, px, py, &pFilmX, &pFilmY, &fweight);
+        if (P.film.filter_type != 0) P.ps.weight[id] = fweight;
         const float *r = P.cam.raster;
         float xp = r[0] * pFilmX + r[1] * pFilmY + r[2] * 0.f + r[3];
         float yp = r[4] * pFilmX + r[5] * pFilmY + r[6] * 0.f + r[7];
@@ -383,8 +430,7 @@ __global__ void __launch_bounds__(256) k_camera(Params P) {
         P.ps.r_u[id] = make_float4(1.f, 1.f, 1.f, 1.f);
         P.ps.r_l[id] = make_float4(1.f, 1.f, 1.f, 1.f);
         P.ps.L[id] = make_float4(0.f, 0.f, 0.f, 0.f);
-        P.ps.smp_state[id] = smp.rng.state;
-        P.ps.smp_inc[id] = smp.rng.inc;
+        smp.save(P, id);
         P.ps.depth[id] = 0;
     }
 }
@@ -392,6 +438,7 @@ __global__ void __launch_bounds__(256) k_camera(Params P) {
 // ---------------------------------------------------------------------------
 // Delta tracking — VolPathIntegrator::Li's medium branch (cpu/integrators.cpp:981-1088),
 // SampleLd's light pick and shadow-ray spawn (1282-1338), escaped rays (1090-1107).
+template <bool kZSobol>
 __global__ void __launch_bounds__(256) k_medium(Params P) {
     __shared__ float s_maj[4096];
     const float *maj = stage_majorant(P.med, s_maj);
@@ -416,9 +463,8 @@ __global__ void __launch_bounds__(256) k_medium(Params P) {
             const Spec lamv = spec4(P.ps.lambda[path]);
             Spec beta = spec4(P.ps.beta[path]), r_u = spec4(P.ps.r_u[path]), r_l = spec4(P.ps.r_l[path]);
             Spec L = spec4(P.ps.L[path]);
-            Sampler smp;
-            smp.rng.state = P.ps.smp_state[path];
-            smp.rng.inc = P.ps.smp_inc[path];
+            PathSampler<kZSobol> smp;
+            smp.load(P, path);
             int depth = P.ps.depth[path];
             const LambdaIdx li = lambda_index(lamv);
             const Spec sig_a = sample_table(P.med.sigma_a, li);
@@ -426,11 +472,11 @@ __global__ void __launch_bounds__(256) k_medium(Params P) {
             const Spec Le_l = P.med.emissive ? sample_table(P.med.Le, li) : Spec::c(0.f);
             const int maxDepth = P.max_depth;
             bool scattered = false, terminated = false;
-            const float h0 = smp.get1d();
-            const float h1 = smp.get1d();
+            const float h0 = smp.get1d(P);
+            const float h1 = smp.get1d(P);
             Pcg32 rng;
             rng.set_sequence(hash_u32(f2u(h0)), hash_u32(f2u(h1)));
-            const float u0 = smp.get1d();
+            const float u0 = smp.get1d(P);
             V3 pScatter{};
             auto cb = [&](V3 p, const MediumSample &ms, const Spec &sigma_maj, const Spec &T_maj) -> bool {
                 if (!beta.nonzero()) { terminated = true; return false; }
@@ -470,8 +516,9 @@ __global__ void __launch_bounds__(256) k_medium(Params P) {
             if (scattered) {
                 // ---- SampleLd for the medium interaction (integrators.cpp:1282-1338) ----
                 const V3 wo = -d;
-                const float ul = smp.get1d();
-                smp.get1d(); smp.get1d();   // uLight (unused by distant lights)
+                const float ul = smp.get1d(P);
+                float uL0, uL1;
+                smp.get2d(P, &uL0, &uL1);   // uLight (unused by distant lights)
                 bool shadowSpawned = false;
                 const int nl = P.lights.n;
                 if (nl > 0) {
@@ -505,7 +552,8 @@ __global__ void __launch_bounds__(256) k_medium(Params P) {
                 if (!shadowSpawned) L = L + Spec::c(0.f);   // L += SampleLd(...) == 0
                 pushShadow = shadowSpawned;
                 // ---- phase-function sampling (integrators.cpp:1046-1061) ----
-                const float up0 = smp.get1d(), up1 = smp.get1d();
+                float up0, up1;
+                smp.get2d(P, &up0, &up1);
                 float phPdf;
                 const V3 wi = hg_sample(wo, P.med.g, up0, up1, &phPdf);
                 if (phPdf == 0) {
@@ -542,7 +590,7 @@ __global__ void __launch_bounds__(256) k_medium(Params P) {
                 P.ps.beta[path] = to4(beta);
                 P.ps.r_u[path] = to4(r_u);
                 P.ps.r_l[path] = to4(r_l);
-                P.ps.smp_state[path] = smp.rng.state;
+                smp.save(P, path);
                 P.ps.depth[path] = depth;
             }
         }
@@ -774,7 +822,7 @@ template <> __device__ __forceinline__ Spec sfrom<Spec>(const Spec &x) { return 
 __device__ __forceinline__ Spec smul(const Spec &a, float b) { return a * b; }
 __device__ __forceinline__ Spec smul(const Spec &a, const Spec &b) { return a * b; }
 
-template <bool kEmissive, bool kGray>
+template <bool kEmissive, bool kGray, bool kZSobol>
 __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_WAVES_SPEC) k_paths(Params P) {
     using S = typename std::conditional<kGray, float, Spec>::type;
     // LDS: majorant grid (16 KiB at pbrt's 16^3) + the 471-entry spectral tables the path
@@ -808,7 +856,7 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
     // path state (Li, integrators.cpp:966-971)
     Spec L{}, lam{}, Le_l{};
     S beta{}, r_u{}, r_l{}, sig_a{}, sig_s{};
-    Sampler smp{};
+    PathSampler<kZSobol> smp{};
     int depth = 0;
     V3 po{}, pd{};         // segment origin (== the path vertex) and the path's ray direction
     // segment state (SampleT_maj)
@@ -840,8 +888,9 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
             if (ev == EV_SCATTER) {
                 // SampleLd: light pick (BVH infinite-light branch) + shadow-ray spawn (1282-1338)
                 const V3 wo = -pd;
-                const float ul = smp.get1d();
-                smp.get1d(); smp.get1d();
+                const float ul = smp.get1d(P);
+                float uL0, uL1;
+                smp.get2d(P, &uL0, &uL1);   // uLight (unused by distant lights)
                 ev = EV_PHASE;                       // unless a shadow ray is spawned
                 L = L + Spec::c(0.f);                // L += SampleLd(...) == 0 if nothing spawns
                 const int nl = P.lights.n;
@@ -898,7 +947,8 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
         if (__ballot(ev == EV_PHASE)) {
             if (ev == EV_PHASE) {
                 // phase-function sampling (integrators.cpp:1046-1061), then the next segment
-                const float up0 = smp.get1d(), up1 = smp.get1d();
+                float up0, up1;
+                smp.get2d(P, &up0, &up1);
                 float phPdf;
                 const V3 wi = hg_sample(-pd, m.g, up0, up1, &phPdf);
                 if (phPdf == 0) {
@@ -907,11 +957,11 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
                     beta = beta * (phPdf / phPdf);
                     r_l = r_u / phPdf;
                     pd = wi;
-                    const float h0 = smp.get1d();
-                    const float h1 = smp.get1d();
+                    const float h0 = smp.get1d(P);
+                    const float h1 = smp.get1d(P);
                     seqA = hash_u32(f2u(h0));
                     seqB = hash_u32(f2u(h1));
-                    u = smp.get1d();
+                    u = smp.get1d(P);
                     sd = pd;
                     segPending = true;
                     mode = M_MEDIUM;
@@ -983,17 +1033,18 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
                     // ---- camera ray (EvaluatePixelSample, integrators.cpp:235-268) ----
                     const int pix = g % npix, sIdx = g / npix;
                     const int px = pix % P.film.width, py = pix / P.film.width;
-                    const uint64_t seq = hash_3u32((uint32_t)px, (uint32_t)py, (uint32_t)P.seed);
-                    smp.rng.set_sequence(seq, mix_bits(seq));
-                    // == smp.rng.advance((sample_base + sIdx) * 65536) (rng.h:132-146), precomputed
-                    smp.rng.state = P.advance[2 * sIdx] * smp.rng.state + smp.rng.inc * P.advance[2 * sIdx + 1];
-                    lam = sample_visible_lambda(smp.get1d());   // pdf: recomputed by k_film
-                    const float fu0 = smp.get1d(), fu1 = smp.get1d();
-                    const float fpx = lerp(fu0, -P.film.filter_rx, P.film.filter_rx);
-                    const float fpy = lerp(fu1, -P.film.filter_ry, P.film.filter_ry);
-                    const float pFilmX = ((float)px + fpx) + 0.5f, pFilmY = ((float)py + fpy) + 0.5f;
-                    smp.get1d();
-                    smp.get1d(); smp.get1d();
+                    if constexpr (kZSobol) {
+                        smp.start(P, px, py, P.sample_base + sIdx);
+                    } else {
+                        const uint64_t seq = hash_3u32((uint32_t)px, (uint32_t)py, (uint32_t)P.seed);
+                        smp.rng.set_sequence(seq, mix_bits(seq));
+                        // == rng.Advance((sample_base + sIdx) * 65536) (rng.h:132-146), precomputed
+                        smp.rng.state = P.advance[2 * sIdx] * smp.rng.state + smp.rng.inc * P.advance[2 * sIdx + 1];
+                    }
+                    lam = sample_visible_lambda(smp.get1d(P));   // pdf: recomputed by k_film
+                    float pFilmX, pFilmY, fweight;
+                    camera_sample(P, smp, px, py, &pFilmX, &pFilmY, &fweight);
+                    if (P.film.filter_type != 0) P.ps.weight[g] = fweight;
                     const float *r = P.cam.raster;
                     V3 pCam = {r[0] * pFilmX + r[1] * pFilmY + r[2] * 0.f + r[3],
                                r[4] * pFilmX + r[5] * pFilmY + r[6] * 0.f + r[7],
@@ -1016,11 +1067,11 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
                         if (kEmissive) Le_l = sample_table(m.Le, li);
                     }
                     // first medium segment: RNG from two sampler dims, u from a third (984-989)
-                    const float h0 = smp.get1d();
-                    const float h1 = smp.get1d();
+                    const float h0 = smp.get1d(P);
+                    const float h1 = smp.get1d(P);
                     seqA = hash_u32(f2u(h0));
                     seqB = hash_u32(f2u(h1));
-                    u = smp.get1d();
+                    u = smp.get1d(P);
                     sd = pd;
                     segPending = true;
                     mode = M_MEDIUM;
@@ -1244,7 +1295,7 @@ __global__ void __launch_bounds__(256) k_film(Params P) {
             float mx = fmaxf_(fmaxf_(rgb[0], rgb[1]), rgb[2]);
             if (mx > P.film.max_component)
                 for (int c = 0; c < 3; ++c) rgb[c] *= P.film.max_component / mx;
-            const float w = 1.f;
+            const float w = P.film.filter_type != 0 ? P.ps.weight[id] : 1.f;   // CameraSample::filterWeight
             s0 += (double)(w * rgb[0]);
             s1 += (double)(w * rgb[1]);
             s2 += (double)(w * rgb[2]);

@@ -1,0 +1,211 @@
+// Pixel-sample generation shared by the device kernels and the host side of the C-ABI:
+// ZSobolSampler (samplers.h:225-330, FastOwen randomisation) and the tabulated
+// FilterSampler of GaussianFilter (filters.h:26-118, filters.cpp:133-147, PiecewiseConstant
+// 1D/2D sampling.h:603-770). Standalone (no HIP headers) so the host tests can compile it
+// with g++ and pin it against the reference goldens; device and oracle agree bit for bit.
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+
+#ifndef AVR_HD
+#define AVR_HD __host__ __device__ __forceinline__
+#endif
+
+namespace avr {
+namespace smp {
+
+AVR_HD uint32_t bitrev32(uint32_t n) {
+#if defined(__clang__)
+    return __builtin_bitreverse32(n);
+#else
+    n = (n << 16) | (n >> 16);
+    n = ((n & 0x00ff00ffu) << 8) | ((n & 0xff00ff00u) >> 8);
+    n = ((n & 0x0f0f0f0fu) << 4) | ((n & 0xf0f0f0f0u) >> 4);
+    n = ((n & 0x33333333u) << 2) | ((n & 0xccccccccu) >> 2);
+    n = ((n & 0x55555555u) << 1) | ((n & 0xaaaaaaaau) >> 1);
+    return n;
+#endif
+}
+
+AVR_HD uint64_t mix64(uint64_t v) {   // MixBits, util/hash.h:84-92
+    v ^= (v >> 31);
+    v *= 0x7fb5d329728ea185ull;
+    v ^= (v >> 27);
+    v *= 0x81dadef4bc2dd44dull;
+    v ^= (v >> 33);
+    return v;
+}
+
+// MurmurHash64A of an 8-byte key (util/hash.h:19-66): Hash(int a, int b)
+AVR_HD uint64_t hash_2u32(uint32_t a, uint32_t b) {
+    const uint64_t m = 0xc6a4a7935bd1e995ull;
+    uint64_t h = 8ull * m;
+    uint64_t k = (uint64_t)a | ((uint64_t)b << 32);
+    k *= m;
+    k ^= k >> 47;
+    k *= m;
+    h ^= k;
+    h *= m;
+    h ^= h >> 47;
+    h *= m;
+    h ^= h >> 47;
+    return h;
+}
+
+AVR_HD uint64_t left_shift2(uint64_t x) {   // util/math.h:83-91
+    x &= 0xffffffff;
+    x = (x ^ (x << 16)) & 0x0000ffff0000ffffull;
+    x = (x ^ (x << 8)) & 0x00ff00ff00ff00ffull;
+    x = (x ^ (x << 4)) & 0x0f0f0f0f0f0f0f0full;
+    x = (x ^ (x << 2)) & 0x3333333333333333ull;
+    x = (x ^ (x << 1)) & 0x5555555555555555ull;
+    return x;
+}
+AVR_HD uint64_t encode_morton2(uint32_t x, uint32_t y) { return (left_shift2(y) << 1) | left_shift2(x); }
+
+// Sobol' dimension 0 (van der Corput: column i = bit 31-i) and dimension 1 (Pascal
+// matrix mod 2: column i has bit 31-k set iff k is a bit-subset of i) for an index < 2^32:
+// dim 0 is the bit reversal; dim 1 is the superset-parity transform of the index bits
+// (out_k = XOR of a_i over i ⊇ k), bit-reversed. Equal to the SobolMatrices32 products
+// (tests/test_sampling_header.py against the reference's SobolSample).
+AVR_HD uint32_t sobol_bits(uint32_t a, int dim) {
+    if (dim == 0) return bitrev32(a);
+    uint32_t w = a;
+    w ^= (w >> 1) & 0x55555555u;
+    w ^= (w >> 2) & 0x33333333u;
+    w ^= (w >> 4) & 0x0f0f0f0fu;
+    w ^= (w >> 8) & 0x00ff00ffu;
+    w ^= (w >> 16) & 0x0000ffffu;
+    return bitrev32(w);
+}
+AVR_HD uint32_t fast_owen(uint32_t v, uint32_t seed) {   // lowdiscrepancy.h:220-237
+    v = bitrev32(v);
+    v ^= v * 0x3d20adeau;
+    v += seed;
+    v *= (seed >> 16) | 1;
+    v ^= v * 0x05526c56u;
+    v ^= v * 0x53a22864u;
+    return bitrev32(v);
+}
+AVR_HD float u32_to_unit(uint32_t v) {   // min(v * 2^-32, OneMinusEpsilon)
+    const float f = (float)v * 0x1p-32f;
+    return f < 0x1.fffffep-1f ? f : 0x1.fffffep-1f;
+}
+
+// The 24 permutations of a base-4 digit in ZSobolSampler::GetSampleIndex's table order,
+// each packed into one byte (2 bits per entry), 8 per word.
+constexpr uint64_t kZPermW0 = 0xb1e19c6c78d8b4e4ull;   // {0,1,2,3} .. {1,0,3,2}
+constexpr uint64_t kZPermW1 = 0x72d236c68d2d39c9ull;   // {1,2,0,3} .. {2,0,3,1}
+constexpr uint64_t kZPermW2 = 0x93634b1b87271e4eull;   // {2,3,0,1} .. {3,0,1,2}
+
+struct ZSobolParams {
+    int log2spp, nBase4Digits, seed;
+};
+
+// ZSobolSampler::GetSampleIndex (samplers.h:296-355) for the current dimension
+AVR_HD uint64_t zsobol_index(uint64_t morton, uint32_t dimension, const ZSobolParams &zp) {
+    uint64_t sampleIndex = 0;
+    const bool pow2 = zp.log2spp & 1;
+    const int lastDigit = pow2 ? 1 : 0;
+    const uint64_t dmix = (uint64_t)(0x55555555u * dimension);
+    for (int i = zp.nBase4Digits - 1; i >= lastDigit; --i) {
+        const int shift = 2 * i - (pow2 ? 1 : 0);
+        const int digit = (int)(morton >> shift) & 3;
+        const uint64_t y = mix64((morton >> (shift + 2)) ^ dmix) >> 24;   // < 2^40
+        // y % 24 with 32-bit pieces: 2^32 = 16 (mod 24)
+        const uint32_t hi = (uint32_t)(y >> 32), lo = (uint32_t)y;
+        const uint32_t p = (hi * 16u + lo % 24u) % 24u;
+        const uint64_t w = p < 8 ? kZPermW0 : (p < 16 ? kZPermW1 : kZPermW2);
+        const uint32_t nd = (uint32_t)(w >> ((p & 7) * 8 + 2 * digit)) & 3u;
+        sampleIndex |= (uint64_t)nd << shift;
+    }
+    if (pow2) {
+        const int digit = (int)(morton & 1);
+        sampleIndex |= (uint64_t)(digit ^ (int)(mix64((morton >> 1) ^ dmix) & 1));
+    }
+    return sampleIndex;
+}
+
+// ZSobolSampler state of one pixel sample
+struct ZSobol {
+    uint64_t morton;
+    uint32_t dimension;
+    AVR_HD void start(int px, int py, int sampleIndex, const ZSobolParams &zp) {
+        morton = (encode_morton2((uint32_t)px, (uint32_t)py) << zp.log2spp) | (uint64_t)(uint32_t)sampleIndex;
+        dimension = 0;
+    }
+    AVR_HD float get1d(const ZSobolParams &zp) {
+        const uint64_t a = zsobol_index(morton, dimension, zp);
+        ++dimension;
+        const uint32_t h = (uint32_t)hash_2u32(dimension, (uint32_t)zp.seed);
+        return u32_to_unit(fast_owen(sobol_bits((uint32_t)a, 0), h));
+    }
+    AVR_HD void get2d(const ZSobolParams &zp, float *u0, float *u1) {
+        const uint64_t a = zsobol_index(morton, dimension, zp);
+        dimension += 2;
+        const uint64_t h = hash_2u32(dimension, (uint32_t)zp.seed);
+        *u0 = u32_to_unit(fast_owen(sobol_bits((uint32_t)a, 0), (uint32_t)h));
+        *u1 = u32_to_unit(fast_owen(sobol_bits((uint32_t)a, 1), (uint32_t)(h >> 32)));
+    }
+};
+
+// ZSobolSampler constructor parameters (samplers.h:228-238)
+inline int ilog2(uint32_t v) { return 31 - __builtin_clz(v); }
+inline uint32_t round_up_pow2(uint32_t v) {
+    v--; v |= v >> 1; v |= v >> 2; v |= v >> 4; v |= v >> 8; v |= v >> 16;
+    return v + 1;
+}
+inline ZSobolParams zsobol_params(int spp, int width, int height, int seed) {
+    ZSobolParams zp;
+    zp.log2spp = ilog2((uint32_t)spp);
+    const int res = (int)round_up_pow2((uint32_t)(width > height ? width : height));
+    zp.nBase4Digits = ilog2((uint32_t)res) + (zp.log2spp + 1) / 2;
+    zp.seed = seed;
+    return zp;
+}
+
+// ---------------------------------------------------------------------------
+// FilterSampler tables of a GaussianFilter: nx = int(32 rx) by ny = int(32 ry) cells.
+// Layout (floats): f[ny*nx] | ccdf[ny*(nx+1)] | cint[ny] | mcdf[ny+1] | {mint}
+struct FilterTables {
+    int nx, ny;
+    float rx, ry;
+    const float *f, *ccdf, *cint, *mcdf;
+    float mint;
+};
+inline int filter_table_floats(int nx, int ny) { return nx * ny + ny * (nx + 1) + ny + (ny + 1) + 1; }
+
+// Sample one PiecewiseConstant1D given as (cdf[n+1], func[n], funcInt) over [mn, mx]
+AVR_HD float pc1d_sample(const float *cdf, const float *func, int n, float funcInt, float mn, float mx, float u,
+                         float *pdf, int *off) {
+    // FindInterval(n + 1, cdf[i] <= u), util/math.h:508-519
+    int size = (n + 1) - 2, first = 1;
+    while (size > 0) {
+        const int half = size >> 1, middle = first + half;
+        const bool pr = cdf[middle] <= u;
+        first = pr ? middle + 1 : first;
+        size = pr ? size - (half + 1) : half;
+    }
+    int o = first - 1;
+    o = o < 0 ? 0 : (o > n - 1 ? n - 1 : o);
+    *off = o;
+    float du = u - cdf[o];
+    if (cdf[o + 1] - cdf[o] > 0) du /= cdf[o + 1] - cdf[o];
+    *pdf = (funcInt > 0) ? func[o] / funcInt : 0;
+    const float t = (o + du) / (float)n;
+    return (1 - t) * mn + t * mx;   // Lerp
+}
+
+// GaussianFilter::Sample(u) -> (p, weight = f[cell] / pdf)
+AVR_HD void gaussian_filter_sample(const FilterTables &T, float u0, float u1, float *px, float *py, float *weight) {
+    float pdf1, pdf0;
+    int v, uo;
+    *py = pc1d_sample(T.mcdf, T.cint, T.ny, T.mint, -T.ry, T.ry, u1, &pdf1, &v);
+    *px = pc1d_sample(T.ccdf + (std::size_t)v * (T.nx + 1), T.f + (std::size_t)v * T.nx, T.nx, T.cint[v], -T.rx, T.rx, u0,
+                      &pdf0, &uo);
+    *weight = T.f[(std::size_t)v * T.nx + uo] / (pdf0 * pdf1);
+}
+
+}  // namespace smp
+}  // namespace avr

@@ -15,7 +15,7 @@ import numpy as np
 
 from . import spectra
 from .scene import (GridMedium, DistantLight, UniformInfiniteLight, OrthographicCamera, PerspectiveCamera, RGBFilm,
-                    Scene)
+                    Scene, BoxFilter, GaussianFilter, IndependentSampler, ZSobolSampler)
 
 CLOUD_G = 0.877
 CLOUD_MAXDEPTH = 100
@@ -62,11 +62,14 @@ def cloud_medium(density):
     return GridMedium(density, sigma_a=0.0, sigma_s=1.0, scale=4.0, g=CLOUD_G)
 
 
-def s_cloud(density, width=1280, height=720, fov=45.0):
+def s_cloud(density, width=1280, height=720, fov=45.0, sampler="independent", spp=16, filter="box"):
+    """sampler "zsobol" / filter "gaussian" are pbrt's defaults (scene.cpp:93-94) and
+    BASELINE.md §2's S-cloud configuration; "independent" / "box" replay-friendly ones."""
     med = cloud_medium(density)
     # key light from upper right behind the cloud (silver lining with g = 0.877) plus a dim sky
     lights = [DistantLight(from_=(0.7, 1.0, 0.6), to=(0.0, 0.0, 0.0), scale=3.0), UniformInfiniteLight(scale=0.15)]
     # framed so the 16:9 view is filled by the [0,1]^3 medium box
     cam = PerspectiveCamera(fov=fov, pos=(0.5, 0.42, -0.75), look=(0.5, 0.38, 0.5), up=(0.0, 1.0, 0.0))
-    film = RGBFilm(width, height)
-    return Scene(cam, film, med, lights)
+    film = RGBFilm(width, height, filter=GaussianFilter() if filter == "gaussian" else BoxFilter())
+    smp = ZSobolSampler(spp) if sampler == "zsobol" else IndependentSampler(spp)
+    return Scene(cam, film, med, lights, sampler=smp)

@@ -122,9 +122,19 @@ int avr_camera(avr_context *ctx, int type, const float camera_from_raster[16], c
 int avr_film(avr_context *ctx, int width, int height, const float filter_radius[2], const float *sensor_rgb,
              float imaging_ratio, float max_component_value);
 int avr_film_clear(avr_context *ctx);
+/* Pixel filter for later renders (GetCameraSample, samplers.h:797-815): type 0 BoxFilter
+ * (filters.h:48-77, radius), 1 GaussianFilter(radius, sigma) (filters.h:80-118; sampled with
+ * FilterSampler's tabulated distribution, filters.cpp:133-147, weight f/pdf; radius <= 4).
+ * pbrt's default filter is gaussian radius 1.5, sigma 0.5 (scene.cpp:94, filters.cpp). */
+int avr_set_filter(avr_context *ctx, int type, const float radius[2], float sigma);
+/* Pixel sampler for later renders: 0 IndependentSampler (samplers.h:442-476, default here),
+ * 1 ZSobolSampler with FastOwen randomisation (samplers.h:225-330; pbrt's default,
+ * scene.cpp:93). samples_per_pixel is the sampler's pixelsamples: ZSobol lays out
+ * (Morton(pixel) << log2(spp)) | sampleIndex, so avr_render must stay below it. */
+int avr_set_sampler(avr_context *ctx, int kind, int samples_per_pixel);
 
-/* Render sample indices [spp_begin, spp_end) of every pixel (IndependentSampler, seed),
- * VolPathIntegrator maxdepth. Asynchronous on the context stream. */
+/* Render sample indices [spp_begin, spp_end) of every pixel (the avr_set_sampler sampler,
+ * seed), VolPathIntegrator maxdepth. Asynchronous on the context stream. */
 int avr_render(avr_context *ctx, int spp_begin, int spp_end, int seed, int max_depth);
 int avr_sync(avr_context *ctx);
 int avr_get_stats(avr_context *ctx, avr_stats *out);   /* waits for queued work */
@@ -144,6 +154,8 @@ int avr_film_export_device(avr_context *ctx, void *d_dst);
  * L, lambda, pdf and returns the pass's first sample index and sample count. */
 int avr_last_pass_samples(avr_context *ctx, float *L, float *lambda, float *pdf, long long n_max,
                           int *first_sample, int *n_samples);
+/* Filter weights (CameraSample::filterWeight) of the last pass's samples, same indexing. */
+int avr_last_pass_weights(avr_context *ctx, float *weight, long long n_max);
 
 #ifdef __cplusplus
 }

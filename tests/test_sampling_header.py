@@ -1,0 +1,55 @@
+"""The device's pixel-sample generation (acceleratedvolrenderer_amd/csrc/avr_sampling.h),
+compiled for the host, against the golden vectors of the reference itself: ZSobolSampler
+streams (samplers.h:225-330) and SobolSample with FastOwen scrambling for the two Sobol'
+dimensions ZSobol uses (lowdiscrepancy.h:168-237; here computed without the matrix table)."""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def hdr(tmp_path_factory):
+    d = tmp_path_factory.mktemp("smp")
+    src = d / "shim.cpp"
+    src.write_text(
+        "#define AVR_HD inline\n"
+        f'#include "{ROOT}/acceleratedvolrenderer_amd/csrc/avr_sampling.h"\n'
+        "using namespace avr::smp;\n"
+        'extern "C" {\n'
+        "void zs(int spp, int rx, int ry, int px, int py, int s, int seed, const char *pat, float *out) {\n"
+        "  ZSobolParams zp = zsobol_params(spp, rx, ry, seed); ZSobol z; z.start(px, py, s, zp);\n"
+        "  for (; *pat; ++pat) { if (*pat == '1') *out++ = z.get1d(zp); else { z.get2d(zp, out, out + 1); out += 2; } }\n"
+        "}\n"
+        "float sob(unsigned long long a, int dim, unsigned seed, int scr) {\n"
+        "  unsigned v = sobol_bits((unsigned)a, dim); return u32_to_unit(scr ? fast_owen(v, seed) : v); }\n"
+        "}\n")
+    so = d / "shim.so"
+    subprocess.check_call(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-shared", "-fPIC", str(src), "-o", str(so)])
+    L = ctypes.CDLL(str(so))
+    L.zs.argtypes = [ctypes.c_int] * 7 + [ctypes.c_char_p, ctypes.POINTER(ctypes.c_float)]
+    L.sob.restype = ctypes.c_float
+    L.sob.argtypes = [ctypes.c_ulonglong, ctypes.c_int, ctypes.c_uint, ctypes.c_int]
+    return L
+
+
+def test_header_zsobol_streams_match_reference(hdr, golden):
+    for c in golden["zsobol"]:
+        n = sum(1 if ch == "1" else 2 for ch in c["pattern"])
+        out = np.zeros(n, np.float32)
+        hdr.zs(c["spp"], c["resx"], c["resy"], c["px"], c["py"], c["s"], c["seed"], c["pattern"].encode(),
+               out.ctypes.data_as(ctypes.POINTER(ctypes.c_float)))
+        assert out.view(np.uint32).tolist() == c["u"], c
+
+
+def test_header_sobol_bits_match_reference(hdr, golden):
+    for a, seed, f0, f1, p0, p1 in golden["sobol_fastowen"]:
+        a = int(a)
+        if a >= 1 << 32:
+            continue
+        got = [hdr.sob(a, 0, seed, 1), hdr.sob(a, 1, seed, 1), hdr.sob(a, 0, 0, 0), hdr.sob(a, 1, 0, 0)]
+        assert np.array(got, np.float32).view(np.uint32).tolist() == [f0, f1, p0, p1]
