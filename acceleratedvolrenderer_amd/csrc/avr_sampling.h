@@ -103,50 +103,71 @@ struct ZSobolParams {
     int log2spp, nBase4Digits, seed;
 };
 
-// ZSobolSampler::GetSampleIndex (samplers.h:296-355) for the current dimension
-AVR_HD uint64_t zsobol_index(uint64_t morton, uint32_t dimension, const ZSobolParams &zp) {
-    uint64_t sampleIndex = 0;
+// MixBits(x) >> 24 for x < 2^32 (a 40-bit value), as (hi 8 bits, lo 32 bits)
+AVR_HD void mix_hi40(uint32_t x, uint32_t *hi, uint32_t *lo) {
+    uint64_t v = (uint64_t)(x ^ (x >> 31));   // v ^= v >> 31 on a zero-extended 32-bit value
+    v *= 0x7fb5d329728ea185ull;
+    v ^= v >> 27;
+    v *= 0x81dadef4bc2dd44dull;
+    v ^= v >> 33;
+    *hi = (uint32_t)(v >> 56);
+    *lo = (uint32_t)(v >> 24);
+}
+
+// ZSobolSampler::GetSampleIndex (samplers.h:296-355) for the current dimension. The host
+// guarantees Morton(pixel) << log2(spp) | index < 2^32 (nBase4Digits <= 16), so the Morton
+// index, every digit prefix and the result fit in 32 bits (the reference's uint64_t values
+// have zero upper halves).
+AVR_HD uint32_t zsobol_index(uint32_t morton, uint32_t dimension, const ZSobolParams &zp) {
+    uint32_t sampleIndex = 0;
     const bool pow2 = zp.log2spp & 1;
     const int lastDigit = pow2 ? 1 : 0;
-    const uint64_t dmix = (uint64_t)(0x55555555u * dimension);
+    const uint32_t dmix = 0x55555555u * dimension;
     for (int i = zp.nBase4Digits - 1; i >= lastDigit; --i) {
         const int shift = 2 * i - (pow2 ? 1 : 0);
-        const int digit = (int)(morton >> shift) & 3;
-        const uint64_t y = mix64((morton >> (shift + 2)) ^ dmix) >> 24;   // < 2^40
-        // y % 24 with 32-bit pieces: 2^32 = 16 (mod 24)
-        const uint32_t hi = (uint32_t)(y >> 32), lo = (uint32_t)y;
+        const uint32_t digit = (morton >> shift) & 3u;
+        const uint32_t higher = shift + 2 >= 32 ? 0u : morton >> (shift + 2);
+        uint32_t hi, lo;
+        mix_hi40(higher ^ dmix, &hi, &lo);
+        // (MixBits(..) >> 24) % 24 from 32-bit pieces: 2^32 = 16 (mod 24)
         const uint32_t p = (hi * 16u + lo % 24u) % 24u;
         const uint64_t w = p < 8 ? kZPermW0 : (p < 16 ? kZPermW1 : kZPermW2);
         const uint32_t nd = (uint32_t)(w >> ((p & 7) * 8 + 2 * digit)) & 3u;
-        sampleIndex |= (uint64_t)nd << shift;
+        sampleIndex |= nd << shift;
     }
     if (pow2) {
-        const int digit = (int)(morton & 1);
-        sampleIndex |= (uint64_t)(digit ^ (int)(mix64((morton >> 1) ^ dmix) & 1));
+        const uint32_t digit = morton & 1u;
+        const uint32_t x = (morton >> 1) ^ dmix;
+        uint64_t v = (uint64_t)(x ^ (x >> 31));
+        v *= 0x7fb5d329728ea185ull;
+        v ^= v >> 27;
+        v *= 0x81dadef4bc2dd44dull;
+        v ^= v >> 33;
+        sampleIndex |= digit ^ (uint32_t)(v & 1);
     }
     return sampleIndex;
 }
 
 // ZSobolSampler state of one pixel sample
 struct ZSobol {
-    uint64_t morton;
+    uint32_t morton;
     uint32_t dimension;
     AVR_HD void start(int px, int py, int sampleIndex, const ZSobolParams &zp) {
-        morton = (encode_morton2((uint32_t)px, (uint32_t)py) << zp.log2spp) | (uint64_t)(uint32_t)sampleIndex;
+        morton = ((uint32_t)encode_morton2((uint32_t)px, (uint32_t)py) << zp.log2spp) | (uint32_t)sampleIndex;
         dimension = 0;
     }
     AVR_HD float get1d(const ZSobolParams &zp) {
-        const uint64_t a = zsobol_index(morton, dimension, zp);
+        const uint32_t a = zsobol_index(morton, dimension, zp);
         ++dimension;
         const uint32_t h = (uint32_t)hash_2u32(dimension, (uint32_t)zp.seed);
-        return u32_to_unit(fast_owen(sobol_bits((uint32_t)a, 0), h));
+        return u32_to_unit(fast_owen(sobol_bits(a, 0), h));
     }
     AVR_HD void get2d(const ZSobolParams &zp, float *u0, float *u1) {
-        const uint64_t a = zsobol_index(morton, dimension, zp);
+        const uint32_t a = zsobol_index(morton, dimension, zp);
         dimension += 2;
         const uint64_t h = hash_2u32(dimension, (uint32_t)zp.seed);
-        *u0 = u32_to_unit(fast_owen(sobol_bits((uint32_t)a, 0), (uint32_t)h));
-        *u1 = u32_to_unit(fast_owen(sobol_bits((uint32_t)a, 1), (uint32_t)(h >> 32)));
+        *u0 = u32_to_unit(fast_owen(sobol_bits(a, 0), (uint32_t)h));
+        *u1 = u32_to_unit(fast_owen(sobol_bits(a, 1), (uint32_t)(h >> 32)));
     }
 };
 

@@ -46,6 +46,10 @@ def parse():
     p.add_argument("--refill-min", type=int, default=0, help="k_paths refill threshold (0 = library default)")
     p.add_argument("--grid-layout", default="fat", choices=["fat", "linear"])
     p.add_argument("--dda-budget", type=int, default=0, help="k_paths DDA cells per iteration (0 = default)")
+    p.add_argument("--sampler", default="zsobol", choices=["zsobol", "independent"],
+                   help="pixel sampler (BASELINE.md S-cloud: zsobol, pbrt's default)")
+    p.add_argument("--filter", default="gaussian", choices=["gaussian", "box"],
+                   help="pixel filter (pbrt's default: gaussian radius 1.5, sigma 0.5)")
     return p.parse_args()
 
 
@@ -111,10 +115,17 @@ def main():
     gen.sync()
     gen.close()
     tgen = time.perf_counter() - tgen
-    scene = scenes.s_cloud(density, width=args.width, height=args.height)
+    # the sampler's pixelsamples covers every sample index the run renders (ZSobol lays out
+    # Morton(pixel) << log2(spp) | index): 256 (config C3) unless more are rendered
+    S = args.spp_per_step
+    needed = (args.warmup + args.steps) * world * S
+    spp_total = 256
+    while spp_total < needed:
+        spp_total *= 2
+    scene = scenes.s_cloud(density, width=args.width, height=args.height, sampler=args.sampler, spp=spp_total,
+                           filter=args.filter)
     integ = VolPathIntegrator(scene, maxdepth=scenes.CLOUD_MAXDEPTH, spp=args.spp_per_step, seed=0, device=dev,
                               max_paths=args.max_paths, kernel=args.kernel, grid_layout=args.grid_layout)
-    S = args.spp_per_step
     if args.refill_min:
         integ.ctx.set_refill_min(args.refill_min)
     if args.dda_budget:
@@ -173,21 +184,22 @@ def main():
     # workload (FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md HBM section); bench.py
     # itself cannot read counters. Null when the profile does not match the run.
     traffic, traffic_src, valu = None, None, None
-    prof = os.path.join(ROOT, "profiles", "r01_pmc_k_paths.json")
+    prof = os.path.join(ROOT, "profiles", f"r01_pmc_k_paths_{args.sampler}_{args.filter}.json")
     if args.kernel == "persistent" and n == 1024 and S == 16 and os.path.exists(prof):
         pm = json.load(open(prof))
         traffic = round(pm["hbm_traffic_bytes_per_launch"] / 1e9, 3)
-        traffic_src = "profiles/r01_pmc_k_paths.json (GB per launch, PMC FETCH_SIZE x2 + WRITE_SIZE)"
+        traffic_src = os.path.relpath(prof, ROOT) + " (GB per launch, PMC FETCH_SIZE x2 + WRITE_SIZE)"
         # the bound that is actually close: VALU issue (wave64 op = 2 SIMD cycles)
         valu = {"wave_instructions_per_launch": pm["valu_wave_instructions_per_launch"],
                 "issue_fraction": round(pm["valu_issue_fraction"], 4),
-                "wave_cycle_split": pm["wave_cycle_split"], "source": "profiles/r01_pmc_k_paths.json"}
+                "wave_cycle_split": pm["wave_cycle_split"], "source": os.path.relpath(prof, ROOT)}
     out = None
     if rank == 0:
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             host_density = density.cpu().numpy()
-            host_scene = scenes.s_cloud(host_density, width=args.width, height=args.height)
+            host_scene = scenes.s_cloud(host_density, width=args.width, height=args.height, sampler=args.sampler,
+                                        spp=spp_total, filter=args.filter)
             cpu = cpu_baseline(host_scene, S, args.cpu_seconds)
         out = {
             "metric": "Msamples/s (whole node) on synthetic S-cloud-1024 720p (disney-cloud stand-in)",
@@ -203,7 +215,8 @@ def main():
             "dtype": "f32",
             "data": "synthetic (CloudMedium::Density 1024^3 generated on device; disney-cloud assets absent)",
             "config": {"workload": f"S-cloud-{n} GridMedium, perspective {args.width}x{args.height}, "
-                                   f"{S} spp/step/GPU, maxdepth {scenes.CLOUD_MAXDEPTH}, independent sampler",
+                                   f"{S} spp/step/GPU, maxdepth {scenes.CLOUD_MAXDEPTH}, {args.sampler} sampler "
+                                   f"(pixelsamples {spp_total}), {args.filter} filter",
                        "global_batch": samples // args.steps, "parallelism": f"sample-shard x{world}"},
             "roofline": {
                 "kernel": kname,
