@@ -66,6 +66,10 @@ SIGNATURES = {
                                   ctypes.c_float]),
     "avr_camera": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, c_float_p, c_float_p]),
     "avr_last_pass_weights": (ctypes.c_int, [ctypes.c_void_p, c_float_p, ctypes.c_longlong]),
+    "avr_transmittance": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_longlong, c_float_p, c_float_p, c_float_p,
+                                         c_float_p]),
+    "avr_transmittance_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_longlong, ctypes.c_void_p,
+                                                ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "avr_set_filter": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, c_float_p, ctypes.c_float]),
     "avr_set_sampler": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]),
     "avr_film": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, c_float_p, c_float_p, ctypes.c_float,
@@ -234,6 +238,15 @@ class Context:
         w = np.zeros(npix * max_samples, np.float32)
         _check(self.lib.avr_last_pass_weights(self.h, _fp(w), len(w)))
         return w
+
+    def transmittance(self, p0, p1, lam):
+        """Integrator::Tr for n queries: p0, p1 (n, 3) render-space points, lam (n, 4) nm."""
+        p0 = np.ascontiguousarray(p0, np.float32)
+        p1 = np.ascontiguousarray(p1, np.float32)
+        lam = np.ascontiguousarray(lam, np.float32)
+        out = np.zeros((len(p0), 4), np.float32)
+        _check(self.lib.avr_transmittance(self.h, len(p0), _fp(p0), _fp(p1), _fp(lam), _fp(out)))
+        return out
 
     def film_export_device(self, d_dst_ptr):
         _check(self.lib.avr_film_export_device(self.h, ctypes.c_void_p(d_dst_ptr)))

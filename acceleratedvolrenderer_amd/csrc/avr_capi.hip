@@ -669,6 +669,45 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
     return AVR_OK;
 }
 
+int avr_transmittance_device(avr_context *c, long long n, const float *p0, const float *p1, const float *lambda,
+                             float *tr) {
+    if (!c || n < 0 || (n > 0 && (!p0 || !p1 || !lambda || !tr))) return fail(AVR_ERR_ARG, "bad transmittance query");
+    if (!c->has_medium) return fail(AVR_ERR_STATE, "medium required");
+    if (n == 0) return AVR_OK;
+    HIP_TRY(hipSetDevice(c->device));
+    avr::Params p{};
+    p.med = c->med;
+    p.stats = c->d_stats;
+    const int blocks = (int)std::min<long long>((n + 255) / 256, 8192);
+    EV_MARK(t0);
+    hipLaunchKernelGGL(avr::k_transmittance, dim3(blocks), dim3(256), 0, c->stream, p, n, p0, p1, lambda, tr);
+    HIP_TRY(hipGetLastError());
+    EV_MARK(t1);
+    c->timed.push_back({t0, t1, &avr_stats::ms_shadow, false});
+    return AVR_OK;
+}
+
+int avr_transmittance(avr_context *c, long long n, const float *p0, const float *p1, const float *lambda, float *tr) {
+    if (!c || n < 0 || (n > 0 && (!p0 || !p1 || !lambda || !tr))) return fail(AVR_ERR_ARG, "bad transmittance query");
+    if (n == 0) return AVR_OK;
+    HIP_TRY(hipSetDevice(c->device));
+    float *d = nullptr;
+    HIP_TRY(dalloc(&d, (size_t)n * 14));
+    float *dp0 = d, *dp1 = d + 3 * n, *dl = d + 6 * n, *dtr = d + 10 * n;
+    HIP_TRY(hipMemcpyAsync(dp0, p0, 3 * n * sizeof(float), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(dp1, p1, 3 * n * sizeof(float), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(dl, lambda, 4 * n * sizeof(float), hipMemcpyHostToDevice, c->stream));
+    int rc = avr_transmittance_device(c, n, dp0, dp1, dl, dtr);
+    if (rc == AVR_OK) {
+        hipError_t e = hipMemcpyAsync(tr, dtr, 4 * n * sizeof(float), hipMemcpyDeviceToHost, c->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+        if (e != hipSuccess) rc = fail(AVR_ERR_HIP, hipGetErrorString(e));
+    }
+    (void)hipStreamSynchronize(c->stream);
+    (void)hipFree(d);
+    return rc;
+}
+
 int avr_sync(avr_context *c) {
     if (!c) return fail(AVR_ERR_ARG, "null context");
     HIP_TRY(hipStreamSynchronize(c->stream));

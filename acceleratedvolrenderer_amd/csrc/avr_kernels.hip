@@ -1309,6 +1309,55 @@ __global__ void __launch_bounds__(256) k_film(Params P) {
 }
 
 // ---------------------------------------------------------------------------
+// Integrator::Tr (cpu/integrators.cpp:324-374): ratio-tracking transmittance between
+// points p0 -> p1 in the medium at four given wavelengths; one query per lane. RNG seeded
+// with Hash(p0), Hash(p1); the ray is p0.SpawnRayTo(p1) (a medium interaction: no origin
+// offset) clipped at 1 - ShadowEpsilon; result Tr / inv_w.Average().
+__global__ void __launch_bounds__(256) k_transmittance(Params P, long long n, const float *__restrict__ p0,
+                                                       const float *__restrict__ p1,
+                                                       const float *__restrict__ lambda, float *__restrict__ out) {
+    __shared__ float s_maj[4096];
+    const float *maj = stage_majorant(P.med, s_maj);
+    unsigned long long nLookup = 0, nSteps = 0, nIn = 0;
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+        ++nIn;
+        const V3 a = {p0[3 * i], p0[3 * i + 1], p0[3 * i + 2]}, b = {p1[3 * i], p1[3 * i + 1], p1[3 * i + 2]};
+        const Spec lamv = {lambda[4 * i], lambda[4 * i + 1], lambda[4 * i + 2], lambda[4 * i + 3]};
+        Spec Tr = Spec::c(1.f), inv_w = Spec::c(1.f);
+        Pcg32 rng;
+        rng.set_sequence(hash_3u32(f2u(a.x), f2u(a.y), f2u(a.z)), hash_3u32(f2u(b.x), f2u(b.y), f2u(b.z)));
+        Ray ray{a, b - a};
+        if (dot(ray.d, ray.d) != 0) {
+            const V3 pExit = ray.o + ray.d * (1 - kShadowEpsilon);
+            ray.d = pExit - ray.o;
+            const LambdaIdx li = lambda_index(lamv);
+            const Spec sig_a = sample_table(P.med.sigma_a, li);
+            const Spec sig_s = sample_table(P.med.sigma_s, li);
+            const float u = rng.uniform();
+            auto cb = [&](V3, const MediumSample &ms, const Spec &sigma_maj, const Spec &T_maj) -> bool {
+                const Spec sigma_n = clamp_zero(sigma_maj - ms.sigma_a - ms.sigma_s);
+                const float pr = T_maj.v0 * sigma_maj.v0;
+                Tr = Tr * (T_maj * sigma_n / pr);
+                inv_w = inv_w * (T_maj * sigma_maj / pr);
+                return Tr.nonzero() && inv_w.nonzero();
+            };
+            const Spec T_maj = sample_t_maj(P.med, maj, ray, 1.f, u, rng, sig_a, sig_s, Spec::c(0.f), nLookup, nSteps,
+                                            cb);
+            Tr = Tr * (T_maj / T_maj.v0);
+            inv_w = inv_w * (T_maj / T_maj.v0);
+            Tr = Tr / inv_w.avg();
+        }
+        out[4 * i] = Tr.v0;
+        out[4 * i + 1] = Tr.v1;
+        out[4 * i + 2] = Tr.v2;
+        out[4 * i + 3] = Tr.v3;
+    }
+    flush_stat(P.stats, 3, nLookup);
+    flush_stat(P.stats, 4, nIn);
+    flush_stat(P.stats, 6, nSteps);
+}
+
+// ---------------------------------------------------------------------------
 // MajorantGrid build — GridMedium ctor (media.cpp:229, 241-246): each cell is
 // SampledGrid::MaxValue over MajorantGrid::VoxelBounds (containers.h:838-857).
 // One workgroup per majorant cell; wave max-reduction, then LDS.

@@ -136,6 +136,14 @@ int avr_set_sampler(avr_context *ctx, int kind, int samples_per_pixel);
 /* Render sample indices [spp_begin, spp_end) of every pixel (the avr_set_sampler sampler,
  * seed), VolPathIntegrator maxdepth. Asynchronous on the context stream. */
 int avr_render(avr_context *ctx, int spp_begin, int spp_end, int seed, int max_depth);
+/* Integrator::Tr (cpu/integrators.cpp:324-374): ratio-tracking transmittance from p0[i] to
+ * p1[i] (render space, xyz) at the four wavelengths lambda[4i..4i+3] (nm), n queries; writes
+ * tr[4i..4i+3] = Tr / inv_w.Average(). RNG per query seeded with Hash(p0), Hash(p1), as pbrt.
+ * avr_transmittance: host arrays, synchronous. _device: device arrays, async on the stream. */
+int avr_transmittance(avr_context *ctx, long long n, const float *p0, const float *p1, const float *lambda,
+                      float *tr);
+int avr_transmittance_device(avr_context *ctx, long long n, const float *p0, const float *p1, const float *lambda,
+                             float *tr);
 int avr_sync(avr_context *ctx);
 int avr_get_stats(avr_context *ctx, avr_stats *out);   /* waits for queued work */
 int avr_reset_stats(avr_context *ctx);

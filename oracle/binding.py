@@ -131,6 +131,8 @@ def lib():
                                                  ctypes.c_int, ctypes.c_int, c_float_p]
         L.oracle_cloud_grid.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, c_float_p]
         L.oracle_set_libm.argtypes = [ctypes.c_int]
+        L.oracle_transmittance4.argtypes = [ctypes.POINTER(OracleScene), ctypes.c_int, c_float_p, c_float_p,
+                                            c_float_p, c_float_p]
         L.oracle_get_libm.restype = ctypes.c_int
     return _lib
 
@@ -264,6 +266,16 @@ class OracleRun:
         out = np.zeros(len(p0), np.float32)
         set_libm(self.libm)
         lib().oracle_transmittance(ctypes.byref(self.s), len(p0), fp(p0), fp(p1), lambda_u, fp(out))
+        return out
+
+    def transmittance4(self, p0, p1, lam):
+        """Integrator::Tr at explicit wavelengths: (n, 4)."""
+        p0 = np.ascontiguousarray(p0, np.float32)
+        p1 = np.ascontiguousarray(p1, np.float32)
+        lam = np.ascontiguousarray(lam, np.float32)
+        out = np.zeros((len(p0), 4), np.float32)
+        set_libm(self.libm)
+        lib().oracle_transmittance4(ctypes.byref(self.s), len(p0), fp(p0), fp(p1), fp(lam), fp(out))
         return out
 
     def dda_segments(self, o, d, tmax=np.inf, lambda_u=0.5, max_segs=256):

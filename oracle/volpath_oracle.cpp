@@ -1380,6 +1380,38 @@ void oracle_transmittance(const OracleScene *s, int n, const float *p0, const fl
     }
 }
 
+// Integrator::Tr at explicit wavelengths (4 per query), all four components.
+void oracle_transmittance4(const OracleScene *s, int n, const float *p0, const float *p1, const float *lambdas,
+                           float *trOut) {
+    SceneView sv(*s);
+    for (int i = 0; i < n; ++i) {
+        Lambda l;
+        for (int k = 0; k < NS; ++k) { l.lambda[k] = lambdas[4 * i + k]; l.pdf[k] = VisibleWavelengthsPDF(l.lambda[k]); }
+        V3 a = {p0[3 * i], p0[3 * i + 1], p0[3 * i + 2]}, b = {p1[3 * i], p1[3 * i + 1], p1[3 * i + 2]};
+        RNG rng(HashBytes(&a, 12), HashBytes(&b, 12));
+        Ray ray = {a, b - a};
+        Spec Tr = Spec::Const(1.f), inv_w = Spec::Const(1.f);
+        if (LengthSquared(ray.d) != 0) {
+            V3 pExit = ray.o + ray.d * (1 - ShadowEpsilon);
+            ray.d = pExit - ray.o;
+            float u = rng.Uniform();
+            Spec T_maj = SampleT_maj(sv, ray, 1.f, u, rng, l,
+                [&](V3, const MediumProps &mp, Spec sigma_maj, Spec Tm) {
+                    Spec sigma_n = ClampZero(sigma_maj - mp.sigma_a - mp.sigma_s);
+                    float pr = Tm[0] * sigma_maj[0];
+                    Tr = Tr * (Tm * sigma_n / pr);
+                    inv_w = inv_w * (Tm * sigma_maj / pr);
+                    if (!Tr || !inv_w) return false;
+                    return true;
+                });
+            Tr = Tr * (T_maj / T_maj[0]);
+            inv_w = inv_w * (T_maj / T_maj[0]);
+            Tr = Tr / inv_w.Average();
+        }
+        for (int k = 0; k < NS; ++k) trOut[4 * i + k] = Tr.v[k];
+    }
+}
+
 // Majorant DDA segments of one ray (for tests): returns count, writes (tMin, tMax, sigma_maj[0]).
 int oracle_dda_segments(const OracleScene *s, const float *o, const float *d, float tMax, float lambda_u, int maxSegs,
                         float *out) {
