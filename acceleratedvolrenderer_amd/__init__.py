@@ -8,7 +8,7 @@ include/avr.h. See DESIGN.md.
 """
 from . import spectra, transform
 from .scene import (GridMedium, DistantLight, UniformInfiniteLight, OrthographicCamera, PerspectiveCamera, RGBFilm,
-                    Scene, film_rgb, BoxFilter, GaussianFilter, IndependentSampler, ZSobolSampler)
+                    Scene, film_rgb, HomogeneousMedium, CloudMedium, BoxFilter, GaussianFilter, IndependentSampler, ZSobolSampler)
 from .integrator import VolPathIntegrator, shard_samples, INTEGRATOR_NAMES
 from . import capi
 from . import scenes

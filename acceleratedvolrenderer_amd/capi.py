@@ -70,6 +70,10 @@ SIGNATURES = {
                                          c_float_p]),
     "avr_transmittance_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_longlong, ctypes.c_void_p,
                                                 ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "avr_medium_homogeneous": (ctypes.c_int, [ctypes.c_void_p, c_float_p, c_float_p, c_float_p, c_float_p,
+                                              c_float_p, ctypes.c_float, c_float_p]),
+    "avr_medium_cloud": (ctypes.c_int, [ctypes.c_void_p, c_float_p, c_float_p, c_float_p, c_float_p, c_float_p,
+                                        ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float]),
     "avr_set_filter": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, c_float_p, ctypes.c_float]),
     "avr_set_sampler": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]),
     "avr_film": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, c_float_p, c_float_p, ctypes.c_float,
@@ -165,7 +169,13 @@ class Context:
         Le = f32(med.Le) if med.Le is not None else None
         ls = f32(med.Lescale)
         self._keep = args + [Le, ls, mres]
-        if med.device_density is not None:
+        if getattr(med, "type_id", 0) == 1:
+            _check(self.lib.avr_medium_homogeneous(self.h, _fp(args[0]), _fp(args[1]), _fp(args[2]), _fp(args[3]),
+                                                   _fp(args[4]), float(med.g), _fp(Le)))
+        elif getattr(med, "type_id", 0) == 2:
+            _check(self.lib.avr_medium_cloud(self.h, _fp(args[0]), _fp(args[1]), _fp(args[2]), _fp(args[3]),
+                                             _fp(args[4]), float(med.g), *[float(v) for v in med.cloud]))
+        elif med.device_density is not None:
             _check(self.lib.avr_medium_grid_device(
                 self.h, ctypes.c_void_p(med.device_density.data_ptr()), med.nx, med.ny, med.nz, _fp(args[0]),
                 _fp(args[1]), _fp(args[2]), _fp(args[3]), _fp(args[4]), float(med.g), _fp(Le), _fp(ls),

@@ -146,7 +146,8 @@ bool affine(const float m[16]) { return m[12] == 0 && m[13] == 0 && m[14] == 0 &
 
 int medium_common(avr_context *c, const float *d_density, int nx, int ny, int nz, const float bounds[6],
                   const float rfm[16], const float mfr[16], const float *sigma_a, const float *sigma_s, float g,
-                  const float *Le, const float *Lescale, int lnx, int lny, int lnz, const int mres[3]) {
+                  const float *Le, const float *Lescale, int lnx, int lny, int lnz, const int mres[3],
+                  int type = 0, const float cloud[3] = nullptr) {
     if (!affine(rfm) || !affine(mfr)) return fail(AVR_ERR_ARG, "medium transforms must be affine");
     if (!sigma_a || !sigma_s) return fail(AVR_ERR_ARG, "sigma_a/sigma_s tables required");
     if (mres[0] < 1 || mres[1] < 1 || mres[2] < 1) return fail(AVR_ERR_ARG, "bad majorant resolution");
@@ -157,6 +158,10 @@ int medium_common(avr_context *c, const float *d_density, int nx, int ny, int nz
     if ((rc = upload_table(&c->d_Le, Le, avr::kNTable, c->stream))) return rc;
     if ((rc = upload_table(&c->d_lescale, Le ? Lescale : nullptr, (size_t)lnx * lny * lnz, c->stream))) return rc;
     avr::DevMedium &m = c->med;
+    m.type = type;
+    m.cloud_density = cloud ? cloud[0] : 0.f;
+    m.cloud_wispiness = cloud ? cloud[1] : 0.f;
+    m.cloud_frequency = cloud ? cloud[2] : 0.f;
     m.density = d_density;
     m.nx = nx; m.ny = ny; m.nz = nz;
     for (int i = 0; i < 3; ++i) { m.bmin[i] = bounds[i]; m.bmax[i] = bounds[3 + i]; m.mres[i] = mres[i]; }
@@ -178,13 +183,18 @@ int medium_common(avr_context *c, const float *d_density, int nx, int ny, int nz
     if (c->d_majorant) (void)hipFree(c->d_majorant);
     const int nm = mres[0] * mres[1] * mres[2];
     HIP_TRY(dalloc(&c->d_majorant, (size_t)nm));
-    hipLaunchKernelGGL(avr::k_majorant, dim3(nm), dim3(256), 0, c->stream, d_density, nx, ny, nz, mres[0], mres[1],
-                       mres[2], c->d_majorant);
-    HIP_TRY(hipGetLastError());
+    if (type == 0) {
+        hipLaunchKernelGGL(avr::k_majorant, dim3(nm), dim3(256), 0, c->stream, d_density, nx, ny, nz, mres[0], mres[1],
+                           mres[2], c->d_majorant);
+        HIP_TRY(hipGetLastError());
+    } else {   // single segment, sigma_maj = sigma_t * 1 (density <= 1 for the cloud)
+        const float one = 1.f;
+        HIP_TRY(hipMemcpyAsync(c->d_majorant, &one, sizeof(float), hipMemcpyHostToDevice, c->stream));
+    }
     m.majorant = c->d_majorant;
     if (c->d_fat) { (void)hipFree(c->d_fat); c->d_fat = nullptr; }
     m.fat = nullptr;
-    if (c->grid_layout == 1) {
+    if (c->grid_layout == 1 && type == 0) {
         const size_t nfat = (size_t)(nx + 1) * (ny + 1) * (nz + 1);
         size_t freeB = 0, totalB = 0;
         HIP_TRY(hipMemGetInfo(&freeB, &totalB));
@@ -340,6 +350,27 @@ int avr_medium_grid_device(avr_context *c, const float *d_density, int nx, int n
     if (c->d_density_owned) { (void)hipFree(c->d_density_owned); c->d_density_owned = nullptr; }
     return medium_common(c, d_density, nx, ny, nz, bounds, rfm, mfr, sigma_a, sigma_s, g, Le, Lescale, lnx, lny, lnz,
                          mres);
+}
+
+int avr_medium_homogeneous(avr_context *c, const float bounds[6], const float rfm[16], const float mfr[16],
+                           const float *sigma_a, const float *sigma_s, float g, const float *Le) {
+    if (!c || !bounds || !rfm || !mfr) return fail(AVR_ERR_ARG, "null medium argument");
+    HIP_TRY(hipSetDevice(c->device));
+    static const float one = 1.f;
+    const int mres[3] = {1, 1, 1};
+    return medium_common(c, nullptr, 1, 1, 1, bounds, rfm, mfr, sigma_a, sigma_s, g, Le, Le ? &one : nullptr, 1, 1, 1,
+                         mres, 1, nullptr);
+}
+
+int avr_medium_cloud(avr_context *c, const float bounds[6], const float rfm[16], const float mfr[16],
+                     const float *sigma_a, const float *sigma_s, float g, float density, float wispiness,
+                     float frequency) {
+    if (!c || !bounds || !rfm || !mfr) return fail(AVR_ERR_ARG, "null medium argument");
+    HIP_TRY(hipSetDevice(c->device));
+    const int mres[3] = {1, 1, 1};
+    const float cloud[3] = {density, wispiness, frequency};
+    return medium_common(c, nullptr, 1, 1, 1, bounds, rfm, mfr, sigma_a, sigma_s, g, nullptr, nullptr, 1, 1, 1, mres,
+                         2, cloud);
 }
 
 int avr_generate_cloud(avr_context *c, float *d_out, int n, long long first, long long count, float density,
@@ -582,8 +613,9 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
         p.stats = c->d_stats;
         const long long n0 = P * S;
         // k_paths keeps the majorant grid in LDS (4096 cells = pbrt's 16^3); larger grids
-        // take the wavefront kernels, which read it through L2
-        const bool persistent = c->kernel_mode == 0 &&
+        // take the wavefront kernels, which read it through L2.
+        // k_paths is specialised for GridMedium: homogeneous and cloud media run wavefront
+        const bool persistent = c->kernel_mode == 0 && c->med.type == 0 &&
                                 c->med.mres[0] * c->med.mres[1] * c->med.mres[2] <= 4096 &&
                                 c->med.mres[0] <= 255 && c->med.mres[1] <= 255 && c->med.mres[2] <= 255;
         c->last_persistent = persistent;

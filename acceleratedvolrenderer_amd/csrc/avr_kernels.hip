@@ -43,6 +43,12 @@ struct DevMedium {
     // in 2-4 lines. 8x the grid's memory ((n+1)^3 x 32 B; 34 GB at 1024^3 of the 288 GB).
     const float4 *fat;
     int unit_box;          // bounds extent exactly 1 on every axis: Offset's divisions are by 1.0f
+    // medium type: 0 GridMedium (media.h:265-352), 1 HomogeneousMedium (media.h:217-262),
+    // 2 CloudMedium (media.h:430-528). Types 1 and 2 have one majorant segment (the
+    // HomogeneousMajorantIterator over the bounds crossing, sigma_maj = sigma_t): a 1^3
+    // majorant of 1.0 whose DDA never crosses a cell face.
+    int type;
+    float cloud_density, cloud_wispiness, cloud_frequency;
 };
 
 constexpr int kMaxLights = 8;
@@ -190,6 +196,89 @@ __global__ void __launch_bounds__(256) k_fatten(const float *__restrict__ v, int
     }
 }
 
+// ---------------------------------------------------------------------------
+// CloudMedium::Density — the procedural medium (medium type 2) and the generator of the
+// synthetic heterogeneous grid (BASELINE.md S-cloud; k_cloud below): CloudMedium::Density
+// (media.h:496-520; density 1, wispiness 1, frequency 5) at voxel centres, with
+// pbrt's Perlin Noise/DNoise (util/noise.cpp). Only +,-,*,floor,fmod: bit-exact vs CPU.
+__constant__ int c_perm[512] = {
+    151, 160, 137, 91, 90, 15, 131, 13, 201, 95, 96, 53, 194, 233, 7, 225, 140, 36, 103, 30, 69, 142,
+    8, 99, 37, 240, 21, 10, 23, 190, 6, 148, 247, 120, 234, 75, 0, 26, 197, 62, 94, 252, 219, 203, 117,
+    35, 11, 32, 57, 177, 33, 88, 237, 149, 56, 87, 174, 20, 125, 136, 171, 168, 68, 175, 74, 165, 71,
+    134, 139, 48, 27, 166, 77, 146, 158, 231, 83, 111, 229, 122, 60, 211, 133, 230, 220, 105, 92, 41,
+    55, 46, 245, 40, 244, 102, 143, 54, 65, 25, 63, 161, 1, 216, 80, 73, 209, 76, 132, 187, 208, 89,
+    18, 169, 200, 196, 135, 130, 116, 188, 159, 86, 164, 100, 109, 198, 173, 186, 3, 64, 52, 217, 226,
+    250, 124, 123, 5, 202, 38, 147, 118, 126, 255, 82, 85, 212, 207, 206, 59, 227, 47, 16, 58, 17, 182,
+    189, 28, 42, 223, 183, 170, 213, 119, 248, 152, 2, 44, 154, 163, 70, 221, 153, 101, 155, 167, 43,
+    172, 9, 129, 22, 39, 253, 19, 98, 108, 110, 79, 113, 224, 232, 178, 185, 112, 104, 218, 246, 97,
+    228, 251, 34, 242, 193, 238, 210, 144, 12, 191, 179, 162, 241, 81, 51, 145, 235, 249, 14, 239,
+    107, 49, 192, 214, 31, 181, 199, 106, 157, 184, 84, 204, 176, 115, 121, 50, 45, 127, 4, 150, 254,
+    138, 236, 205, 93, 222, 114, 67, 29, 24, 72, 243, 141, 128, 195, 78, 66, 215, 61, 156, 180,
+    151, 160, 137, 91, 90, 15, 131, 13, 201, 95, 96, 53, 194, 233, 7, 225, 140, 36, 103, 30, 69, 142,
+    8, 99, 37, 240, 21, 10, 23, 190, 6, 148, 247, 120, 234, 75, 0, 26, 197, 62, 94, 252, 219, 203, 117,
+    35, 11, 32, 57, 177, 33, 88, 237, 149, 56, 87, 174, 20, 125, 136, 171, 168, 68, 175, 74, 165, 71,
+    134, 139, 48, 27, 166, 77, 146, 158, 231, 83, 111, 229, 122, 60, 211, 133, 230, 220, 105, 92, 41,
+    55, 46, 245, 40, 244, 102, 143, 54, 65, 25, 63, 161, 1, 216, 80, 73, 209, 76, 132, 187, 208, 89,
+    18, 169, 200, 196, 135, 130, 116, 188, 159, 86, 164, 100, 109, 198, 173, 186, 3, 64, 52, 217, 226,
+    250, 124, 123, 5, 202, 38, 147, 118, 126, 255, 82, 85, 212, 207, 206, 59, 227, 47, 16, 58, 17, 182,
+    189, 28, 42, 223, 183, 170, 213, 119, 248, 152, 2, 44, 154, 163, 70, 221, 153, 101, 155, 167, 43,
+    172, 9, 129, 22, 39, 253, 19, 98, 108, 110, 79, 113, 224, 232, 178, 185, 112, 104, 218, 246, 97,
+    228, 251, 34, 242, 193, 238, 210, 144, 12, 191, 179, 162, 241, 81, 51, 145, 235, 249, 14, 239,
+    107, 49, 192, 214, 31, 181, 199, 106, 157, 184, 84, 204, 176, 115, 121, 50, 45, 127, 4, 150, 254,
+    138, 236, 205, 93, 222, 114, 67, 29, 24, 72, 243, 141, 128, 195, 78, 66, 215, 61, 156, 180};
+
+__device__ __forceinline__ float noise_grad(int x, int y, int z, float dx, float dy, float dz) {
+    int h = c_perm[c_perm[c_perm[x] + y] + z] & 15;
+    float u = h < 8 || h == 12 || h == 13 ? dx : dy;
+    float v = h < 4 || h == 12 || h == 13 ? dy : dz;
+    return ((h & 1) ? -u : u) + ((h & 2) ? -v : v);
+}
+__device__ __forceinline__ float noise_weight(float t) {
+    float t2 = t * t;
+    return 6 * ((t2 * t2) * t) - 15 * (t2 * t2) + 10 * (t2 * t);
+}
+__device__ float perlin(float x, float y, float z) {
+    x = fmodf(x, float(1 << 30)); y = fmodf(y, float(1 << 30)); z = fmodf(z, float(1 << 30));
+    int ix = (int)__builtin_floorf(x), iy = (int)__builtin_floorf(y), iz = (int)__builtin_floorf(z);
+    float dx = x - ix, dy = y - iy, dz = z - iz;
+    ix &= 255; iy &= 255; iz &= 255;
+    float w000 = noise_grad(ix, iy, iz, dx, dy, dz), w100 = noise_grad(ix + 1, iy, iz, dx - 1, dy, dz);
+    float w010 = noise_grad(ix, iy + 1, iz, dx, dy - 1, dz), w110 = noise_grad(ix + 1, iy + 1, iz, dx - 1, dy - 1, dz);
+    float w001 = noise_grad(ix, iy, iz + 1, dx, dy, dz - 1), w101 = noise_grad(ix + 1, iy, iz + 1, dx - 1, dy, dz - 1);
+    float w011 = noise_grad(ix, iy + 1, iz + 1, dx, dy - 1, dz - 1);
+    float w111 = noise_grad(ix + 1, iy + 1, iz + 1, dx - 1, dy - 1, dz - 1);
+    float wx = noise_weight(dx), wy = noise_weight(dy), wz = noise_weight(dz);
+    float x00 = lerp(wx, w000, w100), x10 = lerp(wx, w010, w110), x01 = lerp(wx, w001, w101), x11 = lerp(wx, w011, w111);
+    return lerp(wz, lerp(wy, x00, x10), lerp(wy, x01, x11));
+}
+__device__ float cloud_density(V3 p, float density, float wispiness, float frequency) {
+    V3 pp = frequency * p;
+    if (wispiness > 0) {
+        float vomega = 0.05f * wispiness, vlambda = 10.f;
+        for (int i = 0; i < 2; ++i) {
+            V3 q = vlambda * pp;
+            const float delta = .01f;
+            float n = perlin(q.x, q.y, q.z);
+            V3 nd = {perlin(q.x + delta, q.y + 0.f, q.z + 0.f), perlin(q.x + 0.f, q.y + delta, q.z + 0.f),
+                     perlin(q.x + 0.f, q.y + 0.f, q.z + delta)};
+            V3 dn = (nd - V3{n, n, n}) / delta;
+            pp = pp + vomega * dn;
+            vomega *= 0.5f;
+            vlambda *= 1.99f;
+        }
+    }
+    float d = 0, omega = 0.5f, lam = 1.f;
+    for (int i = 0; i < 5; ++i) {
+        V3 q = lam * pp;
+        d += omega * perlin(q.x, q.y, q.z);
+        omega *= 0.5f;
+        lam *= 1.99f;
+    }
+    d = clampf((1 - p.y) * 4.5f * density * d, 0, 1);
+    d += 2 * fmaxf_(0.f, 0.5f - p.y);
+    return clampf(d, 0, 1);
+}
+
 struct MediumSample { Spec sigma_a, sigma_s, Le; };
 
 // GridMedium::SamplePoint — media.h:287-319 (no temperature grid); sig_a/sig_s pre-sampled at lambda
@@ -197,12 +286,24 @@ __device__ __forceinline__ MediumSample sample_point(const DevMedium &m, V3 p, c
                                                      const Spec &Le_l, bool emissive = true) {
     MediumSample ms;
     p = xf_point_pair(m.medium_from_render, p);
+    ms.Le = Spec::c(0.f);
+    if (m.type == 1) {             // HomogeneousMedium::SamplePoint: constant properties
+        ms.sigma_a = sig_a;
+        ms.sigma_s = sig_s;
+        if (emissive && m.emissive) ms.Le = Le_l;
+        return ms;
+    }
+    if (m.type == 2) {             // CloudMedium::SamplePoint: density * sigma at the medium-space point
+        const float d = cloud_density(p, m.cloud_density, m.cloud_wispiness, m.cloud_frequency);
+        ms.sigma_a = sig_a * d;
+        ms.sigma_s = sig_s * d;
+        return ms;
+    }
     // Bounds3::Offset (vecmath.h:1323-1332); x / 1.0f == x exactly, so a unit box skips it
     p = m.unit_box ? V3{p.x - m.bmin[0], p.y - m.bmin[1], p.z - m.bmin[2]} : box_offset(m.bmin, m.bmax, p);
     float d = m.fat ? fat_lookup(m.fat, m.density, m.nx, m.ny, m.nz, p) : grid_lookup(m.density, m.nx, m.ny, m.nz, p);
     ms.sigma_a = sig_a * d;
     ms.sigma_s = sig_s * d;
-    ms.Le = Spec::c(0.f);
     if (emissive && m.emissive) {
         float scale = grid_lookup(m.lescale, m.lnx, m.lny, m.lnz, p);
         if (scale > 0) ms.Le = Le_l * scale;
@@ -250,6 +351,10 @@ __device__ __forceinline__ bool dda_init(Dda &it, const DevMedium &m, Ray ray, f
     dda_axis(gi.x, gd.x, m.mres[0], tMin, it.vx, it.nx, it.dx, it.sx);
     dda_axis(gi.y, gd.y, m.mres[1], tMin, it.vy, it.ny, it.dy, it.sy);
     dda_axis(gi.z, gd.z, m.mres[2], tMin, it.vz, it.nz, it.dz, it.sz);
+    if (m.type != 0) {   // HomogeneousMajorantIterator(tMin, tMax, sigma_t): one segment
+        it.vx = it.vy = it.vz = 0;
+        it.nx = it.ny = it.nz = kInf;
+    }
     return true;
 }
 // Returns false when exhausted; majorant values read through `maj` (LDS-staged when it fits)
@@ -1183,7 +1288,8 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
             const S sigma_maj = sig_t * mv;
             T_maj = T_maj * sexp(-(sigma_maj * (t - tMin)));
             const V3 pc = po + sd * t;
-            // GridMedium::SamplePoint (media.h:287-319)
+            // GridMedium::SamplePoint (media.h:287-319); k_paths runs GridMedium only (the host
+            // sends homogeneous and cloud media to the wavefront kernels)
             V3 pm = xf_point_pair(m.medium_from_render, pc);
             pm = m.unit_box ? V3{pm.x - m.bmin[0], pm.y - m.bmin[1], pm.z - m.bmin[2]} : box_offset(m.bmin, m.bmax, pm);
             const float dens = m.fat ? fat_lookup(m.fat, m.density, m.nx, m.ny, m.nz, pm)
@@ -1394,87 +1500,6 @@ __global__ void __launch_bounds__(256) k_majorant(const float *__restrict__ dens
     }
 }
 
-// ---------------------------------------------------------------------------
-// Synthetic heterogeneous grid (BASELINE.md S-cloud): CloudMedium::Density
-// (media.h:496-520; density 1, wispiness 1, frequency 5) at voxel centres, with
-// pbrt's Perlin Noise/DNoise (util/noise.cpp). Only +,-,*,floor,fmod: bit-exact vs CPU.
-__constant__ int c_perm[512] = {
-    151, 160, 137, 91, 90, 15, 131, 13, 201, 95, 96, 53, 194, 233, 7, 225, 140, 36, 103, 30, 69, 142,
-    8, 99, 37, 240, 21, 10, 23, 190, 6, 148, 247, 120, 234, 75, 0, 26, 197, 62, 94, 252, 219, 203, 117,
-    35, 11, 32, 57, 177, 33, 88, 237, 149, 56, 87, 174, 20, 125, 136, 171, 168, 68, 175, 74, 165, 71,
-    134, 139, 48, 27, 166, 77, 146, 158, 231, 83, 111, 229, 122, 60, 211, 133, 230, 220, 105, 92, 41,
-    55, 46, 245, 40, 244, 102, 143, 54, 65, 25, 63, 161, 1, 216, 80, 73, 209, 76, 132, 187, 208, 89,
-    18, 169, 200, 196, 135, 130, 116, 188, 159, 86, 164, 100, 109, 198, 173, 186, 3, 64, 52, 217, 226,
-    250, 124, 123, 5, 202, 38, 147, 118, 126, 255, 82, 85, 212, 207, 206, 59, 227, 47, 16, 58, 17, 182,
-    189, 28, 42, 223, 183, 170, 213, 119, 248, 152, 2, 44, 154, 163, 70, 221, 153, 101, 155, 167, 43,
-    172, 9, 129, 22, 39, 253, 19, 98, 108, 110, 79, 113, 224, 232, 178, 185, 112, 104, 218, 246, 97,
-    228, 251, 34, 242, 193, 238, 210, 144, 12, 191, 179, 162, 241, 81, 51, 145, 235, 249, 14, 239,
-    107, 49, 192, 214, 31, 181, 199, 106, 157, 184, 84, 204, 176, 115, 121, 50, 45, 127, 4, 150, 254,
-    138, 236, 205, 93, 222, 114, 67, 29, 24, 72, 243, 141, 128, 195, 78, 66, 215, 61, 156, 180,
-    151, 160, 137, 91, 90, 15, 131, 13, 201, 95, 96, 53, 194, 233, 7, 225, 140, 36, 103, 30, 69, 142,
-    8, 99, 37, 240, 21, 10, 23, 190, 6, 148, 247, 120, 234, 75, 0, 26, 197, 62, 94, 252, 219, 203, 117,
-    35, 11, 32, 57, 177, 33, 88, 237, 149, 56, 87, 174, 20, 125, 136, 171, 168, 68, 175, 74, 165, 71,
-    134, 139, 48, 27, 166, 77, 146, 158, 231, 83, 111, 229, 122, 60, 211, 133, 230, 220, 105, 92, 41,
-    55, 46, 245, 40, 244, 102, 143, 54, 65, 25, 63, 161, 1, 216, 80, 73, 209, 76, 132, 187, 208, 89,
-    18, 169, 200, 196, 135, 130, 116, 188, 159, 86, 164, 100, 109, 198, 173, 186, 3, 64, 52, 217, 226,
-    250, 124, 123, 5, 202, 38, 147, 118, 126, 255, 82, 85, 212, 207, 206, 59, 227, 47, 16, 58, 17, 182,
-    189, 28, 42, 223, 183, 170, 213, 119, 248, 152, 2, 44, 154, 163, 70, 221, 153, 101, 155, 167, 43,
-    172, 9, 129, 22, 39, 253, 19, 98, 108, 110, 79, 113, 224, 232, 178, 185, 112, 104, 218, 246, 97,
-    228, 251, 34, 242, 193, 238, 210, 144, 12, 191, 179, 162, 241, 81, 51, 145, 235, 249, 14, 239,
-    107, 49, 192, 214, 31, 181, 199, 106, 157, 184, 84, 204, 176, 115, 121, 50, 45, 127, 4, 150, 254,
-    138, 236, 205, 93, 222, 114, 67, 29, 24, 72, 243, 141, 128, 195, 78, 66, 215, 61, 156, 180};
-
-__device__ __forceinline__ float noise_grad(int x, int y, int z, float dx, float dy, float dz) {
-    int h = c_perm[c_perm[c_perm[x] + y] + z] & 15;
-    float u = h < 8 || h == 12 || h == 13 ? dx : dy;
-    float v = h < 4 || h == 12 || h == 13 ? dy : dz;
-    return ((h & 1) ? -u : u) + ((h & 2) ? -v : v);
-}
-__device__ __forceinline__ float noise_weight(float t) {
-    float t2 = t * t;
-    return 6 * ((t2 * t2) * t) - 15 * (t2 * t2) + 10 * (t2 * t);
-}
-__device__ float perlin(float x, float y, float z) {
-    x = fmodf(x, float(1 << 30)); y = fmodf(y, float(1 << 30)); z = fmodf(z, float(1 << 30));
-    int ix = (int)__builtin_floorf(x), iy = (int)__builtin_floorf(y), iz = (int)__builtin_floorf(z);
-    float dx = x - ix, dy = y - iy, dz = z - iz;
-    ix &= 255; iy &= 255; iz &= 255;
-    float w000 = noise_grad(ix, iy, iz, dx, dy, dz), w100 = noise_grad(ix + 1, iy, iz, dx - 1, dy, dz);
-    float w010 = noise_grad(ix, iy + 1, iz, dx, dy - 1, dz), w110 = noise_grad(ix + 1, iy + 1, iz, dx - 1, dy - 1, dz);
-    float w001 = noise_grad(ix, iy, iz + 1, dx, dy, dz - 1), w101 = noise_grad(ix + 1, iy, iz + 1, dx - 1, dy, dz - 1);
-    float w011 = noise_grad(ix, iy + 1, iz + 1, dx, dy - 1, dz - 1);
-    float w111 = noise_grad(ix + 1, iy + 1, iz + 1, dx - 1, dy - 1, dz - 1);
-    float wx = noise_weight(dx), wy = noise_weight(dy), wz = noise_weight(dz);
-    float x00 = lerp(wx, w000, w100), x10 = lerp(wx, w010, w110), x01 = lerp(wx, w001, w101), x11 = lerp(wx, w011, w111);
-    return lerp(wz, lerp(wy, x00, x10), lerp(wy, x01, x11));
-}
-__device__ float cloud_density(V3 p, float density, float wispiness, float frequency) {
-    V3 pp = frequency * p;
-    if (wispiness > 0) {
-        float vomega = 0.05f * wispiness, vlambda = 10.f;
-        for (int i = 0; i < 2; ++i) {
-            V3 q = vlambda * pp;
-            const float delta = .01f;
-            float n = perlin(q.x, q.y, q.z);
-            V3 nd = {perlin(q.x + delta, q.y + 0.f, q.z + 0.f), perlin(q.x + 0.f, q.y + delta, q.z + 0.f),
-                     perlin(q.x + 0.f, q.y + 0.f, q.z + delta)};
-            V3 dn = (nd - V3{n, n, n}) / delta;
-            pp = pp + vomega * dn;
-            vomega *= 0.5f;
-            vlambda *= 1.99f;
-        }
-    }
-    float d = 0, omega = 0.5f, lam = 1.f;
-    for (int i = 0; i < 5; ++i) {
-        V3 q = lam * pp;
-        d += omega * perlin(q.x, q.y, q.z);
-        omega *= 0.5f;
-        lam *= 1.99f;
-    }
-    d = clampf((1 - p.y) * 4.5f * density * d, 0, 1);
-    d += 2 * fmaxf_(0.f, 0.5f - p.y);
-    return clampf(d, 0, 1);
-}
 __global__ void __launch_bounds__(256) k_cloud(float *out, int n, long long first, long long count, float density,
                                                float wispiness, float frequency) {
     for (long long k = blockIdx.x * (long long)blockDim.x + threadIdx.x; k < count; k += (long long)gridDim.x * blockDim.x) {

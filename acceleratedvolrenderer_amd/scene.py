@@ -64,9 +64,66 @@ class GridMedium:
             self.Lescale = (ls * le_norm).astype(np.float32)
         self.majorant_res = tuple(int(r) for r in majorant_res)
 
+    type_id = 0
+
     @property
     def bounds(self):
         return np.concatenate([self.p0, self.p1]).astype(np.float32)
+
+
+class _AnalyticMedium:
+    """Shared surface of the media without a density grid (the C-ABI and the oracle see a
+    1^3 grid of 1.0 and a 1^3 majorant; the kernels never read them)."""
+    device_density = None
+    nx = ny = nz = 1
+    majorant_res = (1, 1, 1)
+
+    def _box(self, p0, p1, world_from_medium):
+        self.p0 = np.asarray(p0, np.float32)
+        self.p1 = np.asarray(p1, np.float32)
+        self.world_from_medium = np.eye(4) if world_from_medium is None else np.asarray(world_from_medium, np.float64)
+        self.density = np.ones((1, 1, 1), np.float32)
+        self.Lescale = np.ones((1, 1, 1), np.float32)
+
+    @property
+    def bounds(self):
+        return np.concatenate([self.p0, self.p1]).astype(np.float32)
+
+
+class HomogeneousMedium(_AnalyticMedium):
+    """pbrt "homogeneous" medium (HomogeneousMedium::Create, media.cpp:166-200): sigma_a,
+    sigma_s (default 1) x scale, g, Le (illuminant) x Lescale / photometric(Le). pbrt's
+    medium is unbounded; here it fills the interface box [p0, p1] (its majorant segment is
+    the box crossing, as the box's interface surfaces would bound it in pbrt)."""
+    type_id = 1
+
+    def __init__(self, p0=(0.0, 0.0, 0.0), p1=(1.0, 1.0, 1.0), world_from_medium=None, sigma_a=None, sigma_s=None,
+                 scale=1.0, g=0.0, Le=None, Lescale=1.0):
+        self._box(p0, p1, world_from_medium)
+        self.g = np.float32(g)
+        self.sigma_a = spectra.scaled(spectra.as_table(sigma_a, 1.0), scale)
+        self.sigma_s = spectra.scaled(spectra.as_table(sigma_s, 1.0), scale)
+        if Le is None or float(np.max(spectra.as_table(Le, 0.0))) == 0.0:
+            self.Le = None
+        else:
+            le = spectra.as_table(Le, 0.0)
+            self.Le = spectra.scaled(le, np.float32(np.float32(Lescale) / spectra.spectrum_to_photometric(le)))
+
+
+class CloudMedium(_AnalyticMedium):
+    """pbrt "cloud" medium (CloudMedium::Create, media.cpp:463-484): procedural Perlin
+    density (density 1, wispiness 1, frequency 5), sigma_a / sigma_s default 1 (no scale
+    parameter in pbrt), g, bounds p0/p1."""
+    type_id = 2
+
+    def __init__(self, p0=(0.0, 0.0, 0.0), p1=(1.0, 1.0, 1.0), world_from_medium=None, sigma_a=None, sigma_s=None,
+                 g=0.0, density=1.0, wispiness=1.0, frequency=5.0):
+        self._box(p0, p1, world_from_medium)
+        self.g = np.float32(g)
+        self.sigma_a = spectra.as_table(sigma_a, 1.0)
+        self.sigma_s = spectra.as_table(sigma_s, 1.0)
+        self.Le = None
+        self.cloud = (np.float32(density), np.float32(wispiness), np.float32(frequency))
 
 
 class DistantLight:

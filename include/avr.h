@@ -97,6 +97,19 @@ int avr_medium_grid_device(avr_context *ctx, const float *d_density, int nx, int
                            const float render_from_medium[16], const float medium_from_render[16],
                            const float *sigma_a, const float *sigma_s, float g, const float *Le,
                            const float *Lescale, int lnx, int lny, int lnz, const int majorant_res[3]);
+/* HomogeneousMedium (media.h:217-262, Create media.cpp:165-210) filling the interface box
+ * `bounds` (medium space): constant sigma_a/sigma_s tables (sigmaScale folded in), g, and
+ * optionally Le (471, LeScale folded in; null = not emissive). Its majorant segment is the
+ * box crossing with sigma_maj = sigma_t (HomogeneousMajorantIterator). */
+int avr_medium_homogeneous(avr_context *ctx, const float bounds[6], const float render_from_medium[16],
+                           const float medium_from_render[16], const float *sigma_a, const float *sigma_s, float g,
+                           const float *Le);
+/* CloudMedium (media.h:430-528, Create media.cpp:455-485): procedural density (Perlin noise;
+ * parameters density, wispiness, frequency) inside `bounds`, one majorant segment per ray
+ * with sigma_maj = sigma_t. */
+int avr_medium_cloud(avr_context *ctx, const float bounds[6], const float render_from_medium[16],
+                     const float medium_from_render[16], const float *sigma_a, const float *sigma_s, float g,
+                     float density, float wispiness, float frequency);
 /* Fill d_out[first .. first+count) of an n^3 grid with CloudMedium::Density
  * (media.h:496-520) at voxel centres (i+0.5)/n — the synthetic S-cloud input. */
 int avr_generate_cloud(avr_context *ctx, float *d_out, int n, long long first, long long count, float density,

@@ -62,6 +62,8 @@ class OracleScene(ctypes.Structure):
         ("samples_per_pixel", ctypes.c_int),
         ("filter_type", ctypes.c_int),
         ("filter_sigma", ctypes.c_float),
+        ("medium_type", ctypes.c_int),
+        ("cloud", ctypes.c_float * 3),
     ]
 
 
@@ -199,6 +201,9 @@ class OracleRun:
         self.majorant = build_majorant(med.density, med.majorant_res)
         s.majorant = arr(self.majorant)
         s.mres[:] = list(med.majorant_res)
+        s.medium_type = int(getattr(med, "type_id", 0))
+        if s.medium_type == 2:
+            s.cloud[:] = [float(v) for v in med.cloud]
         s.nlights = len(scene.lights)
         for i in range(s.nlights):
             s.light_type[i] = int(scene.light_types[i])

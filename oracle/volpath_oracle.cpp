@@ -669,6 +669,10 @@ typedef struct OracleScene {
     // pixel filter (filters.h): 0 BoxFilter, 1 GaussianFilter(radius = filter_radius, sigma)
     int filter_type;
     float filter_sigma;
+    // medium type: 0 GridMedium, 1 HomogeneousMedium (media.h:217-262, filling the
+    // interface box), 2 CloudMedium (media.h:430-528) with {density, wispiness, frequency}
+    int medium_type;
+    float cloud[3];
 } OracleScene;
 
 }  // extern "C"
@@ -908,7 +912,18 @@ static inline MediumProps SamplePoint(const SceneView &sv, V3 p, const Lambda &l
     MediumProps mp;
     mp.sigma_a = SampleDense(sv.s.sigma_a, l);
     mp.sigma_s = SampleDense(sv.s.sigma_s, l);
+    mp.Le = Spec::Const(0.f);
+    if (sv.s.medium_type == 1) {   // HomogeneousMedium::SamplePoint (media.h:241-247)
+        if (sv.s.emissive) mp.Le = SampleDense(sv.s.Le, l);
+        return mp;
+    }
     p = XInvPoint(sv.mediumX, p);
+    if (sv.s.medium_type == 2) {   // CloudMedium::SamplePoint (media.h:456-465)
+        float d = CloudDensity(p, sv.s.cloud[0], sv.s.cloud[1], sv.s.cloud[2]);
+        mp.sigma_a = d * mp.sigma_a;
+        mp.sigma_s = d * mp.sigma_s;
+        return mp;
+    }
     p = Offset(sv.bounds, p);
     float d = sv.density.Lookup(p);
     mp.sigma_a = mp.sigma_a * d;
@@ -929,6 +944,10 @@ struct DDA {
     float nextCrossingT[3], deltaT[3];
     int step[3], voxelLimit[3], voxel[3];
     bool valid = false;
+    bool single = false, called = false;   // HomogeneousMajorantIterator (media.h:80-102)
+    void InitSingle(float tMin_, float tMax_, Spec st) {
+        tMin = tMin_; tMax = tMax_; sigma_t = st; valid = true; single = true;
+    }
     void Init(Ray ray, float tMin_, float tMax_, const Grid *g, const Bounds &gb, Spec st) {
         tMin = tMin_; tMax = tMax_; grid = g; sigma_t = st; valid = true;
         V3 diag = gb.pMax - gb.pMin;
@@ -954,6 +973,12 @@ struct DDA {
     }
     // returns false when exhausted
     bool Next(float *segMin, float *segMax, Spec *sigma_maj) {
+        if (single) {
+            if (!valid || called) return false;
+            called = true;
+            *segMin = tMin; *segMax = tMax; *sigma_maj = sigma_t;
+            return true;
+        }
         if (!valid || tMin >= tMax) return false;
         int bits = ((nextCrossingT[0] < nextCrossingT[1]) << 2) + ((nextCrossingT[0] < nextCrossingT[2]) << 1) +
                    ((nextCrossingT[1] < nextCrossingT[2]));
@@ -979,6 +1004,10 @@ static inline DDA SampleRay(const SceneView &sv, Ray ray, float raytMax, const L
     float tMin, tMax;
     if (!IntersectP(sv.bounds, ray.o, ray.d, raytMax, &tMin, &tMax)) return it;
     Spec sigma_t = SampleDense(sv.s.sigma_a, l) + SampleDense(sv.s.sigma_s, l);
+    if (sv.s.medium_type != 0) {   // CloudMedium::SampleRay (media.h:467-484); homogeneous: the box crossing
+        it.InitSingle(tMin, tMax, sigma_t);
+        return it;
+    }
     it.Init(ray, tMin, tMax, &sv.majorant, sv.bounds, sigma_t);
     return it;
 }
