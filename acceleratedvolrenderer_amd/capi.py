@@ -70,6 +70,7 @@ SIGNATURES = {
                                          c_float_p]),
     "avr_transmittance_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_longlong, ctypes.c_void_p,
                                                 ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "avr_medium_temperature": (ctypes.c_int, [ctypes.c_void_p, c_float_p, ctypes.c_float, ctypes.c_float]),
     "avr_medium_homogeneous": (ctypes.c_int, [ctypes.c_void_p, c_float_p, c_float_p, c_float_p, c_float_p,
                                               c_float_p, ctypes.c_float, c_float_p]),
     "avr_medium_cloud": (ctypes.c_int, [ctypes.c_void_p, c_float_p, c_float_p, c_float_p, c_float_p, c_float_p,
@@ -185,6 +186,11 @@ class Context:
                 self.h, _fp(med.density), med.nx, med.ny, med.nz, _fp(args[0]), _fp(args[1]), _fp(args[2]),
                 _fp(args[3]), _fp(args[4]), float(med.g), _fp(Le), _fp(ls), ls.shape[2], ls.shape[1], ls.shape[0],
                 mres.ctypes.data_as(c_int_p)))
+        temp = getattr(med, "temperature", None)
+        if temp is not None:
+            self._keep.append(temp)
+            _check(self.lib.avr_medium_temperature(self.h, _fp(temp), float(med.temperature_scale),
+                                                   float(med.temperature_offset)))
         types = np.ascontiguousarray(scene.light_types, np.int32)
         w = f32(scene.light_w.reshape(-1))
         L = f32(scene.light_L.reshape(-1))

@@ -81,6 +81,7 @@ struct avr_context {
     int sampler_spp = 16;     // samplesPerPixel of the sampler (ZSobol's Morton layout)
     int filter_type = 0;      // 0 BoxFilter (radius from avr_film), 1 GaussianFilter
     float *d_filter = nullptr;
+    float *d_temperature = nullptr;
     avr::smp::FilterTables ftab{};
     int refill_min = 32;
     int dda_budget = 12;
@@ -158,6 +159,10 @@ int medium_common(avr_context *c, const float *d_density, int nx, int ny, int nz
     if ((rc = upload_table(&c->d_Le, Le, avr::kNTable, c->stream))) return rc;
     if ((rc = upload_table(&c->d_lescale, Le ? Lescale : nullptr, (size_t)lnx * lny * lnz, c->stream))) return rc;
     avr::DevMedium &m = c->med;
+    if (c->d_temperature) { (void)hipFree(c->d_temperature); c->d_temperature = nullptr; }
+    m.temperature = nullptr;
+    m.temp_scale = 1.f;
+    m.temp_offset = 0.f;
     m.type = type;
     m.cloud_density = cloud ? cloud[0] : 0.f;
     m.cloud_wispiness = cloud ? cloud[1] : 0.f;
@@ -311,6 +316,7 @@ int avr_context_destroy(avr_context *c) {
     if (c->d_heads) (void)hipFree(c->d_heads);
     if (c->d_advance) (void)hipFree(c->d_advance);
     if (c->d_filter) (void)hipFree(c->d_filter);
+    if (c->d_temperature) (void)hipFree(c->d_temperature);
     if (c->d_fat) (void)hipFree(c->d_fat);
     if (c->d_stats) (void)hipFree(c->d_stats);
     if (c->h_count) (void)hipHostFree(c->h_count);
@@ -350,6 +356,25 @@ int avr_medium_grid_device(avr_context *c, const float *d_density, int nx, int n
     if (c->d_density_owned) { (void)hipFree(c->d_density_owned); c->d_density_owned = nullptr; }
     return medium_common(c, d_density, nx, ny, nz, bounds, rfm, mfr, sigma_a, sigma_s, g, Le, Lescale, lnx, lny, lnz,
                          mres);
+}
+
+int avr_medium_temperature(avr_context *c, const float *temperature, float temperature_scale,
+                           float temperature_offset) {
+    if (!c || !temperature) return fail(AVR_ERR_ARG, "null temperature grid");
+    if (!c->has_medium || c->med.type != 0) return fail(AVR_ERR_STATE, "temperature needs a grid medium first");
+    if (c->med.Le && c->med.emissive && !c->med.temperature)
+        return fail(AVR_ERR_ARG, "both \"Le\" and \"temperature\" given (media.cpp:283-284)");
+    HIP_TRY(hipSetDevice(c->device));
+    const size_t n = (size_t)c->med.nx * c->med.ny * c->med.nz;
+    if (c->d_temperature) (void)hipFree(c->d_temperature);
+    c->d_temperature = nullptr;
+    HIP_TRY(dalloc(&c->d_temperature, n));
+    HIP_TRY(hipMemcpy(c->d_temperature, temperature, n * sizeof(float), hipMemcpyHostToDevice));
+    c->med.temperature = c->d_temperature;
+    c->med.temp_scale = temperature_scale;
+    c->med.temp_offset = temperature_offset;
+    c->med.emissive = 1;   // isEmissive = temperatureGrid ? true : ... (media.cpp:238)
+    return AVR_OK;
 }
 
 int avr_medium_homogeneous(avr_context *c, const float bounds[6], const float rfm[16], const float mfr[16],

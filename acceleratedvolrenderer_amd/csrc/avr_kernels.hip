@@ -49,7 +49,12 @@ struct DevMedium {
     // majorant of 1.0 whose DDA never crosses a cell face.
     int type;
     float cloud_density, cloud_wispiness, cloud_frequency;
+    // GridMedium temperature grid (media.h:299-316): Le = LeScale * Blackbody(T) normalised,
+    // T = (temperature - offset) * scale, emission only where T > 100 K; null = Le spectrum
+    const float *temperature;
+    float temp_scale, temp_offset;
 };
+
 
 constexpr int kMaxLights = 8;
 struct DevLight {
@@ -279,11 +284,32 @@ __device__ float cloud_density(V3 p, float density, float wispiness, float frequ
     return clampf(d, 0, 1);
 }
 
+// GridMedium emission at medium point p (box-offset, media.h:299-316): LeScale lookup, then
+// the temperature grid's blackbody or the Le spectrum
+__device__ __forceinline__ Spec grid_emission(const DevMedium &m, V3 p, const Spec &lam, const Spec &Le_l) {
+    Spec Le = Spec::c(0.f);
+    const float scale = grid_lookup(m.lescale, m.lnx, m.lny, m.lnz, p);
+    if (scale > 0) {
+        if (m.temperature) {
+            float temp = grid_lookup(m.temperature, m.nx, m.ny, m.nz, p);
+            temp = (temp - m.temp_offset) * m.temp_scale;
+            if (temp > 100.f) {
+                const float nf = blackbody_norm(temp);
+                Le = Spec{blackbody(lam.v0, temp) * nf, blackbody(lam.v1, temp) * nf, blackbody(lam.v2, temp) * nf,
+                          blackbody(lam.v3, temp) * nf} * scale;
+            }
+        } else {
+            Le = Le_l * scale;
+        }
+    }
+    return Le;
+}
+
 struct MediumSample { Spec sigma_a, sigma_s, Le; };
 
 // GridMedium::SamplePoint — media.h:287-319 (no temperature grid); sig_a/sig_s pre-sampled at lambda
 __device__ __forceinline__ MediumSample sample_point(const DevMedium &m, V3 p, const Spec &sig_a, const Spec &sig_s,
-                                                     const Spec &Le_l, bool emissive = true) {
+                                                     const Spec &Le_l, const Spec &lam, bool emissive = true) {
     MediumSample ms;
     p = xf_point_pair(m.medium_from_render, p);
     ms.Le = Spec::c(0.f);
@@ -304,10 +330,7 @@ __device__ __forceinline__ MediumSample sample_point(const DevMedium &m, V3 p, c
     float d = m.fat ? fat_lookup(m.fat, m.density, m.nx, m.ny, m.nz, p) : grid_lookup(m.density, m.nx, m.ny, m.nz, p);
     ms.sigma_a = sig_a * d;
     ms.sigma_s = sig_s * d;
-    if (emissive && m.emissive) {
-        float scale = grid_lookup(m.lescale, m.lnx, m.lny, m.lnz, p);
-        if (scale > 0) ms.Le = Le_l * scale;
-    }
+    if (emissive && m.emissive) ms.Le = grid_emission(m, p, lam, Le_l);
     return ms;
 }
 
@@ -390,7 +413,8 @@ __device__ __forceinline__ bool dda_next(Dda &it, const float *maj, const int *r
 template <typename F>
 __device__ __forceinline__ Spec sample_t_maj(const DevMedium &m, const float *maj, Ray ray, float tMax, float u,
                                             Pcg32 &rng, const Spec &sig_a, const Spec &sig_s, const Spec &Le_l,
-                                            unsigned long long &nLookup, unsigned long long &nSteps, F &&cb) {
+                                            const Spec &lam, unsigned long long &nLookup, unsigned long long &nSteps,
+                                            F &&cb) {
     tMax *= length(ray.d);
     ray.d = normalize(ray.d);
     Dda it;
@@ -416,7 +440,7 @@ __device__ __forceinline__ Spec sample_t_maj(const DevMedium &m, const float *ma
                 T_maj = T_maj * fast_exp(-(sigma_maj * (t - tMin)));
                 V3 p = ray.o + ray.d * t;
                 ++nLookup;
-                MediumSample ms = sample_point(m, p, sig_a, sig_s, Le_l);
+                MediumSample ms = sample_point(m, p, sig_a, sig_s, Le_l, lam);
                 if (!cb(p, ms, sigma_maj, T_maj)) return Spec::c(1.f);
                 T_maj = Spec::c(1.f);
                 tMin = t;
@@ -616,7 +640,7 @@ __global__ void __launch_bounds__(256) k_medium(Params P) {
                 r_l = r_l * (T_maj * sigma_maj / pdf);
                 return beta.nonzero() && r_u.nonzero();
             };
-            Spec T_maj = sample_t_maj(P.med, maj, Ray{o, d}, kInf, u0, rng, sig_a, sig_s, Le_l, nLookup, nSteps, cb);
+            Spec T_maj = sample_t_maj(P.med, maj, Ray{o, d}, kInf, u0, rng, sig_a, sig_s, Le_l, lamv, nLookup, nSteps, cb);
 
             if (scattered) {
                 // ---- SampleLd for the medium interaction (integrators.cpp:1282-1338) ----
@@ -754,8 +778,8 @@ __global__ void __launch_bounds__(256) k_shadow(Params P) {
             }
             return T_ray.nonzero();
         };
-        Spec T_maj = sample_t_maj(P.med, maj, Ray{o, d}, 1 - kShadowEpsilon, u, rng, sig_a, sig_s, Le_l, nLookup,
-                                  nSteps, cb);
+        Spec T_maj = sample_t_maj(P.med, maj, Ray{o, d}, 1 - kShadowEpsilon, u, rng, sig_a, sig_s, Le_l, lamv,
+                                  nLookup, nSteps, cb);
         T_ray = T_ray * (T_maj / T_maj.v0);
         r_l = r_l * (T_maj / T_maj.v0);
         r_u = r_u * (T_maj / T_maj.v0);
@@ -1304,9 +1328,7 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
                     ev = EV_END;
                 } else {
                     if (kEmissive && depth < P.max_depth) {
-                        Spec Le = Spec::c(0.f);
-                        const float sc = grid_lookup(m.lescale, m.lnx, m.lny, m.lnz, pm);
-                        if (sc > 0) Le = Le_l * sc;
+                        const Spec Le = grid_emission(m, pm, lam, Le_l);
                         if (Le.nonzero()) {
                             float pdf = sv0(sigma_maj) * sv0(T_maj);
                             S betap = beta * T_maj / pdf;
@@ -1447,8 +1469,8 @@ __global__ void __launch_bounds__(256) k_transmittance(Params P, long long n, co
                 inv_w = inv_w * (T_maj * sigma_maj / pr);
                 return Tr.nonzero() && inv_w.nonzero();
             };
-            const Spec T_maj = sample_t_maj(P.med, maj, ray, 1.f, u, rng, sig_a, sig_s, Spec::c(0.f), nLookup, nSteps,
-                                            cb);
+            const Spec T_maj = sample_t_maj(P.med, maj, ray, 1.f, u, rng, sig_a, sig_s, Spec::c(0.f), lamv, nLookup,
+                                            nSteps, cb);
             Tr = Tr * (T_maj / T_maj.v0);
             inv_w = inv_w * (T_maj / T_maj.v0);
             Tr = Tr / inv_w.avg();

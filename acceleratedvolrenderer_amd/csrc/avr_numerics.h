@@ -181,6 +181,17 @@ AVR_HD float cr_cosh(float x) { return coshf(x); }
 AVR_HD void cr_sincos(float x, float *s, float *c) { *s = sinf(x); *c = cosf(x); }
 #endif
 
+// Blackbody (spectrum.h:69-80) with FastExp, and BlackbodySpectrum's normalisation
+// 1 / Blackbody(lambdaMax, T), lambdaMax = 2.8977721e-3 / T (spectrum.h:500-530)
+AVR_HD float blackbody(float lambda, float T) {
+    if (T <= 0) return 0;
+    const float c = 299792458.f, h = 6.62606957e-34f, kb = 1.3806488e-23f;
+    const float l = lambda * 1e-9f;
+    const float l2 = l * l;
+    return (2 * h * c * c) / (((l2 * l2) * l) * (fast_exp((h * c) / (l * kb * T)) - 1));
+}
+AVR_HD float blackbody_norm(float T) { return 1 / blackbody((2.8977721e-3f / T) * 1e9f, T); }
+
 // Wavelength sampling — sampling.h:163-171, spectrum.h:334-347
 AVR_HD float sample_visible_wavelength(float u) { return 538 - 138.888889f * cr_atanh(0.85691062f - 1.82750197f * u); }
 AVR_HD float visible_wavelength_pdf(float l) {

@@ -28,7 +28,8 @@ class GridMedium:
     """
 
     def __init__(self, density, p0=(0.0, 0.0, 0.0), p1=(1.0, 1.0, 1.0), world_from_medium=None, sigma_a=None,
-                 sigma_s=None, scale=1.0, g=0.0, Le=None, Lescale=None, majorant_res=(16, 16, 16)):
+                 sigma_s=None, scale=1.0, g=0.0, Le=None, Lescale=None, majorant_res=(16, 16, 16), temperature=None,
+                 temperaturescale=1.0, temperatureoffset=0.0):
         if hasattr(density, "data_ptr"):
             self.device_density = density
             self.density = None
@@ -63,6 +64,17 @@ class GridMedium:
                 raise ValueError("Lescale must match the density grid shape")
             self.Lescale = (ls * le_norm).astype(np.float32)
         self.majorant_res = tuple(int(r) for r in majorant_res)
+        # temperature grid (media.cpp:255-266, 321-326): blackbody emission, exclusive with Le
+        self.temperature = None
+        if temperature is not None:
+            if self.Le is not None:
+                raise ValueError('Both "Le" and "temperature" values were provided.')
+            t = np.ascontiguousarray(np.asarray(temperature, np.float32))
+            if t.shape != (nz, ny, nx):
+                raise ValueError("temperature must match the density grid shape")
+            self.temperature = t
+        self.temperature_scale = np.float32(temperaturescale)
+        self.temperature_offset = np.float32(temperatureoffset)
 
     type_id = 0
 

@@ -97,6 +97,13 @@ int avr_medium_grid_device(avr_context *ctx, const float *d_density, int nx, int
                            const float render_from_medium[16], const float medium_from_render[16],
                            const float *sigma_a, const float *sigma_s, float g, const float *Le,
                            const float *Lescale, int lnx, int lny, int lnz, const int majorant_res[3]);
+/* Attach a temperature grid (nx*ny*nz f32, same layout as the density) to the current
+ * GridMedium: emission Le = LeScale(p) * BlackbodySpectrum(T)(lambda) with
+ * T = (temperature(p) - offset) * scale where T > 100 K (media.h:299-316, media.cpp:
+ * 256-329: "temperature", "temperaturescale", "temperatureoffset"). The medium must have
+ * been created without an Le spectrum (pbrt rejects both). */
+int avr_medium_temperature(avr_context *ctx, const float *temperature, float temperature_scale,
+                           float temperature_offset);
 /* HomogeneousMedium (media.h:217-262, Create media.cpp:165-210) filling the interface box
  * `bounds` (medium space): constant sigma_a/sigma_s tables (sigmaScale folded in), g, and
  * optionally Le (471, LeScale folded in; null = not emissive). Its majorant segment is the

@@ -64,6 +64,9 @@ class OracleScene(ctypes.Structure):
         ("filter_sigma", ctypes.c_float),
         ("medium_type", ctypes.c_int),
         ("cloud", ctypes.c_float * 3),
+        ("temperature", c_float_p),
+        ("temperature_scale", ctypes.c_float),
+        ("temperature_offset", ctypes.c_float),
     ]
 
 
@@ -202,6 +205,12 @@ class OracleRun:
         s.majorant = arr(self.majorant)
         s.mres[:] = list(med.majorant_res)
         s.medium_type = int(getattr(med, "type_id", 0))
+        temp = getattr(med, "temperature", None)
+        if temp is not None:
+            s.temperature = arr(temp)
+            s.temperature_scale = float(med.temperature_scale)
+            s.temperature_offset = float(med.temperature_offset)
+            s.emissive = 1
         if s.medium_type == 2:
             s.cloud[:] = [float(v) for v in med.cloud]
         s.nlights = len(scene.lights)

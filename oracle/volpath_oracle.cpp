@@ -673,6 +673,9 @@ typedef struct OracleScene {
     // interface box), 2 CloudMedium (media.h:430-528) with {density, wispiness, frequency}
     int medium_type;
     float cloud[3];
+    // GridMedium temperature grid (media.h:299-316; null = Le spectrum), scale, offset
+    const float *temperature;
+    float temperature_scale, temperature_offset;
 } OracleScene;
 
 }  // extern "C"
@@ -887,7 +890,7 @@ struct SceneView {
     const OracleScene &s;
     Xform mediumX, cameraX, rasterX;
     Bounds bounds;
-    Grid density, lescale, majorant;
+    Grid density, lescale, majorant, temperature;
     GaussianSampler gauss;
     explicit SceneView(const OracleScene &sc) : s(sc) {
         if (sc.filter_type == 1) gauss.Build(sc.filter_radius[0], sc.filter_radius[1], sc.filter_sigma);
@@ -901,6 +904,7 @@ struct SceneView {
         }
         bounds = {{sc.bounds[0], sc.bounds[1], sc.bounds[2]}, {sc.bounds[3], sc.bounds[4], sc.bounds[5]}};
         density = {sc.density, sc.nx, sc.ny, sc.nz};
+        temperature = {sc.temperature, sc.nx, sc.ny, sc.nz};
         lescale = {sc.Lescale, sc.lnx, sc.lny, sc.lnz};
         majorant = {sc.majorant, sc.mres[0], sc.mres[1], sc.mres[2]};
     }
@@ -931,7 +935,22 @@ static inline MediumProps SamplePoint(const SceneView &sv, V3 p, const Lambda &l
     mp.Le = Spec::Const(0.f);
     if (sv.s.emissive) {
         float scale = sv.lescale.Lookup(p);
-        if (scale > 0) mp.Le = scale * SampleDense(sv.s.Le, l);
+        if (scale > 0) {
+            if (sv.s.temperature) {   // media.h:304-312
+                float temp = sv.temperature.Lookup(p);
+                temp = (temp - sv.s.temperature_offset) * sv.s.temperature_scale;
+                if (temp > 100.f) {
+                    // BlackbodySpectrum(temp).Sample(lambda) (spectrum.h:500-521)
+                    float lambdaMax = 2.8977721e-3f / temp;
+                    float normalizationFactor = 1 / Blackbody(lambdaMax * 1e9f, temp);
+                    Spec b;
+                    for (int i = 0; i < NS; ++i) b.v[i] = Blackbody(l.lambda[i], temp) * normalizationFactor;
+                    mp.Le = scale * b;
+                }
+            } else {
+                mp.Le = scale * SampleDense(sv.s.Le, l);
+            }
+        }
     }
     return mp;
 }

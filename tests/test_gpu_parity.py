@@ -385,3 +385,34 @@ def test_homogeneous_and_cloud_media_replay(kind):
     assert frac >= 0.999
     assert err <= 0.5 * noise
     integ.close()
+
+
+@pytest.mark.parametrize("kernel", ["persistent", "wavefront"])
+@pytest.mark.parametrize("chromatic", [False, True])
+def test_temperature_blackbody_emission_replay(kernel, chromatic):
+    """GridMedium temperature grid (media.h:299-316): Le = LeScale * normalised blackbody at
+    T = (temperature - offset) * scale, emitting only above 100 K."""
+    from acceleratedvolrenderer_amd import scenes, GridMedium
+    from acceleratedvolrenderer_amd.scene import Scene
+    from oracle import binding
+    n, W, H, spp = 12, 24, 20, 8
+    base = scenes.s_uniform(n=n, width=W, height=H, variant="scatter")
+    z, y, x = np.meshgrid(*(np.linspace(0, 1, n, dtype=np.float32),) * 3, indexing="ij")
+    temp = (50 + 4000 * x * (1 - y) + 300 * z).astype(np.float32)     # includes cells below 100 K
+    dens = (0.3 + 0.7 * np.random.default_rng(3).random((n, n, n), dtype=np.float32)).astype(np.float32)
+    sa = np.linspace(0.5, 1.5, 471).astype(np.float32) if chromatic else 1.0
+    med = GridMedium(dens, sigma_a=sa, sigma_s=0.5, g=0.2, temperature=temp, temperaturescale=1.1,
+                     temperatureoffset=20.0)
+    scene = Scene(base.camera, base.film, med, base.lights)
+    integ = _integrator(scene, maxdepth=6, spp=spp, kernel=kernel)
+    rgb, w = integ.render()
+    canon = binding.OracleRun(scene, max_depth=6, seed=0, libm="canonical")
+    frac, _ = _compare_samples(integ, canon, 0, spp)
+    ref = binding.OracleRun(scene, max_depth=6, seed=0)
+    rgb_o, w_o = ref.render(0, spp, nthreads=8)
+    err = _rel_rms(integ.image(rgb, w), integ.image(rgb_o, w_o))
+    noise = _oracle_noise(scene, 6, spp, integ, rgb_o, w_o)
+    print(f"temperature/{kernel}/chromatic={chromatic}: bit-exact {frac:.5f}, film rel RMS {err:.3e} (noise {noise:.3e})")
+    assert frac >= 0.999
+    assert err <= 0.5 * noise
+    integ.close()
