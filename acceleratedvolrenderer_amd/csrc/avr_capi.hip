@@ -152,12 +152,18 @@ int medium_common(avr_context *c, const float *d_density, int nx, int ny, int nz
     if (!affine(rfm) || !affine(mfr)) return fail(AVR_ERR_ARG, "medium transforms must be affine");
     if (!sigma_a || !sigma_s) return fail(AVR_ERR_ARG, "sigma_a/sigma_s tables required");
     if (mres[0] < 1 || mres[1] < 1 || mres[2] < 1) return fail(AVR_ERR_ARG, "bad majorant resolution");
-    if (Le && (!Lescale || lnx < 1 || lny < 1 || lnz < 1)) return fail(AVR_ERR_ARG, "Le needs a Lescale grid");
+    if (Lescale && (lnx < 1 || lny < 1 || lnz < 1)) return fail(AVR_ERR_ARG, "bad Lescale grid");
     int rc;
     if ((rc = upload_table(&c->d_sigma_a, sigma_a, avr::kNTable, c->stream))) return rc;
     if ((rc = upload_table(&c->d_sigma_s, sigma_s, avr::kNTable, c->stream))) return rc;
-    if ((rc = upload_table(&c->d_Le, Le, avr::kNTable, c->stream))) return rc;
-    if ((rc = upload_table(&c->d_lescale, Le ? Lescale : nullptr, (size_t)lnx * lny * lnz, c->stream))) return rc;
+    // Le and LeScale are always resident: a temperature grid attached later makes the medium
+    // emissive without an Le spectrum (zeros), and LeScale defaults to pbrt's 1^3 {LeNorm}
+    // grid with LeNorm = 1 (media.cpp:288-296)
+    static const float zeros[avr::kNTable] = {};
+    static const float one = 1.f;
+    if ((rc = upload_table(&c->d_Le, Le ? Le : zeros, avr::kNTable, c->stream))) return rc;
+    if (!Lescale) { Lescale = &one; lnx = lny = lnz = 1; }
+    if ((rc = upload_table(&c->d_lescale, Lescale, (size_t)lnx * lny * lnz, c->stream))) return rc;
     avr::DevMedium &m = c->med;
     if (c->d_temperature) { (void)hipFree(c->d_temperature); c->d_temperature = nullptr; }
     m.temperature = nullptr;
@@ -184,7 +190,7 @@ int medium_common(avr_context *c, const float *d_density, int nx, int ny, int nz
     m.emissive = emissive ? 1 : 0;
     m.Le = c->d_Le;
     m.lescale = c->d_lescale;
-    m.lnx = Le ? lnx : 1; m.lny = Le ? lny : 1; m.lnz = Le ? lnz : 1;
+    m.lnx = lnx; m.lny = lny; m.lnz = lnz;
     if (c->d_majorant) (void)hipFree(c->d_majorant);
     const int nm = mres[0] * mres[1] * mres[2];
     HIP_TRY(dalloc(&c->d_majorant, (size_t)nm));
@@ -362,6 +368,7 @@ int avr_medium_temperature(avr_context *c, const float *temperature, float tempe
                            float temperature_offset) {
     if (!c || !temperature) return fail(AVR_ERR_ARG, "null temperature grid");
     if (!c->has_medium || c->med.type != 0) return fail(AVR_ERR_STATE, "temperature needs a grid medium first");
+    if (!c->med.Le || !c->med.lescale) return fail(AVR_ERR_STATE, "medium emission tables missing");
     if (c->med.Le && c->med.emissive && !c->med.temperature)
         return fail(AVR_ERR_ARG, "both \"Le\" and \"temperature\" given (media.cpp:283-284)");
     HIP_TRY(hipSetDevice(c->device));
