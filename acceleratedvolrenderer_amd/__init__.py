@@ -8,11 +8,14 @@ include/avr.h. See DESIGN.md.
 """
 from . import spectra, transform
 from .scene import (GridMedium, DistantLight, UniformInfiniteLight, OrthographicCamera, PerspectiveCamera, RGBFilm,
-                    Scene, film_rgb, HomogeneousMedium, CloudMedium, BoxFilter, GaussianFilter, IndependentSampler, ZSobolSampler)
+                    Scene, film_rgb, HomogeneousMedium, CloudMedium, NanoVDBMedium, BoxFilter, GaussianFilter,
+                    IndependentSampler, ZSobolSampler)
+from .vdb import NanoVDBGrid
 from .integrator import VolPathIntegrator, shard_samples, INTEGRATOR_NAMES
 from . import capi
 from . import scenes
 
 __all__ = ["spectra", "transform", "GridMedium", "DistantLight", "UniformInfiniteLight", "OrthographicCamera",
            "PerspectiveCamera", "RGBFilm", "Scene", "film_rgb", "VolPathIntegrator", "shard_samples",
-           "INTEGRATOR_NAMES", "capi", "scenes"]
+           "INTEGRATOR_NAMES", "capi", "scenes", "HomogeneousMedium", "CloudMedium", "NanoVDBMedium", "NanoVDBGrid",
+           "BoxFilter", "GaussianFilter", "IndependentSampler", "ZSobolSampler"]

@@ -41,6 +41,41 @@ class AvrStats(ctypes.Structure):
         return {k: getattr(self, k) for k, _ in self._fields_}
 
 
+class AvrVdbGrid(ctypes.Structure):
+    """avr_vdb_grid (include/avr.h): one NanoVDB FloatGrid's tree."""
+    _fields_ = [
+        ("n_leaves", ctypes.c_int),
+        ("leaf_origin", c_int_p),
+        ("leaf_values", c_float_p),
+        ("n_tiles", ctypes.c_int),
+        ("tile_origin", c_int_p),
+        ("tile_size", c_int_p),
+        ("tile_value", c_float_p),
+        ("background", ctypes.c_float),
+        ("index_bbox", ctypes.c_int * 6),
+        ("index_to_world", ctypes.c_double * 12),
+        ("world_to_index", ctypes.c_double * 9),
+    ]
+
+    @classmethod
+    def of(cls, grid):
+        """Struct view of a vdb.NanoVDBGrid (the grid's arrays must outlive the call)."""
+        g = cls()
+        ip = lambda a: a.ctypes.data_as(c_int_p) if a.size else None
+        g.n_leaves = len(grid.leaf_origins)
+        g.leaf_origin = ip(grid.leaf_origins)
+        g.leaf_values = grid.leaf_values.ctypes.data_as(c_float_p) if grid.leaf_values.size else None
+        g.n_tiles = len(grid.tile_values)
+        g.tile_origin = ip(grid.tile_origins)
+        g.tile_size = ip(grid.tile_sizes)
+        g.tile_value = grid.tile_values.ctypes.data_as(c_float_p) if grid.tile_values.size else None
+        g.background = float(grid.background)
+        g.index_bbox[:] = [int(v) for v in grid.index_bbox]
+        g.index_to_world[:] = [float(v) for v in grid.index_to_world.reshape(-1)]
+        g.world_to_index[:] = [float(v) for v in grid.world_to_index.reshape(-1)]
+        return g
+
+
 # name -> (restype, argtypes); every symbol include/avr.h declares
 SIGNATURES = {
     "avr_last_error": (ctypes.c_char_p, []),
@@ -75,6 +110,10 @@ SIGNATURES = {
                                               c_float_p, ctypes.c_float, c_float_p]),
     "avr_medium_cloud": (ctypes.c_int, [ctypes.c_void_p, c_float_p, c_float_p, c_float_p, c_float_p, c_float_p,
                                         ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float]),
+    "avr_medium_nanovdb": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(AvrVdbGrid), ctypes.POINTER(AvrVdbGrid),
+                                          c_float_p, c_float_p, c_float_p, c_float_p, ctypes.c_float, ctypes.c_float,
+                                          ctypes.c_float, ctypes.c_float]),
+    "avr_medium_bounds": (ctypes.c_int, [ctypes.c_void_p, c_float_p]),
     "avr_set_filter": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, c_float_p, ctypes.c_float]),
     "avr_set_sampler": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]),
     "avr_film": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, c_float_p, c_float_p, ctypes.c_float,
@@ -173,6 +212,13 @@ class Context:
         if getattr(med, "type_id", 0) == 1:
             _check(self.lib.avr_medium_homogeneous(self.h, _fp(args[0]), _fp(args[1]), _fp(args[2]), _fp(args[3]),
                                                    _fp(args[4]), float(med.g), _fp(Le)))
+        elif getattr(med, "type_id", 0) == 3:
+            dg = AvrVdbGrid.of(med.grid)
+            tg = AvrVdbGrid.of(med.temperature_grid) if med.temperature_grid is not None else None
+            _check(self.lib.avr_medium_nanovdb(self.h, ctypes.byref(dg), ctypes.byref(tg) if tg is not None else None,
+                                               _fp(args[1]), _fp(args[2]), _fp(args[3]), _fp(args[4]), float(med.g),
+                                               float(med.Lescale_value), float(med.temperature_offset),
+                                               float(med.temperature_scale)))
         elif getattr(med, "type_id", 0) == 2:
             _check(self.lib.avr_medium_cloud(self.h, _fp(args[0]), _fp(args[1]), _fp(args[2]), _fp(args[3]),
                                              _fp(args[4]), float(med.g), *[float(v) for v in med.cloud]))
@@ -209,6 +255,11 @@ class Context:
     def generate_cloud(self, d_out_ptr, n, first, count, density=1.0, wispiness=1.0, frequency=5.0):
         _check(self.lib.avr_generate_cloud(self.h, ctypes.c_void_p(d_out_ptr), int(n), int(first), int(count),
                                            float(density), float(wispiness), float(frequency)))
+
+    def medium_bounds(self):
+        out = np.zeros(6, np.float32)
+        _check(self.lib.avr_medium_bounds(self.h, _fp(out)))
+        return out
 
     def majorant(self, n):
         out = np.empty(n, np.float32)

@@ -12,6 +12,8 @@
 #include "avr_kernels.hip"
 #include "../../include/avr.h"
 
+#include <climits>
+#include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -82,6 +84,10 @@ struct avr_context {
     int filter_type = 0;      // 0 BoxFilter (radius from avr_film), 1 GaussianFilter
     float *d_filter = nullptr;
     float *d_temperature = nullptr;
+    // NanoVDBMedium grids (0 density, 1 temperature): block slots, leaves, tile values
+    int *d_vdb_slot[2] = {nullptr, nullptr};
+    float *d_vdb_leaves[2] = {nullptr, nullptr}, *d_vdb_tiles[2] = {nullptr, nullptr};
+    int vdb_ibbox[6] = {};    // density grid's active index bbox (majorant clamp)
     avr::smp::FilterTables ftab{};
     int refill_min = 32;
     int dda_budget = 12;
@@ -145,6 +151,110 @@ int blocks_for(long long n, int per = 256, int cap = 256 * 16) {
 
 bool affine(const float m[16]) { return m[12] == 0 && m[13] == 0 && m[14] == 0 && m[15] == 1; }
 
+void free_vdb(avr_context *c) {
+    for (int k = 0; k < 2; ++k) {
+        if (c->d_vdb_slot[k]) (void)hipFree(c->d_vdb_slot[k]);
+        if (c->d_vdb_leaves[k]) (void)hipFree(c->d_vdb_leaves[k]);
+        if (c->d_vdb_tiles[k]) (void)hipFree(c->d_vdb_tiles[k]);
+        c->d_vdb_slot[k] = nullptr;
+        c->d_vdb_leaves[k] = c->d_vdb_tiles[k] = nullptr;
+    }
+    c->med.vdb = {};
+    c->med.vdb_temp = {};
+}
+
+// Map::set (NanoVDB): the float inverse matrix and translation are roundings of the f64 map
+bool vdb_map(const avr_vdb_grid *G, avr::vdb::Grid &g) {
+    for (int k = 0; k < 9; ++k) {
+        if (!std::isfinite(G->world_to_index[k])) return false;
+        g.inv[k] = (float)G->world_to_index[k];
+    }
+    for (int r = 0; r < 3; ++r) g.vec[r] = (float)G->index_to_world[4 * r + 3];
+    return true;
+}
+
+// GridData::mWorldBBox: the map (Map::applyMap, f64) of the 8 corners of [min, max + 1]
+void vdb_world_bbox(const avr_vdb_grid *G, double lo[3], double hi[3]) {
+    for (int k = 0; k < 3; ++k) { lo[k] = INFINITY; hi[k] = -INFINITY; }
+    const double *M = G->index_to_world;
+    for (int corner = 0; corner < 8; ++corner) {
+        const double x = (corner & 1) ? G->index_bbox[3] + 1.0 : G->index_bbox[0];
+        const double y = (corner & 2) ? G->index_bbox[4] + 1.0 : G->index_bbox[1];
+        const double z = (corner & 4) ? G->index_bbox[5] + 1.0 : G->index_bbox[2];
+        for (int r = 0; r < 3; ++r) {
+            const double w = M[4 * r] * x + M[4 * r + 1] * y + M[4 * r + 2] * z + M[4 * r + 3];
+            lo[r] = std::min(lo[r], w);
+            hi[r] = std::max(hi[r], w);
+        }
+    }
+}
+
+// Flatten one tree into the block-slot layout of avr_vdb.h and upload it
+int upload_vdb(avr_context *c, const avr_vdb_grid *G, int k, avr::vdb::Grid &g) {
+    if (G->n_leaves < 0 || G->n_tiles < 0 || (G->n_leaves && (!G->leaf_origin || !G->leaf_values)) ||
+        (G->n_tiles && (!G->tile_origin || !G->tile_size || !G->tile_value)))
+        return fail(AVR_ERR_ARG, "bad vdb grid arrays");
+    for (int a = 0; a < 3; ++a)
+        if (G->index_bbox[a] > G->index_bbox[3 + a]) return fail(AVR_ERR_ARG, "empty vdb index bbox");
+    g = {};
+    if (!vdb_map(G, g)) return fail(AVR_ERR_ARG, "non-finite vdb world-to-index map");
+    g.background = G->background;
+    long long lo[3] = {LLONG_MAX, LLONG_MAX, LLONG_MAX}, hi[3] = {LLONG_MIN, LLONG_MIN, LLONG_MIN};
+    auto extend = [&](const int *o, long long size) {
+        for (int a = 0; a < 3; ++a) { lo[a] = std::min<long long>(lo[a], o[a]); hi[a] = std::max<long long>(hi[a], o[a] + size); }
+    };
+    for (int l = 0; l < G->n_leaves; ++l) {
+        const int *o = G->leaf_origin + 3 * l;
+        if ((o[0] & 7) || (o[1] & 7) || (o[2] & 7)) return fail(AVR_ERR_ARG, "leaf origin not a multiple of 8");
+        extend(o, 8);
+    }
+    for (int t = 0; t < G->n_tiles; ++t) {
+        const int *o = G->tile_origin + 3 * t;
+        const int sz = G->tile_size[t];
+        if (sz < 8 || (sz & 7) || (o[0] & 7) || (o[1] & 7) || (o[2] & 7))
+            return fail(AVR_ERR_ARG, "tile origin/size not multiples of 8");
+        extend(o, sz);
+    }
+    long long nb[3] = {0, 0, 0};
+    if (G->n_leaves + G->n_tiles > 0)
+        for (int a = 0; a < 3; ++a) nb[a] = (hi[a] - lo[a]) / 8;
+    const long long nslot = nb[0] * nb[1] * nb[2];
+    if (nslot > (1ll << 31)) return fail(AVR_ERR_ARG, "vdb grid extent too large (> 2^31 blocks)");
+    std::vector<int> slot((size_t)std::max<long long>(nslot, 1), avr::vdb::kBackgroundSlot);
+    auto sidx = [&](long long bx, long long by, long long bz) { return (size_t)((bz * nb[1] + by) * nb[0] + bx); };
+    for (int t = 0; t < G->n_tiles; ++t) {
+        const int *o = G->tile_origin + 3 * t;
+        const long long s = G->tile_size[t] / 8;
+        const long long bx0 = (o[0] - lo[0]) / 8, by0 = (o[1] - lo[1]) / 8, bz0 = (o[2] - lo[2]) / 8;
+        for (long long bz = bz0; bz < bz0 + s; ++bz)
+            for (long long by = by0; by < by0 + s; ++by)
+                for (long long bx = bx0; bx < bx0 + s; ++bx) slot[sidx(bx, by, bz)] = -(t + 1);
+    }
+    for (int l = 0; l < G->n_leaves; ++l) {
+        const int *o = G->leaf_origin + 3 * l;
+        int &s = slot[sidx((o[0] - lo[0]) / 8, (o[1] - lo[1]) / 8, (o[2] - lo[2]) / 8)];
+        if (s >= 0) return fail(AVR_ERR_ARG, "duplicate leaf origin");
+        s = l;
+    }
+    g.ox = nslot ? (int)lo[0] : 0; g.oy = nslot ? (int)lo[1] : 0; g.oz = nslot ? (int)lo[2] : 0;
+    g.lnx = (int)nb[0]; g.lny = (int)nb[1]; g.lnz = (int)nb[2];
+    HIP_TRY(dalloc(&c->d_vdb_slot[k], slot.size()));
+    HIP_TRY(hipMemcpyAsync(c->d_vdb_slot[k], slot.data(), slot.size() * sizeof(int), hipMemcpyHostToDevice, c->stream));
+    const size_t nleaf = (size_t)G->n_leaves * 512;
+    HIP_TRY(dalloc(&c->d_vdb_leaves[k], nleaf));
+    if (nleaf)
+        HIP_TRY(hipMemcpyAsync(c->d_vdb_leaves[k], G->leaf_values, nleaf * sizeof(float), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(dalloc(&c->d_vdb_tiles[k], (size_t)G->n_tiles));
+    if (G->n_tiles)
+        HIP_TRY(hipMemcpyAsync(c->d_vdb_tiles[k], G->tile_value, G->n_tiles * sizeof(float), hipMemcpyHostToDevice, c->stream));
+    // the slot vector dies here: finish the copies first
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    g.slot = c->d_vdb_slot[k];
+    g.leaves = c->d_vdb_leaves[k];
+    g.tiles = c->d_vdb_tiles[k];
+    return AVR_OK;
+}
+
 int medium_common(avr_context *c, const float *d_density, int nx, int ny, int nz, const float bounds[6],
                   const float rfm[16], const float mfr[16], const float *sigma_a, const float *sigma_s, float g,
                   const float *Le, const float *Lescale, int lnx, int lny, int lnz, const int mres[3],
@@ -165,6 +275,7 @@ int medium_common(avr_context *c, const float *d_density, int nx, int ny, int nz
     if (!Lescale) { Lescale = &one; lnx = lny = lnz = 1; }
     if ((rc = upload_table(&c->d_lescale, Lescale, (size_t)lnx * lny * lnz, c->stream))) return rc;
     avr::DevMedium &m = c->med;
+    if (type != 3) free_vdb(c);
     if (c->d_temperature) { (void)hipFree(c->d_temperature); c->d_temperature = nullptr; }
     m.temperature = nullptr;
     m.temp_scale = 1.f;
@@ -197,6 +308,13 @@ int medium_common(avr_context *c, const float *d_density, int nx, int ny, int nz
     if (type == 0) {
         hipLaunchKernelGGL(avr::k_majorant, dim3(nm), dim3(256), 0, c->stream, d_density, nx, ny, nz, mres[0], mres[1],
                            mres[2], c->d_majorant);
+        HIP_TRY(hipGetLastError());
+    } else if (type == 3) {
+        const int *b = c->vdb_ibbox;
+        hipLaunchKernelGGL(avr::k_majorant_vdb, dim3(nm), dim3(256), 0, c->stream, m.vdb,
+                           make_float3(bounds[0], bounds[1], bounds[2]), make_float3(bounds[3], bounds[4], bounds[5]),
+                           make_int4(b[0], b[1], b[2], 0), make_int4(b[3], b[4], b[5], 0), mres[0], mres[1], mres[2],
+                           c->d_majorant);
         HIP_TRY(hipGetLastError());
     } else {   // single segment, sigma_maj = sigma_t * 1 (density <= 1 for the cloud)
         const float one = 1.f;
@@ -323,6 +441,7 @@ int avr_context_destroy(avr_context *c) {
     if (c->d_advance) (void)hipFree(c->d_advance);
     if (c->d_filter) (void)hipFree(c->d_filter);
     if (c->d_temperature) (void)hipFree(c->d_temperature);
+    free_vdb(c);
     if (c->d_fat) (void)hipFree(c->d_fat);
     if (c->d_stats) (void)hipFree(c->d_stats);
     if (c->h_count) (void)hipHostFree(c->h_count);
@@ -403,6 +522,49 @@ int avr_medium_cloud(avr_context *c, const float bounds[6], const float rfm[16],
     const float cloud[3] = {density, wispiness, frequency};
     return medium_common(c, nullptr, 1, 1, 1, bounds, rfm, mfr, sigma_a, sigma_s, g, nullptr, nullptr, 1, 1, 1, mres,
                          2, cloud);
+}
+
+int avr_medium_nanovdb(avr_context *c, const avr_vdb_grid *density, const avr_vdb_grid *temperature, const float rfm[16],
+                       const float mfr[16], const float *sigma_a, const float *sigma_s, float g, float Lescale,
+                       float temperature_offset, float temperature_scale) {
+    if (!c || !density || !rfm || !mfr) return fail(AVR_ERR_ARG, "null medium argument");
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    free_vdb(c);
+    int rc;
+    avr::vdb::Grid gd{}, gt{};
+    if ((rc = upload_vdb(c, density, 0, gd))) return rc;
+    if (temperature && (rc = upload_vdb(c, temperature, 1, gt))) return rc;
+    // bounds: density world bbox, union the temperature grid's (media.cpp:531-549)
+    double lo[3], hi[3];
+    vdb_world_bbox(density, lo, hi);
+    float bounds[6];
+    for (int a = 0; a < 3; ++a) { bounds[a] = (float)lo[a]; bounds[3 + a] = (float)hi[a]; }
+    if (temperature) {
+        vdb_world_bbox(temperature, lo, hi);
+        for (int a = 0; a < 3; ++a) {
+            bounds[a] = std::min(bounds[a], (float)lo[a]);
+            bounds[3 + a] = std::max(bounds[3 + a], (float)hi[a]);
+        }
+    }
+    for (int a = 0; a < 6; ++a) c->vdb_ibbox[a] = density->index_bbox[a];
+    c->med.vdb = gd;
+    c->med.vdb_temp = gt;
+    const int mres[3] = {64, 64, 64};   // majorantGrid(Bounds3f(), {64, 64, 64}) (media.cpp:520)
+    if ((rc = medium_common(c, nullptr, 1, 1, 1, bounds, rfm, mfr, sigma_a, sigma_s, g, nullptr, nullptr, 1, 1, 1, mres,
+                            3, nullptr)))
+        return rc;
+    c->med.vdb_lescale = Lescale;
+    c->med.temp_offset = temperature_offset;
+    c->med.temp_scale = temperature_scale;
+    c->med.emissive = temperature ? 1 : 0;
+    return AVR_OK;
+}
+
+int avr_medium_bounds(avr_context *c, float bounds[6]) {
+    if (!c || !c->has_medium || !bounds) return fail(AVR_ERR_STATE, "no medium");
+    for (int a = 0; a < 3; ++a) { bounds[a] = c->med.bmin[a]; bounds[3 + a] = c->med.bmax[a]; }
+    return AVR_OK;
 }
 
 int avr_generate_cloud(avr_context *c, float *d_out, int n, long long first, long long count, float density,

@@ -18,6 +18,7 @@
 //                (bit-identical order to ImageTileIntegrator::Render's per-pixel loop).
 #include "avr_numerics.h"
 #include "avr_sampling.h"
+#include "avr_vdb.h"
 
 #include <type_traits>
 
@@ -53,6 +54,11 @@ struct DevMedium {
     // T = (temperature - offset) * scale, emission only where T > 100 K; null = Le spectrum
     const float *temperature;
     float temp_scale, temp_offset;
+    // 3 NanoVDBMedium (media.h:602-685): density and optional temperature as sparse grids
+    // sampled in index space (avr_vdb.h); Le = LeScale * Blackbody(T) where T > 100 K,
+    // emissive iff a temperature grid is present (the integrator tests mp.Le itself)
+    vdb::Grid vdb, vdb_temp;
+    float vdb_lescale;
 };
 
 
@@ -325,6 +331,21 @@ __device__ __forceinline__ MediumSample sample_point(const DevMedium &m, V3 p, c
         ms.sigma_s = sig_s * d;
         return ms;
     }
+    if (m.type == 3) {             // NanoVDBMedium::SamplePoint (media.h:624-637) and Le (media.h:660-672)
+        const float d = vdb::sample_world(m.vdb, p.x, p.y, p.z);
+        ms.sigma_a = sig_a * d;
+        ms.sigma_s = sig_s * d;
+        if (emissive && m.emissive) {
+            float temp = vdb::sample_world(m.vdb_temp, p.x, p.y, p.z);
+            temp = (temp - m.temp_offset) * m.temp_scale;
+            if (temp > 100.f) {
+                const float nf = blackbody_norm(temp);
+                ms.Le = Spec{m.vdb_lescale * (blackbody(lam.v0, temp) * nf), m.vdb_lescale * (blackbody(lam.v1, temp) * nf),
+                             m.vdb_lescale * (blackbody(lam.v2, temp) * nf), m.vdb_lescale * (blackbody(lam.v3, temp) * nf)};
+            }
+        }
+        return ms;
+    }
     // Bounds3::Offset (vecmath.h:1323-1332); x / 1.0f == x exactly, so a unit box skips it
     p = m.unit_box ? V3{p.x - m.bmin[0], p.y - m.bmin[1], p.z - m.bmin[2]} : box_offset(m.bmin, m.bmax, p);
     float d = m.fat ? fat_lookup(m.fat, m.density, m.nx, m.ny, m.nz, p) : grid_lookup(m.density, m.nx, m.ny, m.nz, p);
@@ -374,7 +395,7 @@ __device__ __forceinline__ bool dda_init(Dda &it, const DevMedium &m, Ray ray, f
     dda_axis(gi.x, gd.x, m.mres[0], tMin, it.vx, it.nx, it.dx, it.sx);
     dda_axis(gi.y, gd.y, m.mres[1], tMin, it.vy, it.ny, it.dy, it.sy);
     dda_axis(gi.z, gd.z, m.mres[2], tMin, it.vz, it.nz, it.dz, it.sz);
-    if (m.type != 0) {   // HomogeneousMajorantIterator(tMin, tMax, sigma_t): one segment
+    if (m.type == 1 || m.type == 2) {   // HomogeneousMajorantIterator(tMin, tMax, sigma_t): one segment
         it.vx = it.vy = it.vz = 0;
         it.nx = it.ny = it.nz = kInf;
     }
@@ -1518,6 +1539,51 @@ __global__ void __launch_bounds__(256) k_majorant(const float *__restrict__ dens
     if (threadIdx.x == 0) {
         float r = red[0];
         for (int w = 1; w < (int)(blockDim.x / 64); ++w) r = fmaxf_(r, red[w]);
+        out[cell] = r;
+    }
+}
+
+// NanoVDBMedium's 64^3 majorant (media.cpp:556-613): each cell's world box is
+// bounds.Lerp of its corners, mapped to index space by worldToIndexF, widened by one voxel
+// of filter slop (int truncation of the f64 i -/+ 1), clamped to the active index bbox
+// (inclusive); the cell holds the max of getValue over that box (0 when it is empty).
+// One workgroup per cell.
+__global__ void __launch_bounds__(256) k_majorant_vdb(vdb::Grid g, float3 bmin, float3 bmax, int4 ibmin, int4 ibmax,
+                                                      int rx, int ry, int rz, float *out) {
+    const int cell = blockIdx.x;
+    const int x = cell % rx, y = (cell / rx) % ry, z = cell / (rx * ry);
+    const float t0x = float(x) / rx, t0y = float(y) / ry, t0z = float(z) / rz;
+    const float t1x = float(x + 1) / rx, t1y = float(y + 1) / ry, t1z = float(z + 1) / rz;
+    const float ax = (1 - t0x) * bmin.x + t0x * bmax.x, ay = (1 - t0y) * bmin.y + t0y * bmax.y,
+                az = (1 - t0z) * bmin.z + t0z * bmax.z;
+    const float bx = (1 - t1x) * bmin.x + t1x * bmax.x, by = (1 - t1y) * bmin.y + t1y * bmax.y,
+                bz = (1 - t1z) * bmin.z + t1z * bmax.z;
+    float i0x, i0y, i0z, i1x, i1y, i1z;
+    vdb::world_to_index(g, fminf_(ax, bx), fminf_(ay, by), fminf_(az, bz), &i0x, &i0y, &i0z);
+    vdb::world_to_index(g, fmaxf_(ax, bx), fmaxf_(ay, by), fmaxf_(az, bz), &i1x, &i1y, &i1z);
+    const int x0 = max((int)((double)i0x - 1.0), ibmin.x), x1 = min((int)((double)i1x + 1.0), ibmax.x);
+    const int y0 = max((int)((double)i0y - 1.0), ibmin.y), y1 = min((int)((double)i1y + 1.0), ibmax.y);
+    const int z0 = max((int)((double)i0z - 1.0), ibmin.z), z1 = min((int)((double)i1z + 1.0), ibmax.z);
+    float m = 0.f;
+    if (x0 <= x1 && y0 <= y1 && z0 <= z1) {
+        const int ex = x1 - x0 + 1, ey = y1 - y0 + 1, ez = z1 - z0 + 1;
+        const long long total = (long long)ex * ey * ez;
+        for (long long k = threadIdx.x; k < total; k += blockDim.x) {
+            const int kx = (int)(k % ex), ky = (int)((k / ex) % ey), kz = (int)(k / ((long long)ex * ey));
+            const float v = vdb::get_value(g, x0 + kx, y0 + ky, z0 + kz);
+            m = m < v ? v : m;   // std::max(maxValue, v)
+        }
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        const float o = __shfl_xor(m, off);
+        m = m < o ? o : m;
+    }
+    __shared__ float red[4];
+    if (lane_id() == 0) red[threadIdx.x / 64] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float r = red[0];
+        for (int w = 1; w < (int)(blockDim.x / 64); ++w) r = r < red[w] ? red[w] : r;
         out[cell] = r;
     }
 }

@@ -138,6 +138,44 @@ class CloudMedium(_AnalyticMedium):
         self.cloud = (np.float32(density), np.float32(wispiness), np.float32(frequency))
 
 
+class NanoVDBMedium:
+    """pbrt "nanovdb" medium (NanoVDBMedium::Create, media.cpp:618-665; ctor 511-616):
+    `density` and optional `temperature` are NanoVDBGrid trees (vdb.py) in place of the
+    "filename" / "gridname" / "temperaturename" file read. sigma_a / sigma_s default 1,
+    x "scale"; "g"; "Lescale" (default 1); "temperatureoffset" (falls back to
+    "temperaturecutoff", default 0); "temperaturescale" (default 1). Bounds = the density
+    grid's world bbox union the temperature grid's; 64^3 majorant."""
+    type_id = 3
+    device_density = None
+    nx = ny = nz = 1
+    majorant_res = (64, 64, 64)
+    temperature = None   # (GridMedium's dense temperature grid; this medium's is temperature_grid)
+
+    def __init__(self, density, temperature=None, world_from_medium=None, sigma_a=None, sigma_s=None, scale=1.0,
+                 g=0.0, Lescale=1.0, temperatureoffset=None, temperaturecutoff=0.0, temperaturescale=1.0):
+        self.grid = density
+        self.temperature_grid = temperature
+        p0, p1 = density.world_bbox()
+        if temperature is not None:
+            t0, t1 = temperature.world_bbox()
+            p0, p1 = np.minimum(p0, t0), np.maximum(p1, t1)
+        self.p0, self.p1 = p0.astype(np.float32), p1.astype(np.float32)
+        self.world_from_medium = np.eye(4) if world_from_medium is None else np.asarray(world_from_medium, np.float64)
+        self.g = np.float32(g)
+        self.sigma_a = spectra.scaled(spectra.as_table(sigma_a, 1.0), scale)
+        self.sigma_s = spectra.scaled(spectra.as_table(sigma_s, 1.0), scale)
+        self.Le = None
+        self.Lescale_value = np.float32(Lescale)
+        self.temperature_offset = np.float32(temperaturecutoff if temperatureoffset is None else temperatureoffset)
+        self.temperature_scale = np.float32(temperaturescale)
+        self.density = None
+        self.Lescale = np.ones((1, 1, 1), np.float32)
+
+    @property
+    def bounds(self):
+        return np.concatenate([self.p0, self.p1]).astype(np.float32)
+
+
 class DistantLight:
     """DistantLight::Create (lights.cpp:246-276). L defaults to the color space illuminant."""
     type_id = 0

@@ -10,12 +10,15 @@ S-uniform  (config C2): GridMedium n^3 of 1.0 on [0,1]^3, orthographic camera lo
 S-cloud    (metric input): GridMedium n^3 filled with CloudMedium::Density (media.h:496-520,
            density 1, wispiness 1, frequency 5) at voxel centres; sigma_a=0, sigma_s=1,
            scale 4 (albedo 1), g 0.877, distant light + dim sky, perspective 1280x720, maxdepth 100.
+S-vdb      NanoVDBMedium over a sparse copy of a dense grid (index i at world i / n, so the
+           world bbox of an n^3 grid is [0, 1]^3), S-uniform's camera and light variants.
 """
 import numpy as np
 
 from . import spectra
 from .scene import (GridMedium, DistantLight, UniformInfiniteLight, OrthographicCamera, PerspectiveCamera, RGBFilm,
-                    Scene, BoxFilter, GaussianFilter, IndependentSampler, ZSobolSampler)
+                    Scene, BoxFilter, GaussianFilter, IndependentSampler, ZSobolSampler, NanoVDBMedium)
+from .vdb import NanoVDBGrid
 
 CLOUD_G = 0.877
 CLOUD_MAXDEPTH = 100
@@ -56,6 +59,32 @@ def s_uniform(n=256, width=512, height=512, variant="absorber", density=None):
                              screenwindow=(-0.5, 0.5, -0.5, 0.5))
     film = RGBFilm(width, height)
     return Scene(cam, film, med, lights)
+
+
+def vdb_grid(density, index_to_world=None, index_min=(0, 0, 0), background=0.0):
+    """Sparse NanoVDB-style copy of a dense (nz, ny, nx) grid; default map: index i at world
+    i / n per axis."""
+    d = np.asarray(density, np.float32)
+    if index_to_world is None:
+        index_to_world = np.eye(4)
+        index_to_world[0, 0], index_to_world[1, 1], index_to_world[2, 2] = (1.0 / d.shape[2], 1.0 / d.shape[1],
+                                                                            1.0 / d.shape[0])
+    return NanoVDBGrid.from_dense(d, index_min=index_min, index_to_world=index_to_world, background=background)
+
+
+def s_vdb(density, width=64, height=64, variant="scatter", temperature=None, index_to_world=None, **medium):
+    """NanoVDBMedium scene: `density` dense (nz, ny, nx) or a NanoVDBGrid; `temperature`
+    likewise (optional). variants as S-uniform's ("absorber", "furnace", "scatter")."""
+    grid = density if isinstance(density, NanoVDBGrid) else vdb_grid(density, index_to_world)
+    tgrid = None
+    if temperature is not None:
+        tgrid = temperature if isinstance(temperature, NanoVDBGrid) else vdb_grid(temperature, index_to_world)
+    base = s_uniform(n=1, width=width, height=height, variant=variant)
+    kw = {"absorber": dict(sigma_a=1.0, sigma_s=0.0), "furnace": dict(sigma_a=0.0, sigma_s=4.0),
+          "scatter": dict(sigma_a=0.5, sigma_s=2.0, g=0.3)}[variant]
+    kw.update(medium)
+    med = NanoVDBMedium(grid, temperature=tgrid, **kw)
+    return Scene(base.camera, base.film, med, base.lights)
 
 
 def cloud_medium(density):

@@ -1,0 +1,162 @@
+"""Sparse float grids for NanoVDBMedium (media.h:602-685, media.cpp:487-665).
+
+pbrt reads `.nvdb` files with NanoVDB (openvdb @ 414bed84, feature/nanovdb — an un-vendored
+submodule, absent here) and samples the FloatGrid's tree. `NanoVDBGrid` holds what that
+tree provides to the medium, in the form the C-ABI's `avr_vdb_grid` takes (include/avr.h):
+
+  * 8^3 leaf nodes: origin (multiples of 8) and 512 values, x-major ([x][y][z]) as
+    NanoVDB's LeafNode stores them;
+  * constant tiles of the upper tree levels (origin, edge length, value);
+  * the background value (every voxel not in a leaf or tile);
+  * the active-voxel index bbox (GridData::mIndexBBox, inclusive);
+  * the index -> world map (Map::mMatD | mVecD) and its inverse (Map::mInvMatD).
+
+`from_dense` builds one from a dense (nz, ny, nx) array; `to_grid_medium` is
+cmd/nanovdb2pbrt.cpp (the dense "uniformgrid" dump of a NanoVDB grid over its index bbox).
+"""
+import numpy as np
+
+
+class NanoVDBGrid:
+    def __init__(self, leaf_origins, leaf_values, background=0.0, tile_origins=None, tile_sizes=None,
+                 tile_values=None, index_bbox=None, index_to_world=None):
+        self.leaf_origins = np.ascontiguousarray(np.asarray(leaf_origins, np.int32).reshape(-1, 3))
+        self.leaf_values = np.ascontiguousarray(np.asarray(leaf_values, np.float32).reshape(-1, 8, 8, 8))
+        if len(self.leaf_origins) != len(self.leaf_values):
+            raise ValueError("one origin per leaf")
+        if np.any(self.leaf_origins % 8):
+            raise ValueError("leaf origins must be multiples of 8")
+        n_t = 0 if tile_origins is None else len(tile_origins)
+        self.tile_origins = np.ascontiguousarray(np.asarray(tile_origins if n_t else np.zeros((0, 3)), np.int32)
+                                                 .reshape(-1, 3))
+        self.tile_sizes = np.ascontiguousarray(np.asarray(tile_sizes if n_t else [], np.int32).reshape(-1))
+        self.tile_values = np.ascontiguousarray(np.asarray(tile_values if n_t else [], np.float32).reshape(-1))
+        if not (len(self.tile_origins) == len(self.tile_sizes) == len(self.tile_values)):
+            raise ValueError("tile arrays must have equal lengths")
+        if np.any(self.tile_origins % 8) or np.any(self.tile_sizes % 8) or np.any(self.tile_sizes < 8):
+            raise ValueError("tile origins and sizes must be multiples of 8")
+        self.background = np.float32(background)
+        m = np.eye(4) if index_to_world is None else np.asarray(index_to_world, np.float64)
+        if m.shape == (4, 4):
+            m = m[:3]
+        if m.shape != (3, 4):
+            raise ValueError("index_to_world must be 3x4 or affine 4x4")
+        self.index_to_world = np.ascontiguousarray(m, np.float64)
+        self.world_to_index = np.ascontiguousarray(np.linalg.inv(m[:, :3]), np.float64)
+        if index_bbox is None:
+            index_bbox = self._active_bbox()
+        self.index_bbox = np.asarray(index_bbox, np.int32).reshape(6)
+        if np.any(self.index_bbox[:3] > self.index_bbox[3:]):
+            raise ValueError("grid has no active voxels")
+
+    def _active_bbox(self):
+        """Bounding box of the voxels whose value differs from the background."""
+        lo = np.full(3, np.iinfo(np.int32).max, np.int64)
+        hi = np.full(3, np.iinfo(np.int32).min, np.int64)
+        for o, v in zip(self.leaf_origins, self.leaf_values):
+            idx = np.argwhere(v != self.background)
+            if len(idx):
+                lo = np.minimum(lo, o + idx.min(axis=0))
+                hi = np.maximum(hi, o + idx.max(axis=0))
+        for o, s, v in zip(self.tile_origins, self.tile_sizes, self.tile_values):
+            if v != self.background:
+                lo = np.minimum(lo, o)
+                hi = np.maximum(hi, o + s - 1)
+        return np.concatenate([lo, hi])
+
+    @classmethod
+    def from_dense(cls, values, index_min=(0, 0, 0), index_to_world=None, voxel_size=None, origin=(0.0, 0.0, 0.0),
+                   background=0.0, tiles=True):
+        """Dense (nz, ny, nx) values with voxel (x, y, z) at index index_min + (x, y, z).
+        Blocks equal to the background everywhere are dropped; with `tiles`, blocks of one
+        other constant become 8^3 tiles. The map is `index_to_world`, or a uniform scale
+        `voxel_size` plus translation `origin` (identity when neither is given)."""
+        v = np.asarray(values, np.float32)
+        if v.ndim != 3:
+            raise ValueError("values must be (nz, ny, nx)")
+        if index_to_world is None:
+            index_to_world = np.eye(4)
+            if voxel_size is not None:
+                index_to_world[:3, :3] *= float(voxel_size)
+            index_to_world[:3, 3] = np.asarray(origin, np.float64)
+        bg = np.float32(background)
+        mn = np.asarray(index_min, np.int64)[::-1]   # (z, y, x)
+        base = (mn // 8) * 8
+        pad_lo = mn - base
+        ext = pad_lo + np.asarray(v.shape)
+        nb = (ext + 7) // 8
+        full = np.full(tuple(nb * 8), bg, np.float32)
+        full[pad_lo[0]:pad_lo[0] + v.shape[0], pad_lo[1]:pad_lo[1] + v.shape[1], pad_lo[2]:pad_lo[2] + v.shape[2]] = v
+        # blocks[bz, by, bx, lx, ly, lz]
+        blocks = full.reshape(nb[0], 8, nb[1], 8, nb[2], 8).transpose(0, 2, 4, 5, 3, 1)
+        flat = blocks.reshape(-1, 512)
+        bz, by, bx = np.meshgrid(np.arange(nb[0]), np.arange(nb[1]), np.arange(nb[2]), indexing="ij")
+        org = np.stack([base[2] + 8 * bx.ravel(), base[1] + 8 * by.ravel(), base[0] + 8 * bz.ravel()], 1)
+        mx, mnv = flat.max(axis=1), flat.min(axis=1)
+        const = mx == mnv
+        empty = const & (mx == bg)
+        is_tile = const & ~empty & bool(tiles)
+        is_leaf = ~empty & ~is_tile
+        active = np.argwhere(v != bg)
+        if len(active) == 0:
+            raise ValueError("grid has no active voxels")
+        lo = active.min(axis=0)[::-1] + np.asarray(index_min)
+        hi = active.max(axis=0)[::-1] + np.asarray(index_min)
+        return cls(org[is_leaf], flat[is_leaf].reshape(-1, 8, 8, 8), bg, org[is_tile],
+                   np.full(int(is_tile.sum()), 8, np.int32), mx[is_tile], np.concatenate([lo, hi]), index_to_world)
+
+    def values(self, ijk):
+        """ReadAccessor::getValue for integer index coordinates ijk (n, 3)."""
+        ijk = np.asarray(ijk, np.int64).reshape(-1, 3)
+        out = np.full(len(ijk), self.background, np.float32)
+        for o, s, v in zip(self.tile_origins, self.tile_sizes, self.tile_values):
+            inside = np.all((ijk >= o) & (ijk < o + s), axis=1)
+            out[inside] = v
+        if len(self.leaf_origins):
+            key = {tuple(o): i for i, o in enumerate(self.leaf_origins.tolist())}
+            blk = (ijk // 8) * 8
+            loc = ijk - blk
+            for n, b in enumerate(map(tuple, blk.tolist())):
+                li = key.get(b)
+                if li is not None:
+                    out[n] = self.leaf_values[li, loc[n, 0], loc[n, 1], loc[n, 2]]
+        return out
+
+    def world_bbox(self):
+        """GridData::mWorldBBox: the map of the corners of [min, max + 1], each row
+        ((m0*x + m1*y) + m2*z) + t in f64 (the C-ABI's and the oracle's convention)."""
+        b = self.index_bbox.astype(np.float64)
+        m = self.index_to_world
+        lo = np.full(3, np.inf)
+        hi = np.full(3, -np.inf)
+        for x in (b[0], b[3] + 1.0):
+            for y in (b[1], b[4] + 1.0):
+                for z in (b[2], b[5] + 1.0):
+                    for r in range(3):
+                        w = float(m[r, 0]) * x + float(m[r, 1]) * y + float(m[r, 2]) * z + float(m[r, 3])
+                        lo[r] = min(lo[r], w)
+                        hi[r] = max(hi[r], w)
+        return lo.astype(np.float32), hi.astype(np.float32)
+
+    def to_grid_medium(self):
+        """cmd/nanovdb2pbrt.cpp: the values over [min, max + 1] per axis (inclusive) as a
+        dense (nz, ny, nx) array, plus the world bbox as p0 / p1."""
+        b = self.index_bbox
+        xs = np.arange(b[0], b[3] + 2)
+        ys = np.arange(b[1], b[4] + 2)
+        zs = np.arange(b[2], b[5] + 2)
+        z, y, x = np.meshgrid(zs, ys, xs, indexing="ij")
+        vals = self.values(np.stack([x.ravel(), y.ravel(), z.ravel()], 1)).reshape(len(zs), len(ys), len(xs))
+        p0, p1 = self.world_bbox()
+        return vals, p0, p1
+
+    def save(self, path):
+        np.savez(path, leaf_origins=self.leaf_origins, leaf_values=self.leaf_values, tile_origins=self.tile_origins,
+                 tile_sizes=self.tile_sizes, tile_values=self.tile_values, background=self.background,
+                 index_bbox=self.index_bbox, index_to_world=self.index_to_world)
+
+    @classmethod
+    def load(cls, path):
+        z = np.load(path, allow_pickle=False)
+        return cls(z["leaf_origins"], z["leaf_values"], z["background"], z["tile_origins"], z["tile_sizes"],
+                   z["tile_values"], z["index_bbox"], z["index_to_world"])

@@ -117,6 +117,41 @@ int avr_medium_homogeneous(avr_context *ctx, const float bounds[6], const float 
 int avr_medium_cloud(avr_context *ctx, const float bounds[6], const float render_from_medium[16],
                      const float medium_from_render[16], const float *sigma_a, const float *sigma_s, float g,
                      float density, float wispiness, float frequency);
+/* One NanoVDB FloatGrid as NanoVDBMedium reads it (media.h:624-672; NanoVDB is the
+ * un-vendored openvdb@414bed84 feature/nanovdb submodule): the 8^3 leaf nodes (origin =
+ * index coordinate of the leaf's voxel (0,0,0), multiples of 8; 512 values each, x-major
+ * ((x&7)*8 + (y&7))*8 + (z&7) as LeafNode stores them), the constant tiles of the upper tree
+ * levels (origin and edge length in voxels, multiples of 8), the background value returned
+ * everywhere else, the active-voxel index bbox (inclusive, GridData::mIndexBBox) and the map:
+ * index->world as a row-major 3x4 (Map::mMatD with mVecD as the last column) and the inverse
+ * 3x3 (Map::mInvMatD); the float copies worldToIndexF uses are their roundings, as Map::set
+ * makes them. World bbox = the map of the corners of [min, max + 1], each row evaluated
+ * ((m0*x + m1*y) + m2*z) + t in f64. */
+typedef struct avr_vdb_grid {
+    int n_leaves;
+    const int *leaf_origin;      /* 3 per leaf */
+    const float *leaf_values;    /* 512 per leaf */
+    int n_tiles;
+    const int *tile_origin;      /* 3 per tile (may be NULL when n_tiles == 0) */
+    const int *tile_size;        /* 1 per tile */
+    const float *tile_value;     /* 1 per tile */
+    float background;
+    int index_bbox[6];           /* min xyz, max xyz */
+    double index_to_world[12];
+    double world_to_index[9];
+} avr_vdb_grid;
+/* NanoVDBMedium (media.h:602-685, ctor media.cpp:511-616, Create media.cpp:618-665):
+ * density grid, optional temperature grid (NULL = not emissive), sigma tables with
+ * sigmaScale folded in, g, LeScale, temperatureoffset, temperaturescale. Bounds are the
+ * density grid's world bbox (union the temperature grid's); the 64^3 majorant is built on
+ * the device with pbrt's one-voxel filter slop. Replaces NanoVDBMedium::Create's
+ * readGrid + ctor: the caller hands over the tree it read. */
+int avr_medium_nanovdb(avr_context *ctx, const avr_vdb_grid *density, const avr_vdb_grid *temperature,
+                       const float render_from_medium[16], const float medium_from_render[16],
+                       const float *sigma_a, const float *sigma_s, float g, float Lescale,
+                       float temperature_offset, float temperature_scale);
+/* The medium bounds the last avr_medium_* call set (medium space, min xyz then max xyz). */
+int avr_medium_bounds(avr_context *ctx, float bounds[6]);
 /* Fill d_out[first .. first+count) of an n^3 grid with CloudMedium::Density
  * (media.h:496-520) at voxel centres (i+0.5)/n — the synthetic S-cloud input. */
 int avr_generate_cloud(avr_context *ctx, float *d_out, int n, long long first, long long count, float density,

@@ -67,6 +67,9 @@ class OracleScene(ctypes.Structure):
         ("temperature", c_float_p),
         ("temperature_scale", ctypes.c_float),
         ("temperature_offset", ctypes.c_float),
+        ("vdb", ctypes.c_void_p),
+        ("vdb_temperature", ctypes.c_void_p),
+        ("vdb_lescale", ctypes.c_float),
     ]
 
 
@@ -139,6 +142,18 @@ def lib():
         L.oracle_transmittance4.argtypes = [ctypes.POINTER(OracleScene), ctypes.c_int, c_float_p, c_float_p,
                                             c_float_p, c_float_p]
         L.oracle_get_libm.restype = ctypes.c_int
+        c_int_p = ctypes.POINTER(ctypes.c_int)
+        L.oracle_vdb_create.restype = ctypes.c_void_p
+        L.oracle_vdb_create.argtypes = [ctypes.c_int, c_int_p, c_float_p, ctypes.c_int, c_int_p, c_int_p, c_float_p,
+                                        ctypes.c_float, c_int_p, c_double_p, c_double_p]
+        L.oracle_vdb_free.argtypes = [ctypes.c_void_p]
+        L.oracle_vdb_value.restype = ctypes.c_float
+        L.oracle_vdb_value.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+        L.oracle_vdb_sample_world.restype = ctypes.c_float
+        L.oracle_vdb_sample_world.argtypes = [ctypes.c_void_p, ctypes.c_float, ctypes.c_float, ctypes.c_float]
+        L.oracle_vdb_bounds.argtypes = [ctypes.c_void_p, ctypes.c_void_p, c_float_p]
+        L.oracle_vdb_majorant.argtypes = [ctypes.c_void_p, c_float_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                          c_float_p]
     return _lib
 
 
@@ -170,6 +185,46 @@ def cloud_grid(n, z0=0, z1=None):
     return out
 
 
+class VdbTree:
+    """The oracle's NanoVDB tree restatement built from a vdb.NanoVDBGrid."""
+
+    def __init__(self, grid):
+        ip = lambda a: np.ascontiguousarray(a, np.int32).ctypes.data_as(ctypes.POINTER(ctypes.c_int))
+        self._keep = [np.ascontiguousarray(a) for a in (grid.leaf_origins, grid.leaf_values, grid.tile_origins,
+                                                          grid.tile_sizes, grid.tile_values, grid.index_bbox,
+                                                          grid.index_to_world, grid.world_to_index)]
+        lo, lv, to, ts, tv, bb, m, mi = self._keep
+        self.h = lib().oracle_vdb_create(len(lo), ip(lo), fp(lv.astype(np.float32)), len(tv), ip(to), ip(ts),
+                                         fp(tv.astype(np.float32)), float(grid.background), ip(bb),
+                                         m.astype(np.float64).ctypes.data_as(c_double_p),
+                                         mi.astype(np.float64).ctypes.data_as(c_double_p))
+
+    def value(self, x, y, z):
+        return lib().oracle_vdb_value(self.h, int(x), int(y), int(z))
+
+    def sample_world(self, p):
+        return np.array([lib().oracle_vdb_sample_world(self.h, *map(float, q)) for q in np.asarray(p, np.float32)],
+                        np.float32)
+
+    def __del__(self):
+        if getattr(self, "h", None) and _lib is not None:
+            _lib.oracle_vdb_free(self.h)
+            self.h = None
+
+
+def vdb_bounds(dtree, ttree=None):
+    out = np.zeros(6, np.float32)
+    lib().oracle_vdb_bounds(dtree.h, ttree.h if ttree is not None else None, fp(out))
+    return out
+
+
+def vdb_majorant(dtree, bounds, res=(64, 64, 64)):
+    b = np.ascontiguousarray(bounds, np.float32)
+    out = np.zeros(res[0] * res[1] * res[2], np.float32)
+    lib().oracle_vdb_majorant(dtree.h, fp(b), res[0], res[1], res[2], fp(out))
+    return out
+
+
 class OracleRun:
     """Holds an OracleScene and the numpy buffers it points into."""
 
@@ -178,7 +233,8 @@ class OracleRun:
             raise ValueError(f"libm must be one of {sorted(LIBM_MODES)}")
         self.libm = libm
         med = scene.medium
-        if med.density is None:
+        is_vdb = int(getattr(med, "type_id", 0)) == 3
+        if med.density is None and not is_vdb:
             raise ValueError("oracle needs a host density grid")
         s = OracleScene()
         keep = []
@@ -188,7 +244,7 @@ class OracleRun:
             keep.append(a)
             return fp(a)
 
-        s.density = arr(med.density)
+        s.density = arr(med.density if not is_vdb else np.zeros((1, 1, 1), np.float32))
         s.nx, s.ny, s.nz = med.nx, med.ny, med.nz
         s.bounds[:] = [float(v) for v in med.bounds]
         s.render_from_medium[:] = [float(v) for v in scene.render_from_medium.reshape(-1)]
@@ -201,7 +257,19 @@ class OracleRun:
         ls = np.ascontiguousarray(med.Lescale, np.float32)
         s.Lescale = arr(ls)
         s.lnz, s.lny, s.lnx = ls.shape
-        self.majorant = build_majorant(med.density, med.majorant_res)
+        if is_vdb:
+            self.vdb = VdbTree(med.grid)
+            self.vdb_temperature = VdbTree(med.temperature_grid) if med.temperature_grid is not None else None
+            self.bounds = vdb_bounds(self.vdb, self.vdb_temperature)
+            s.bounds[:] = [float(v) for v in self.bounds]
+            s.vdb = self.vdb.h
+            s.vdb_temperature = self.vdb_temperature.h if self.vdb_temperature is not None else None
+            s.vdb_lescale = float(med.Lescale_value)
+            s.temperature_scale = float(med.temperature_scale)
+            s.temperature_offset = float(med.temperature_offset)
+            self.majorant = vdb_majorant(self.vdb, self.bounds, med.majorant_res)
+        else:
+            self.majorant = build_majorant(med.density, med.majorant_res)
         s.majorant = arr(self.majorant)
         s.mres[:] = list(med.majorant_res)
         s.medium_type = int(getattr(med, "type_id", 0))

@@ -28,6 +28,7 @@
 #include <cstring>
 #include <limits>
 #include <thread>
+#include <unordered_map>
 #include <vector>
 
 namespace oracle {
@@ -618,6 +619,104 @@ static inline float Blackbody(float lambda, float T) {
     return (2 * h * c * c) / (Pow5(l) * (FastExp((h * c) / (l * kb * T)) - 1));
 }
 
+// ---------------------------------------------------------------------------
+// NanoVDB FloatGrid as NanoVDBMedium reads it (media.h:624-672). NanoVDB itself
+// (openvdb @ 414bed84, feature/nanovdb) is an empty submodule here: its published
+// semantics are restated — ReadAccessor::getValue (leaf value, else tile value, else
+// background), Map::applyInverseMapF (InvMatF * (p - VecF) with fmaf rows),
+// SampleFromVoxels<Tree, 1, false> (floor / fraction, 2x2x2 stencil, lerp a + w(b - a)
+// along z, y, then x). PARITY UNPINNED: no reference test or asset exercises it.
+// Storage here is a hash map from leaf origin to its 512 values (x-major), independent
+// of the device's block-slot layout.
+struct VdbTree {
+    std::unordered_map<uint64_t, const float *> leaves;
+    std::vector<float> leafStore;
+    std::vector<int> tileBox;      // ox, oy, oz, size per tile
+    std::vector<float> tileValue;
+    float background = 0;
+    int ibbox[6] = {0, 0, 0, -1, -1, -1};
+    double matD[12] = {};          // index -> world (3x3 row-major, translation in column 3)
+    float invF[9] = {}, vecF[3] = {};
+    static uint64_t Key(int x, int y, int z) {
+        return ((uint64_t)(uint32_t)(x >> 3) & 0x1fffff) | (((uint64_t)(uint32_t)(y >> 3) & 0x1fffff) << 21) |
+               (((uint64_t)(uint32_t)(z >> 3) & 0x1fffff) << 42);
+    }
+    float GetValue(int x, int y, int z) const {
+        auto it = leaves.find(Key(x, y, z));
+        if (it != leaves.end()) return it->second[(x & 7) * 64 + (y & 7) * 8 + (z & 7)];
+        for (int t = (int)tileValue.size() - 1; t >= 0; --t) {   // tiles do not overlap in a valid tree
+            const int *b = &tileBox[4 * t];
+            if (x >= b[0] && x < b[0] + b[3] && y >= b[1] && y < b[1] + b[3] && z >= b[2] && z < b[2] + b[3])
+                return tileValue[t];
+        }
+        return background;
+    }
+    V3 WorldToIndexF(V3 p) const {
+        const float x = p.x - vecF[0], y = p.y - vecF[1], z = p.z - vecF[2];
+        return {std::fmaf(x, invF[0], std::fmaf(y, invF[1], z * invF[2])),
+                std::fmaf(x, invF[3], std::fmaf(y, invF[4], z * invF[5])),
+                std::fmaf(x, invF[6], std::fmaf(y, invF[7], z * invF[8]))};
+    }
+    float Sample(V3 q) const {
+        const float fl[3] = {std::floor(q.x), std::floor(q.y), std::floor(q.z)};
+        const int i = (int)fl[0], j = (int)fl[1], k = (int)fl[2];
+        const float u = q.x - fl[0], v = q.y - fl[1], w = q.z - fl[2];
+        float c[2][2][2];
+        for (int a = 0; a < 2; ++a)
+            for (int b = 0; b < 2; ++b)
+                for (int d = 0; d < 2; ++d) c[a][b][d] = GetValue(i + a, j + b, k + d);
+        auto lerp = [](float a, float b, float t) { return a + t * (b - a); };
+        const float x0 = lerp(lerp(c[0][0][0], c[0][0][1], w), lerp(c[0][1][0], c[0][1][1], w), v);
+        const float x1 = lerp(lerp(c[1][0][0], c[1][0][1], w), lerp(c[1][1][0], c[1][1][1], w), v);
+        return lerp(x0, x1, u);
+    }
+    // world bbox: the map of the corners of [min, max + 1] (f64, evaluated left to right)
+    void WorldBBox(double lo[3], double hi[3]) const {
+        for (int a = 0; a < 3; ++a) { lo[a] = HUGE_VAL; hi[a] = -HUGE_VAL; }
+        for (int cx = 0; cx < 2; ++cx)
+            for (int cy = 0; cy < 2; ++cy)
+                for (int cz = 0; cz < 2; ++cz) {
+                    const double x = cx ? ibbox[3] + 1.0 : ibbox[0];
+                    const double y = cy ? ibbox[4] + 1.0 : ibbox[1];
+                    const double z = cz ? ibbox[5] + 1.0 : ibbox[2];
+                    for (int r = 0; r < 3; ++r) {
+                        const double wv = matD[4 * r] * x + matD[4 * r + 1] * y + matD[4 * r + 2] * z + matD[4 * r + 3];
+                        lo[r] = std::min(lo[r], wv);
+                        hi[r] = std::max(hi[r], wv);
+                    }
+                }
+    }
+};
+
+// NanoVDBMedium ctor's 64^3 majorant (media.cpp:556-613)
+static void VdbMajorant(const VdbTree &g, const float b[6], int rx, int ry, int rz, float *out) {
+    const int res[3] = {rx, ry, rz};
+    for (int z = 0; z < rz; ++z)
+        for (int y = 0; y < ry; ++y)
+            for (int x = 0; x < rx; ++x) {
+                const int c[3] = {x, y, z};
+                float p0[3], p1[3], lo[3], hi[3];
+                for (int a = 0; a < 3; ++a) {   // bounds.Lerp (vecmath.h Bounds3::Lerp, math.h Lerp)
+                    p0[a] = Lerp(float(c[a]) / res[a], b[a], b[3 + a]);
+                    p1[a] = Lerp(float(c[a] + 1) / res[a], b[a], b[3 + a]);
+                    lo[a] = std::min(p0[a], p1[a]);
+                    hi[a] = std::max(p0[a], p1[a]);
+                }
+                const V3 i0 = g.WorldToIndexF({lo[0], lo[1], lo[2]}), i1 = g.WorldToIndexF({hi[0], hi[1], hi[2]});
+                const float delta = 1.f;   // filter slop
+                int n0[3], n1[3];
+                for (int a = 0; a < 3; ++a) {
+                    n0[a] = std::max(int((double)i0[a] - delta), g.ibbox[a]);
+                    n1[a] = std::min(int((double)i1[a] + delta), g.ibbox[3 + a]);
+                }
+                float maxValue = 0;
+                for (int nz = n0[2]; nz <= n1[2]; ++nz)
+                    for (int ny = n0[1]; ny <= n1[1]; ++ny)
+                        for (int nx = n0[0]; nx <= n1[0]; ++nx) maxValue = std::max(maxValue, g.GetValue(nx, ny, nz));
+                out[x + rx * (y + ry * z)] = maxValue;
+            }
+}
+
 }  // namespace oracle
 
 // ===========================================================================
@@ -676,6 +775,11 @@ typedef struct OracleScene {
     // GridMedium temperature grid (media.h:299-316; null = Le spectrum), scale, offset
     const float *temperature;
     float temperature_scale, temperature_offset;
+    // medium_type 3, NanoVDBMedium (media.h:602-685): oracle_vdb_create handles for the
+    // density and (nullable) temperature grids, LeScale
+    const void *vdb;
+    const void *vdb_temperature;
+    float vdb_lescale;
 } OracleScene;
 
 }  // extern "C"
@@ -922,6 +1026,25 @@ static inline MediumProps SamplePoint(const SceneView &sv, V3 p, const Lambda &l
         return mp;
     }
     p = XInvPoint(sv.mediumX, p);
+    if (sv.s.medium_type == 3) {   // NanoVDBMedium::SamplePoint (media.h:624-637)
+        const VdbTree &dg = *(const VdbTree *)sv.s.vdb;
+        const float d = dg.Sample(dg.WorldToIndexF(p));
+        mp.sigma_a = mp.sigma_a * d;
+        mp.sigma_s = mp.sigma_s * d;
+        if (sv.s.vdb_temperature) {   // NanoVDBMedium::Le (media.h:660-672)
+            const VdbTree &tg = *(const VdbTree *)sv.s.vdb_temperature;
+            float temp = tg.Sample(tg.WorldToIndexF(p));
+            temp = (temp - sv.s.temperature_offset) * sv.s.temperature_scale;
+            if (temp > 100.f) {
+                float lambdaMax = 2.8977721e-3f / temp;
+                float normalizationFactor = 1 / Blackbody(lambdaMax * 1e9f, temp);
+                Spec b;
+                for (int i = 0; i < NS; ++i) b.v[i] = Blackbody(l.lambda[i], temp) * normalizationFactor;
+                mp.Le = sv.s.vdb_lescale * b;
+            }
+        }
+        return mp;
+    }
     if (sv.s.medium_type == 2) {   // CloudMedium::SamplePoint (media.h:456-465)
         float d = CloudDensity(p, sv.s.cloud[0], sv.s.cloud[1], sv.s.cloud[2]);
         mp.sigma_a = d * mp.sigma_a;
@@ -1023,7 +1146,7 @@ static inline DDA SampleRay(const SceneView &sv, Ray ray, float raytMax, const L
     float tMin, tMax;
     if (!IntersectP(sv.bounds, ray.o, ray.d, raytMax, &tMin, &tMax)) return it;
     Spec sigma_t = SampleDense(sv.s.sigma_a, l) + SampleDense(sv.s.sigma_s, l);
-    if (sv.s.medium_type != 0) {   // CloudMedium::SampleRay (media.h:467-484); homogeneous: the box crossing
+    if (sv.s.medium_type == 1 || sv.s.medium_type == 2) {   // CloudMedium::SampleRay (media.h:467-484); homogeneous: the box crossing
         it.InitSingle(tMin, tMax, sigma_t);
         return it;
     }
@@ -1295,6 +1418,51 @@ void oracle_canon_sincos(float x, float *s, float *c) {
     *c = (float)cd;
 }
 
+
+// NanoVDB grids (test infrastructure handles; see VdbTree)
+void *oracle_vdb_create(int nLeaves, const int *leafOrigin, const float *leafValues, int nTiles, const int *tileOrigin,
+                        const int *tileSize, const float *tileValue, float background, const int ibbox[6],
+                        const double indexToWorld[12], const double worldToIndex[9]) {
+    auto *g = new VdbTree();
+    g->leafStore.assign(leafValues, leafValues + (size_t)nLeaves * 512);
+    for (int l = 0; l < nLeaves; ++l) {
+        const int *o = leafOrigin + 3 * l;
+        g->leaves[VdbTree::Key(o[0], o[1], o[2])] = g->leafStore.data() + (size_t)l * 512;
+    }
+    for (int t = 0; t < nTiles; ++t) {
+        for (int a = 0; a < 3; ++a) g->tileBox.push_back(tileOrigin[3 * t + a]);
+        g->tileBox.push_back(tileSize[t]);
+        g->tileValue.push_back(tileValue[t]);
+    }
+    g->background = background;
+    for (int a = 0; a < 6; ++a) g->ibbox[a] = ibbox[a];
+    for (int a = 0; a < 12; ++a) g->matD[a] = indexToWorld[a];
+    for (int a = 0; a < 9; ++a) g->invF[a] = (float)worldToIndex[a];   // Map::set: mInvMatF = float(mInvMatD)
+    for (int a = 0; a < 3; ++a) g->vecF[a] = (float)indexToWorld[4 * a + 3];
+    return g;
+}
+void oracle_vdb_free(void *g) { delete (VdbTree *)g; }
+float oracle_vdb_value(const void *g, int x, int y, int z) { return ((const VdbTree *)g)->GetValue(x, y, z); }
+float oracle_vdb_sample_world(const void *g, float x, float y, float z) {
+    const VdbTree &t = *(const VdbTree *)g;
+    return t.Sample(t.WorldToIndexF({x, y, z}));
+}
+// NanoVDBMedium bounds: density world bbox, Union with the temperature grid's (media.cpp:531-549)
+void oracle_vdb_bounds(const void *density, const void *temperature, float out[6]) {
+    double lo[3], hi[3];
+    ((const VdbTree *)density)->WorldBBox(lo, hi);
+    for (int a = 0; a < 3; ++a) { out[a] = (float)lo[a]; out[3 + a] = (float)hi[a]; }
+    if (temperature) {
+        ((const VdbTree *)temperature)->WorldBBox(lo, hi);
+        for (int a = 0; a < 3; ++a) {
+            out[a] = std::min(out[a], (float)lo[a]);
+            out[3 + a] = std::max(out[3 + a], (float)hi[a]);
+        }
+    }
+}
+void oracle_vdb_majorant(const void *density, const float bounds[6], int rx, int ry, int rz, float *out) {
+    VdbMajorant(*(const VdbTree *)density, bounds, rx, ry, rz, out);
+}
 
 // MajorantGrid build — media.cpp:229,241-246 with MajorantGrid::VoxelBounds media.h:123-127
 void oracle_build_majorant(const float *density, int nx, int ny, int nz, int rx, int ry, int rz, float *out) {
