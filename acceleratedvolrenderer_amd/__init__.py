@@ -8,14 +8,15 @@ include/avr.h. See DESIGN.md.
 """
 from . import spectra, transform
 from .scene import (GridMedium, DistantLight, UniformInfiniteLight, OrthographicCamera, PerspectiveCamera, RGBFilm,
-                    Scene, film_rgb, HomogeneousMedium, CloudMedium, NanoVDBMedium, BoxFilter, GaussianFilter,
+                    Scene, film_rgb, HomogeneousMedium, CloudMedium, NanoVDBMedium, RGBGridMedium, BoxFilter, GaussianFilter,
                     IndependentSampler, ZSobolSampler)
 from .vdb import NanoVDBGrid
+from .rgbspectrum import RGBToSpectrumTable
 from .integrator import VolPathIntegrator, shard_samples, INTEGRATOR_NAMES
 from . import capi
 from . import scenes
 
 __all__ = ["spectra", "transform", "GridMedium", "DistantLight", "UniformInfiniteLight", "OrthographicCamera",
            "PerspectiveCamera", "RGBFilm", "Scene", "film_rgb", "VolPathIntegrator", "shard_samples",
-           "INTEGRATOR_NAMES", "capi", "scenes", "HomogeneousMedium", "CloudMedium", "NanoVDBMedium", "NanoVDBGrid",
+           "INTEGRATOR_NAMES", "capi", "scenes", "HomogeneousMedium", "CloudMedium", "NanoVDBMedium", "NanoVDBGrid", "RGBGridMedium", "RGBToSpectrumTable",
            "BoxFilter", "GaussianFilter", "IndependentSampler", "ZSobolSampler"]

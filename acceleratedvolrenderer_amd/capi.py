@@ -114,6 +114,9 @@ SIGNATURES = {
                                           c_float_p, c_float_p, c_float_p, c_float_p, ctypes.c_float, ctypes.c_float,
                                           ctypes.c_float, ctypes.c_float]),
     "avr_medium_bounds": (ctypes.c_int, [ctypes.c_void_p, c_float_p]),
+    "avr_medium_rgbgrid": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_float_p,
+                                          c_float_p, c_float_p, c_float_p, c_float_p, ctypes.c_float, ctypes.c_float,
+                                          c_float_p, c_float_p, ctypes.c_float]),
     "avr_set_filter": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, c_float_p, ctypes.c_float]),
     "avr_set_sampler": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]),
     "avr_film": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, c_float_p, c_float_p, ctypes.c_float,
@@ -212,6 +215,13 @@ class Context:
         if getattr(med, "type_id", 0) == 1:
             _check(self.lib.avr_medium_homogeneous(self.h, _fp(args[0]), _fp(args[1]), _fp(args[2]), _fp(args[3]),
                                                    _fp(args[4]), float(med.g), _fp(Le)))
+        elif getattr(med, "type_id", 0) == 4:
+            grids = [f32(g) if g is not None else None for g in (med.rgb_sigma_a, med.rgb_sigma_s, med.rgb_Le)]
+            ill = f32(med.illuminant)
+            self._keep += grids + [ill]
+            _check(self.lib.avr_medium_rgbgrid(self.h, med.nx, med.ny, med.nz, _fp(args[0]), _fp(args[1]),
+                                               _fp(args[2]), _fp(grids[0]), _fp(grids[1]), float(med.sigma_scale),
+                                               float(med.g), _fp(grids[2]), _fp(ill), float(med.Le_scale)))
         elif getattr(med, "type_id", 0) == 3:
             dg = AvrVdbGrid.of(med.grid)
             tg = AvrVdbGrid.of(med.temperature_grid) if med.temperature_grid is not None else None

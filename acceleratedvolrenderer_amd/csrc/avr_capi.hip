@@ -88,6 +88,9 @@ struct avr_context {
     int *d_vdb_slot[2] = {nullptr, nullptr};
     float *d_vdb_leaves[2] = {nullptr, nullptr}, *d_vdb_tiles[2] = {nullptr, nullptr};
     int vdb_ibbox[6] = {};    // density grid's active index bbox (majorant clamp)
+    // RGBGridMedium grids (sigma_a, sigma_s, Le as float4 {c0, c1, c2, scale}) and illuminant
+    float4 *d_rgb[3] = {nullptr, nullptr, nullptr};
+    float *d_illum = nullptr;
     avr::smp::FilterTables ftab{};
     int refill_min = 32;
     int dda_budget = 12;
@@ -150,6 +153,13 @@ int blocks_for(long long n, int per = 256, int cap = 256 * 16) {
 }
 
 bool affine(const float m[16]) { return m[12] == 0 && m[13] == 0 && m[14] == 0 && m[15] == 1; }
+
+void free_rgb(avr_context *c) {
+    for (auto &p : c->d_rgb) if (p) (void)hipFree(p), p = nullptr;
+    if (c->d_illum) (void)hipFree(c->d_illum), c->d_illum = nullptr;
+    c->med.rgb_a = c->med.rgb_s = c->med.rgb_le = nullptr;
+    c->med.illuminant = nullptr;
+}
 
 void free_vdb(avr_context *c) {
     for (int k = 0; k < 2; ++k) {
@@ -276,6 +286,7 @@ int medium_common(avr_context *c, const float *d_density, int nx, int ny, int nz
     if ((rc = upload_table(&c->d_lescale, Lescale, (size_t)lnx * lny * lnz, c->stream))) return rc;
     avr::DevMedium &m = c->med;
     if (type != 3) free_vdb(c);
+    if (type != 4) free_rgb(c);
     if (c->d_temperature) { (void)hipFree(c->d_temperature); c->d_temperature = nullptr; }
     m.temperature = nullptr;
     m.temp_scale = 1.f;
@@ -308,6 +319,10 @@ int medium_common(avr_context *c, const float *d_density, int nx, int ny, int nz
     if (type == 0) {
         hipLaunchKernelGGL(avr::k_majorant, dim3(nm), dim3(256), 0, c->stream, d_density, nx, ny, nz, mres[0], mres[1],
                            mres[2], c->d_majorant);
+        HIP_TRY(hipGetLastError());
+    } else if (type == 4) {
+        hipLaunchKernelGGL(avr::k_majorant_rgb, dim3(nm), dim3(256), 0, c->stream, m.rgb_a, m.rgb_s, nx, ny, nz,
+                           mres[0], mres[1], mres[2], m.rgb_sigma_scale, c->d_majorant);
         HIP_TRY(hipGetLastError());
     } else if (type == 3) {
         const int *b = c->vdb_ibbox;
@@ -442,6 +457,7 @@ int avr_context_destroy(avr_context *c) {
     if (c->d_filter) (void)hipFree(c->d_filter);
     if (c->d_temperature) (void)hipFree(c->d_temperature);
     free_vdb(c);
+    free_rgb(c);
     if (c->d_fat) (void)hipFree(c->d_fat);
     if (c->d_stats) (void)hipFree(c->d_stats);
     if (c->h_count) (void)hipHostFree(c->h_count);
@@ -558,6 +574,46 @@ int avr_medium_nanovdb(avr_context *c, const avr_vdb_grid *density, const avr_vd
     c->med.temp_offset = temperature_offset;
     c->med.temp_scale = temperature_scale;
     c->med.emissive = temperature ? 1 : 0;
+    return AVR_OK;
+}
+
+int avr_medium_rgbgrid(avr_context *c, int nx, int ny, int nz, const float bounds[6], const float rfm[16],
+                       const float mfr[16], const float *sigma_a, const float *sigma_s, float sigma_scale, float g,
+                       const float *Le, const float *illuminant, float Le_scale) {
+    if (!c || !bounds || !rfm || !mfr) return fail(AVR_ERR_ARG, "null medium argument");
+    if (nx < 1 || ny < 1 || nz < 1) return fail(AVR_ERR_ARG, "bad grid");
+    if (!sigma_a && !sigma_s)
+        return fail(AVR_ERR_ARG, "RGB grid requires \"sigma_a\" and/or \"sigma_s\" (media.cpp:404-406)");
+    if (Le && !sigma_a) return fail(AVR_ERR_ARG, "RGB grid requires \"sigma_a\" if \"Le\" given (media.cpp:418-419)");
+    if (Le && !illuminant) return fail(AVR_ERR_ARG, "Le needs the colour space's illuminant table");
+    const size_t n = (size_t)nx * ny * nz;
+    if (n > (size_t)INT32_MAX) return fail(AVR_ERR_ARG, "grid too large for int32 indexing");
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    free_rgb(c);
+    const float *src[3] = {sigma_a, sigma_s, Le};
+    for (int k = 0; k < 3; ++k) {
+        if (!src[k]) continue;
+        HIP_TRY(dalloc(&c->d_rgb[k], n));
+        HIP_TRY(hipMemcpyAsync(c->d_rgb[k], src[k], n * sizeof(float4), hipMemcpyHostToDevice, c->stream));
+    }
+    int rc;
+    if (Le && (rc = upload_table(&c->d_illum, illuminant, avr::kNTable, c->stream))) return rc;
+    c->med.rgb_a = c->d_rgb[0];
+    c->med.rgb_s = c->d_rgb[1];
+    c->med.rgb_le = c->d_rgb[2];
+    c->med.illuminant = c->d_illum;
+    c->med.rgb_sigma_scale = sigma_scale;
+    c->med.rgb_le_scale = Le_scale;
+    // SampleRay's sigma_t = 1 (media.h:417): tables {1} + {0} make the segments' sigma_maj the
+    // majorant value itself; SamplePoint reads the RGB grids instead of the tables
+    static float ones[avr::kNTable], zeros[avr::kNTable];
+    for (int i = 0; i < avr::kNTable; ++i) ones[i] = 1.f;
+    const int mres[3] = {16, 16, 16};   // majorantGrid(bounds, {16, 16, 16}) (media.cpp:352)
+    if ((rc = medium_common(c, nullptr, nx, ny, nz, bounds, rfm, mfr, ones, zeros, g, nullptr, nullptr, 1, 1, 1, mres,
+                            4, nullptr)))
+        return rc;
+    c->med.emissive = (Le && Le_scale > 0) ? 1 : 0;   // IsEmissive (media.h:374)
     return AVR_OK;
 }
 

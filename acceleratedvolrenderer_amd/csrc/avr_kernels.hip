@@ -59,6 +59,13 @@ struct DevMedium {
     // emissive iff a temperature grid is present (the integrator tests mp.Le itself)
     vdb::Grid vdb, vdb_temp;
     float vdb_lescale;
+    // 4 RGBGridMedium (media.h:355-427): per-voxel RGBUnboundedSpectrum sigma_a / sigma_s and
+    // RGBIlluminantSpectrum Le as {c0, c1, c2, scale} (nx*ny*nz each, null = absent), the
+    // colour space's illuminant table, sigmaScale and LeScale; sigma tables are {1, 0} so
+    // the majorant segments carry SampleRay's sigma_t = 1
+    const float4 *rgb_a, *rgb_s, *rgb_le;
+    const float *illuminant;
+    float rgb_sigma_scale, rgb_le_scale;
 };
 
 
@@ -290,6 +297,47 @@ __device__ float cloud_density(V3 p, float density, float wispiness, float frequ
     return clampf(d, 0, 1);
 }
 
+// RGBSigmoidPolynomial (util/color.h:332-365): s(EvaluatePolynomial(lambda, c2, c1, c0))
+__device__ __forceinline__ float rsp_eval(float c0, float c1, float c2, float lambda) {
+    const float x = __builtin_fmaf(lambda, __builtin_fmaf(lambda, c0, c1), c2);
+    if (__builtin_isinf(x)) return x > 0 ? 1.f : 0.f;
+    return .5f + x / (2 * __builtin_sqrtf(1 + x * x));
+}
+__device__ __forceinline__ float rsp_max(float c0, float c1, float c2) {
+    const float a = rsp_eval(c0, c1, c2, 360), b = rsp_eval(c0, c1, c2, 830);
+    float result = a < b ? b : a;
+    const float lambda = -c1 / (2 * c0);
+    if (lambda >= 360 && lambda <= 830) {
+        const float v = rsp_eval(c0, c1, c2, lambda);
+        result = result < v ? v : result;
+    }
+    return result;
+}
+// SampledGrid<RGB*Spectrum>::Lookup(p, convert) (containers.h:785-800): the 8 taps are
+// converted to sampled spectra (scale * rsp(lambda_i), times the illuminant for Le) and
+// lerped per wavelength; taps outside the grid convert T{} = 0
+__device__ __forceinline__ Spec rgb_tap(const float4 *__restrict__ g, int nx, int ny, int nz, int x, int y, int z,
+                                        const Spec &lam, const Spec &illum, bool illuminant) {
+    if (x < 0 || x >= nx || y < 0 || y >= ny || z < 0 || z >= nz) return Spec::c(0.f);
+    const float4 c = g[(z * ny + y) * nx + x];
+    Spec s{c.w * rsp_eval(c.x, c.y, c.z, lam.v0), c.w * rsp_eval(c.x, c.y, c.z, lam.v1),
+           c.w * rsp_eval(c.x, c.y, c.z, lam.v2), c.w * rsp_eval(c.x, c.y, c.z, lam.v3)};
+    return illuminant ? s * illum : s;
+}
+__device__ __forceinline__ Spec spec_lerp(float t, const Spec &a, const Spec &b) { return a * (1 - t) + b * t; }
+__device__ Spec rgb_lookup(const float4 *__restrict__ g, int nx, int ny, int nz, V3 p, const Spec &lam,
+                           const Spec &illum, bool illuminant) {
+    const float psx = p.x * nx - .5f, psy = p.y * ny - .5f, psz = p.z * nz - .5f;
+    const int ix = (int)__builtin_floorf(psx), iy = (int)__builtin_floorf(psy), iz = (int)__builtin_floorf(psz);
+    const float dx = psx - (float)ix, dy = psy - (float)iy, dz = psz - (float)iz;
+    auto T = [&](int a, int b, int c) { return rgb_tap(g, nx, ny, nz, ix + a, iy + b, iz + c, lam, illum, illuminant); };
+    const Spec d00 = spec_lerp(dx, T(0, 0, 0), T(1, 0, 0));
+    const Spec d10 = spec_lerp(dx, T(0, 1, 0), T(1, 1, 0));
+    const Spec d01 = spec_lerp(dx, T(0, 0, 1), T(1, 0, 1));
+    const Spec d11 = spec_lerp(dx, T(0, 1, 1), T(1, 1, 1));
+    return spec_lerp(dz, spec_lerp(dy, d00, d10), spec_lerp(dy, d01, d11));
+}
+
 // GridMedium emission at medium point p (box-offset, media.h:299-316): LeScale lookup, then
 // the temperature grid's blackbody or the Le spectrum
 __device__ __forceinline__ Spec grid_emission(const DevMedium &m, V3 p, const Spec &lam, const Spec &Le_l) {
@@ -329,6 +377,19 @@ __device__ __forceinline__ MediumSample sample_point(const DevMedium &m, V3 p, c
         const float d = cloud_density(p, m.cloud_density, m.cloud_wispiness, m.cloud_frequency);
         ms.sigma_a = sig_a * d;
         ms.sigma_s = sig_s * d;
+        return ms;
+    }
+    if (m.type == 4) {             // RGBGridMedium::SamplePoint (media.h:377-403)
+        p = m.unit_box ? V3{p.x - m.bmin[0], p.y - m.bmin[1], p.z - m.bmin[2]} : box_offset(m.bmin, m.bmax, p);
+        const Spec none = Spec::c(0.f);
+        const Spec sa = m.rgb_a ? rgb_lookup(m.rgb_a, m.nx, m.ny, m.nz, p, lam, none, false) : Spec::c(1.f);
+        const Spec ss = m.rgb_s ? rgb_lookup(m.rgb_s, m.nx, m.ny, m.nz, p, lam, none, false) : Spec::c(1.f);
+        ms.sigma_a = sa * m.rgb_sigma_scale;
+        ms.sigma_s = ss * m.rgb_sigma_scale;
+        if (emissive && m.emissive) {
+            const Spec il = sample_table(m.illuminant, lambda_index(lam));
+            ms.Le = rgb_lookup(m.rgb_le, m.nx, m.ny, m.nz, p, lam, il, true) * m.rgb_le_scale;
+        }
         return ms;
     }
     if (m.type == 3) {             // NanoVDBMedium::SamplePoint (media.h:624-637) and Le (media.h:660-672)
@@ -1585,6 +1646,59 @@ __global__ void __launch_bounds__(256) k_majorant_vdb(vdb::Grid g, float3 bmin, 
         float r = red[0];
         for (int w = 1; w < (int)(blockDim.x / 64); ++w) r = r < red[w] ? red[w] : r;
         out[cell] = r;
+    }
+}
+
+// RGBGridMedium's 16^3 majorant (media.cpp:364-377): per cell, sigmaScale * (max over the
+// cell's voxel range of sigma_a's scale * rsp.MaxValue() (1 without a grid) + the same for
+// sigma_s), the voxel range as SampledGrid::MaxValue (containers.h:838-857).
+__global__ void __launch_bounds__(256) k_majorant_rgb(const float4 *__restrict__ ga, const float4 *__restrict__ gs,
+                                                      int nx, int ny, int nz, int rx, int ry, int rz, float sigma_scale,
+                                                      float *out) {
+    const int cell = blockIdx.x;
+    const int x = cell % rx, y = (cell / rx) % ry, z = cell / (rx * ry);
+    const float b0[3] = {float(x) / rx, float(y) / ry, float(z) / rz};
+    const float b1[3] = {float(x + 1) / rx, float(y + 1) / ry, float(z + 1) / rz};
+    const int n[3] = {nx, ny, nz};
+    int lo[3], hi[3];
+    _Pragma("unroll") for (int a = 0; a < 3; ++a) {
+        float ps0 = b0[a] * n[a] - .5f, ps1 = b1[a] * n[a] - .5f;
+        int l = (int)__builtin_floorf(ps0);
+        lo[a] = l > 0 ? l : 0;
+        int h = (int)__builtin_floorf(ps1) + 1;
+        hi[a] = h < n[a] - 1 ? h : n[a] - 1;
+    }
+    const int ex = hi[0] - lo[0] + 1, ey = hi[1] - lo[1] + 1, ez = hi[2] - lo[2] + 1;
+    const long long total = (long long)ex * ey * ez;
+    __shared__ float red[2][4];
+    for (int gi = 0; gi < 2; ++gi) {
+        const float4 *g = gi == 0 ? ga : gs;
+        if (!g) continue;
+        auto conv = [&](int vx, int vy, int vz) {
+            const float4 c = g[(vz * ny + vy) * nx + vx];
+            return c.w * rsp_max(c.x, c.y, c.z);
+        };
+        float m = conv(lo[0], lo[1], lo[2]);
+        for (long long k = threadIdx.x; k < total; k += blockDim.x) {
+            const int kx = (int)(k % ex), ky = (int)((k / ex) % ey), kz = (int)(k / ((long long)ex * ey));
+            const float v = conv(lo[0] + kx, lo[1] + ky, lo[2] + kz);
+            m = m < v ? v : m;
+        }
+        for (int off = 32; off > 0; off >>= 1) {
+            const float o = __shfl_xor(m, off);
+            m = m < o ? o : m;
+        }
+        if (lane_id() == 0) red[gi][threadIdx.x / 64] = m;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float r[2] = {1.f, 1.f};
+        for (int gi = 0; gi < 2; ++gi) {
+            if (!(gi == 0 ? ga : gs)) continue;
+            r[gi] = red[gi][0];
+            for (int w = 1; w < (int)(blockDim.x / 64); ++w) r[gi] = r[gi] < red[gi][w] ? red[gi][w] : r[gi];
+        }
+        out[cell] = sigma_scale * (r[0] + r[1]);
     }
 }
 

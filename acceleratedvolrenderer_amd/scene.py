@@ -176,6 +176,67 @@ class NanoVDBMedium:
         return np.concatenate([self.p0, self.p1]).astype(np.float32)
 
 
+class RGBGridMedium:
+    """pbrt "rgbgrid" medium (RGBGridMedium::Create, media.cpp:380-453): per-voxel RGB
+    "sigma_a" / "sigma_s" (RGBUnboundedSpectrum) and "Le" (RGBIlluminantSpectrum) arrays
+    shaped (nz, ny, nx, 3), converted with `rgb_table` (rgbspectrum.RGBToSpectrumTable of
+    the colour space, sRGB by default); or the converted {c0, c1, c2, scale} arrays
+    (nz, ny, nx, 4) directly as sigma_a_coeffs / sigma_s_coeffs / Le_coeffs. "p0"/"p1"
+    bounds, "scale" (sigmaScale), "g", "Lescale" (default 1). `illuminant`: the colour
+    space's illuminant table (default D65 = sRGB's)."""
+    type_id = 4
+    device_density = None
+    majorant_res = (16, 16, 16)
+    temperature = None
+    Le = None
+
+    def __init__(self, sigma_a=None, sigma_s=None, Le=None, p0=(0.0, 0.0, 0.0), p1=(1.0, 1.0, 1.0),
+                 world_from_medium=None, scale=1.0, g=0.0, Lescale=1.0, rgb_table=None, illuminant=None,
+                 sigma_a_coeffs=None, sigma_s_coeffs=None, Le_coeffs=None):
+        def conv(rgb, coeffs, name):
+            if coeffs is not None:
+                c = np.ascontiguousarray(np.asarray(coeffs, np.float32))
+                if c.ndim != 4 or c.shape[3] != 4:
+                    raise ValueError(f"{name}_coeffs must be (nz, ny, nx, 4)")
+                return c
+            if rgb is None:
+                return None
+            v = np.asarray(rgb, np.float32)
+            if v.ndim != 4 or v.shape[3] != 3:
+                raise ValueError(f"{name} must be (nz, ny, nx, 3) RGB")
+            if rgb_table is None:
+                raise ValueError(f"{name} given as RGB needs rgb_table (rgbspectrum.RGBToSpectrumTable)")
+            return np.ascontiguousarray(rgb_table.spectrum_coeffs(v))
+
+        self.rgb_sigma_a = conv(sigma_a, sigma_a_coeffs, "sigma_a")
+        self.rgb_sigma_s = conv(sigma_s, sigma_s_coeffs, "sigma_s")
+        self.rgb_Le = conv(Le, Le_coeffs, "Le")
+        if self.rgb_sigma_a is None and self.rgb_sigma_s is None:
+            raise ValueError('RGB grid requires "sigma_a" and/or "sigma_s" parameter values.')
+        if self.rgb_Le is not None and self.rgb_sigma_a is None:
+            raise ValueError('RGB grid requires "sigma_a" if "Le" value provided.')
+        grids = [x for x in (self.rgb_sigma_a, self.rgb_sigma_s, self.rgb_Le) if x is not None]
+        if any(x.shape != grids[0].shape for x in grids):
+            raise ValueError("sigma_a, sigma_s and Le must have the same number of samples")
+        self.nz, self.ny, self.nx = grids[0].shape[:3]
+        self.p0 = np.asarray(p0, np.float32)
+        self.p1 = np.asarray(p1, np.float32)
+        self.world_from_medium = np.eye(4) if world_from_medium is None else np.asarray(world_from_medium, np.float64)
+        self.g = np.float32(g)
+        self.sigma_scale = np.float32(scale)
+        self.Le_scale = np.float32(Lescale)
+        self.illuminant = (spectra.TABLES["D65"] if illuminant is None else spectra.as_table(illuminant, 0.0)).astype(np.float32)
+        # SampleRay's sigma_t = 1 (media.h:417) through the shared tables
+        self.sigma_a = np.ones(spectra.N, np.float32)
+        self.sigma_s = np.zeros(spectra.N, np.float32)
+        self.density = None
+        self.Lescale = np.ones((1, 1, 1), np.float32)
+
+    @property
+    def bounds(self):
+        return np.concatenate([self.p0, self.p1]).astype(np.float32)
+
+
 class DistantLight:
     """DistantLight::Create (lights.cpp:246-276). L defaults to the color space illuminant."""
     type_id = 0

@@ -150,6 +150,18 @@ int avr_medium_nanovdb(avr_context *ctx, const avr_vdb_grid *density, const avr_
                        const float render_from_medium[16], const float medium_from_render[16],
                        const float *sigma_a, const float *sigma_s, float g, float Lescale,
                        float temperature_offset, float temperature_scale);
+/* RGBGridMedium (media.h:355-427, ctor media.cpp:339-378, Create media.cpp:380-453): an
+ * nx*ny*nz grid (x fastest) on the box `bounds` whose voxels hold RGBUnboundedSpectrum
+ * sigma_a / sigma_s and RGBIlluminantSpectrum Le as 4 floats {c0, c1, c2, scale} — the
+ * RGBSigmoidPolynomial coefficients RGBColorSpace::ToRGBCoeffs gave the caller and the
+ * spectrum's scale (spectrum.cpp:236-247). sigma_a or sigma_s may be NULL (treated as 1);
+ * Le (NULL = none) needs sigma_a and the colour space's illuminant table (471, e.g. D65
+ * for sRGB). sigma_scale is "scale", Le_scale "Lescale". The 16^3 majorant
+ * sigma_scale * (max sigma_a + max sigma_s) is built on the device. */
+int avr_medium_rgbgrid(avr_context *ctx, int nx, int ny, int nz, const float bounds[6],
+                       const float render_from_medium[16], const float medium_from_render[16],
+                       const float *sigma_a, const float *sigma_s, float sigma_scale, float g, const float *Le,
+                       const float *illuminant, float Le_scale);
 /* The medium bounds the last avr_medium_* call set (medium space, min xyz then max xyz). */
 int avr_medium_bounds(avr_context *ctx, float bounds[6]);
 /* Fill d_out[first .. first+count) of an n^3 grid with CloudMedium::Density

@@ -70,6 +70,9 @@ class OracleScene(ctypes.Structure):
         ("vdb", ctypes.c_void_p),
         ("vdb_temperature", ctypes.c_void_p),
         ("vdb_lescale", ctypes.c_float),
+        ("rgb_sigma_a", c_float_p), ("rgb_sigma_s", c_float_p), ("rgb_Le", c_float_p),
+        ("rgb_illuminant", c_float_p),
+        ("rgb_sigma_scale", ctypes.c_float), ("rgb_Le_scale", ctypes.c_float),
     ]
 
 
@@ -147,6 +150,12 @@ def lib():
         L.oracle_vdb_create.argtypes = [ctypes.c_int, c_int_p, c_float_p, ctypes.c_int, c_int_p, c_int_p, c_float_p,
                                         ctypes.c_float, c_int_p, c_double_p, c_double_p]
         L.oracle_vdb_free.argtypes = [ctypes.c_void_p]
+        for name in ("oracle_rsp_eval", "oracle_rsp_max"):
+            getattr(L, name).restype = ctypes.c_float
+        L.oracle_rsp_eval.argtypes = [ctypes.c_float] * 4
+        L.oracle_rsp_max.argtypes = [ctypes.c_float] * 3
+        L.oracle_rgb_majorant.argtypes = [c_float_p, c_float_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                          ctypes.c_float, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_float_p]
         L.oracle_vdb_value.restype = ctypes.c_float
         L.oracle_vdb_value.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int]
         L.oracle_vdb_sample_world.restype = ctypes.c_float
@@ -212,6 +221,17 @@ class VdbTree:
             self.h = None
 
 
+def rgb_majorant(med):
+    """RGBGridMedium's 16^3 majorant (media.cpp:364-377) for a scene.RGBGridMedium."""
+    a = np.ascontiguousarray(med.rgb_sigma_a, np.float32) if med.rgb_sigma_a is not None else None
+    s = np.ascontiguousarray(med.rgb_sigma_s, np.float32) if med.rgb_sigma_s is not None else None
+    res = med.majorant_res
+    out = np.zeros(res[0] * res[1] * res[2], np.float32)
+    lib().oracle_rgb_majorant(fp(a) if a is not None else None, fp(s) if s is not None else None, med.nx, med.ny,
+                              med.nz, float(med.sigma_scale), res[0], res[1], res[2], fp(out))
+    return out
+
+
 def vdb_bounds(dtree, ttree=None):
     out = np.zeros(6, np.float32)
     lib().oracle_vdb_bounds(dtree.h, ttree.h if ttree is not None else None, fp(out))
@@ -234,7 +254,8 @@ class OracleRun:
         self.libm = libm
         med = scene.medium
         is_vdb = int(getattr(med, "type_id", 0)) == 3
-        if med.density is None and not is_vdb:
+        is_rgb = int(getattr(med, "type_id", 0)) == 4
+        if med.density is None and not (is_vdb or is_rgb):
             raise ValueError("oracle needs a host density grid")
         s = OracleScene()
         keep = []
@@ -244,7 +265,7 @@ class OracleRun:
             keep.append(a)
             return fp(a)
 
-        s.density = arr(med.density if not is_vdb else np.zeros((1, 1, 1), np.float32))
+        s.density = arr(med.density if med.density is not None else np.zeros((1, 1, 1), np.float32))
         s.nx, s.ny, s.nz = med.nx, med.ny, med.nz
         s.bounds[:] = [float(v) for v in med.bounds]
         s.render_from_medium[:] = [float(v) for v in scene.render_from_medium.reshape(-1)]
@@ -268,6 +289,13 @@ class OracleRun:
             s.temperature_scale = float(med.temperature_scale)
             s.temperature_offset = float(med.temperature_offset)
             self.majorant = vdb_majorant(self.vdb, self.bounds, med.majorant_res)
+        elif is_rgb:
+            opt = lambda g: arr(g.reshape(-1)) if g is not None else None
+            s.rgb_sigma_a, s.rgb_sigma_s, s.rgb_Le = opt(med.rgb_sigma_a), opt(med.rgb_sigma_s), opt(med.rgb_Le)
+            s.rgb_illuminant = arr(med.illuminant)
+            s.rgb_sigma_scale = float(med.sigma_scale)
+            s.rgb_Le_scale = float(med.Le_scale)
+            self.majorant = rgb_majorant(med)
         else:
             self.majorant = build_majorant(med.density, med.majorant_res)
         s.majorant = arr(self.majorant)

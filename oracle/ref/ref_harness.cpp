@@ -40,6 +40,35 @@
 
 using namespace pbrt;
 
+// Reads the sRGB RGBToSpectrumTable data that the reference's rgb2spec_opt wrote
+// (oracle/ref/Makefile): the 64 z nodes, then 3 x 64^3 x 3 coefficients.
+static bool ReadRgbTable(const char *path, std::vector<float> &scale, std::vector<float> &data) {
+    FILE *f = fopen(path, "rb");
+    if (!f) return false;
+    std::string text;
+    char buf[1 << 16];
+    size_t n;
+    while ((n = fread(buf, 1, sizeof(buf), f)) > 0) text.append(buf, n);
+    fclose(f);
+    auto parse = [&](const char *marker, size_t count, std::vector<float> &out) {
+        size_t pos = text.find(marker);
+        if (pos == std::string::npos) return false;
+        pos = text.find('=', pos) + 1;
+        const char *c = text.c_str() + pos;
+        while (out.size() < count && *c) {
+            if ((*c >= '0' && *c <= '9') || *c == '-' || *c == '.') {
+                char *end;
+                out.push_back(strtof(c, &end));
+                c = end;
+            } else {
+                ++c;
+            }
+        }
+        return out.size() == count;
+    };
+    return parse("ToSpectrumTable_Scale", 64, scale) && parse("ToSpectrumTable_Data", 3 * 64 * 64 * 64 * 3, data);
+}
+
 static uint32_t fb(float f) { uint32_t u; std::memcpy(&u, &f, 4); return u; }
 
 struct J {
@@ -61,9 +90,11 @@ static void arr_u64(const std::vector<uint64_t> &v) {
 int main(int argc, char **argv) {
     Allocator alloc;
     Spectra::Init(alloc);
-    const char *tablePath = nullptr;
-    for (int i = 1; i < argc; ++i)
+    const char *tablePath = nullptr, *rgbTablePath = nullptr;
+    for (int i = 1; i < argc; ++i) {
         if (!strcmp(argv[i], "--tables") && i + 1 < argc) tablePath = argv[++i];
+        if (!strcmp(argv[i], "--rgbtable") && i + 1 < argc) rgbTablePath = argv[++i];
+    }
 
     printf("{");
     J j;
@@ -448,6 +479,53 @@ int main(int argc, char **argv) {
             fwrite(t.data(), 4, t.size(), fp);
             fclose(fp);
         }
+    }
+    // ---- RGB -> spectrum (RGBGridMedium's grids) ----------------------------------
+    // RGBToSpectrumTable::operator() (color.cpp:31-68) on the table rgb2spec_opt produced,
+    // RGBSigmoidPolynomial eval / MaxValue (color.h:332-365), RGBUnboundedSpectrum and
+    // RGBIlluminantSpectrum (spectrum.h:560-631, spectrum.cpp:236-247) in sRGB.
+    std::vector<float> zNodes, coeffs;
+    if (rgbTablePath && ReadRgbTable(rgbTablePath, zNodes, coeffs)) {
+        RGBToSpectrumTable table(zNodes.data(), (const RGBToSpectrumTable::CoefficientArray *)coeffs.data());
+        Spectrum d65 = GetNamedSpectrum("stdillum-D65");
+        RGBColorSpace srgb(Point2f(.64, .33), Point2f(.3, .6), Point2f(.15, .06), d65, &table, alloc);
+        const float ls[] = {360.f, 412.5f, 500.3f, 555.f, 611.7f, 700.f, 829.6f};
+        std::vector<RGB> rgbs = {RGB(0, 0, 0), RGB(1, 1, 1), RGB(.5f, .5f, .5f), RGB(.25f, .25f, .25f),
+                                 RGB(1, 0, 0), RGB(0, 1, 0), RGB(0, 0, 1), RGB(.9f, .1f, .3f),
+                                 RGB(.2f, .7f, .4f), RGB(.05f, .02f, .9f), RGB(1e-4f, 2e-4f, 3e-4f)};
+        RNG rng(77, 5);
+        for (int i = 0; i < 40; ++i)
+            rgbs.push_back(RGB(rng.Uniform<float>(), rng.Uniform<float>(), rng.Uniform<float>()));
+        j.key("rgb_table");   // rgb in [0,1]: [r,g,b, rsp(l) x 7, MaxValue]
+        printf("[");
+        for (size_t i = 0; i < rgbs.size(); ++i) {
+            RGBSigmoidPolynomial rsp = table(rgbs[i]);
+            printf("%s[%u,%u,%u", i ? "," : "", fb(rgbs[i].r), fb(rgbs[i].g), fb(rgbs[i].b));
+            for (float l : ls) printf(",%u", fb(rsp(l)));
+            printf(",%u]", fb(rsp.MaxValue()));
+        }
+        printf("]");
+        // unbounded / illuminant: rgb scaled past 1
+        j.key("rgb_unbounded");   // [r,g,b, s(l) x 7, MaxValue]
+        printf("[");
+        for (size_t i = 0; i < rgbs.size(); ++i) {
+            RGB c = rgbs[i] * (i % 3 == 0 ? 7.5f : (i % 3 == 1 ? 0.3f : 1.f));
+            RGBUnboundedSpectrum s(srgb, c);
+            printf("%s[%u,%u,%u", i ? "," : "", fb(c.r), fb(c.g), fb(c.b));
+            for (float l : ls) printf(",%u", fb(s(l)));
+            printf(",%u]", fb(s.MaxValue()));
+        }
+        printf("]");
+        j.key("rgb_illuminant");   // [r,g,b, s(l) x 7]
+        printf("[");
+        for (size_t i = 0; i < rgbs.size(); ++i) {
+            RGB c = rgbs[i] * (i % 2 ? 3.f : 1.f);
+            RGBIlluminantSpectrum s(srgb, c);
+            printf("%s[%u,%u,%u", i ? "," : "", fb(c.r), fb(c.g), fb(c.b));
+            for (float l : ls) printf(",%u", fb(s(l)));
+            printf("]");
+        }
+        printf("]");
     }
     printf("}\n");
     return 0;

@@ -780,6 +780,11 @@ typedef struct OracleScene {
     const void *vdb;
     const void *vdb_temperature;
     float vdb_lescale;
+    // medium_type 4, RGBGridMedium (media.h:355-427): nx*ny*nz voxels of {c0, c1, c2, scale}
+    // for sigma_a / sigma_s (RGBUnboundedSpectrum) and Le (RGBIlluminantSpectrum); nullable
+    const float *rgb_sigma_a, *rgb_sigma_s, *rgb_Le;
+    const float *rgb_illuminant;      // 471, the colour space's illuminant
+    float rgb_sigma_scale, rgb_Le_scale;
 } OracleScene;
 
 }  // extern "C"
@@ -990,6 +995,69 @@ struct GaussianSampler {
     }
 };
 
+// ---------------------------------------------------------------------------
+// RGBSigmoidPolynomial (util/color.h:332-365) and the RGB*Spectrum grids of RGBGridMedium
+struct Rsp {
+    float c0, c1, c2;
+    static float S(float x) {   // color.h:356-360
+        if (std::isinf(x)) return x > 0 ? 1 : 0;
+        return .5f + x / (2 * std::sqrt(1 + Sqr(x)));
+    }
+    float operator()(float lambda) const { return S(std::fma(lambda, std::fma(lambda, c0, c1), c2)); }   // EvaluatePolynomial(lambda, c2, c1, c0)
+    float MaxValue() const {
+        float result = std::max((*this)(360), (*this)(830));
+        float lambda = -c1 / (2 * c0);
+        if (lambda >= 360 && lambda <= 830) result = std::max(result, (*this)(lambda));
+        return result;
+    }
+};
+// SampledGrid<RGBUnboundedSpectrum / RGBIlluminantSpectrum> (containers.h:785-857)
+struct RgbGrid {
+    const float *v;   // 4 per voxel: c0, c1, c2, scale
+    int nx, ny, nz;
+    const float *illuminant;   // non-null: RGBIlluminantSpectrum
+    bool Inside(int x, int y, int z) const { return x >= 0 && x < nx && y >= 0 && y < ny && z >= 0 && z < nz; }
+    Spec Convert(int x, int y, int z, const Lambda &l) const {
+        Spec s = Spec::Const(0.f);
+        if (!Inside(x, y, z)) return s;   // convert(T{}) = 0 (an illuminant spectrum without illuminant)
+        const float *c = v + 4 * ((size_t)(z * ny + y) * nx + x);
+        Rsp rsp{c[0], c[1], c[2]};
+        for (int i = 0; i < NS; ++i) s.v[i] = c[3] * rsp(l.lambda[i]);
+        if (illuminant) s = s * SampleDense(illuminant, l);
+        return s;
+    }
+    static Spec LerpS(float t, const Spec &a, const Spec &b) { return (1 - t) * a + t * b; }
+    Spec Lookup(V3 p, const Lambda &l) const {
+        float px = p.x * nx - .5f, py = p.y * ny - .5f, pz = p.z * nz - .5f;
+        int ix = (int)std::floor(px), iy = (int)std::floor(py), iz = (int)std::floor(pz);
+        float dx = px - ix, dy = py - iy, dz = pz - iz;
+        Spec d00 = LerpS(dx, Convert(ix, iy, iz, l), Convert(ix + 1, iy, iz, l));
+        Spec d10 = LerpS(dx, Convert(ix, iy + 1, iz, l), Convert(ix + 1, iy + 1, iz, l));
+        Spec d01 = LerpS(dx, Convert(ix, iy, iz + 1, l), Convert(ix + 1, iy, iz + 1, l));
+        Spec d11 = LerpS(dx, Convert(ix, iy + 1, iz + 1, l), Convert(ix + 1, iy + 1, iz + 1, l));
+        return LerpS(dz, LerpS(dy, d00, d10), LerpS(dy, d01, d11));
+    }
+    float MaxAt(int x, int y, int z) const {   // RGBUnboundedSpectrum::MaxValue
+        const float *c = v + 4 * ((size_t)(z * ny + y) * nx + x);
+        return c[3] * Rsp{c[0], c[1], c[2]}.MaxValue();
+    }
+    float MaxValue(const Bounds &b) const {   // SampledGrid::MaxValue(bounds, convert)
+        float ps0[3] = {b.pMin.x * nx - .5f, b.pMin.y * ny - .5f, b.pMin.z * nz - .5f};
+        float ps1[3] = {b.pMax.x * nx - .5f, b.pMax.y * ny - .5f, b.pMax.z * nz - .5f};
+        const int n[3] = {nx, ny, nz};
+        int lo[3], hi[3];
+        for (int a = 0; a < 3; ++a) {
+            lo[a] = std::max((int)std::floor(ps0[a]), 0);
+            hi[a] = std::min((int)std::floor(ps1[a]) + 1, n[a] - 1);
+        }
+        float m = MaxAt(lo[0], lo[1], lo[2]);
+        for (int z = lo[2]; z <= hi[2]; ++z)
+            for (int y = lo[1]; y <= hi[1]; ++y)
+                for (int x = lo[0]; x <= hi[0]; ++x) m = std::max(m, MaxAt(x, y, z));
+        return m;
+    }
+};
+
 struct SceneView {
     const OracleScene &s;
     Xform mediumX, cameraX, rasterX;
@@ -1026,6 +1094,17 @@ static inline MediumProps SamplePoint(const SceneView &sv, V3 p, const Lambda &l
         return mp;
     }
     p = XInvPoint(sv.mediumX, p);
+    if (sv.s.medium_type == 4) {   // RGBGridMedium::SamplePoint (media.h:377-403)
+        p = Offset(sv.bounds, p);
+        const OracleScene &s = sv.s;
+        Spec sa = s.rgb_sigma_a ? RgbGrid{s.rgb_sigma_a, s.nx, s.ny, s.nz, nullptr}.Lookup(p, l) : Spec::Const(1.f);
+        Spec ss = s.rgb_sigma_s ? RgbGrid{s.rgb_sigma_s, s.nx, s.ny, s.nz, nullptr}.Lookup(p, l) : Spec::Const(1.f);
+        mp.sigma_a = s.rgb_sigma_scale * sa;
+        mp.sigma_s = s.rgb_sigma_scale * ss;
+        if (s.rgb_Le && s.rgb_Le_scale > 0)
+            mp.Le = s.rgb_Le_scale * RgbGrid{s.rgb_Le, s.nx, s.ny, s.nz, s.rgb_illuminant}.Lookup(p, l);
+        return mp;
+    }
     if (sv.s.medium_type == 3) {   // NanoVDBMedium::SamplePoint (media.h:624-637)
         const VdbTree &dg = *(const VdbTree *)sv.s.vdb;
         const float d = dg.Sample(dg.WorldToIndexF(p));
@@ -1418,6 +1497,23 @@ void oracle_canon_sincos(float x, float *s, float *c) {
     *c = (float)cd;
 }
 
+
+// RGBGridMedium (test infrastructure)
+float oracle_rsp_eval(float c0, float c1, float c2, float lambda) { return Rsp{c0, c1, c2}(lambda); }
+float oracle_rsp_max(float c0, float c1, float c2) { return Rsp{c0, c1, c2}.MaxValue(); }
+// ctor's 16^3 majorant (media.cpp:364-377) over MajorantGrid::VoxelBounds
+void oracle_rgb_majorant(const float *sa, const float *ss, int nx, int ny, int nz, float sigmaScale, int rx, int ry,
+                         int rz, float *out) {
+    for (int z = 0; z < rz; ++z)
+        for (int y = 0; y < ry; ++y)
+            for (int x = 0; x < rx; ++x) {
+                Bounds b{{float(x) / rx, float(y) / ry, float(z) / rz},
+                         {float(x + 1) / rx, float(y + 1) / ry, float(z + 1) / rz}};
+                float maxSigma_t = (sa ? RgbGrid{sa, nx, ny, nz, nullptr}.MaxValue(b) : 1) +
+                                   (ss ? RgbGrid{ss, nx, ny, nz, nullptr}.MaxValue(b) : 1);
+                out[x + rx * (y + ry * z)] = sigmaScale * maxSigma_t;
+            }
+}
 
 // NanoVDB grids (test infrastructure handles; see VdbTree)
 void *oracle_vdb_create(int nLeaves, const int *leafOrigin, const float *leafValues, int nTiles, const int *tileOrigin,
