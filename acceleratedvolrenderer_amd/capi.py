@@ -100,6 +100,9 @@ SIGNATURES = {
     "avr_lights": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, c_int_p, c_float_p, c_float_p, c_float_p,
                                   ctypes.c_float]),
     "avr_camera": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, c_float_p, c_float_p]),
+    "avr_film_image_device": (ctypes.c_int, [ctypes.c_void_p, c_float_p, ctypes.c_int, ctypes.c_void_p]),
+    "avr_film_set_reference": (ctypes.c_int, [ctypes.c_void_p, c_float_p, c_float_p, ctypes.c_int]),
+    "avr_film_metric": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, c_float_p]),
     "avr_last_pass_weights": (ctypes.c_int, [ctypes.c_void_p, c_float_p, ctypes.c_longlong]),
     "avr_transmittance": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_longlong, c_float_p, c_float_p, c_float_p,
                                          c_float_p]),
@@ -327,6 +330,24 @@ class Context:
 
     def film_export_device(self, d_dst_ptr):
         _check(self.lib.avr_film_export_device(self.h, ctypes.c_void_p(d_dst_ptr)))
+
+    METRICS = {"MSE": 0, "MAE": 1, "MRSE": 2, "ME": 3}
+
+    def film_image_device(self, d_out_ptr, output_from_sensor, fp16=True):
+        m = np.ascontiguousarray(output_from_sensor, np.float32).reshape(9)
+        _check(self.lib.avr_film_image_device(self.h, _fp(m), 1 if fp16 else 0, ctypes.c_void_p(d_out_ptr)))
+
+    def film_set_reference(self, reference_rgb, output_from_sensor, fp16=True):
+        ref = np.ascontiguousarray(reference_rgb, np.float32)
+        m = np.ascontiguousarray(output_from_sensor, np.float32).reshape(9)
+        _check(self.lib.avr_film_set_reference(self.h, _fp(ref), _fp(m), 1 if fp16 else 0))
+
+    def film_metric(self, metric="MSE"):
+        """Per-channel metric of the film's image against the reference (ME: (3, 3) rows
+        absolute / positive / negative)."""
+        out = np.zeros(9, np.float32)
+        _check(self.lib.avr_film_metric(self.h, self.METRICS[metric], _fp(out)))
+        return out.reshape(3, 3) if metric == "ME" else out[:3].copy()
 
     def film_device_ptrs(self):
         a, b = ctypes.c_void_p(), ctypes.c_void_p()

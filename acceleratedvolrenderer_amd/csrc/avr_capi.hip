@@ -91,6 +91,11 @@ struct avr_context {
     // RGBGridMedium grids (sigma_a, sigma_s, Le as float4 {c0, c1, c2, scale}) and illuminant
     float4 *d_rgb[3] = {nullptr, nullptr, nullptr};
     float *d_illum = nullptr;
+    // film image / --mse-reference-image state
+    float *d_image = nullptr, *d_reference = nullptr;
+    double *d_metric = nullptr;      // kMetricBlocks * kMetricSlots partials + kMetricSlots totals
+    avr::Mat3 ref_out_from_sensor{};
+    int ref_fp16 = 1;
     avr::smp::FilterTables ftab{};
     int refill_min = 32;
     int dda_budget = 12;
@@ -458,6 +463,9 @@ int avr_context_destroy(avr_context *c) {
     if (c->d_temperature) (void)hipFree(c->d_temperature);
     free_vdb(c);
     free_rgb(c);
+    if (c->d_image) (void)hipFree(c->d_image);
+    if (c->d_reference) (void)hipFree(c->d_reference);
+    if (c->d_metric) (void)hipFree(c->d_metric);
     if (c->d_fat) (void)hipFree(c->d_fat);
     if (c->d_stats) (void)hipFree(c->d_stats);
     if (c->h_count) (void)hipHostFree(c->h_count);
@@ -1013,6 +1021,66 @@ int avr_reset_stats(avr_context *c) {
     c->stats = {};
     HIP_TRY(hipMemsetAsync(c->d_stats, 0, sizeof(unsigned long long) * avr::kNumStats, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
+    return AVR_OK;
+}
+
+static constexpr int kMetricBlocks = 1024;
+
+static int film_image(avr_context *c, const avr::Mat3 &M, int fp16, float *d_out) {
+    const long long np = (long long)c->film.width * c->film.height;
+    hipLaunchKernelGGL(avr::k_film_image, dim3(blocks_for(np, 256, 4096)), dim3(256), 0, c->stream, c->film, M,
+                       fp16, d_out);
+    HIP_TRY(hipGetLastError());
+    return AVR_OK;
+}
+
+int avr_film_image_device(avr_context *c, const float out_from_sensor[9], int fp16, float *d_out) {
+    if (!c || !c->has_film || !out_from_sensor || !d_out) return fail(AVR_ERR_STATE, "no film or null argument");
+    HIP_TRY(hipSetDevice(c->device));
+    avr::Mat3 M;
+    for (int i = 0; i < 9; ++i) M.m[i] = out_from_sensor[i];
+    return film_image(c, M, fp16 ? 1 : 0, d_out);
+}
+
+int avr_film_set_reference(avr_context *c, const float *reference_rgb, const float out_from_sensor[9], int fp16) {
+    if (!c || !c->has_film || !reference_rgb || !out_from_sensor) return fail(AVR_ERR_STATE, "no film or null argument");
+    HIP_TRY(hipSetDevice(c->device));
+    const size_t np = (size_t)c->film.width * c->film.height;
+    if (c->d_reference) (void)hipFree(c->d_reference);
+    if (c->d_image) (void)hipFree(c->d_image);
+    c->d_reference = nullptr;
+    c->d_image = nullptr;
+    HIP_TRY(dalloc(&c->d_reference, 3 * np));
+    HIP_TRY(dalloc(&c->d_image, 3 * np));
+    if (!c->d_metric) HIP_TRY(dalloc(&c->d_metric, (size_t)(kMetricBlocks + 1) * avr::kMetricSlots));
+    HIP_TRY(hipMemcpyAsync(c->d_reference, reference_rgb, 3 * np * sizeof(float), hipMemcpyHostToDevice, c->stream));
+    for (int i = 0; i < 9; ++i) c->ref_out_from_sensor.m[i] = out_from_sensor[i];
+    c->ref_fp16 = fp16 ? 1 : 0;
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return AVR_OK;
+}
+
+int avr_film_metric(avr_context *c, int metric, float *out) {
+    if (!c || !c->has_film || !out) return fail(AVR_ERR_STATE, "no film");
+    if (!c->d_reference) return fail(AVR_ERR_STATE, "no reference image (avr_film_set_reference)");
+    if (metric < 0 || metric > 3) return fail(AVR_ERR_ARG, "metric must be 0 MSE, 1 MAE, 2 MRSE, 3 ME");
+    HIP_TRY(hipSetDevice(c->device));
+    int rc;
+    if ((rc = film_image(c, c->ref_out_from_sensor, c->ref_fp16, c->d_image))) return rc;
+    const int np = c->film.width * c->film.height;
+    double *tot = c->d_metric + (size_t)kMetricBlocks * avr::kMetricSlots;
+    hipLaunchKernelGGL(avr::k_metric, dim3(kMetricBlocks), dim3(256), 0, c->stream, c->d_image, c->d_reference, np,
+                       metric, c->d_metric);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(avr::k_metric_final, dim3(1), dim3(64), 0, c->stream, c->d_metric, kMetricBlocks, tot);
+    HIP_TRY(hipGetLastError());
+    double h[avr::kMetricSlots];
+    HIP_TRY(hipMemcpyAsync(h, tot, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    // / (Float(xres) * Float(yres)); ME rounds its sums to float first (image.cpp:573-577)
+    const float npix = (float)c->film.width * (float)c->film.height;
+    const int n = metric == 3 ? 9 : 3;
+    for (int k = 0; k < n; ++k) out[k] = metric == 3 ? (float)h[k] / npix : (float)(h[k] / npix);
     return AVR_OK;
 }
 

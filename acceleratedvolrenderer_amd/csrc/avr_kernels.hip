@@ -1702,6 +1702,80 @@ __global__ void __launch_bounds__(256) k_majorant_rgb(const float4 *__restrict__
     }
 }
 
+// RGBFilm::GetImage on the device (film.cpp:533-565): GetPixelRGB (film.h:258-274; rgbSum and
+// weightSum rounded to float, divided, outputRGBFromSensorRGB applied as Mul's
+// ((0 + m0 r) + m1 g) + m2 b; no splats) and, for the fp16 image, the 65504 clamp and the
+// round-to-nearest-even half conversion.
+struct Mat3 { float m[9]; };
+__global__ void __launch_bounds__(256) k_film_image(DevFilm F, Mat3 M, int fp16, float *__restrict__ out) {
+    const int np = F.width * F.height;
+    for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < np; p += gridDim.x * blockDim.x) {
+        float r = (float)F.rgb_sum[3 * p], g = (float)F.rgb_sum[3 * p + 1], b = (float)F.rgb_sum[3 * p + 2];
+        const float w = (float)F.w_sum[p];
+        if (w != 0) { r /= w; g /= w; b /= w; }
+        float o[3];
+        for (int i = 0; i < 3; ++i) o[i] = (M.m[3 * i] * r + M.m[3 * i + 1] * g) + M.m[3 * i + 2] * b;
+        if (fp16) {
+            const float mx = fmaxf_(o[0], fmaxf_(o[1], o[2]));
+            for (int i = 0; i < 3; ++i) {
+                if (mx > 65504.f && o[i] > 65504.f) o[i] = 65504.f;
+                o[i] = (float)(_Float16)o[i];   // IEEE round-to-nearest-even
+            }
+        }
+        out[3 * p] = o[0];
+        out[3 * p + 1] = o[1];
+        out[3 * p + 2] = o[2];
+    }
+}
+
+// Image::ME / MAE / MSE / MRSE terms (util/image.cpp:543-678) summed in f64: per thread over a
+// grid-strided pixel range, then a fixed-order tree per block (deterministic for a fixed
+// grid); k_metric_final adds the block partials in order. Slots per channel c: [c] for
+// MAE/MSE/MRSE; ME: [c] absolute, [3 + c] positive, [6 + c] negative. Infinite terms skipped.
+constexpr int kMetricSlots = 9;
+__global__ void __launch_bounds__(256) k_metric(const float *__restrict__ img, const float *__restrict__ ref, int np,
+                                                int metric, double *__restrict__ partial) {
+    double acc[kMetricSlots];
+    for (int k = 0; k < kMetricSlots; ++k) acc[k] = 0;
+    for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < np; p += gridDim.x * blockDim.x) {
+        for (int c = 0; c < 3; ++c) {
+            const double v = img[3 * p + c], vr = ref[3 * p + c];
+            const double d = v - vr;
+            double t;
+            if (metric == 0) t = d * d;
+            else if (metric == 1) t = d < 0 ? -d : d;
+            else if (metric == 2) { const double q = vr + 0.01; t = (d * d) / (q * q); }
+            else t = d;
+            if (__builtin_isinf(t)) continue;
+            if (metric == 3) {
+                acc[c] += d < 0 ? -d : d;
+                if (d > 0) acc[3 + c] += d;
+                else acc[6 + c] += d;
+            } else {
+                acc[c] += t;
+            }
+        }
+    }
+    __shared__ double red[256];
+    for (int k = 0; k < kMetricSlots; ++k) {
+        red[threadIdx.x] = acc[k];
+        __syncthreads();
+        for (int s = blockDim.x / 2; s > 0; s >>= 1) {
+            if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) partial[blockIdx.x * kMetricSlots + k] = red[0];
+        __syncthreads();
+    }
+}
+__global__ void k_metric_final(const double *__restrict__ partial, int nblocks, double *__restrict__ out) {
+    const int k = threadIdx.x;
+    if (k >= kMetricSlots) return;
+    double s = 0;
+    for (int b = 0; b < nblocks; ++b) s += partial[b * kMetricSlots + k];
+    out[k] = s;
+}
+
 __global__ void __launch_bounds__(256) k_cloud(float *out, int n, long long first, long long count, float density,
                                                float wispiness, float frequency) {
     for (long long k = blockIdx.x * (long long)blockDim.x + threadIdx.x; k < count; k += (long long)gridDim.x * blockDim.x) {

@@ -12,9 +12,12 @@ split across ranks (rank k renders sample indices [k*spp/N, (k+1)*spp/N) of ever
 samplers.h:457-460 indexes by (pixel, sampleIndex), so the union equals the 1-GPU run
 up to fp64 summation order), and the fp64 film sums are reduced once with a SUM.
 """
+import time
+
 import numpy as np
 
-from . import capi
+from . import capi, imageio
+from .imgtool import channel_average
 from .scene import film_rgb
 
 INTEGRATOR_NAMES = ("volpath", "volpathcustom", "volpath_mi355x")
@@ -82,6 +85,62 @@ class VolPathIntegrator:
 
     def stats(self):
         return self.ctx.stats()
+
+    def get_image(self, rgb_sum=None, w_sum=None, fp16=True):
+        """RGBFilm::GetImage (film.cpp:533-565): GetPixelRGB per pixel, and for the fp16
+        image ("savefp16", default true) the 65504 clamp and the half rounding."""
+        img = self.image(rgb_sum, w_sum)
+        if fp16:
+            img = np.minimum(img, np.float32(65504)).astype(np.float16).astype(np.float32)
+        return img
+
+    def write_image(self, path, rgb_sum=None, w_sum=None, spp=None, render_time=None, mse=None, fp16=True):
+        """RGBFilm::WriteImage -> Image::Write: EXR (pbrt's attributes, ZIP) or PFM by extension."""
+        img = self.get_image(rgb_sum, w_sum, fp16)
+        if str(path).lower().endswith(".pfm"):
+            imageio.write_pfm(path, img)
+        else:
+            imageio.write_exr(path, img, half=fp16, samples_per_pixel=spp if spp is not None else self.spp,
+                              render_time_seconds=render_time, mse=mse)
+        return img
+
+    def render_waves(self, mse_reference=None, mse_out=None, metric="MSE"):
+        """ImageTileIntegrator::Render's wave loop (integrators.cpp:166-232): waves of
+        1, 1, 2, 4, ... 64 sample indices; with an MSE reference image every wave is one
+        sample and after each the film's (fp16) image is compared with the reference on the
+        device, written as pbrt's "spp, mse" lines (integrators.cpp:209-219) to `mse_out`.
+        Returns (rgb_sum, w_sum, [(spp, error), ...])."""
+        f = self.scene.film
+        if mse_reference is not None:
+            ref = np.asarray(mse_reference, np.float32)
+            if ref.shape != (f.height, f.width, 3):
+                raise ValueError(f"reference image must be {(f.height, f.width, 3)}")
+            self.ctx.film_set_reference(ref, f.output_from_sensor, fp16=True)
+        self.ctx.film_clear()
+        log = []
+        wave_start, wave_end, next_wave = 0, 1, 1
+        out = open(mse_out, "w") if mse_out else None
+        t0 = time.time()
+        try:
+            while wave_start < self.spp:
+                self.ctx.render(wave_start, wave_end, self.seed, self.maxdepth)
+                wave_start = wave_end
+                wave_end = min(self.spp, wave_end + next_wave)
+                if mse_reference is None:
+                    next_wave = min(2 * next_wave, 64)
+                else:
+                    v = self.ctx.film_metric(metric)
+                    err = float(channel_average(v[0] if metric == "ME" else v))
+                    log.append((wave_start, err))
+                    if out:
+                        out.write(f"{wave_start}, {err:.9g}\n")
+                        out.flush()
+        finally:
+            if out:
+                out.close()
+        self.last_render_seconds = time.time() - t0
+        rgb, w = self.film_sums()
+        return rgb, w, log
 
     def render_distributed(self, rank, world_size, group=None):
         """Render this rank's sample shard and SUM-reduce the fp64 film to rank 0 (RCCL).

@@ -223,6 +223,19 @@ int avr_film_device_ptrs(avr_context *ctx, void **d_rgb_sum, void **d_w_sum);
  * [rgb_sum (W*H*3) | w_sum (W*H)] as doubles — the buffer handed to the RCCL reduce. */
 int avr_film_export_device(avr_context *ctx, void *d_dst);
 
+/* RGBFilm::GetImage on the device (film.cpp:533-565): per pixel GetPixelRGB (film.h:258-274)
+ * with the caller's outputRGBFromSensorRGB (row-major 3x3), optionally as the fp16 image
+ * ("savefp16": clamp to 65504, round to half). d_out: W*H*3 floats on this GPU. */
+int avr_film_image_device(avr_context *ctx, const float output_from_sensor[9], int fp16, float *d_out);
+/* --mse-reference-image (integrators.cpp:119-148, 209-219): keep a W*H*3 reference image
+ * (host, row-major RGB) on the device; avr_film_metric then compares the film's GetImage
+ * with it: metric 0 MSE, 1 MAE, 2 MRSE -> 3 per-channel values; 3 ME -> 9 values
+ * (absolute, positive, negative per channel) with Image::MSE/MAE/MRSE/ME's definitions
+ * (util/image.cpp:543-678), f64 sums by a fixed-order device reduction. */
+int avr_film_set_reference(avr_context *ctx, const float *reference_rgb, const float output_from_sensor[9],
+                           int fp16);
+int avr_film_metric(avr_context *ctx, int metric, float *out);
+
 /* Per-sample radiance of the LAST wavefront pass of the last avr_render (replay checks;
  * pbrt's --debugstart analogue, integrators.cpp:74-102). Element id = s*W*H + pixel,
  * s = sampleIndex - first sample of that pass. Writes n_max*4 floats into each of

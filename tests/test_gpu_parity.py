@@ -537,3 +537,43 @@ def test_rgbgrid_medium_replay(case):
     assert frac >= 0.999
     assert err <= 0.5 * noise
     integ.close()
+
+
+def test_film_image_metric_and_mse_waves(tmp_path):
+    """RGBFilm::GetImage on the device equals the host restatement bit for bit (fp16 and
+    fp32); the device MSE/MAE/MRSE/ME against a reference equal imgtool's pbrt-order f64 sums
+    (to f64 reduction order); the --mse-reference-image wave loop logs one line per sample
+    and ends on the same film as one render; the EXR written reads back as GetImage."""
+    from acceleratedvolrenderer_amd import scenes, imgtool, imageio
+    n, W, H, spp = 12, 40, 28, 8
+    dens = (0.3 + np.random.default_rng(8).random((n, n, n), dtype=np.float32)).astype(np.float32)
+    scene = scenes.s_uniform(n=n, width=W, height=H, variant="emissive_chromatic", density=dens)
+    integ = _integrator(scene, maxdepth=6, spp=spp)
+    rgb, w = integ.render()
+    f = scene.film
+    for fp16 in (True, False):
+        buf = torch.empty(W * H * 3, dtype=torch.float32, device="cuda:0")
+        integ.ctx.film_image_device(buf.data_ptr(), f.output_from_sensor, fp16=fp16)
+        torch.cuda.synchronize()
+        dev = buf.cpu().numpy().reshape(H, W, 3)
+        host = integ.get_image(rgb, w, fp16=fp16)
+        assert dev.view(np.uint32).tolist() == host.view(np.uint32).tolist()
+    ref = (integ.get_image(rgb, w) * np.float32(1.1) + np.float32(0.01)).astype(np.float32)
+    integ.ctx.film_set_reference(ref, f.output_from_sensor, fp16=True)
+    img = integ.get_image(rgb, w)
+    for m in ("MSE", "MAE", "MRSE"):
+        got = integ.ctx.film_metric(m)
+        want = imgtool.metric(img, ref, m)
+        assert np.allclose(got, want, rtol=1e-6, atol=0), (m, got, want)
+    me = integ.ctx.film_metric("ME")
+    assert np.allclose(me, np.stack(imgtool.metric(img, ref, "ME")), rtol=1e-6, atol=0)
+    rgb2, w2, log = integ.render_waves(mse_reference=ref, mse_out=str(tmp_path / "mse.txt"))
+    assert [s for s, _ in log] == list(range(1, spp + 1))
+    assert np.array_equal(rgb2, rgb) and np.array_equal(w2, w)
+    lines = open(tmp_path / "mse.txt").read().splitlines()
+    assert len(lines) == spp and lines[-1].startswith(f"{spp}, ")
+    assert abs(float(lines[-1].split(",")[1]) - float(imgtool.channel_average(imgtool.metric(img, ref, "MSE")))) \
+        <= 1e-6 * abs(float(lines[-1].split(",")[1]))
+    integ.write_image(str(tmp_path / "a.exr"), rgb, w, spp=spp)
+    assert np.array_equal(imageio.read_rgb(str(tmp_path / "a.exr")), img)
+    integ.close()
