@@ -35,6 +35,7 @@ class AvrStats(ctypes.Structure):
         ("ms_shadow", ctypes.c_double),
         ("ms_film", ctypes.c_double),
         ("ms_total", ctypes.c_double),
+        ("ms_setup", ctypes.c_double),
     ]
 
     def as_dict(self):
@@ -122,6 +123,7 @@ SIGNATURES = {
                                           c_float_p, c_float_p, ctypes.c_float]),
     "avr_set_filter": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, c_float_p, ctypes.c_float]),
     "avr_set_sampler": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]),
+    "avr_set_sampler_table": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "avr_film": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, c_float_p, c_float_p, ctypes.c_float,
                                 ctypes.c_float]),
     "avr_film_clear": (ctypes.c_int, [ctypes.c_void_p]),
@@ -202,6 +204,10 @@ class Context:
 
     def set_refill_min(self, lanes):
         _check(self.lib.avr_set_refill_min(self.h, int(lanes)))
+
+    def set_sampler_table(self, dims):
+        """ZSobol pixel-table dimensions (0 = compute every digit per call)."""
+        _check(self.lib.avr_set_sampler_table(self.h, int(dims)))
 
     def set_stream(self, stream_ptr):
         _check(self.lib.avr_set_stream(self.h, ctypes.c_void_p(stream_ptr)))

@@ -97,6 +97,11 @@ struct avr_context {
     avr::Mat3 ref_out_from_sensor{};
     int ref_fp16 = 1;
     avr::smp::FilterTables ftab{};
+    // ZSobol pixel table (zsobol_upper per Morton(pixel) x dimension < zs_dims), rebuilt
+    // when the sampler's spp or the film resolution change; zs_dims 0 = no table
+    uint32_t *d_zs_table = nullptr;
+    int zs_dims = 256;
+    int zs_key[3] = {-1, -1, -1};
     int refill_min = 32;
     int dda_budget = 12;
     int grid_layout = 1;
@@ -463,6 +468,7 @@ int avr_context_destroy(avr_context *c) {
     if (c->d_temperature) (void)hipFree(c->d_temperature);
     free_vdb(c);
     free_rgb(c);
+    if (c->d_zs_table) (void)hipFree(c->d_zs_table);
     if (c->d_image) (void)hipFree(c->d_image);
     if (c->d_reference) (void)hipFree(c->d_reference);
     if (c->d_metric) (void)hipFree(c->d_metric);
@@ -765,6 +771,13 @@ int avr_set_filter(avr_context *c, int type, const float radius[2], float sigma)
     return AVR_OK;
 }
 
+int avr_set_sampler_table(avr_context *c, int dims) {
+    if (!c || dims < 0 || dims > 4096) return fail(AVR_ERR_ARG, "sampler table dimensions must be 0..4096");
+    c->zs_dims = dims;
+    c->zs_key[0] = -1;   // rebuild (or drop) at the next render
+    return AVR_OK;
+}
+
 int avr_set_sampler(avr_context *c, int kind, int samples_per_pixel) {
     if (!c || (kind != 0 && kind != 1) || samples_per_pixel < 1)
         return fail(AVR_ERR_ARG, "sampler: kind 0 (independent) or 1 (zsobol), samples_per_pixel >= 1");
@@ -843,6 +856,36 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
         if (zs.nBase4Digits > 16) return fail(AVR_ERR_ARG, "zsobol: resolution x spp beyond 2^32 sample indices");
     }
     HIP_TRY(hipSetDevice(c->device));
+    if (c->sampler_kind == 1) {
+        // The digits of GetSampleIndex above log2(spp) depend on (pixel, dimension) only:
+        // tabulate them once per film/sampler (k_zsobol_table), so each sampler call computes
+        // the log2(spp)/2 sample digits plus one load instead of all nBase4Digits
+        const int key[3] = {c->sampler_spp, c->film.width, c->film.height};
+        if (c->zs_key[0] != key[0] || c->zs_key[1] != key[1] || c->zs_key[2] != key[2]) {
+            if (c->d_zs_table) (void)hipFree(c->d_zs_table);
+            c->d_zs_table = nullptr;
+            for (int k = 0; k < 3; ++k) c->zs_key[k] = key[k];
+            if (c->zs_dims > 0) {
+                const size_t rows =
+                    (size_t)avr::smp::encode_morton2((uint32_t)c->film.width - 1, (uint32_t)c->film.height - 1) + 1;
+                if (hipMalloc((void **)&c->d_zs_table, rows * c->zs_dims * sizeof(uint32_t)) != hipSuccess) {
+                    (void)hipGetLastError();
+                    c->d_zs_table = nullptr;   // no room: every call computes all digits
+                } else {
+                    EV_MARK(t0);
+                    hipLaunchKernelGGL(avr::k_zsobol_table, dim3(blocks_for((long long)c->film.width * c->film.height *
+                                                                            c->zs_dims, 256, 256 * 64)),
+                                       dim3(256), 0, c->stream, zs, c->film.width, c->film.height, c->zs_dims,
+                                       c->d_zs_table);
+                    HIP_TRY(hipGetLastError());
+                    EV_MARK(t1);
+                    c->timed.push_back({t0, t1, &avr_stats::ms_setup, false});
+                }
+            }
+        }
+        zs.upper = c->d_zs_table;
+        zs.dmax = c->d_zs_table ? c->zs_dims : 0;
+    }
     const long long P = (long long)c->film.width * c->film.height;
     if (P > (1ll << 30)) return fail(AVR_ERR_ARG, "film too large");
     const long long Smax = std::max<long long>(1, c->max_paths / P);

@@ -1702,6 +1702,19 @@ __global__ void __launch_bounds__(256) k_majorant_rgb(const float4 *__restrict__
     }
 }
 
+// ZSobol pixel table: zsobol_upper for every pixel of the film and the first dmax
+// dimensions, row Morton(pixel) (zp.upper must be null here: the digits are computed).
+__global__ void __launch_bounds__(256) k_zsobol_table(smp::ZSobolParams zp, int width, int height, int dmax,
+                                                      uint32_t *__restrict__ table) {
+    const long long n = (long long)width * height * dmax;
+    for (long long k = blockIdx.x * (long long)blockDim.x + threadIdx.x; k < n; k += (long long)gridDim.x * blockDim.x) {
+        const int d = (int)(k % dmax);
+        const long long pix = k / dmax;
+        const uint32_t pm = (uint32_t)smp::encode_morton2((uint32_t)(pix % width), (uint32_t)(pix / width));
+        table[(size_t)pm * dmax + d] = smp::zsobol_upper(pm << zp.log2spp, (uint32_t)d, zp);
+    }
+}
+
 // RGBFilm::GetImage on the device (film.cpp:533-565): GetPixelRGB (film.h:258-274; rgbSum and
 // weightSum rounded to float, divided, outputRGBFromSensorRGB applied as Mul's
 // ((0 + m0 r) + m1 g) + m2 b; no splats) and, for the fp16 image, the 65504 clamp and the

@@ -101,6 +101,10 @@ constexpr uint64_t kZPermW2 = 0x93634b1b87271e4eull;   // {2,3,0,1} .. {3,0,1,2}
 
 struct ZSobolParams {
     int log2spp, nBase4Digits, seed;
+    // Optional table of the pixel-only part of GetSampleIndex (zsobol_upper) for the first
+    // `dmax` dimensions, row (Morton(pixel) * dmax + dimension); null = computed per call
+    const uint32_t *upper;
+    int dmax;
 };
 
 // MixBits(x) >> 24 for x < 2^32 (a 40-bit value), as (hi 8 bits, lo 32 bits)
@@ -114,16 +118,15 @@ AVR_HD void mix_hi40(uint32_t x, uint32_t *hi, uint32_t *lo) {
     *lo = (uint32_t)(v >> 24);
 }
 
-// ZSobolSampler::GetSampleIndex (samplers.h:296-355) for the current dimension. The host
-// guarantees Morton(pixel) << log2(spp) | index < 2^32 (nBase4Digits <= 16), so the Morton
-// index, every digit prefix and the result fit in 32 bits (the reference's uint64_t values
-// have zero upper halves).
-AVR_HD uint32_t zsobol_index(uint32_t morton, uint32_t dimension, const ZSobolParams &zp) {
+// ZSobolSampler::GetSampleIndex (samplers.h:296-355), digits i in [iLo, iHi] (most
+// significant first) of the current dimension. The host guarantees Morton(pixel) <<
+// log2(spp) | index < 2^32 (nBase4Digits <= 16), so the Morton index, every digit prefix and
+// the result fit in 32 bits (the reference's uint64_t values have zero upper halves).
+AVR_HD uint32_t zsobol_digits(uint32_t morton, uint32_t dimension, const ZSobolParams &zp, int iHi, int iLo) {
     uint32_t sampleIndex = 0;
     const bool pow2 = zp.log2spp & 1;
-    const int lastDigit = pow2 ? 1 : 0;
     const uint32_t dmix = 0x55555555u * dimension;
-    for (int i = zp.nBase4Digits - 1; i >= lastDigit; --i) {
+    for (int i = iHi; i >= iLo; --i) {
         const int shift = 2 * i - (pow2 ? 1 : 0);
         const uint32_t digit = (morton >> shift) & 3u;
         const uint32_t higher = shift + 2 >= 32 ? 0u : morton >> (shift + 2);
@@ -135,7 +138,24 @@ AVR_HD uint32_t zsobol_index(uint32_t morton, uint32_t dimension, const ZSobolPa
         const uint32_t nd = (uint32_t)(w >> ((p & 7) * 8 + 2 * digit)) & 3u;
         sampleIndex |= nd << shift;
     }
+    return sampleIndex;
+}
+
+// First digit whose bits (and all higher bits) lie in Morton(pixel): shift = 2i - pow2 >= log2spp.
+AVR_HD int zsobol_split(const ZSobolParams &zp) { return (zp.log2spp + (zp.log2spp & 1)) / 2; }
+
+// The digits that depend on the pixel only (not on the sample index): a function of
+// (Morton(pixel), dimension), shared by every sample of the pixel.
+AVR_HD uint32_t zsobol_upper(uint32_t morton, uint32_t dimension, const ZSobolParams &zp) {
+    return zsobol_digits(morton, dimension, zp, zp.nBase4Digits - 1, zsobol_split(zp));
+}
+
+// The remaining digits and the final base-2 digit of an odd log2(spp)
+AVR_HD uint32_t zsobol_lower(uint32_t morton, uint32_t dimension, const ZSobolParams &zp) {
+    const bool pow2 = zp.log2spp & 1;
+    uint32_t sampleIndex = zsobol_digits(morton, dimension, zp, zsobol_split(zp) - 1, pow2 ? 1 : 0);
     if (pow2) {
+        const uint32_t dmix = 0x55555555u * dimension;
         const uint32_t digit = morton & 1u;
         const uint32_t x = (morton >> 1) ^ dmix;
         uint64_t v = (uint64_t)(x ^ (x >> 31));
@@ -146,6 +166,15 @@ AVR_HD uint32_t zsobol_index(uint32_t morton, uint32_t dimension, const ZSobolPa
         sampleIndex |= digit ^ (uint32_t)(v & 1);
     }
     return sampleIndex;
+}
+
+AVR_HD uint32_t zsobol_index(uint32_t morton, uint32_t dimension, const ZSobolParams &zp) {
+    uint32_t up;
+    if (zp.upper && (int)dimension < zp.dmax)
+        up = zp.upper[(size_t)(morton >> zp.log2spp) * (size_t)zp.dmax + dimension];
+    else
+        up = zsobol_upper(morton, dimension, zp);
+    return up | zsobol_lower(morton, dimension, zp);
 }
 
 // ZSobolSampler state of one pixel sample
@@ -183,6 +212,8 @@ inline ZSobolParams zsobol_params(int spp, int width, int height, int seed) {
     const int res = (int)round_up_pow2((uint32_t)(width > height ? width : height));
     zp.nBase4Digits = ilog2((uint32_t)res) + (zp.log2spp + 1) / 2;
     zp.seed = seed;
+    zp.upper = nullptr;
+    zp.dmax = 0;
     return zp;
 }
 

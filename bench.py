@@ -46,6 +46,8 @@ def parse():
     p.add_argument("--refill-min", type=int, default=0, help="k_paths refill threshold (0 = library default)")
     p.add_argument("--grid-layout", default="fat", choices=["fat", "linear"])
     p.add_argument("--dda-budget", type=int, default=0, help="k_paths DDA cells per iteration (0 = default)")
+    p.add_argument("--zsobol-table", type=int, default=256,
+                   help="ZSobol pixel-table dimensions (0 = every digit per sampler call)")
     p.add_argument("--sampler", default="zsobol", choices=["zsobol", "independent"],
                    help="pixel sampler (BASELINE.md S-cloud: zsobol, pbrt's default)")
     p.add_argument("--filter", default="gaussian", choices=["gaussian", "box"],
@@ -130,6 +132,7 @@ def main():
         integ.ctx.set_refill_min(args.refill_min)
     if args.dda_budget:
         integ.ctx.set_dda_budget(args.dda_budget)
+    integ.ctx.set_sampler_table(args.zsobol_table)
 
     def step(k):
         # asynchronous on the context stream: steps queue back to back
@@ -139,6 +142,8 @@ def main():
     for k in range(args.warmup):
         step(k)
     integ.ctx.film_clear()
+    # one-off device tables (ZSobol pixel table) are built by the first (warmup) render
+    setup_ms = integ.ctx.stats()["ms_setup"]
     integ.ctx.reset_stats()   # waits for the warmup; counters and kernel times restart
     torch.cuda.synchronize()
     if world > 1:
@@ -238,6 +243,7 @@ def main():
             "cpu_baseline": cpu,
             "detail": {
                 "grid_gen_s": round(tgen, 3),
+                "setup_ms": round(setup_ms, 3), "zsobol_table_dims": args.zsobol_table,
                 "ms_camera": agg["ms_camera"], "ms_medium": agg["ms_medium"], "ms_shadow": agg["ms_shadow"],
                 "ms_film": agg["ms_film"], "medium_lookups": agg["medium_lookups"],
                 "shadow_lookups": agg["shadow_lookups"], "medium_items_in": agg["medium_items_in"],

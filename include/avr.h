@@ -49,6 +49,7 @@ typedef struct avr_stats {
     unsigned long long active_lane_iterations; /* k_paths: sum of busy lanes per iteration */
     double ms_camera, ms_medium, ms_shadow, ms_film; /* summed hipEvent times      */
     double ms_total;                                  /* first launch .. film done  */
+    double ms_setup;   /* one-off device tables built by avr_render (ZSobol pixel table) */
 } avr_stats;
 
 /* Last error message of the calling thread ("" if none). */
@@ -199,6 +200,11 @@ int avr_set_filter(avr_context *ctx, int type, const float radius[2], float sigm
  * scene.cpp:93). samples_per_pixel is the sampler's pixelsamples: ZSobol lays out
  * (Morton(pixel) << log2(spp)) | sampleIndex, so avr_render must stay below it. */
 int avr_set_sampler(avr_context *ctx, int kind, int samples_per_pixel);
+/* ZSobolSampler: GetSampleIndex's digits above log2(spp) depend on (pixel, dimension) only;
+ * the first render after a sampler/film change tabulates them for the first `dims`
+ * dimensions (4 B per pixel-Morton row and dimension; default 256, 0 = compute every digit
+ * per call). Results are identical either way. */
+int avr_set_sampler_table(avr_context *ctx, int dims);
 
 /* Render sample indices [spp_begin, spp_end) of every pixel (the avr_set_sampler sampler,
  * seed), VolPathIntegrator maxdepth. Asynchronous on the context stream. */

@@ -577,3 +577,30 @@ def test_film_image_metric_and_mse_waves(tmp_path):
     integ.write_image(str(tmp_path / "a.exr"), rgb, w, spp=spp)
     assert np.array_equal(imageio.read_rgb(str(tmp_path / "a.exr")), img)
     integ.close()
+
+
+@pytest.mark.parametrize("kernel", ["persistent", "wavefront"])
+def test_zsobol_pixel_table_identical(kernel):
+    """The ZSobol pixel table (avr_set_sampler_table) changes nothing: films and per-sample
+    records equal the per-call computation, with paths running past the table's dimensions."""
+    from acceleratedvolrenderer_amd import scenes
+    n, W, H, spp = 12, 33, 21, 16
+    dens = (0.5 + np.random.default_rng(9).random((n, n, n), dtype=np.float32)).astype(np.float32)
+    scene = scenes.s_uniform(n=n, width=W, height=H, variant="chromatic", density=dens)
+    from acceleratedvolrenderer_amd import ZSobolSampler, GaussianFilter
+    from acceleratedvolrenderer_amd.scene import Scene, RGBFilm
+    scene = Scene(scene.camera, RGBFilm(W, H, filter=GaussianFilter()), scene.medium, scene.lights,
+                  sampler=ZSobolSampler(spp))
+    out = []
+    for dims in (0, 24, 256):
+        integ = _integrator(scene, maxdepth=20, spp=spp, kernel=kernel)
+        integ.ctx.set_sampler_table(dims)
+        rgb, w = integ.render()
+        _, ns, L, lam, _ = integ.ctx.last_pass_samples(W * H, spp)
+        st = integ.stats()
+        assert (st["ms_setup"] > 0) == (dims > 0)
+        out.append((rgb, w, L, lam))
+        integ.close()
+    for o in out[1:]:
+        for a, b in zip(out[0], o):
+            assert np.array_equal(a, b)
