@@ -1,0 +1,19 @@
+#!/bin/bash
+# GPU pass w: ZSobol pixel table — identity tests, suite, bench A/B (table 256 vs none).
+set -u
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/w
+mkdir -p $O
+export PYTHONUNBUFFERED=1
+step() {
+  local name=$1 t=$2; shift 2
+  timeout -k 10 $t "$@" > $O/$name.log 2>&1; local rc=$?
+  echo "$name rc=$rc"
+  [ $rc -eq 0 ] || { echo "stop: $name rc=$rc"; tail -30 $O/$name.log; exit $rc; }
+}
+step zs_tests 300 python -m pytest tests/test_gpu_parity.py -m gpu -x -q -s -rA -k zsobol_pixel_table
+step gpu_tests 900 python -m pytest tests -m gpu -x -q -s -rA
+step bench_table 400 python bench.py --steps 6 --warmup 2 --no-cpu-baseline
+step bench_notable 400 python bench.py --steps 6 --warmup 2 --no-cpu-baseline --zsobol-table 0
+step bench_indep 400 python bench.py --steps 6 --warmup 2 --no-cpu-baseline --sampler independent --filter box
+exit 0
