@@ -101,6 +101,8 @@ SIGNATURES = {
     "avr_lights": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, c_int_p, c_float_p, c_float_p, c_float_p,
                                   ctypes.c_float]),
     "avr_camera": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, c_float_p, c_float_p]),
+    "avr_light_image": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, c_float_p, c_float_p, c_float_p,
+                                       c_float_p, c_float_p]),
     "avr_film_image_device": (ctypes.c_int, [ctypes.c_void_p, c_float_p, ctypes.c_int, ctypes.c_void_p]),
     "avr_film_set_reference": (ctypes.c_int, [ctypes.c_void_p, c_float_p, c_float_p, ctypes.c_int]),
     "avr_film_metric": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, c_float_p]),
@@ -262,6 +264,12 @@ class Context:
         sc = f32(scene.light_scale)
         _check(self.lib.avr_lights(self.h, len(scene.lights), types.ctypes.data_as(c_int_p), _fp(w), _fp(L), _fp(sc),
                                    float(scene.scene_radius)))
+        for i, light in enumerate(scene.lights):
+            if light.type_id == 2:
+                arrs = [f32(light.coeffs), f32(light.distribution), f32(light.illuminant), f32(scene.light_rfl[i]),
+                        f32(scene.light_lfr[i])]
+                self._keep += arrs
+                _check(self.lib.avr_light_image(self.h, i, int(light.res), *[_fp(a) for a in arrs]))
         _check(self.lib.avr_camera(self.h, int(scene.camera.type_id), _fp(f32(scene.camera_from_raster)),
                                    _fp(f32(scene.render_from_camera))))
         film = scene.film

@@ -14,6 +14,7 @@
 // sincos: [0, 2pi); cosh: |x| < 3).
 #pragma once
 
+#include <cmath>
 #include <cstdint>
 #include <cstring>
 

@@ -91,6 +91,10 @@ struct avr_context {
     // RGBGridMedium grids (sigma_a, sigma_s, Le as float4 {c0, c1, c2, scale}) and illuminant
     float4 *d_rgb[3] = {nullptr, nullptr, nullptr};
     float *d_illum = nullptr;
+    // lights: host copy of the device list, ImageInfiniteLight buffers
+    avr::DevLight h_lights[avr::kMaxLights] = {};
+    void *d_light_img[avr::kMaxLights] = {};
+    int n_image_lights = 0, image_lights_ready = 0;
     // film image / --mse-reference-image state
     float *d_image = nullptr, *d_reference = nullptr;
     double *d_metric = nullptr;      // kMetricBlocks * kMetricSlots partials + kMetricSlots totals
@@ -115,13 +119,14 @@ namespace {
 
 void free_paths(avr_context *c) {
     float4 *f4[] = {c->ps.o, c->ps.d, c->ps.lambda, c->ps.pdf, c->ps.beta, c->ps.r_u, c->ps.r_l, c->ps.L,
-                    c->sh.o, c->sh.d, c->sh.bf, c->sh.Ls, c->sh.rp_pl};
+                    c->sh.o, c->sh.d, c->sh.bf, c->sh.Ls, c->sh.rp};
     for (auto p : f4) if (p) (void)hipFree(p);
     if (c->ps.smp_state) (void)hipFree(c->ps.smp_state);
     if (c->ps.smp_inc) (void)hipFree(c->ps.smp_inc);
     if (c->ps.depth) (void)hipFree(c->ps.depth);
     if (c->ps.weight) (void)hipFree(c->ps.weight);
     if (c->sh.path) (void)hipFree(c->sh.path);
+    if (c->sh.pdfs) (void)hipFree(c->sh.pdfs);
     for (auto &q : c->d_queue) if (q) (void)hipFree(q), q = nullptr;
     c->ps = {};
     c->sh = {};
@@ -138,7 +143,8 @@ int ensure_paths(avr_context *c, long long n) {
     HIP_TRY(dalloc(&c->ps.smp_state, N)); HIP_TRY(dalloc(&c->ps.smp_inc, N)); HIP_TRY(dalloc(&c->ps.depth, N));
     HIP_TRY(dalloc(&c->ps.weight, N));
     HIP_TRY(dalloc(&c->sh.path, N)); HIP_TRY(dalloc(&c->sh.o, N)); HIP_TRY(dalloc(&c->sh.d, N));
-    HIP_TRY(dalloc(&c->sh.bf, N)); HIP_TRY(dalloc(&c->sh.Ls, N)); HIP_TRY(dalloc(&c->sh.rp_pl, N));
+    HIP_TRY(dalloc(&c->sh.bf, N)); HIP_TRY(dalloc(&c->sh.Ls, N)); HIP_TRY(dalloc(&c->sh.rp, N));
+    HIP_TRY(dalloc(&c->sh.pdfs, N));
     HIP_TRY(dalloc(&c->d_queue[0], N)); HIP_TRY(dalloc(&c->d_queue[1], N));
     c->cap = n;
     return AVR_OK;
@@ -468,6 +474,7 @@ int avr_context_destroy(avr_context *c) {
     if (c->d_temperature) (void)hipFree(c->d_temperature);
     free_vdb(c);
     free_rgb(c);
+    for (auto &b : c->d_light_img) if (b) (void)hipFree(b), b = nullptr;
     if (c->d_zs_table) (void)hipFree(c->d_zs_table);
     if (c->d_image) (void)hipFree(c->d_image);
     if (c->d_reference) (void)hipFree(c->d_reference);
@@ -655,6 +662,8 @@ int avr_read_majorant(avr_context *c, float *out) {
     return AVR_OK;
 }
 
+static void pc1d_build(const float *f, int n, float mn, float mx, float *cdf, float *funcInt);
+
 int avr_lights(avr_context *c, int n, const int *types, const float *w3, const float *L, const float *scale,
                float scene_radius) {
     if (!c || n < 0 || n > avr::kMaxLights) return fail(AVR_ERR_ARG, "0..8 lights supported");
@@ -664,7 +673,8 @@ int avr_lights(avr_context *c, int n, const int *types, const float *w3, const f
     if (rc) return rc;
     avr::DevLight h[avr::kMaxLights] = {};
     for (int i = 0; i < n; ++i) {
-        if (types[i] != 0 && types[i] != 1) return fail(AVR_ERR_ARG, "light type must be 0 (distant) or 1 (uniform infinite)");
+        if (types[i] < 0 || types[i] > 2)
+            return fail(AVR_ERR_ARG, "light type must be 0 (distant), 1 (uniform infinite) or 2 (image infinite)");
         h[i].type = types[i];
         for (int k = 0; k < 3; ++k) h[i].w[k] = w3[3 * i + k];
         h[i].L = c->d_lightL + (size_t)i * avr::kNTable;
@@ -673,10 +683,75 @@ int avr_lights(avr_context *c, int n, const int *types, const float *w3, const f
     if (!c->d_lights) HIP_TRY(dalloc(&c->d_lights, avr::kMaxLights));
     HIP_TRY(hipMemcpyAsync(c->d_lights, h, sizeof(h), hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
+    for (auto &b : c->d_light_img) if (b) (void)hipFree(b), b = nullptr;
+    for (int i = 0; i < avr::kMaxLights; ++i) c->h_lights[i] = h[i];
     c->lights = {};
     c->lights.n = n;
     c->lights.list = c->d_lights;
     c->lights.scene_radius = scene_radius;
+    c->n_image_lights = 0;
+    for (int i = 0; i < n; ++i) c->n_image_lights += types[i] == 2 ? 1 : 0;
+    c->image_lights_ready = 0;
+    return AVR_OK;
+}
+
+// ImageInfiniteLight: pixel spectra, the compensated PiecewiseConstant2D (lights.cpp:1026-1038)
+int avr_light_image(avr_context *c, int index, int res, const float *pixel_coeffs, const float *distribution,
+                    const float *illuminant, const float render_from_light[16], const float light_from_render[16]) {
+    if (!c || index < 0 || index >= c->lights.n || c->h_lights[index].type != 2)
+        return fail(AVR_ERR_ARG, "avr_light_image: index must name a type-2 light of the last avr_lights call");
+    if (res < 1 || !pixel_coeffs || !distribution || !illuminant || !render_from_light || !light_from_render)
+        return fail(AVR_ERR_ARG, "avr_light_image: bad image arguments");
+    HIP_TRY(hipSetDevice(c->device));
+    const size_t np = (size_t)res * res;
+    // compensated distribution: d - average (f64 accumulate, lights.cpp:1031), clamped at 0;
+    // all zero -> ones
+    double sum = 0.;
+    for (size_t i = 0; i < np; ++i) sum += distribution[i];
+    const float average = (float)(sum / np);
+    std::vector<float> d(np);
+    bool allZero = true;
+    for (size_t i = 0; i < np; ++i) {
+        d[i] = std::max<float>(distribution[i] - average, 0);
+        allZero &= d[i] == 0;
+    }
+    if (allZero) std::fill(d.begin(), d.end(), 1.f);
+    const int nx = res, ny = res;
+    const size_t ntab = (size_t)avr::smp::filter_table_floats(nx, ny);
+    const size_t bytes = np * sizeof(float4) + ntab * sizeof(float) + avr::kNTable * sizeof(float);
+    std::vector<unsigned char> blob(bytes);
+    std::memcpy(blob.data(), pixel_coeffs, np * sizeof(float4));
+    float *t = (float *)(blob.data() + np * sizeof(float4));
+    float *f = t, *ccdf = f + nx * ny, *cint = ccdf + ny * (nx + 1), *mcdf = cint + ny, *mint = mcdf + ny + 1;
+    for (size_t i = 0; i < np; ++i) f[i] = std::abs(d[i]);
+    for (int y = 0; y < ny; ++y) pc1d_build(f + (size_t)y * nx, nx, 0.f, 1.f, ccdf + (size_t)y * (nx + 1), cint + y);
+    pc1d_build(cint, ny, 0.f, 1.f, mcdf, mint);
+    std::memcpy(t + ntab, illuminant, avr::kNTable * sizeof(float));
+    if (c->d_light_img[index]) (void)hipFree(c->d_light_img[index]);
+    c->d_light_img[index] = nullptr;
+    HIP_TRY(hipMalloc((void **)&c->d_light_img[index], bytes));
+    HIP_TRY(hipMemcpy(c->d_light_img[index], blob.data(), bytes, hipMemcpyHostToDevice));
+    unsigned char *base = (unsigned char *)c->d_light_img[index];
+    avr::DevLight &L = c->h_lights[index];
+    L.img = (const float4 *)base;
+    L.res = res;
+    const float *dt = (const float *)(base + np * sizeof(float4));
+    L.dist.nx = nx;
+    L.dist.ny = ny;
+    L.dist.f = dt;
+    L.dist.ccdf = dt + nx * ny;
+    L.dist.cint = L.dist.ccdf + ny * (nx + 1);
+    L.dist.mcdf = L.dist.cint + ny;
+    L.dist.mint = *mint;
+    L.illum = dt + ntab;
+    for (int r = 0; r < 3; ++r)
+        for (int k = 0; k < 3; ++k) {
+            L.rfl[3 * r + k] = render_from_light[4 * r + k];
+            L.lfr[3 * r + k] = light_from_render[4 * r + k];
+        }
+    HIP_TRY(hipMemcpyAsync(c->d_lights, c->h_lights, sizeof(c->h_lights), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    ++c->image_lights_ready;
     return AVR_OK;
 }
 
@@ -847,6 +922,7 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
     if (!c) return fail(AVR_ERR_ARG, "null context");
     if (!c->has_medium || !c->has_camera || !c->has_film) return fail(AVR_ERR_STATE, "medium, camera and film required");
     if (spp_begin < 0 || spp_end < spp_begin || max_depth < 0) return fail(AVR_ERR_ARG, "bad sample range");
+    if (c->image_lights_ready < c->n_image_lights) return fail(AVR_ERR_STATE, "image light without avr_light_image");
     avr::smp::ZSobolParams zs{};
     if (c->sampler_kind == 1) {
         // ZSobolSampler indexes (Morton(pixel) << log2(spp)) | sampleIndex: indices must stay
@@ -916,7 +992,8 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
         // k_paths keeps the majorant grid in LDS (4096 cells = pbrt's 16^3); larger grids
         // take the wavefront kernels, which read it through L2.
         // k_paths is specialised for GridMedium: homogeneous and cloud media run wavefront
-        const bool persistent = c->kernel_mode == 0 && c->med.type == 0 &&
+        // image infinite lights (non-delta, MIS-weighted) run wavefront as well
+        const bool persistent = c->kernel_mode == 0 && c->med.type == 0 && c->n_image_lights == 0 &&
                                 c->med.mres[0] * c->med.mres[1] * c->med.mres[2] <= 4096 &&
                                 c->med.mres[0] <= 255 && c->med.mres[1] <= 255 && c->med.mres[2] <= 255;
         c->last_persistent = persistent;

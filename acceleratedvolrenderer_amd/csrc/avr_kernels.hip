@@ -19,6 +19,7 @@
 #include "avr_numerics.h"
 #include "avr_sampling.h"
 #include "avr_vdb.h"
+#include "avr_envmap.h"
 
 #include <type_traits>
 
@@ -71,10 +72,18 @@ struct DevMedium {
 
 constexpr int kMaxLights = 8;
 struct DevLight {
-    int type;                         // 0 distant (delta), 1 uniform infinite
+    int type;                         // 0 distant (delta), 1 uniform infinite, 2 image infinite
     float w[3];                       // render-space direction towards a distant light
     float scale;
     const float *L;                   // 471-entry table
+    // type 2, ImageInfiniteLight (lights.h:552-640): res x res equal-area image, per pixel the
+    // RGBIlluminantSpectrum {c0, c1, c2, scale}; the colour space's illuminant; the
+    // compensated sampling distribution; renderFromLight and its inverse (3x3)
+    const float4 *img;
+    int res;
+    const float *illum;
+    env::Distrib2D dist;
+    float rfl[9], lfr[9];
 };
 struct DevLights {
     int n;
@@ -108,7 +117,8 @@ struct PathSoA {
 };
 struct ShadowSoA {
     int *path;
-    float4 *o, *d, *bf, *Ls, *rp_pl;
+    float4 *o, *d, *bf, *Ls, *rp;     // rp: the path's r_u at the scatter (SampleLd's r_p)
+    float2 *pdfs;                     // {p_l, scatterPDF}; scatterPDF < 0 marks a delta light
 };
 
 // Per-launch work counters (u64): [0] lookups k_medium, [1] items in k_medium,
@@ -357,6 +367,34 @@ __device__ __forceinline__ Spec grid_emission(const DevMedium &m, V3 p, const Sp
         }
     }
     return Le;
+}
+
+// ImageInfiniteLight::ImageLe (lights.h:620-627): nearest pixel (octahedral wrap), its
+// RGBIlluminantSpectrum sampled at lambda, times the light scale
+__device__ __forceinline__ Spec image_le(const DevLight &lt, float u, float v, const Spec &lam) {
+    const float4 c = lt.img[env::octahedral_pixel(u, v, lt.res)];
+    const Spec il = sample_table(lt.illum, lambda_index(lam));
+    const Spec s{c.w * rsp_eval(c.x, c.y, c.z, lam.v0), c.w * rsp_eval(c.x, c.y, c.z, lam.v1),
+                 c.w * rsp_eval(c.x, c.y, c.z, lam.v2), c.w * rsp_eval(c.x, c.y, c.z, lam.v3)};
+    return s * il * lt.scale;
+}
+// Transform::operator()(Vector3f) with a 3x3 (row-major): ((m0 x + m1 y) + m2 z)
+__device__ __forceinline__ V3 xf_vec3(const float *m, V3 v) {
+    return {(m[0] * v.x + m[1] * v.y) + m[2] * v.z, (m[3] * v.x + m[4] * v.y) + m[5] * v.z,
+            (m[6] * v.x + m[7] * v.y) + m[8] * v.z};
+}
+// ImageInfiniteLight::Le(ray) (lights.h:581-585): Le and the equal-area (u, v) of direction d
+__device__ __forceinline__ Spec image_le_dir(const DevLight &lt, V3 d, const Spec &lam, float *u, float *v) {
+    const V3 wl = normalize(xf_vec3(lt.lfr, d));
+    env::sphere_to_square(wl.x, wl.y, wl.z, u, v);
+    return image_le(lt, *u, *v, lam);
+}
+// PDF_Li(ctx, w, allowIncompletePDF = true) (lights.cpp:1042-1052): wLight not normalised
+__device__ __forceinline__ float image_pdf_li(const DevLight &lt, V3 w) {
+    const V3 wl = xf_vec3(lt.lfr, w);
+    float u, v;
+    env::sphere_to_square(wl.x, wl.y, wl.z, &u, &v);
+    return env::distrib_pdf(lt.dist, u, v) / (4 * kPi);
 }
 
 struct MediumSample { Spec sigma_a, sigma_s, Le; };
@@ -666,6 +704,7 @@ __global__ void __launch_bounds__(256) k_medium(Params P) {
         int path = 0;
         V3 newO{}, newD{};
         float4 shO{}, shD{}, shBF{}, shLs{}, shRP{};
+        float2 shPdfs{};
         if (valid) {
             ++nIn;
             path = P.queue_in ? P.queue_in[i] : i;
@@ -740,12 +779,28 @@ __global__ void __launch_bounds__(256) k_medium(Params P) {
                         idx = idx < nl - 1 ? idx : nl - 1;
                         float pmf = pInf / nl;
                         const DevLight &lt = P.lights.list[idx];
-                        if (lt.type == 0) {
-                            const V3 wi = {lt.w[0], lt.w[1], lt.w[2]};
-                            const V3 pOut = pScatter + wi * (2 * P.lights.scene_radius);
-                            const Spec Ls = sample_table(lt.L, li) * lt.scale;
-                            if (Ls.nonzero()) {
-                                const float p_l = pmf * 1.f;
+                        if (lt.type == 0 || lt.type == 2) {
+                            V3 wi = {lt.w[0], lt.w[1], lt.w[2]};
+                            Spec Ls;
+                            float lsPdf = 1.f;
+                            if (lt.type == 0) {
+                                Ls = sample_table(lt.L, li) * lt.scale;
+                            } else {   // ImageInfiniteLight::SampleLi, compensated distribution (lights.h:588-613)
+                                float su, sv;
+                                env::distrib_sample(lt.dist, uL0, uL1, &su, &sv, &lsPdf);
+                                if (lsPdf != 0) {
+                                    V3 wl;
+                                    env::square_to_sphere(su, sv, &wl.x, &wl.y, &wl.z);
+                                    wi = xf_vec3(lt.rfl, wl);
+                                    lsPdf = lsPdf / (4 * kPi);
+                                    Ls = image_le(lt, su, sv, lamv);
+                                } else {
+                                    Ls = Spec::c(0.f);
+                                }
+                            }
+                            if (Ls.nonzero() && lsPdf != 0) {
+                                const V3 pOut = pScatter + wi * (2 * P.lights.scene_radius);
+                                const float p_l = pmf * lsPdf;
                                 const float fval = hg_eval(dot(wo, wi), P.med.g);
                                 const Spec f_hat = Spec::c(fval);
                                 if (f_hat.nonzero()) {
@@ -753,7 +808,8 @@ __global__ void __launch_bounds__(256) k_medium(Params P) {
                                     shD = to4(pOut - pScatter);
                                     shBF = to4(beta * f_hat);
                                     shLs = to4(Ls);
-                                    shRP = to4(r_u * p_l);
+                                    shRP = to4(r_u);
+                                    shPdfs = make_float2(p_l, lt.type == 0 ? -1.f : fval);
                                     shadowSpawned = true;
                                 }
                             }
@@ -783,12 +839,14 @@ __global__ void __launch_bounds__(256) k_medium(Params P) {
                 // escaped: infinite lights (integrators.cpp:1090-1107)
                 for (int k = 0; k < P.lights.n; ++k) {
                     const DevLight &lt = P.lights.list[k];
-                    if (lt.type != 1) continue;
-                    const Spec Le = sample_table(lt.L, li) * lt.scale;
+                    if (lt.type == 0) continue;
+                    float eu = 0, ev = 0;
+                    const Spec Le = lt.type == 1 ? sample_table(lt.L, li) * lt.scale : image_le_dir(lt, d, lamv, &eu, &ev);
                     if (!Le.nonzero()) continue;
                     if (depth == 0) L = L + beta * Le / r_u.avg();
                     else {
-                        float p_l = (1.f / (P.lights.n + 0)) * 0.f;
+                        // lightSampler.PMF * PDF_Li(prevIntrContext, ray.d, true): 0 for the uniform light
+                        float p_l = (1.f / (P.lights.n + 0)) * (lt.type == 1 ? 0.f : image_pdf_li(lt, d));
                         r_l = r_l * p_l;
                         L = L + beta * Le / (r_u + r_l).avg();
                     }
@@ -815,7 +873,8 @@ __global__ void __launch_bounds__(256) k_medium(Params P) {
             P.sh.d[sslot] = shD;
             P.sh.bf[sslot] = shBF;
             P.sh.Ls[sslot] = shLs;
-            P.sh.rp_pl[sslot] = shRP;
+            P.sh.rp[sslot] = shRP;
+            P.sh.pdfs[sslot] = shPdfs;
         }
     }
     flush_stat(P.stats, 0, nLookup);
@@ -867,8 +926,16 @@ __global__ void __launch_bounds__(256) k_shadow(Params P) {
         r_u = r_u * (T_maj / T_maj.v0);
         Spec contrib = Spec::c(0.f);
         if (T_ray.nonzero()) {
-            r_l = r_l * spec4(P.sh.rp_pl[i]);
-            contrib = spec4(P.sh.bf[i]) * T_ray * spec4(P.sh.Ls[i]) / r_l.avg();
+            // r_l *= r_p * p_l; r_u *= r_p * scatterPDF (integrators.cpp:1391-1398)
+            const Spec rp = spec4(P.sh.rp[i]);
+            const float2 pd = P.sh.pdfs[i];
+            r_l = r_l * (rp * pd.x);
+            if (pd.y < 0) {
+                contrib = spec4(P.sh.bf[i]) * T_ray * spec4(P.sh.Ls[i]) / r_l.avg();
+            } else {
+                r_u = r_u * (rp * pd.y);
+                contrib = spec4(P.sh.bf[i]) * T_ray * spec4(P.sh.Ls[i]) / (r_l + r_u).avg();
+            }
         }
         P.ps.L[path] = to4(spec4(P.ps.L[path]) + contrib);
     }

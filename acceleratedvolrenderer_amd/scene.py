@@ -270,6 +270,72 @@ class UniformInfiniteLight:
         return np.zeros(3, np.float32)
 
 
+class ImageInfiniteLight:
+    """"infinite" light with "filename" (ImageInfiniteLight, lights.h:552-640; Create
+    lights.cpp:1568-1660): a square equal-area octahedral RGB map. `image` is an (res, res, 3)
+    array or `filename` an EXR/PFM; "scale" / SpectrumToPhotometric(illuminant) and the
+    optional "illuminance" normalisation as Create computes them. The per-pixel
+    RGBIlluminantSpectrum conversion needs the colour space's `rgb_table`
+    (rgbspectrum.RGBToSpectrumTable; sRGB by default with the D65 illuminant)."""
+    type_id = 2
+
+    def __init__(self, image=None, filename=None, scale=1.0, illuminance=None, world_from_light=None,
+                 rgb_table=None, illuminant=None):
+        if (image is None) == (filename is None):
+            raise ValueError("give exactly one of image / filename")
+        if filename is not None:
+            from . import imageio
+            image = imageio.read_rgb(filename)
+        img = np.ascontiguousarray(np.asarray(image, np.float32)[:, :, :3])
+        if img.ndim != 3 or img.shape[0] != img.shape[1]:
+            raise ValueError("image resolution is non-square: not an equal-area environment map")
+        if not np.all(np.isfinite(img)):
+            raise ValueError("image has infinite or NaN pixel values and so is not suitable as a light")
+        if rgb_table is None:
+            raise ValueError("ImageInfiniteLight needs rgb_table (rgbspectrum.RGBToSpectrumTable)")
+        self.res = img.shape[0]
+        self.image = img
+        self.illuminant = (spectra.TABLES["D65"] if illuminant is None else spectra.as_table(illuminant, 0.0)
+                           ).astype(np.float32)
+        sc = np.float32(np.float32(scale) / spectra.spectrum_to_photometric(self.illuminant))
+        if illuminance is not None and illuminance > 0:
+            sc = np.float32(sc * np.float32(illuminance) / np.float32(self._illuminance(img)))
+        self.scale = sc
+        self.L = np.zeros(spectra.N, np.float32)
+        self.world_from_light = np.eye(4) if world_from_light is None else np.asarray(world_from_light, np.float64)
+        # ImageLe: RGBIlluminantSpectrum(cs, ClampZero(rgb)) per pixel (lights.h:620-627)
+        self.coeffs = np.ascontiguousarray(rgb_table.spectrum_coeffs(np.maximum(img, np.float32(0))))
+        # Image::GetSamplingDistribution (util/image.h:451-470): ImageChannelValues::Average
+        # (float sum in channel order / 3) times dxdA = 1
+        avg = ((np.float32(0) + img[:, :, 0]) + img[:, :, 1]) + img[:, :, 2]
+        self.distribution = np.ascontiguousarray((avg / np.float32(3)).astype(np.float32))
+
+    @staticmethod
+    def _illuminance(img):
+        """Upper-hemisphere illuminance of the map (lights.cpp:1621-1641) with the colour
+        space's LuminanceVector (row Y of XYZFromRGB); accumulated in f64."""
+        res = img.shape[0]
+        lum = np.linalg.inv(spectra.TABLES["srgb_rgb_from_xyz"].astype(np.float64))[1]
+        total = 0.0
+        for y in range(res):
+            v = (y + 0.5) / res
+            for x in range(res):
+                u = (x + 0.5) / res
+                uu, vv = 2 * u - 1, 2 * v - 1
+                up, vp = abs(uu), abs(vv)
+                sd = 1 - (up + vp)
+                r = 1 - abs(sd)
+                phi = (1 if r == 0 else (vp - up) / r + 1) * math.pi / 4
+                z = math.copysign(1 - r * r, sd)
+                if z <= 0:
+                    continue
+                total += float(np.dot(img[y, x].astype(np.float64), lum)) * z
+        return total * 2 * math.pi / (res * res)
+
+    def render_direction(self, render_from_world):
+        return np.zeros(3, np.float32)
+
+
 class _ProjectiveCamera:
     type_id = -1
 
@@ -423,6 +489,11 @@ class Scene:
         self.light_L = np.stack([l.L for l in self.lights]).astype(np.float32) if self.lights else np.zeros(
             (0, spectra.N), np.float32)
         self.light_scale = np.array([l.scale for l in self.lights], np.float32)
+        # image lights: renderFromLight and its inverse (ImageInfiniteLight's transform)
+        self.light_rfl = [xf.f32(self.render_from_world @ l.world_from_light) if l.type_id == 2 else None
+                          for l in self.lights]
+        self.light_lfr = [xf.f32(np.linalg.inv(self.render_from_world @ l.world_from_light)) if l.type_id == 2
+                          else None for l in self.lights]
 
 
 def film_rgb(film, rgb_sum, w_sum):

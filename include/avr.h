@@ -174,11 +174,24 @@ int avr_read_majorant(avr_context *ctx, float *out);
 
 /* Lights (lights.h:244-305 DistantLight, lights.cpp:950-972 UniformInfiniteLight).
  * type 0 = distant: w = render-space unit vector towards the light
- *          (Normalize(renderFromLight(0,0,1)), lights.h:287); type 1 = uniform infinite.
+ *          (Normalize(renderFromLight(0,0,1)), lights.h:287); type 1 = uniform infinite;
+ * type 2 = image infinite (then avr_light_image).
  * L = n tables of 471 floats; scale = final light scale (1/SpectrumToPhotometric folded in).
  * scene_radius = Bounds3::BoundingSphere radius of the scene bounds (lights.h:280). */
 int avr_lights(avr_context *ctx, int n, const int *types, const float *w3, const float *L, const float *scale,
                float scene_radius);
+/* ImageInfiniteLight (lights.h:552-640, ctor lights.cpp:1007-1040, Create lights.cpp:1527-1660)
+ * for light `index` of the last avr_lights call, which lists it with type 2 (its L table is
+ * ignored; `scale` is the final scale: "scale" / SpectrumToPhotometric(illuminant), times the
+ * "illuminance" factor when given). A res x res equal-area octahedral map: per pixel the
+ * RGBIlluminantSpectrum {c0, c1, c2, scale} of ClampZero(rgb) in the image's colour space,
+ * `distribution` = Image::GetSamplingDistribution() (res*res, row y), the colour space's
+ * illuminant (471) and renderFromLight / its inverse (row-major 4x4, the 3x3 part is used).
+ * The library builds the compensated PiecewiseConstant2D that SampleLi / PDF_Li use with
+ * allowIncompletePDF (VolPath always passes true). Scenes with image lights render with
+ * the wavefront kernels. */
+int avr_light_image(avr_context *ctx, int index, int res, const float *pixel_coeffs, const float *distribution,
+                    const float *illuminant, const float render_from_light[16], const float light_from_render[16]);
 
 /* Camera: type 0 orthographic, 1 perspective (cameras.cpp:284-306, 404-427).
  * camera_from_raster: full 4x4 (projective for perspective); render_from_camera: affine 4x4. */

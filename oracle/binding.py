@@ -73,6 +73,9 @@ class OracleScene(ctypes.Structure):
         ("rgb_sigma_a", c_float_p), ("rgb_sigma_s", c_float_p), ("rgb_Le", c_float_p),
         ("rgb_illuminant", c_float_p),
         ("rgb_sigma_scale", ctypes.c_float), ("rgb_Le_scale", ctypes.c_float),
+        ("light_img", c_float_p * 8), ("light_res", ctypes.c_int * 8), ("light_dist", c_float_p * 8),
+        ("light_rfl", (ctypes.c_float * 9) * 8), ("light_lfr", (ctypes.c_float * 9) * 8),
+        ("light_illuminant", c_float_p),
     ]
 
 
@@ -150,6 +153,10 @@ def lib():
         L.oracle_vdb_create.argtypes = [ctypes.c_int, c_int_p, c_float_p, ctypes.c_int, c_int_p, c_int_p, c_float_p,
                                         ctypes.c_float, c_int_p, c_double_p, c_double_p]
         L.oracle_vdb_free.argtypes = [ctypes.c_void_p]
+        L.oracle_equal_area_square_to_sphere.argtypes = [ctypes.c_float, ctypes.c_float, c_float_p]
+        L.oracle_equal_area_sphere_to_square.argtypes = [ctypes.c_float] * 3 + [c_float_p]
+        L.oracle_remap_octahedral.argtypes = [ctypes.c_int] * 3 + [c_int_p]
+        L.oracle_pc2d.argtypes = [c_float_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_float_p, c_float_p]
         for name in ("oracle_rsp_eval", "oracle_rsp_max"):
             getattr(L, name).restype = ctypes.c_float
         L.oracle_rsp_eval.argtypes = [ctypes.c_float] * 4
@@ -316,6 +323,14 @@ class OracleRun:
                 s.light_w[i][k] = float(scene.light_w[i][k])
             s.light_L[i] = arr(scene.light_L[i])
             s.light_scale[i] = float(scene.light_scale[i])
+            lt = scene.lights[i]
+            if lt.type_id == 2:
+                s.light_img[i] = arr(lt.coeffs.reshape(-1))
+                s.light_res[i] = int(lt.res)
+                s.light_dist[i] = arr(lt.distribution.reshape(-1))
+                s.light_rfl[i][:] = [float(v) for v in scene.light_rfl[i][:3, :3].reshape(-1)]
+                s.light_lfr[i][:] = [float(v) for v in scene.light_lfr[i][:3, :3].reshape(-1)]
+                s.light_illuminant = arr(lt.illuminant)
         s.scene_radius = float(scene.scene_radius)
         s.camera_type = int(scene.camera.type_id)
         s.camera_from_raster[:] = [float(v) for v in scene.camera_from_raster.reshape(-1)]

@@ -30,6 +30,7 @@
 #include <pbrt/util/transform.h>
 #include <pbrt/util/noise.h>
 #include <pbrt/util/colorspace.h>
+#include <pbrt/util/image.h>
 #include <pbrt/samplers.h>
 #include <pbrt/filters.h>
 
@@ -524,6 +525,64 @@ int main(int argc, char **argv) {
             printf("%s[%u,%u,%u", i ? "," : "", fb(c.r), fb(c.g), fb(c.b));
             for (float l : ls) printf(",%u", fb(s(l)));
             printf("]");
+        }
+        printf("]");
+    }
+    // ---- ImageInfiniteLight pieces ---------------------------------------------
+    // EqualAreaSquareToSphere / EqualAreaSphereToSquare (util/math.cpp:292-361),
+    // RemapPixelCoords with WrapMode::OctahedralSphere (util/image.h:96-123),
+    // PiecewiseConstant2D Sample / PDF (util/sampling.h:698-779)
+    {
+        RNG rng(31, 7);
+        j.key("equal_area");   // [u, v, x, y, z, u', v'] with (u', v') = SphereToSquare(x, y, z)
+        printf("[");
+        std::vector<Point2f> pts = {{0, 0}, {1, 1}, {0.5f, 0.5f}, {0, 1}, {1, 0}, {0.25f, 0.75f}, {0.5f, 0}};
+        for (int i = 0; i < 60; ++i) pts.push_back({rng.Uniform<float>(), rng.Uniform<float>()});
+        for (size_t i = 0; i < pts.size(); ++i) {
+            Vector3f w = EqualAreaSquareToSphere(pts[i]);
+            Point2f q = EqualAreaSphereToSquare(w);
+            printf("%s[%u,%u,%u,%u,%u,%u,%u]", i ? "," : "", fb(pts[i].x), fb(pts[i].y), fb(w.x), fb(w.y), fb(w.z),
+                   fb(q.x), fb(q.y));
+        }
+        printf("]");
+        j.key("equal_area_dirs");   // [x, y, z, u, v] for normalised random directions
+        printf("[");
+        for (int i = 0; i < 60; ++i) {
+            Vector3f d = Normalize(Vector3f(rng.Uniform<float>() * 2 - 1, rng.Uniform<float>() * 2 - 1,
+                                            rng.Uniform<float>() * 2 - 1));
+            Point2f q = EqualAreaSphereToSquare(d);
+            printf("%s[%u,%u,%u,%u,%u]", i ? "," : "", fb(d.x), fb(d.y), fb(d.z), fb(q.x), fb(q.y));
+        }
+        printf("]");
+        j.key("octahedral_wrap");   // [res, x, y, x', y']
+        printf("[");
+        bool f = true;
+        for (int res : {1, 8}) {
+            for (int x = -2; x <= res + 1; ++x)
+                for (int y = -2; y <= res + 1; ++y) {
+                    Point2i pp(x, y);
+                    RemapPixelCoords(&pp, Point2i(res, res), WrapMode::OctahedralSphere);
+                    printf("%s[%d,%d,%d,%d,%d]", f ? "" : ",", res, x, y, pp.x, pp.y);
+                    f = false;
+                }
+        }
+        printf("]");
+        // a 7 x 5 function with a zero row and zero entries
+        const int nu = 7, nv = 5;
+        std::vector<Float> func(nu * nv);
+        for (int i = 0; i < nu * nv; ++i) func[i] = (i / nu == 2) ? 0.f : (i % 3 == 0 ? 0.f : rng.Uniform<float>() * 3);
+        PiecewiseConstant2D d2(func, nu, nv);
+        j.key("pc2d_func");
+        printf("[");
+        for (int i = 0; i < nu * nv; ++i) printf("%s%u", i ? "," : "", fb(func[i]));
+        printf("]");
+        j.key("pc2d_sample");   // [u0, u1, x, y, pdf, PDF(x, y)]
+        printf("[");
+        for (int i = 0; i < 50; ++i) {
+            Point2f u(rng.Uniform<float>(), rng.Uniform<float>());
+            Float pdf;
+            Point2f q = d2.Sample(u, &pdf);
+            printf("%s[%u,%u,%u,%u,%u,%u]", i ? "," : "", fb(u.x), fb(u.y), fb(q.x), fb(q.y), fb(pdf), fb(d2.PDF(q)));
         }
         printf("]");
     }

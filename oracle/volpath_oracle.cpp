@@ -27,6 +27,7 @@
 #include <cstdint>
 #include <cstring>
 #include <limits>
+#include <numeric>
 #include <thread>
 #include <unordered_map>
 #include <vector>
@@ -785,6 +786,14 @@ typedef struct OracleScene {
     const float *rgb_sigma_a, *rgb_sigma_s, *rgb_Le;
     const float *rgb_illuminant;      // 471, the colour space's illuminant
     float rgb_sigma_scale, rgb_Le_scale;
+    // light_type 2, ImageInfiniteLight (lights.h:552-640): res x res equal-area image as
+    // per-pixel RGBIlluminantSpectrum {c0, c1, c2, scale}, GetSamplingDistribution (res*res),
+    // renderFromLight / lightFromRender (3x3), the colour space's illuminant
+    const float *light_img[8];
+    int light_res[8];
+    const float *light_dist[8];
+    float light_rfl[8][9], light_lfr[8][9];
+    const float *light_illuminant;
 } OracleScene;
 
 }  // extern "C"
@@ -1058,14 +1067,131 @@ struct RgbGrid {
     }
 };
 
+
+// ImageInfiniteLight support (lights.h:552-640, lights.cpp:1007-1052)
+static V3 EqualAreaSquareToSphere(float px, float py) {   // util/math.cpp:292-315
+    float u = 2 * px - 1, v = 2 * py - 1;
+    float up = std::abs(u), vp = std::abs(v);
+    float signedDistance = 1 - (up + vp);
+    float d = std::abs(signedDistance);
+    float r = 1 - d;
+    float phi = (r == 0 ? 1 : (vp - up) / r + 1) * Pi / 4;
+    float z = std::copysign(1 - Sqr(r), signedDistance);
+    float sn, cs;
+    LmSinCos(phi, &sn, &cs);
+    float cosPhi = std::copysign(cs, u), sinPhi = std::copysign(sn, v);
+    return {cosPhi * r * SafeSqrt(2 - Sqr(r)), sinPhi * r * SafeSqrt(2 - Sqr(r)), z};
+}
+static void EqualAreaSphereToSquare(V3 d, float *ou, float *ov) {   // util/math.cpp:317-361
+    float x = std::abs(d.x), y = std::abs(d.y), z = std::abs(d.z);
+    float r = SafeSqrt(1 - z);
+    float a = std::max(x, y), b = std::min(x, y);
+    b = a == 0 ? 0 : b / a;
+    const float t1 = 0.406758566246788489601959989e-5;
+    const float t2 = 0.636226545274016134946890922156;
+    const float t3 = 0.61572017898280213493197203466e-2;
+    const float t4 = -0.247333733281268944196501420480;
+    const float t5 = 0.881770664775316294736387951347e-1;
+    const float t6 = 0.419038818029165735901852432784e-1;
+    const float t7 = -0.251390972343483509333252996350e-1;
+    // EvaluatePolynomial(b, t1, ..., t7): FMA(b, EvaluatePolynomial(b, t2, ...), t1)
+    const float c[7] = {t1, t2, t3, t4, t5, t6, t7};
+    float phi = c[6];
+    for (int i = 5; i >= 0; --i) phi = std::fma(b, phi, c[i]);
+    if (x < y) phi = 1 - phi;
+    float v = phi * r;
+    float u = r - v;
+    if (d.z < 0) {
+        std::swap(u, v);
+        u = 1 - u;
+        v = 1 - v;
+    }
+    u = std::copysign(u, d.x);
+    v = std::copysign(v, d.y);
+    *ou = 0.5f * (u + 1);
+    *ov = 0.5f * (v + 1);
+}
+// RemapPixelCoords with WrapMode::OctahedralSphere (util/image.h:96-123)
+static void RemapOctahedral(int *x, int *y, int res) {
+    int &p0 = *x, &p1 = *y;
+    if (p0 < 0) { p0 = -p0; p1 = res - 1 - p1; }
+    else if (p0 >= res) { p0 = 2 * res - 1 - p0; p1 = res - 1 - p1; }
+    if (p1 < 0) { p0 = res - 1 - p0; p1 = -p1; }
+    else if (p1 >= res) { p0 = res - 1 - p0; p1 = 2 * res - 1 - p1; }
+    if (res == 1) p0 = p1 = 0;
+}
+// Image::LookupNearestChannel(uv, c, OctahedralSphere): Point2i(p.x * res, p.y * res), remapped
+static int OctahedralPixel(float u, float v, int res) {
+    int p0 = (int)(u * res), p1 = (int)(v * res);
+    RemapOctahedral(&p0, &p1, res);
+    return p1 * res + p0;
+}
+struct PC2D {   // PiecewiseConstant2D over [0,1]^2 (util/sampling.h:698-779)
+    std::vector<PC1D> cond;
+    PC1D marg;
+    int nu = 0, nv = 0;
+    void Build(const float *d, int nu_, int nv_) {
+        nu = nu_; nv = nv_;
+        cond.resize(nv);
+        std::vector<float> mf(nv);
+        for (int v = 0; v < nv; ++v) {
+            cond[v].Build(d + (size_t)v * nu, nu, 0, 1);
+            mf[v] = cond[v].funcInt;
+        }
+        marg.Build(mf.data(), nv, 0, 1);
+    }
+    void Sample(float u0, float u1, float *su, float *sv, float *pdf) const {
+        float p0, p1;
+        int ov, ou;
+        *sv = marg.Sample(u1, &p1, &ov);
+        *su = cond[ov].Sample(u0, &p0, &ou);
+        *pdf = p0 * p1;
+    }
+    float PDF(float u, float v) const {
+        int iu = std::clamp(int(u * nu), 0, nu - 1), iv = std::clamp(int(v * nv), 0, nv - 1);
+        return cond[iv].func[iu] / marg.funcInt;
+    }
+};
+struct ImageLight {
+    const float *img = nullptr;
+    int res = 0;
+    PC2D compensated;
+    const float *rfl = nullptr, *lfr = nullptr;
+    void Build(const float *image, int r, const float *dist, const float *rfl_, const float *lfr_) {
+        img = image; res = r; rfl = rfl_; lfr = lfr_;
+        const size_t n = (size_t)r * r;
+        std::vector<float> d(dist, dist + n);
+        float average = std::accumulate(d.begin(), d.end(), 0.) / d.size();   // lights.cpp:1031
+        for (float &v : d) v = std::max<float>(v - average, 0);
+        if (std::all_of(d.begin(), d.end(), [](float v) { return v == 0; })) std::fill(d.begin(), d.end(), 1.f);
+        compensated.Build(d.data(), r, r);
+    }
+    static V3 Mul(const float *m, V3 v) {   // Transform::operator()(Vector3f)
+        return {m[0] * v.x + m[1] * v.y + m[2] * v.z, m[3] * v.x + m[4] * v.y + m[5] * v.z,
+                m[6] * v.x + m[7] * v.y + m[8] * v.z};
+    }
+    Spec ImageLe(float u, float v, const Lambda &l, const float *illum, float scale) const {   // lights.h:620-627
+        const float *c = img + 4 * (size_t)OctahedralPixel(u, v, res);
+        Rsp rsp{c[0], c[1], c[2]};
+        Spec s;
+        for (int i = 0; i < NS; ++i) s.v[i] = c[3] * rsp(l.lambda[i]);
+        s = s * SampleDense(illum, l);
+        return scale * s;
+    }
+};
+
 struct SceneView {
     const OracleScene &s;
     Xform mediumX, cameraX, rasterX;
     Bounds bounds;
     Grid density, lescale, majorant, temperature;
     GaussianSampler gauss;
+    ImageLight img[8];
     explicit SceneView(const OracleScene &sc) : s(sc) {
         if (sc.filter_type == 1) gauss.Build(sc.filter_radius[0], sc.filter_radius[1], sc.filter_sigma);
+        for (int i = 0; i < sc.nlights; ++i)
+            if (sc.light_type[i] == 2)
+                img[i].Build(sc.light_img[i], sc.light_res[i], sc.light_dist[i], sc.light_rfl[i], sc.light_lfr[i]);
         for (int i = 0; i < 16; ++i) {
             mediumX.m[i / 4][i % 4] = sc.render_from_medium[i];
             mediumX.mInv[i / 4][i % 4] = sc.medium_from_render[i];
@@ -1281,26 +1407,37 @@ static Spec SampleLd(const SceneView &sv, V3 p, V3 wo, const Lambda &l, Sampler 
     float u = sampler.Get1D();
     float uL0, uL1;
     sampler.Get2D(&uL0, &uL1);   // uLight (unused by distant lights)
-    (void)uL0; (void)uL1;
     if (s.nlights == 0) return Spec::Const(0.f);
     float pInfinite = float(s.nlights) / float(s.nlights + 0);
     if (!(u < pInfinite)) return Spec::Const(0.f);
     u /= pInfinite;
     int index = std::min<int>(u * s.nlights, s.nlights - 1);
     float pmf = pInfinite / s.nlights;
-    if (s.light_type[index] != 0) return Spec::Const(0.f);  // UniformInfiniteLight::SampleLi with allowIncompletePDF
-    // DistantLight::SampleLi — lights.h:284-291
-    V3 wi = {s.light_w[index][0], s.light_w[index][1], s.light_w[index][2]};
-    V3 pOutside = p + wi * (2 * s.scene_radius);
-    Spec Ls = s.light_scale[index] * SampleDense(s.light_L[index], l);
-    if (!Ls) return Spec::Const(0.f);
+    if (s.light_type[index] == 1) return Spec::Const(0.f);  // UniformInfiniteLight::SampleLi with allowIncompletePDF
+    V3 wi;
+    Spec Ls;
     float lsPdf = 1;
+    const bool delta = s.light_type[index] == 0;
+    if (delta) {   // DistantLight::SampleLi — lights.h:284-291
+        wi = {s.light_w[index][0], s.light_w[index][1], s.light_w[index][2]};
+        Ls = s.light_scale[index] * SampleDense(s.light_L[index], l);
+    } else {       // ImageInfiniteLight::SampleLi(allowIncompletePDF = true) — lights.h:588-613
+        const ImageLight &il = sv.img[index];
+        float su, sv_, mapPDF = 0;
+        il.compensated.Sample(uL0, uL1, &su, &sv_, &mapPDF);
+        if (mapPDF == 0) return Spec::Const(0.f);
+        V3 wLight = EqualAreaSquareToSphere(su, sv_);
+        wi = ImageLight::Mul(il.rfl, wLight);
+        lsPdf = mapPDF / (4 * Pi);
+        Ls = il.ImageLe(su, sv_, l, s.light_illuminant, s.light_scale[index]);
+    }
+    V3 pOutside = p + wi * (2 * s.scene_radius);
+    if (!Ls || lsPdf == 0) return Spec::Const(0.f);
     float p_l = pmf * lsPdf;
     // phase function
     float fval = HenyeyGreenstein(Dot(wo, wi), s.g);
     Spec f_hat = Spec::Const(fval);
     float scatterPDF = fval;
-    (void)scatterPDF;
     if (!f_hat) return Spec::Const(0.f);
     // SpawnRayTo from a medium interaction (ray.h:75-108: zero error, zero normal)
     Ray lightRay = {p, pOutside - p};
@@ -1330,8 +1467,8 @@ static Spec SampleLd(const SceneView &sv, V3 p, V3 wo, const Lambda &l, Sampler 
     if (!T_ray) return Spec::Const(0.f);
     r_l = r_l * (r_p * p_l);
     r_u = r_u * (r_p * scatterPDF);
-    // DistantLight is a delta light
-    return beta * f_hat * T_ray * Ls / r_l.Average();
+    if (delta) return beta * f_hat * T_ray * Ls / r_l.Average();
+    return beta * f_hat * T_ray * Ls / (r_l + r_u).Average();
 }
 
 // VolPathIntegrator::Li — integrators.cpp:962-1280, restricted to the interface-box scene.
@@ -1406,13 +1543,30 @@ static Spec Li(const SceneView &sv, Ray ray, Lambda &l, Sampler &sampler, int *n
         r_l = r_l * (T_maj / T_maj[0]);
         // Escaped: infinite lights (integrators.cpp:1090-1107)
         for (int i = 0; i < s.nlights; ++i) {
-            if (s.light_type[i] != 1) continue;
-            Spec Le = s.light_scale[i] * SampleDense(s.light_L[i], l);
+            if (s.light_type[i] == 0) continue;
+            Spec Le;
+            if (s.light_type[i] == 1) {
+                Le = s.light_scale[i] * SampleDense(s.light_L[i], l);
+            } else {   // ImageInfiniteLight::Le (lights.h:581-585)
+                const ImageLight &il = sv.img[i];
+                V3 wl = Normalize(ImageLight::Mul(il.lfr, ray.d));
+                float eu, ev;
+                EqualAreaSphereToSquare(wl, &eu, &ev);
+                Le = il.ImageLe(eu, ev, l, s.light_illuminant, s.light_scale[i]);
+            }
             if (!Le) continue;
             if (depth == 0 || specularBounce)
                 L = L + beta * Le / r_u.Average();
             else {
-                float p_l = (1.f / (s.nlights + 0)) * 0.f;  // PMF * PDF_Li(allowIncompletePDF=true) = 0
+                // lightSampler.PMF * PDF_Li(prevIntrContext, ray.d, allowIncompletePDF = true)
+                float pdfLi = 0;
+                if (s.light_type[i] == 2) {   // lights.cpp:1042-1052 (wLight not normalised)
+                    const ImageLight &il = sv.img[i];
+                    float eu, ev;
+                    EqualAreaSphereToSquare(ImageLight::Mul(il.lfr, ray.d), &eu, &ev);
+                    pdfLi = il.compensated.PDF(eu, ev) / (4 * Pi);
+                }
+                float p_l = (1.f / (s.nlights + 0)) * pdfLi;
                 r_l = r_l * p_l;
                 L = L + beta * Le / (r_u + r_l).Average();
             }
@@ -1497,6 +1651,29 @@ void oracle_canon_sincos(float x, float *s, float *c) {
     *c = (float)cd;
 }
 
+
+// ImageInfiniteLight pieces (test infrastructure)
+void oracle_equal_area_square_to_sphere(float u, float v, float *out) {
+    V3 w = EqualAreaSquareToSphere(u, v);
+    out[0] = w.x; out[1] = w.y; out[2] = w.z;
+}
+void oracle_equal_area_sphere_to_square(float x, float y, float z, float *out) {
+    EqualAreaSphereToSquare({x, y, z}, out, out + 1);
+}
+void oracle_remap_octahedral(int x, int y, int res, int *out) {
+    RemapOctahedral(&x, &y, res);
+    out[0] = x; out[1] = y;
+}
+// PiecewiseConstant2D over [0,1]^2 of func (nu x nv): n samples (u0, u1) -> (x, y, pdf, PDF(x, y))
+void oracle_pc2d(const float *func, int nu, int nv, int n, const float *u, float *out) {
+    PC2D d;
+    d.Build(func, nu, nv);
+    for (int i = 0; i < n; ++i) {
+        float x, y, pdf;
+        d.Sample(u[2 * i], u[2 * i + 1], &x, &y, &pdf);
+        out[4 * i] = x; out[4 * i + 1] = y; out[4 * i + 2] = pdf; out[4 * i + 3] = d.PDF(x, y);
+    }
+}
 
 // RGBGridMedium (test infrastructure)
 float oracle_rsp_eval(float c0, float c1, float c2, float lambda) { return Rsp{c0, c1, c2}(lambda); }
