@@ -124,6 +124,18 @@ def main():
     spp_total = 256
     while spp_total < needed:
         spp_total *= 2
+    # ZSobol's 32-bit index needs Morton(pixel) << log2(spp) < 2^32: at most 2^(32 - 2 log2 res)
+    # sample indices (1024 at 720p/1080p). Longer runs wrap the index range: every step still
+    # traces S fresh paths per pixel (nothing is reused), later steps repeat earlier indices.
+    res_pow2 = 1
+    while res_pow2 < max(args.width, args.height):
+        res_pow2 *= 2
+    spp_cap = 1 << (32 - 2 * (res_pow2.bit_length() - 1))
+    wrap = spp_total > spp_cap and args.sampler == "zsobol"
+    if wrap:
+        spp_total = spp_cap
+        if spp_total % S:
+            raise SystemExit(f"--spp-per-step {S} must divide the ZSobol index range {spp_total} for this run length")
     scene = scenes.s_cloud(density, width=args.width, height=args.height, sampler=args.sampler, spp=spp_total,
                            filter=args.filter)
     integ = VolPathIntegrator(scene, maxdepth=scenes.CLOUD_MAXDEPTH, spp=args.spp_per_step, seed=0, device=dev,
@@ -136,7 +148,7 @@ def main():
 
     def step(k):
         # asynchronous on the context stream: steps queue back to back
-        base = (k * world + rank) * S
+        base = ((k * world + rank) * S) % spp_total if wrap else (k * world + rank) * S
         integ.ctx.render(base, base + S, 0, scenes.CLOUD_MAXDEPTH)
 
     for k in range(args.warmup):
@@ -222,7 +234,8 @@ def main():
             "config": {"workload": f"S-cloud-{n} GridMedium, perspective {args.width}x{args.height}, "
                                    f"{S} spp/step/GPU, maxdepth {scenes.CLOUD_MAXDEPTH}, {args.sampler} sampler "
                                    f"(pixelsamples {spp_total}), {args.filter} filter",
-                       "global_batch": samples // args.steps, "parallelism": f"sample-shard x{world}"},
+                       "global_batch": samples // args.steps, "parallelism": f"sample-shard x{world}",
+                       "sample_index_wrap": wrap},
             "roofline": {
                 "kernel": kname,
                 "bound": "hbm",
