@@ -103,6 +103,8 @@ SIGNATURES = {
     "avr_camera": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, c_float_p, c_float_p]),
     "avr_light_image": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, c_float_p, c_float_p, c_float_p,
                                        c_float_p, c_float_p]),
+    "avr_flip": (ctypes.c_int, [ctypes.c_void_p, c_float_p, c_float_p, ctypes.c_int, ctypes.c_int, ctypes.c_float,
+                                c_float_p]),
     "avr_film_image_device": (ctypes.c_int, [ctypes.c_void_p, c_float_p, ctypes.c_int, ctypes.c_void_p]),
     "avr_film_set_reference": (ctypes.c_int, [ctypes.c_void_p, c_float_p, c_float_p, ctypes.c_int]),
     "avr_film_metric": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, c_float_p]),
@@ -346,6 +348,16 @@ class Context:
         _check(self.lib.avr_film_export_device(self.h, ctypes.c_void_p(d_dst_ptr)))
 
     METRICS = {"MSE": 0, "MAE": 1, "MRSE": 2, "ME": 3}
+
+    def flip(self, test_rgb, reference_rgb, ppd=0.0):
+        """FLIP error map (H, W) of two (H, W, 3) sRGB-encoded images (ComputeFLIPError)."""
+        t = np.ascontiguousarray(test_rgb, np.float32)
+        r = np.ascontiguousarray(reference_rgb, np.float32)
+        if t.shape != r.shape or t.ndim != 3 or t.shape[2] != 3:
+            raise ValueError("FLIP needs two (H, W, 3) images of the same resolution")
+        out = np.zeros(t.shape[:2], np.float32)
+        _check(self.lib.avr_flip(self.h, _fp(t), _fp(r), t.shape[1], t.shape[0], float(ppd), _fp(out)))
+        return out
 
     def film_image_device(self, d_out_ptr, output_from_sensor, fp16=True):
         m = np.ascontiguousarray(output_from_sensor, np.float32).reshape(9)

@@ -1204,6 +1204,52 @@ int avr_film_metric(avr_context *c, int metric, float *out) {
     return AVR_OK;
 }
 
+// FLIP for `imgtool diff --metric FLIP` (src/ext/flip/flip.cpp:1085-1112, ComputeFLIPError)
+int avr_flip(avr_context *c, const float *test, const float *ref, int width, int height, float ppd, float *error) {
+    if (!c || !test || !ref || !error || width < 1 || height < 1) return fail(AVR_ERR_ARG, "avr_flip: bad arguments");
+    HIP_TRY(hipSetDevice(c->device));
+    if (!(ppd > 0)) ppd = avr::flip::ppd_default();
+    std::vector<float> sf, ef, pf;
+    const int rs = avr::flip::spatial_filter(ppd, sf);
+    const int rd = avr::flip::detection_filter(ppd, false, ef);
+    (void)avr::flip::detection_filter(ppd, true, pf);
+    const float cmax = avr::flip::max_distance();
+    const size_t n = (size_t)width * height;
+    float *d_in = nullptr, *d_f = nullptr, *d_out = nullptr;
+    avr::flip::F4 *d_yc = nullptr;
+    auto cleanup = [&]() {
+        if (d_in) (void)hipFree(d_in);
+        if (d_f) (void)hipFree(d_f);
+        if (d_out) (void)hipFree(d_out);
+        if (d_yc) (void)hipFree(d_yc);
+    };
+    const size_t nf = sf.size() + ef.size() + pf.size();
+    if (dalloc(&d_in, 6 * n) != hipSuccess || dalloc(&d_f, nf) != hipSuccess || dalloc(&d_out, n) != hipSuccess ||
+        dalloc(&d_yc, 2 * n) != hipSuccess) {
+        cleanup();
+        return fail(AVR_ERR_HIP, "avr_flip: allocation failed");
+    }
+    std::vector<float> filt(nf);
+    std::copy(sf.begin(), sf.end(), filt.begin());
+    std::copy(ef.begin(), ef.end(), filt.begin() + sf.size());
+    std::copy(pf.begin(), pf.end(), filt.begin() + sf.size() + ef.size());
+    hipError_t e = hipMemcpyAsync(d_in, test, 3 * n * sizeof(float), hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(d_in + 3 * n, ref, 3 * n * sizeof(float), hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(d_f, filt.data(), nf * sizeof(float), hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(avr::k_flip_prep, dim3(blocks_for((long long)n)), dim3(256), 0, c->stream, d_in, d_in + 3 * n,
+                           (int)n, d_yc, d_yc + n);
+        hipLaunchKernelGGL(avr::k_flip_error, dim3(blocks_for((long long)n)), dim3(256), 0, c->stream, d_yc, d_yc + n,
+                           width, height, d_f, rs, d_f + sf.size(), d_f + sf.size() + ef.size(), rd, cmax, d_out);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(error, d_out, n * sizeof(float), hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    cleanup();
+    if (e != hipSuccess) return fail(AVR_ERR_HIP, std::string("avr_flip: ") + hipGetErrorString(e));
+    return AVR_OK;
+}
+
 int avr_film_read(avr_context *c, double *rgb, double *w) {
     if (!c || !c->has_film || !rgb || !w) return fail(AVR_ERR_STATE, "no film");
     const size_t np = (size_t)c->film.width * c->film.height;

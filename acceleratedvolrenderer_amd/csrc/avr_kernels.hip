@@ -20,6 +20,7 @@
 #include "avr_sampling.h"
 #include "avr_vdb.h"
 #include "avr_envmap.h"
+#include "avr_flip.h"
 
 #include <type_traits>
 
@@ -1854,6 +1855,26 @@ __global__ void k_metric_final(const double *__restrict__ partial, int nblocks, 
     double s = 0;
     for (int b = 0; b < nblocks; ++b) s += partial[b * kMetricSlots + k];
     out[k] = s;
+}
+
+// FLIP (src/ext/flip/flip.cpp:941-984) — k_flip_prep: both images to YCxCz, w = the achromatic
+// channel (Y + 16) / 116 the feature detectors read; k_flip_error: per pixel, the CSF
+// convolution of both images (taps in the reference's row-major order, borders replicated),
+// Lab + Hunt, HyAB colour difference, edge / point detector responses, error = cdiff^(1-fdiff).
+__global__ void __launch_bounds__(256) k_flip_prep(const float *__restrict__ test, const float *__restrict__ ref, int n,
+                                                   flip::F4 *__restrict__ ycT, flip::F4 *__restrict__ ycR) {
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        ycT[i] = flip::prep_pixel(test[3 * i], test[3 * i + 1], test[3 * i + 2]);
+        ycR[i] = flip::prep_pixel(ref[3 * i], ref[3 * i + 1], ref[3 * i + 2]);
+    }
+}
+__global__ void __launch_bounds__(256) k_flip_error(const flip::F4 *__restrict__ ycT, const flip::F4 *__restrict__ ycR,
+                                                    int w, int h, const float *__restrict__ sf, int rs,
+                                                    const float *__restrict__ ef, const float *__restrict__ pf, int rd,
+                                                    float cmax, float *__restrict__ out) {
+    const int n = w * h;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+        out[i] = flip::error_at(ycT, ycR, w, h, i % w, i / w, sf, rs, ef, pf, rd, cmax);
 }
 
 __global__ void __launch_bounds__(256) k_cloud(float *out, int n, long long first, long long count, float density,

@@ -255,6 +255,13 @@ int avr_film_set_reference(avr_context *ctx, const float *reference_rgb, const f
                            int fp16);
 int avr_film_metric(avr_context *ctx, int metric, float *out);
 
+/* FLIP error map (src/ext/flip/flip.cpp ComputeFLIPError, used by `imgtool diff --metric
+ * FLIP`): test and reference are width*height RGB (interleaved, row-major) sRGB-encoded
+ * values as the caller passes them (imgtool clamps to [0,1] first); ppd <= 0 takes the
+ * reference's default 0.7 m / 0.7 m / 3840 px monitor. error: width*height floats. */
+int avr_flip(avr_context *ctx, const float *test_rgb, const float *reference_rgb, int width, int height, float ppd,
+             float *error);
+
 /* Per-sample radiance of the LAST wavefront pass of the last avr_render (replay checks;
  * pbrt's --debugstart analogue, integrators.cpp:74-102). Element id = s*W*H + pixel,
  * s = sampleIndex - first sample of that pass. Writes n_max*4 floats into each of

@@ -646,3 +646,26 @@ def test_image_infinite_light_replay(with_distant):
     assert frac >= 0.999
     assert err <= 0.5 * noise
     integ.close()
+
+
+def test_flip_on_device_matches_reference():
+    """avr_flip (k_flip_prep / k_flip_error) against the reference FLIP's error maps
+    (tests/golden/flip_vectors.npz). The taps are summed in the reference's order and powf is
+    the canonical f64 exp(y log x) rounded once (99.9 % equal to the host libm's powf), so
+    ~99 % of pixels are bit-identical, |difference| <= 2e-6 on errors in [0, 1], means to 1e-6."""
+    import os
+    from acceleratedvolrenderer_amd import capi, imgtool
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    z = np.load(os.path.join(root, "tests", "golden", "flip_vectors.npz"))
+    ctx = capi.Context(0)
+    for case in ("smooth_noise", "edges_ppd20", "identical"):
+        got = ctx.flip(z[case + "_test"], z[case + "_ref"], float(z[case + "_ppd"]))
+        want = z[case + "_flip"]
+        same = float(np.mean(got.view(np.uint32) == want.view(np.uint32)))
+        print(f"flip {case}: max |d| {np.abs(got - want).max():.2e}, bit-identical pixels {same:.4f}")
+        assert np.abs(got - want).max() <= 2e-6
+        assert same >= 0.95
+        assert abs(float(got.mean()) - float(want.mean())) <= 1e-6
+    ctx.close()
+    e = imgtool.diff(z["smooth_noise_test"], z["smooth_noise_ref"], "FLIP")
+    assert abs(e["FLIP"] - float(z["smooth_noise_flip"].mean())) < 1e-5
