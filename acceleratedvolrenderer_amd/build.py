@@ -6,7 +6,7 @@ import subprocess
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 SRC = os.path.join(HERE, "csrc", "avr_capi.hip")
-DEPS = [os.path.join(HERE, "csrc", f) for f in ("avr_capi.hip", "avr_kernels.hip", "avr_numerics.h", "avr_canon.h", "avr_sampling.h", "avr_vdb.h", "avr_envmap.h", "avr_flip.h")] + [
+DEPS = [os.path.join(HERE, "csrc", f) for f in ("avr_capi.hip", "avr_kernels.hip", "avr_numerics.h", "avr_canon.h", "avr_sampling.h", "avr_vdb.h", "avr_envmap.h", "avr_flip.h", "avr_graph.hip", "avr_graph_capi.hip", "avr_graph_host.h")] + [
     os.path.join(ROOT, "include", "avr.h")]
 OUT = os.path.join(HERE, "libavr_hip.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")

@@ -42,6 +42,12 @@ class AvrStats(ctypes.Structure):
         return {k: getattr(self, k) for k, _ in self._fields_}
 
 
+class AvrGraphSampling(ctypes.Structure):
+    """avr_graph_sampling (include/avr.h): the graph tools' sampler setup."""
+    _fields_ = [("sampler", ctypes.c_int), ("seed", ctypes.c_int), ("samples_per_pixel", ctypes.c_int),
+                ("film_width", ctypes.c_int), ("film_height", ctypes.c_int), ("resolution_x", ctypes.c_int)]
+
+
 class AvrVdbGrid(ctypes.Structure):
     """avr_vdb_grid (include/avr.h): one NanoVDB FloatGrid's tree."""
     _fields_ = [
@@ -141,6 +147,27 @@ SIGNATURES = {
     "avr_film_export_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "avr_last_pass_samples": (ctypes.c_int, [ctypes.c_void_p, c_float_p, c_float_p, c_float_p, ctypes.c_longlong,
                                              c_int_p, c_int_p]),
+    "avr_graph_walks": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(AvrGraphSampling), ctypes.c_longlong, c_float_p,
+                                       c_float_p, c_float_p, ctypes.POINTER(ctypes.c_longlong), ctypes.c_int,
+                                       ctypes.c_int, ctypes.c_int, c_float_p, c_int_p]),
+    "avr_graph_light": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(AvrGraphSampling), ctypes.c_int, c_float_p,
+                                       c_float_p, ctypes.c_float, ctypes.c_int, ctypes.c_int, ctypes.c_float,
+                                       c_float_p]),
+    "avr_graph_propagate": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, c_int_p, c_int_p, c_float_p, c_float_p,
+                                           ctypes.c_int, c_float_p, c_int_p]),
+    "avr_graph_propagate_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_longlong, ctypes.c_void_p,
+                                                  ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                                                  ctypes.c_void_p, c_int_p]),
+    "avr_graph_create": (ctypes.c_int, [ctypes.c_float, ctypes.POINTER(ctypes.c_void_p)]),
+    "avr_graph_destroy": (ctypes.c_int, [ctypes.c_void_p]),
+    "avr_graph_add_walks": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_longlong, ctypes.c_int, c_float_p, c_int_p]),
+    "avr_graph_size": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_longlong),
+                                      ctypes.POINTER(ctypes.c_longlong)]),
+    "avr_graph_vertices": (ctypes.c_int, [ctypes.c_void_p, c_float_p, c_int_p]),
+    "avr_graph_edges": (ctypes.c_int, [ctypes.c_void_p, c_int_p, c_int_p, c_int_p]),
+    "avr_graph_transport": (ctypes.c_int, [ctypes.c_void_p, c_int_p, c_int_p, c_float_p]),
+    "avr_graph_in_node_path_length": (ctypes.c_int, [ctypes.c_void_p, c_float_p,
+                                                     ctypes.POINTER(ctypes.c_longlong)]),
 }
 
 _lib = None
@@ -344,6 +371,45 @@ class Context:
         _check(self.lib.avr_transmittance(self.h, len(p0), _fp(p0), _fp(p1), _fp(lam), _fp(out)))
         return out
 
+    # ---- lighting graph (src/graph) ----
+    def graph_walks(self, sampling, o, d, t_first, index0, iterations, sample_index, max_depth):
+        """FreeGraphBuilder::TracePath walks: (points (n_rays*iterations, max_depth, 3), counts)."""
+        o = np.ascontiguousarray(o, np.float32).reshape(-1, 3)
+        d = np.ascontiguousarray(d, np.float32).reshape(-1, 3)
+        t_first = np.ascontiguousarray(t_first, np.float32)
+        index0 = np.ascontiguousarray(index0, np.int64)
+        n = len(o) * int(iterations)
+        pts = np.zeros((n, max(1, int(max_depth)), 3), np.float32)
+        counts = np.zeros(n, np.int32)
+        _check(self.lib.avr_graph_walks(self.h, ctypes.byref(sampling), len(o), _fp(o), _fp(d), _fp(t_first),
+                                        index0.ctypes.data_as(ctypes.POINTER(ctypes.c_longlong)), int(iterations),
+                                        int(sample_index), int(max_depth), _fp(pts),
+                                        counts.ctypes.data_as(c_int_p)))
+        return pts, counts
+
+    def graph_light(self, sampling, vertices, in_dir, radius, points_on_radius, iterations, max_dist_to_center):
+        """LightingCalculator::GetLightVector: per-vertex light (Inv4Pi applied)."""
+        v = np.ascontiguousarray(vertices, np.float32).reshape(-1, 3)
+        dr = np.ascontiguousarray(in_dir, np.float32)
+        out = np.zeros(len(v), np.float32)
+        _check(self.lib.avr_graph_light(self.h, ctypes.byref(sampling), len(v), _fp(v), _fp(dr), float(radius),
+                                        int(points_on_radius), int(iterations), float(max_dist_to_center),
+                                        _fp(out)))
+        return out
+
+    def graph_propagate(self, row_ptr, col, val, light, bounces):
+        """LightingCalculator::ComputeFinalLight: (total light, bounces completed)."""
+        row_ptr = np.ascontiguousarray(row_ptr, np.int32)
+        col = np.ascontiguousarray(col, np.int32)
+        val = np.ascontiguousarray(val, np.float32)
+        light = np.ascontiguousarray(light, np.float32)
+        total = np.zeros(len(light), np.float32)
+        it = ctypes.c_int(0)
+        _check(self.lib.avr_graph_propagate(self.h, len(light), row_ptr.ctypes.data_as(c_int_p),
+                                            col.ctypes.data_as(c_int_p), _fp(val), _fp(light), int(bounces),
+                                            _fp(total), ctypes.byref(it)))
+        return total, it.value
+
     def film_export_device(self, d_dst_ptr):
         _check(self.lib.avr_film_export_device(self.h, ctypes.c_void_p(d_dst_ptr)))
 
@@ -379,3 +445,64 @@ class Context:
         a, b = ctypes.c_void_p(), ctypes.c_void_p()
         _check(self.lib.avr_film_device_ptrs(self.h, ctypes.byref(a), ctypes.byref(b)))
         return a.value, b.value
+
+
+class Graph:
+    """Host FreeGraph assembly (avr_graph_*): walks merged in order, transport CSR."""
+
+    def __init__(self, vertex_radius):
+        self.lib = load()
+        h = ctypes.c_void_p()
+        _check(self.lib.avr_graph_create(float(vertex_radius), ctypes.byref(h)))
+        self.h = h
+        self.radius = float(vertex_radius)
+
+    def close(self):
+        if self.h:
+            self.lib.avr_graph_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def add_walks(self, points, counts, max_depth):
+        points = np.ascontiguousarray(points, np.float32)
+        counts = np.ascontiguousarray(counts, np.int32)
+        _check(self.lib.avr_graph_add_walks(self.h, len(counts), int(max_depth), _fp(points),
+                                            counts.ctypes.data_as(c_int_p)))
+
+    def size(self):
+        nv, ne = ctypes.c_longlong(), ctypes.c_longlong()
+        _check(self.lib.avr_graph_size(self.h, ctypes.byref(nv), ctypes.byref(ne)))
+        return nv.value, ne.value
+
+    def vertices(self):
+        nv, _ = self.size()
+        xyz = np.zeros((nv, 3), np.float32)
+        smp = np.zeros(nv, np.int32)
+        _check(self.lib.avr_graph_vertices(self.h, _fp(xyz), smp.ctypes.data_as(c_int_p)))
+        return xyz, smp
+
+    def edges(self):
+        _, ne = self.size()
+        f, t, s = (np.zeros(ne, np.int32) for _ in range(3))
+        _check(self.lib.avr_graph_edges(self.h, f.ctypes.data_as(c_int_p), t.ctypes.data_as(c_int_p),
+                                        s.ctypes.data_as(c_int_p)))
+        return f, t, s
+
+    def transport(self):
+        nv, ne = self.size()
+        rp = np.zeros(nv + 1, np.int32)
+        col = np.zeros(ne, np.int32)
+        val = np.zeros(ne, np.float32)
+        _check(self.lib.avr_graph_transport(self.h, rp.ctypes.data_as(c_int_p), col.ctypes.data_as(c_int_p),
+                                            _fp(val)))
+        return rp, col, val
+
+    def in_node_path_length(self):
+        a, n = ctypes.c_float(), ctypes.c_longlong()
+        _check(self.lib.avr_graph_in_node_path_length(self.h, ctypes.byref(a), ctypes.byref(n)))
+        return a.value, n.value

@@ -10,6 +10,7 @@
 // Everything is enqueued on one HIP stream; the host reads back one int (the
 // survivor count) per depth iteration to size the next launch and stop early.
 #include "avr_kernels.hip"
+#include "avr_graph.hip"
 #include "../../include/avr.h"
 
 #include <climits>
@@ -1304,3 +1305,5 @@ int avr_film_export_device(avr_context *c, void *dst) {
 }
 
 }  // extern "C"
+
+#include "avr_graph_capi.hip"

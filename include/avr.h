@@ -262,6 +262,71 @@ int avr_film_metric(avr_context *ctx, int metric, float *out);
 int avr_flip(avr_context *ctx, const float *test_rgb, const float *reference_rgb, int width, int height, float ppd,
              float *error);
 
+/* ---- Lighting graph (src/graph/, the fork's own SampleT_maj callers) ----
+ * The medium is the context's (avr_medium_*); geometry model: the medium's bounds box is
+ * the boundary primitive. Sampling follows the reference's graph tools
+ * (cmd/graph_maker.cpp:97-104): the scene sampler at its film resolution with
+ * Options->pixelSamples, sampling index i -> pixel (i % resolution_x, i / resolution_x)
+ * (graph/util.h:816-817). */
+typedef struct avr_graph_sampling {
+    int sampler;             /* 0 IndependentSampler, 1 ZSobolSampler                     */
+    int seed;                /* sampler seed (Options->seed)                              */
+    int samples_per_pixel;   /* Options->pixelSamples (RoundUpPow2(lightIterations))      */
+    int film_width, film_height; /* the sampler's full resolution (ZSobol Morton layout)  */
+    int resolution_x;        /* Options->graph.samplingResolution.x                       */
+} avr_graph_sampling;
+
+/* FreeGraphBuilder::TracePath (free/free_graph_builder.cpp:19-141), the medium walk: for
+ * each of n_rays rays (origin o, direction d, first segment end t_first = the medium exit
+ * after SkipIntersection, BuildGraph :166-196) `iterations` walks, walk w = ray*iterations+i
+ * started with StartPixelSample(pixel(index0[ray] + i), sample_index). Writes up to
+ * max_depth scatter points per walk to points[(w*max_depth + k)*3 ..] and the count to
+ * counts[w] (count == max_depth: the reference's forcedEnd). Host arrays, synchronous. */
+int avr_graph_walks(avr_context *ctx, const avr_graph_sampling *smp, long long n_rays, const float *o, const float *d,
+                    const float *t_first, const long long *index0, int iterations, int sample_index, int max_depth,
+                    float *points, int *counts);
+
+/* LightingCalculator::GetLightVector (lighting_calculator.cpp:84-155) with
+ * ComputeRaysToSphere (graph/util.h:814-840) and SampleTransmittance (util.h:344-366):
+ * light[v] = Inv4Pi * average over the disk points of vertex v (GetDiskPoints(vertex -
+ * in_dir * max_dist_to_center * 2, sphere_radius, points_on_radius, in_dir)) whose ray along
+ * in_dir crosses the medium box and the vertex's sphere inside the medium, of the average of
+ * `iterations` ratio-tracking transmittances to a uniform point of the sphere chord.
+ * vertices: n_vertices*3 (ids 0..n-1 in order). Host arrays, synchronous. */
+int avr_graph_light(avr_context *ctx, const avr_graph_sampling *smp, int n_vertices, const float *vertices,
+                    const float in_dir[3], float sphere_radius, int points_on_radius, int iterations,
+                    float max_dist_to_center, float *light);
+
+/* LightingCalculator::ComputeFinalLight (lighting_calculator.cpp:23-59): total = light +
+ * sum of T^k light for k = 1..bounces, T in CSR (row_ptr[n+1], col ascending per row, val),
+ * stopping before the first bounce whose vector holds a NaN/Inf; *iterations = bounces
+ * completed. _device: device arrays, async on the context's stream (iterations read back
+ * synchronously when non-null). */
+int avr_graph_propagate(avr_context *ctx, int n, const int *row_ptr, const int *col, const float *val,
+                        const float *light, int bounces, float *total, int *iterations);
+int avr_graph_propagate_device(avr_context *ctx, int n, long long nnz, const int *row_ptr, const int *col,
+                               const float *val, const float *light, int bounces, float *total, int *iterations);
+
+/* FreeGraph assembly on the host (free_graph_builder.cpp:100-131, graph.cpp:134-229):
+ * walks merged in walk order into vertices of radius `vertex_radius` — a scatter point joins
+ * the nearest vertex strictly within the radius (nanoflann's RadiusResultSet bound; the
+ * reference takes the first one its kd-tree reports), else the path's previous vertex when
+ * within the radius, else becomes a new vertex; consecutive path vertices add edge samples;
+ * each traced segment after a scatter counts a sample of the path's last vertex
+ * (HandlePotentialPathEnd). avr_graph_transport: GetTransportMatrix (:61-82) as CSR rows
+ * (row = vertex, col ascending, val = edge samples / vertex samples); row_ptr n+1, col/val
+ * n_edges entries. */
+typedef struct avr_graph avr_graph;
+int avr_graph_create(float vertex_radius, avr_graph **out);
+int avr_graph_destroy(avr_graph *g);
+int avr_graph_add_walks(avr_graph *g, long long n_walks, int max_depth, const float *points, const int *counts);
+int avr_graph_size(avr_graph *g, long long *n_vertices, long long *n_edges);
+int avr_graph_vertices(avr_graph *g, float *xyz, int *samples);
+int avr_graph_edges(avr_graph *g, int *from, int *to, int *samples);
+int avr_graph_transport(avr_graph *g, int *row_ptr, int *col, float *val);
+/* UseAndRemovePathInfo's in-node path length average (free_graph_builder.cpp:241-273) */
+int avr_graph_in_node_path_length(avr_graph *g, float *average, long long *count);
+
 /* Per-sample radiance of the LAST wavefront pass of the last avr_render (replay checks;
  * pbrt's --debugstart analogue, integrators.cpp:74-102). Element id = s*W*H + pixel,
  * s = sampleIndex - first sample of that pass. Writes n_max*4 floats into each of

@@ -170,7 +170,60 @@ def lib():
         L.oracle_vdb_bounds.argtypes = [ctypes.c_void_p, ctypes.c_void_p, c_float_p]
         L.oracle_vdb_majorant.argtypes = [ctypes.c_void_p, c_float_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                           c_float_p]
+        c_ll_p = ctypes.POINTER(ctypes.c_longlong)
+        L.oracle_graph_light.argtypes = [ctypes.POINTER(OracleScene), ctypes.c_int, c_float_p, c_float_p,
+                                         ctypes.c_float, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float,
+                                         c_float_p]
+        L.oracle_graph_walks.argtypes = [ctypes.POINTER(OracleScene), ctypes.c_int, c_float_p, c_float_p, c_float_p,
+                                         c_ll_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_float_p,
+                                         c_int_p]
+        L.oracle_graph_propagate.restype = ctypes.c_int
+        L.oracle_graph_propagate.argtypes = [ctypes.c_int, c_int_p, c_int_p, c_float_p, c_float_p, ctypes.c_int,
+                                             c_float_p]
+        L.oracle_graph_sphere_hits.restype = ctypes.c_int
+        L.oracle_graph_sphere_hits.argtypes = [ctypes.c_float] * 4 + [c_float_p, c_float_p, c_float_p]
+        L.oracle_graph_box_hits.restype = ctypes.c_int
+        L.oracle_graph_box_hits.argtypes = [ctypes.POINTER(OracleScene), c_float_p, c_float_p, c_float_p]
+        L.oracle_graph_disk_points.restype = ctypes.c_int
+        L.oracle_graph_disk_points.argtypes = [c_float_p, ctypes.c_float, ctypes.c_int, c_float_p, c_float_p,
+                                               ctypes.c_int]
     return _lib
+
+
+# ---------------------------------------------------------------------------
+# Lighting graph (src/graph) — oracle_graph_* in volpath_oracle.cpp
+
+def _ip(a):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_int))
+
+
+def graph_sphere_hits(c, r, o, d):
+    """(type, t0, t1) of the model's GetHits(sphere) — 0 OutsideTwoHits, 2 zero, 3 InsideOneHit."""
+    t = np.zeros(2, np.float32)
+    o = np.ascontiguousarray(o, np.float32)
+    d = np.ascontiguousarray(d, np.float32)
+    ty = lib().oracle_graph_sphere_hits(float(c[0]), float(c[1]), float(c[2]), float(r), fp(o), fp(d), fp(t))
+    return ty, t[0], t[1]
+
+
+def graph_disk_points(center, radius, n, direction):
+    cap = (2 * n + 1) ** 2
+    out = np.zeros((cap, 3), np.float32)
+    c = np.ascontiguousarray(center, np.float32)
+    d = np.ascontiguousarray(direction, np.float32)
+    k = lib().oracle_graph_disk_points(fp(c), float(radius), int(n), fp(d), fp(out), cap)
+    return out[:k]
+
+
+def graph_propagate(n, rowptr, col, val, light, bounces):
+    """ComputeFinalLight restated: (total light, iterations completed)."""
+    rowptr = np.ascontiguousarray(rowptr, np.int32)
+    col = np.ascontiguousarray(col, np.int32)
+    val = np.ascontiguousarray(val, np.float32)
+    light = np.ascontiguousarray(light, np.float32)
+    total = np.zeros(n, np.float32)
+    it = lib().oracle_graph_propagate(int(n), _ip(rowptr), _ip(col), fp(val), fp(light), int(bounces), fp(total))
+    return total, it
 
 
 LIBM_MODES = {"platform": 0, "canonical": 1}
@@ -392,6 +445,57 @@ class OracleRun:
         set_libm(self.libm)
         lib().oracle_transmittance(ctypes.byref(self.s), len(p0), fp(p0), fp(p1), lambda_u, fp(out))
         return out
+
+    def graph_light(self, verts, in_dir, radius, points_on_radius, iterations, res_x, max_dist_to_center,
+                    sampler=None):
+        """LightingCalculator::GetLightVector (per-vertex light, Inv4Pi applied).
+        sampler = (type, seed, spp, width, height) of the scene sampler, default: the scene's."""
+        verts = np.ascontiguousarray(verts, np.float32)
+        d = np.ascontiguousarray(in_dir, np.float32)
+        out = np.zeros(len(verts), np.float32)
+        set_libm(self.libm)
+        with self._graph_sampler(sampler) as s:
+            lib().oracle_graph_light(ctypes.byref(s), len(verts), fp(verts), fp(d), float(radius),
+                                     int(points_on_radius), int(iterations), int(res_x), float(max_dist_to_center),
+                                     fp(out))
+        return out
+
+    def graph_walks(self, o, d, t_first, index0, iterations, sample_index, res_x, max_depth, sampler=None):
+        """FreeGraphBuilder::TracePath walks: (points[nrays*iterations, max_depth, 3], counts)."""
+        o = np.ascontiguousarray(o, np.float32)
+        d = np.ascontiguousarray(d, np.float32)
+        t_first = np.ascontiguousarray(t_first, np.float32)
+        index0 = np.ascontiguousarray(index0, np.int64)
+        n = len(o) * int(iterations)
+        pts = np.zeros((n, max(1, int(max_depth)), 3), np.float32)
+        counts = np.zeros(n, np.int32)
+        set_libm(self.libm)
+        with self._graph_sampler(sampler) as s:
+            lib().oracle_graph_walks(ctypes.byref(s), len(o), fp(o), fp(d), fp(t_first),
+                                     index0.ctypes.data_as(ctypes.POINTER(ctypes.c_longlong)), int(iterations),
+                                     int(sample_index), int(res_x), int(max_depth), fp(pts), _ip(counts))
+        return pts, counts
+
+    def graph_box_hits(self, o, d):
+        t = np.zeros(2, np.float32)
+        ty = lib().oracle_graph_box_hits(ctypes.byref(self.s), fp(np.ascontiguousarray(o, np.float32)),
+                                         fp(np.ascontiguousarray(d, np.float32)), fp(t))
+        return ty, t[0], t[1]
+
+    def _graph_sampler(self, sampler):
+        import contextlib
+
+        @contextlib.contextmanager
+        def ctx():
+            s = self.s
+            saved = (s.sampler_type, s.seed, s.samples_per_pixel, s.width, s.height)
+            if sampler is not None:
+                s.sampler_type, s.seed, s.samples_per_pixel, s.width, s.height = [int(v) for v in sampler]
+            try:
+                yield s
+            finally:
+                s.sampler_type, s.seed, s.samples_per_pixel, s.width, s.height = saved
+        return ctx()
 
     def transmittance4(self, p0, p1, lam):
         """Integrator::Tr at explicit wavelengths: (n, 4)."""

@@ -2007,6 +2007,324 @@ float oracle_blackbody(float lambda, float T) { return Blackbody(lambda, T); }
 float oracle_cloud_density(float x, float y, float z, float density, float wispiness, float frequency) {
     return CloudDensity(V3{x, y, z}, density, wispiness, frequency);
 }
+
+// ===========================================================================
+// Lighting graph (src/graph/): the fork's own SampleT_maj callers.
+//
+// Geometry model: the medium's boundary primitive is its bounds box, hit
+// by a slab test in medium space (the ray mapped by medium_from_render without error
+// offsets; Bounds3::IntersectP, vecmath.h:1547-1571), so GetHits(primitive)
+// (graph/util.h:419-458) yields OutsideTwoHits {t0, t1} for an origin outside and
+// InsideOneHit {t1} for one inside; SkipIntersection moves the origin to ray(t) with no
+// surface offset. Spheres (util.h:280-300, 460-463) use Sphere::BasicIntersect's interval
+// solve (shapes.h:152-200) once: both roots come from one quadratic, where pbrt re-intersects
+// from the spawned exit-side point (t1 differs by round-off; t0 is pbrt's bit for bit).
+namespace graphm {
+enum { OutsideTwoHits = 0, OutsideOneHit = 1, OutsideZeroHits = 2, InsideOneHit = 3 };
+struct Hits { int type; float t[2]; };
+
+static Hits BoxHits(const SceneView &sv, V3 o, V3 d) {
+    V3 om = XPoint(sv.mediumX.mInv, o), dm = XVector(sv.mediumX.mInv, d);
+    float t0, t1;
+    if (!IntersectP(sv.bounds, om, dm, Infinity, &t0, &t1)) return {OutsideZeroHits, {0, 0}};
+    if (t0 > 0) return {OutsideTwoHits, {t0, t1}};
+    return {InsideOneHit, {t1, 0}};
+}
+// Primitive::Intersect(ray, Infinity)->tHit in the same model: the first crossing
+static bool BoxFirstHit(const SceneView &sv, V3 o, V3 d, float *tHit) {
+    Hits h = BoxHits(sv, o, d);
+    if (h.type == OutsideZeroHits) return false;
+    *tHit = h.t[0];
+    return true;
+}
+
+// Interval ops of util/math.h:818-1070 (CPU rounding: NextFloatUp/Down of the float op)
+static inline float MulRoundUp(float a, float b) { return NextFloatUp(a * b); }
+static inline float MulRoundDown(float a, float b) { return NextFloatDown(a * b); }
+static inline float DivRoundUp(float a, float b) { return NextFloatUp(a / b); }
+static inline float DivRoundDown(float a, float b) { return NextFloatDown(a / b); }
+static inline Interval Iv(float lo, float hi) { return {std::min(lo, hi), std::max(lo, hi)}; }
+static inline Interval IAdd(Interval a, Interval b) { return Iv(AddRoundDown(a.low, b.low), AddRoundUp(a.high, b.high)); }
+static inline Interval ISub(Interval a, Interval b) { return Iv(SubRoundDown(a.low, b.high), SubRoundUp(a.high, b.low)); }
+static inline Interval IMul(Interval a, Interval b) {
+    float lp[4] = {MulRoundDown(a.low, b.low), MulRoundDown(a.high, b.low), MulRoundDown(a.low, b.high),
+                   MulRoundDown(a.high, b.high)};
+    float hp[4] = {MulRoundUp(a.low, b.low), MulRoundUp(a.high, b.low), MulRoundUp(a.low, b.high),
+                   MulRoundUp(a.high, b.high)};
+    return Iv(std::min({lp[0], lp[1], lp[2], lp[3]}), std::max({hp[0], hp[1], hp[2], hp[3]}));
+}
+static inline bool InRange0(Interval i) { return 0 >= i.low && 0 <= i.high; }
+static inline Interval IDiv(Interval a, Interval b) {
+    if (InRange0(b)) return Iv(-Infinity, Infinity);
+    float lq[4] = {DivRoundDown(a.low, b.low), DivRoundDown(a.high, b.low), DivRoundDown(a.low, b.high),
+                   DivRoundDown(a.high, b.high)};
+    float hq[4] = {DivRoundUp(a.low, b.low), DivRoundUp(a.high, b.low), DivRoundUp(a.low, b.high),
+                   DivRoundUp(a.high, b.high)};
+    return Iv(std::min({lq[0], lq[1], lq[2], lq[3]}), std::max({hq[0], hq[1], hq[2], hq[3]}));
+}
+static inline Interval IScale(float f, Interval i) {   // Float * Interval (math.h:1007-1012)
+    if (f > 0) return Iv(MulRoundDown(f, i.low), MulRoundUp(f, i.high));
+    return Iv(MulRoundDown(f, i.high), MulRoundUp(f, i.low));
+}
+static inline Interval ISqr(Interval i) {              // Sqr(Interval), math.h:988-995
+    float alow = std::abs(i.low), ahigh = std::abs(i.high);
+    if (alow > ahigh) std::swap(alow, ahigh);
+    if (InRange0(i)) return Iv(0, MulRoundUp(ahigh, ahigh));
+    return Iv(MulRoundDown(alow, alow), MulRoundUp(ahigh, ahigh));
+}
+static inline Interval ISqrt(Interval i) {             // Sqrt(Interval), math.h:1069-1071
+    return Iv(std::max<float>(0, NextFloatDown(std::sqrt(i.low))), NextFloatUp(std::sqrt(i.high)));
+}
+
+// Sphere of radius r at c: objectFromRender = Inverse(Translate(c)) (util.h:289-291), the ray
+// mapped as exact Point3fi / Vector3fi (transform.h:136-180, 276-310), then the quadric
+// solve of Sphere::BasicIntersect (shapes.h:152-191) with tMax = Infinity. A full sphere
+// never clips. Returns hit-type and (Float) midpoints of the roots.
+static Hits SphereHits(V3 c, float r, V3 o, V3 d) {
+    const float m[3][4] = {{1, 0, 0, -c.x}, {0, 1, 0, -c.y}, {0, 0, 1, -c.z}};
+    Interval oi[3], di[3];
+    const float ov[3] = {o.x, o.y, o.z}, dv[3] = {d.x, d.y, d.z};
+    for (int k = 0; k < 3; ++k) {
+        float xp = (m[k][0] * ov[0] + m[k][1] * ov[1]) + (m[k][2] * ov[2] + m[k][3]);
+        float e = gamma(3) * (std::abs(m[k][0] * ov[0]) + std::abs(m[k][1] * ov[1]) + std::abs(m[k][2] * ov[2]) +
+                              std::abs(m[k][3]));
+        oi[k] = Interval::FromValueAndError(xp, e);
+        float vp = m[k][0] * dv[0] + m[k][1] * dv[1] + m[k][2] * dv[2];
+        float ve = gamma(3) * (std::abs(m[k][0] * dv[0]) + std::abs(m[k][1] * dv[1]) + std::abs(m[k][2] * dv[2]));
+        di[k] = Interval::FromValueAndError(vp, ve);
+    }
+    Interval a = IAdd(IAdd(ISqr(di[0]), ISqr(di[1])), ISqr(di[2]));
+    Interval b = IScale(2, IAdd(IAdd(IMul(di[0], oi[0]), IMul(di[1], oi[1])), IMul(di[2], oi[2])));
+    Interval R = Interval::Exact(r);
+    Interval cc = ISub(IAdd(IAdd(ISqr(oi[0]), ISqr(oi[1])), ISqr(oi[2])), ISqr(R));
+    Interval bq = IDiv(b, IScale(2, a));
+    Interval v[3];
+    for (int k = 0; k < 3; ++k) v[k] = ISub(oi[k], IMul(bq, di[k]));   // bq * di = {bq * di.x, ..} (vecmath.h:351-353, 387-389)
+    Interval len = ISqrt(IAdd(IAdd(ISqr(v[0]), ISqr(v[1])), ISqr(v[2])));
+    Interval discrim = IMul(IMul(IScale(4, a), IAdd(R, len)), ISub(R, len));
+    if (discrim.low < 0) return {OutsideZeroHits, {0, 0}};
+    Interval rootDiscrim = ISqrt(discrim);
+    Interval q = (b.Midpoint() < 0) ? IScale(-.5f, ISub(b, rootDiscrim)) : IScale(-.5f, IAdd(b, rootDiscrim));
+    Interval t0 = IDiv(q, a), t1 = IDiv(cc, q);
+    if (t0.low > t1.low) std::swap(t0, t1);
+    if (t0.high > Infinity || t1.low <= 0) return {OutsideZeroHits, {0, 0}};
+    if (t0.low <= 0) return {InsideOneHit, {t1.Midpoint(), 0}};
+    return {OutsideTwoHits, {t0.Midpoint(), t1.Midpoint()}};
+}
+
+// util::GetDiskPoints — graph/util.h:179-204
+static void DiskPoints(V3 center, float radius, int n, V3 dir, std::vector<V3> &out) {
+    out.clear();
+    if (n == 0) { out.push_back(center); return; }
+    V3 xv, yv;
+    CoordinateSystem(dir, &xv, &yv);
+    float step = radius / (float)(n + 1);
+    xv = xv * step;
+    yv = yv * step;
+    for (int x = -n; x <= n; ++x)
+        for (int y = -n; y <= n; ++y) {
+            V3 p = (center + (float)x * xv) + (float)y * yv;
+            if (Length(p - center) <= radius) out.push_back(p);
+        }
+}
+
+// util::StartEndT / GetStartEndT — util.h:469-503
+struct StartEnd { float startT, endT, startScatterT, endScatterT; bool notInMedium; };
+static StartEnd GetStartEnd(const Hits &mh, const Hits &sh) {
+    float mEntry = mh.type == OutsideTwoHits ? mh.t[0] : 0, sEntry = sh.type == OutsideTwoHits ? sh.t[0] : 0;
+    float mExit = mh.type == OutsideTwoHits ? mh.t[1] : mh.t[0], sExit = sh.type == OutsideTwoHits ? sh.t[1] : sh.t[0];
+    StartEnd se;
+    se.startT = mEntry;
+    se.endT = std::min(mExit, sExit);
+    se.startScatterT = std::max(mEntry, sEntry);
+    se.endScatterT = se.endT;
+    se.notInMedium = se.endT < se.startScatterT || se.endScatterT < se.startT;
+    return se;
+}
+
+// Pixel of a graph sampling index (util.h:816-817): samplingResolution.x wide rows
+static inline void IndexPixel(uint64_t index, int resX, int *px, int *py) {
+    *py = (int)(index / (uint64_t)resX);
+    *px = (int)(index - (uint64_t)*py * (uint64_t)resX);
+}
+
+// util::SampleTransmittance — util.h:344-366: single-channel ratio tracking. The RNG's
+// two constructor arguments are unsequenced in the reference (`RNG rng(Hash(Get1D()),
+// Hash(Get1D()))`); GCC — the compiler oracle/ref builds the reference with — evaluates
+// them right to left, so the FIRST draw seeds the offset and the SECOND the sequence.
+static float SampleTransmittance(const SceneView &sv, Ray ray, float tMax, Sampler &smp, const OracleScene &s,
+                                 const Lambda &l) {
+    float uOff = smp.Get1D();
+    float uSeq = smp.Get1D();
+    RNG rng(HashFloat(uSeq), HashFloat(uOff));
+    float Tr = 1;
+    float u = smp.Get1D();
+    SampleT_maj(sv, ray, tMax, u, rng, l, [&](V3, const MediumProps &mp, Spec sigma_maj, Spec) {
+        Spec sigma_n = ClampZero(sigma_maj - mp.sigma_a - mp.sigma_s);
+        Tr *= sigma_n[0] / sigma_maj[0];
+        return Tr != 0;
+    });
+    (void)s;
+    return Tr;
+}
+
+// util::Averager::GetAverage (util.h:545-565) with unit weights
+static inline float Average(const std::vector<float> &v) {
+    if (v.empty()) return 0;
+    float avg = 0, w = 0;
+    for (float x : v) { avg += x * 1; w += 1; }
+    return avg / w;
+}
+}  // namespace graphm
+
+// LightingCalculator::GetLightVector (lighting_calculator.cpp:84-155) with
+// ComputeRaysToSphere(rayInSphere = nullopt) (util.h:814-840): per vertex (list index =
+// vertex id), disk points around vertex - inDir * maxDistToCenter * 2, a ray along inDir
+// from each; rays that cross both the medium box and the vertex's sphere average
+// `iterations` ratio-tracking estimates to a uniform point of the sphere chord; the light is
+// that average over disk points times Inv4Pi. Sampler = the scene's (s->sampler_type, seed,
+// samples_per_pixel, width x height), StartPixelSample(pixel(index), i).
+void oracle_graph_light(const OracleScene *s, int nv, const float *verts, const float *inDir, float radius,
+                        int pointsOnRadius, int iterations, int resX, float maxDistToCenter, float *out) {
+    using namespace graphm;
+    SceneView sv(*s);
+    Lambda l = SampleVisible(0.f);
+    V3 dir = {inDir[0], inDir[1], inDir[2]};
+    std::vector<V3> disk;
+    Sampler smp;
+    for (int v = 0; v < nv; ++v) {
+        V3 c = {verts[3 * v], verts[3 * v + 1], verts[3 * v + 2]};
+        V3 origin = c - (dir * maxDistToCenter) * 2.f;
+        DiskPoints(origin, radius, pointsOnRadius, dir, disk);
+        std::vector<float> perPoint;
+        uint64_t startIndex = (uint64_t)v * disk.size();
+        for (size_t k = 0; k < disk.size(); ++k) {
+            uint64_t curIndex = startIndex + k;
+            Hits mh = BoxHits(sv, disk[k], dir), sh = SphereHits(c, radius, disk[k], dir);
+            if (mh.type != OutsideTwoHits || sh.type != OutsideTwoHits) continue;
+            StartEnd se = GetStartEnd(mh, sh);
+            if (se.notInMedium) continue;
+            Ray ray = {disk[k] + dir * se.startT, dir};   // SkipIntersection (model: no offset)
+            float st = se.startT;
+            se.startT -= st; se.endT -= st; se.startScatterT -= st; se.endScatterT -= st;
+            int px, py;
+            IndexPixel(curIndex, resX, &px, &py);
+            float distInSphere = se.endScatterT - se.startScatterT;
+            std::vector<float> trs;
+            for (int i = 0; i < iterations; ++i) {
+                smp.Start(*s, px, py, i);
+                float curDist = distInSphere * smp.Get1D();
+                float curT = se.startScatterT + curDist;
+                trs.push_back(SampleTransmittance(sv, ray, curT, smp, *s, l));
+            }
+            perPoint.push_back(Average(trs));
+        }
+        out[v] = Average(perPoint) * Inv4Pi;
+    }
+}
+
+// FreeGraphBuilder::TracePath (free/free_graph_builder.cpp:19-141), its medium part: from
+// each ray, `iterations` walks (path index ray * iterations + i, sampling index index0[ray]
+// + i, StartPixelSample(pixel, sampleIndex)). Per segment: two sampler draws hash into the
+// segment RNG (sequenced: RNG(hash0, hash1)), one draw is the first free-flight u; delta
+// tracking with absorb / scatter / null choice; the first segment ends at tFirst, later ones
+// at the box crossing; a real scatter records its point and, below maxDepth, samples the HG
+// phase function (Get2D) for the next direction. Writes up to maxDepth points per walk.
+void oracle_graph_walks(const OracleScene *s, int nrays, const float *o, const float *d, const float *tFirst,
+                        const long long *index0, int iterations, int sampleIndex, int resX, int maxDepth,
+                        float *points, int *counts) {
+    using namespace graphm;
+    SceneView sv(*s);
+    Lambda l = SampleVisible(0.f);
+    Sampler smp;
+    for (int r = 0; r < nrays; ++r)
+        for (int i = 0; i < iterations; ++i) {
+            long long path = (long long)r * iterations + i;
+            int px, py;
+            IndexPixel((uint64_t)(index0[r] + i), resX, &px, &py);
+            smp.Start(*s, px, py, sampleIndex);
+            V3 ro = {o[3 * r], o[3 * r + 1], o[3 * r + 2]}, rd = {d[3 * r], d[3 * r + 1], d[3 * r + 2]};
+            bool usedTHit = false;
+            int k = 0;
+            while (k < maxDepth) {
+                float h0 = smp.Get1D();
+                float h1 = smp.Get1D();
+                RNG rng(HashFloat(h0), HashFloat(h1));
+                float tMax;
+                if (!usedTHit) { tMax = tFirst[r]; usedTHit = true; }
+                else if (!BoxFirstHit(sv, ro, rd, &tMax)) break;
+                bool scattered = false;
+                V3 pScatter = {0, 0, 0};
+                float u = smp.Get1D();
+                SampleT_maj(sv, Ray{ro, rd}, tMax, u, rng, l, [&](V3 p, const MediumProps &mp, Spec sigma_maj, Spec) {
+                    float pAbsorb = mp.sigma_a[0] / sigma_maj[0];
+                    float pScat = mp.sigma_s[0] / sigma_maj[0];
+                    float w[3] = {pAbsorb, pScat, std::max<float>(0, 1 - pAbsorb - pScat)};
+                    float um = rng.Uniform();
+                    int mode = SampleDiscrete3(w, um);
+                    if (mode == 0) return false;
+                    if (mode == 1) { scattered = true; pScatter = p; return false; }
+                    return true;
+                });
+                if (!scattered) break;
+                float *dst = points + 3 * (path * maxDepth + k);
+                dst[0] = pScatter.x; dst[1] = pScatter.y; dst[2] = pScatter.z;
+                ++k;
+                if (k == maxDepth) break;
+                float u0, u1, pdf;
+                smp.Get2D(&u0, &u1);
+                V3 wi = SampleHenyeyGreenstein(-rd, s->g, u0, u1, &pdf);
+                ro = pScatter;
+                rd = wi;
+            }
+            counts[path] = k;
+        }
+}
+
+// LightingCalculator::ComputeFinalLight (lighting_calculator.cpp:23-59) with Eigen's
+// SparseMatrix<float> (column-major) x SparseVector product (the conservative sparse-sparse
+// product: row i accumulates T(i,k) * x(k) over k ascending, starting from the first
+// product) and SparseVector +=. Dense restatement: with nonnegative finite entries the
+// terms Eigen skips (unstored x(k)) add +0. CSR rows must hold ascending columns.
+// Returns the iterations completed (a NaN/Inf in the new vector stops before adding it).
+int oracle_graph_propagate(int n, const int *rowptr, const int *col, const float *val, const float *light, int bounces,
+                           float *total) {
+    std::vector<float> cur(light, light + n), next(n);
+    for (int i = 0; i < n; ++i) total[i] = light[i];
+    int it = 0;
+    for (; it < bounces; ++it) {
+        bool bad = false;
+        for (int i = 0; i < n; ++i) {
+            float acc = 0;
+            for (int e = rowptr[i]; e < rowptr[i + 1]; ++e) acc = (e == rowptr[i]) ? val[e] * cur[col[e]] : acc + val[e] * cur[col[e]];
+            next[i] = acc;
+            if (std::isnan(acc) || std::isinf(acc)) bad = true;
+        }
+        if (bad) break;
+        for (int i = 0; i < n; ++i) total[i] += next[i];
+        cur.swap(next);
+    }
+    return it;
+}
+// Sphere hits / disk points of the model (tests)
+int oracle_graph_sphere_hits(float cx, float cy, float cz, float r, const float *o, const float *d, float *t) {
+    graphm::Hits h = graphm::SphereHits(V3{cx, cy, cz}, r, V3{o[0], o[1], o[2]}, V3{d[0], d[1], d[2]});
+    t[0] = h.t[0]; t[1] = h.t[1];
+    return h.type;
+}
+int oracle_graph_box_hits(const OracleScene *s, const float *o, const float *d, float *t) {
+    SceneView sv(*s);
+    graphm::Hits h = graphm::BoxHits(sv, V3{o[0], o[1], o[2]}, V3{d[0], d[1], d[2]});
+    t[0] = h.t[0]; t[1] = h.t[1];
+    return h.type;
+}
+int oracle_graph_disk_points(const float *center, float radius, int n, const float *dir, float *out, int cap) {
+    std::vector<V3> pts;
+    graphm::DiskPoints(V3{center[0], center[1], center[2]}, radius, n, V3{dir[0], dir[1], dir[2]}, pts);
+    for (size_t i = 0; i < pts.size() && (int)i < cap; ++i) { out[3 * i] = pts[i].x; out[3 * i + 1] = pts[i].y; out[3 * i + 2] = pts[i].z; }
+    return (int)pts.size();
+}
+
 // Fill an n^3 grid with CloudMedium::Density at voxel centres (i+0.5)/n (BASELINE.md S-cloud).
 void oracle_cloud_grid(int n, int z0, int z1, float *out) {
     for (int z = z0; z < z1; ++z)
