@@ -370,6 +370,17 @@ __device__ __forceinline__ Spec grid_emission(const DevMedium &m, V3 p, const Sp
     return Le;
 }
 
+// NanoVDBMedium emission at medium point p (media.h:660-672): LeScale * normalised blackbody
+// of the temperature grid where T > 100 K
+__device__ __forceinline__ Spec vdb_emission(const DevMedium &m, V3 p, const Spec &lam) {
+    float temp = vdb::sample_world(m.vdb_temp, p.x, p.y, p.z);
+    temp = (temp - m.temp_offset) * m.temp_scale;
+    if (!(temp > 100.f)) return Spec::c(0.f);
+    const float nf = blackbody_norm(temp);
+    return Spec{m.vdb_lescale * (blackbody(lam.v0, temp) * nf), m.vdb_lescale * (blackbody(lam.v1, temp) * nf),
+                m.vdb_lescale * (blackbody(lam.v2, temp) * nf), m.vdb_lescale * (blackbody(lam.v3, temp) * nf)};
+}
+
 // ImageInfiniteLight::ImageLe (lights.h:620-627): nearest pixel (octahedral wrap), its
 // RGBIlluminantSpectrum sampled at lambda, times the light scale
 __device__ __forceinline__ Spec image_le(const DevLight &lt, float u, float v, const Spec &lam) {
@@ -435,15 +446,7 @@ __device__ __forceinline__ MediumSample sample_point(const DevMedium &m, V3 p, c
         const float d = vdb::sample_world(m.vdb, p.x, p.y, p.z);
         ms.sigma_a = sig_a * d;
         ms.sigma_s = sig_s * d;
-        if (emissive && m.emissive) {
-            float temp = vdb::sample_world(m.vdb_temp, p.x, p.y, p.z);
-            temp = (temp - m.temp_offset) * m.temp_scale;
-            if (temp > 100.f) {
-                const float nf = blackbody_norm(temp);
-                ms.Le = Spec{m.vdb_lescale * (blackbody(lam.v0, temp) * nf), m.vdb_lescale * (blackbody(lam.v1, temp) * nf),
-                             m.vdb_lescale * (blackbody(lam.v2, temp) * nf), m.vdb_lescale * (blackbody(lam.v3, temp) * nf)};
-            }
-        }
+        if (emissive && m.emissive) ms.Le = vdb_emission(m, p, lam);
         return ms;
     }
     // Bounds3::Offset (vecmath.h:1323-1332); x / 1.0f == x exactly, so a unit box skips it
@@ -1101,15 +1104,20 @@ template <> __device__ __forceinline__ Spec sfrom<Spec>(const Spec &x) { return 
 __device__ __forceinline__ Spec smul(const Spec &a, float b) { return a * b; }
 __device__ __forceinline__ Spec smul(const Spec &a, const Spec &b) { return a * b; }
 
-template <bool kEmissive, bool kGray, bool kZSobol>
+// NanoVDBMedium (kVdb, media.h:602-685): the same loop over the sparse tree. Its 64^3
+// majorant (1 MiB) does not fit LDS and is read through L2 (per-XCD 4 MiB); the density
+// fetch is NanoVDB's index-space trilinear sampler (avr_vdb.h) and emission comes from the
+// temperature grid. GridMedium (!kVdb) keeps its 16^3 majorant in LDS.
+template <bool kEmissive, bool kGray, bool kZSobol, bool kVdb>
 __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_WAVES_SPEC) k_paths(Params P) {
     using S = typename std::conditional<kGray, float, Spec>::type;
     // LDS: majorant grid (16 KiB at pbrt's 16^3) + the 471-entry spectral tables the path
     // samples at path start, NEE and escape (sigma_a, sigma_s, up to 4 light spectra).
-    __shared__ float s_maj[4096];
+    __shared__ float s_maj[kVdb ? 1 : 4096];
     __shared__ float s_tab[(2 + 4) * kNTable];
-    // the host routes majorant grids of more than 4096 cells to the wavefront kernels
-    stage_majorant(P.med, s_maj);
+    // the host routes GridMedium majorant grids of more than 4096 cells to the wavefront kernels
+    if constexpr (!kVdb) stage_majorant(P.med, s_maj);
+    const float *__restrict__ majp = kVdb ? P.med.majorant : s_maj;
     const int nlds = P.lights.n < 4 ? P.lights.n : 4;
     for (int i = threadIdx.x; i < kNTable; i += blockDim.x) {
         s_tab[i] = P.med.sigma_a[i];
@@ -1343,7 +1351,7 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
                         const LambdaIdx li = lambda_index(lam);
                         sig_a = sfrom<S>(sample_table(tab_sa, li));
                         sig_s = sfrom<S>(sample_table(tab_ss, li));
-                        if (kEmissive) Le_l = sample_table(m.Le, li);
+                        if (kEmissive && !kVdb) Le_l = sample_table(m.Le, li);
                     }
                     // first medium segment: RNG from two sampler dims, u from a third (984-989)
                     const float h0 = smp.get1d(P);
@@ -1398,7 +1406,7 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
             for (int b = 0; b < P.dda_budget; ++b) {
                 if (walk == 0 && needNext) {
                     float s0, s1;
-                    if (!ddal_next(it, s_maj, maj_sy, maj_sz, &s0, &s1, &mv)) {
+                    if (!ddal_next(it, majp, maj_sy, maj_sz, &s0, &s1, &mv)) {
                         walk = 2;
                     } else {
                         ++nSteps;
@@ -1462,12 +1470,16 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
             const S sigma_maj = sig_t * mv;
             T_maj = T_maj * sexp(-(sigma_maj * (t - tMin)));
             const V3 pc = po + sd * t;
-            // GridMedium::SamplePoint (media.h:287-319); k_paths runs GridMedium only (the host
-            // sends homogeneous and cloud media to the wavefront kernels)
+            // GridMedium::SamplePoint (media.h:287-319) / NanoVDBMedium::SamplePoint (624-637);
+            // k_paths runs these two (the host sends the other media to the wavefront kernels)
             V3 pm = xf_point_pair(m.medium_from_render, pc);
-            pm = m.unit_box ? V3{pm.x - m.bmin[0], pm.y - m.bmin[1], pm.z - m.bmin[2]} : box_offset(m.bmin, m.bmax, pm);
-            const float dens = m.fat ? fat_lookup(m.fat, m.density, m.nx, m.ny, m.nz, pm)
-                                     : grid_lookup(m.density, m.nx, m.ny, m.nz, pm);
+            float dens;
+            if constexpr (kVdb) {
+                dens = vdb::sample_world(m.vdb, pm.x, pm.y, pm.z);
+            } else {
+                pm = m.unit_box ? V3{pm.x - m.bmin[0], pm.y - m.bmin[1], pm.z - m.bmin[2]} : box_offset(m.bmin, m.bmax, pm);
+                dens = m.fat ? fat_lookup(m.fat, m.density, m.nx, m.ny, m.nz, pm) : grid_lookup(m.density, m.nx, m.ny, m.nz, pm);
+            }
             const S ms_a = sig_a * dens, ms_s = sig_s * dens;
             bool stop = false;
             if (mode == M_MEDIUM) {
@@ -1478,7 +1490,7 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
                     ev = EV_END;
                 } else {
                     if (kEmissive && depth < P.max_depth) {
-                        const Spec Le = grid_emission(m, pm, lam, Le_l);
+                        const Spec Le = kVdb ? vdb_emission(m, pm, lam) : grid_emission(m, pm, lam, Le_l);
                         if (Le.nonzero()) {
                             float pdf = sv0(sigma_maj) * sv0(T_maj);
                             S betap = beta * T_maj / pdf;

@@ -102,3 +102,17 @@ def s_cloud(density, width=1280, height=720, fov=45.0, sampler="independent", sp
     film = RGBFilm(width, height, filter=GaussianFilter() if filter == "gaussian" else BoxFilter())
     smp = ZSobolSampler(spp) if sampler == "zsobol" else IndependentSampler(spp)
     return Scene(cam, film, med, lights, sampler=smp)
+
+
+def cloud_vdb_medium(grid):
+    """The S-cloud medium as a NanoVDBMedium (the disney-cloud's medium type, C3/C4): same
+    sigma (sigma_a 0, sigma_s 1 x scale 4) and g over a sparse tree of the cloud density."""
+    return NanoVDBMedium(grid, sigma_a=0.0, sigma_s=1.0, scale=4.0, g=CLOUD_G)
+
+
+def s_cloud_vdb(density, width=1280, height=720, fov=45.0, sampler="independent", spp=16, filter="box"):
+    """S-cloud framing and lights over a NanoVDBMedium built from a dense (n, n, n) host
+    density (index i at world i / n) or a NanoVDBGrid."""
+    grid = density if isinstance(density, NanoVDBGrid) else vdb_grid(density)
+    base = s_cloud(np.zeros((1, 1, 1), np.float32), width, height, fov, sampler, spp, filter)
+    return Scene(base.camera, base.film, cloud_vdb_medium(grid), base.lights, sampler=base.sampler)

@@ -43,6 +43,8 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU-baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--kernel", default="persistent", choices=["persistent", "wavefront"])
+    p.add_argument("--medium", default="grid", choices=["grid", "nanovdb"],
+                   help="S-cloud as GridMedium (default) or as a NanoVDBMedium tree (disney-cloud's type)")
     p.add_argument("--refill-min", type=int, default=0, help="k_paths refill threshold (0 = library default)")
     p.add_argument("--grid-layout", default="fat", choices=["fat", "linear"])
     p.add_argument("--dda-budget", type=int, default=0, help="k_paths DDA cells per iteration (0 = default)")
@@ -55,7 +57,7 @@ def parse():
     return p.parse_args()
 
 
-def cpu_baseline(scene_host, spp_per_step, budget_s):
+def cpu_baseline(scene_host, spp_per_step, budget_s, label="S-cloud"):
     """Time the CPU oracle (pbrt VolPath restatement, `port`) on a bounded sample of the
     SAME workload: a strided pixel subset across the whole 1280x720 frame, spp_per_step
     samples each, on the host cores this process may use."""
@@ -85,7 +87,7 @@ def cpu_baseline(scene_host, spp_per_step, budget_s):
     done_px = len(order)
     return {"value": done_s / t_used / 1e6, "unit": "Msamples/s", "cores": cores, "kind": "port",
             "sample": f"{done_s} samples: pixels every {stride}th of {f.width}x{f.height} ({done_px} px), "
-                      f"sample indices from 0 in sweeps of {spp_per_step}, same S-cloud-{scene_host.medium.nx} "
+                      f"sample indices from 0 in sweeps of {spp_per_step}, same {label} "
                       f"scene, {t_used:.1f} s on {cores} threads"}
 
 
@@ -136,8 +138,21 @@ def main():
         spp_total = spp_cap
         if spp_total % S:
             raise SystemExit(f"--spp-per-step {S} must divide the ZSobol index range {spp_total} for this run length")
-    scene = scenes.s_cloud(density, width=args.width, height=args.height, sampler=args.sampler, spp=spp_total,
-                           filter=args.filter)
+    vdb = None
+    if args.medium == "nanovdb":
+        # sparse tree of the same cloud (leaf blocks where the density is nonzero), built on
+        # the host; outside the timed region like the grid generation
+        tvdb = time.perf_counter()
+        vdb = scenes.vdb_grid(density.cpu().numpy())
+        del density
+        density = None
+        torch.cuda.empty_cache()
+        tgen += time.perf_counter() - tvdb
+        scene = scenes.s_cloud_vdb(vdb, width=args.width, height=args.height, sampler=args.sampler, spp=spp_total,
+                                   filter=args.filter)
+    else:
+        scene = scenes.s_cloud(density, width=args.width, height=args.height, sampler=args.sampler, spp=spp_total,
+                               filter=args.filter)
     integ = VolPathIntegrator(scene, maxdepth=scenes.CLOUD_MAXDEPTH, spp=args.spp_per_step, seed=0, device=dev,
                               max_paths=args.max_paths, kernel=args.kernel, grid_layout=args.grid_layout)
     if args.refill_min:
@@ -202,7 +217,7 @@ def main():
     # itself cannot read counters. Null when the profile does not match the run.
     traffic, traffic_src, valu = None, None, None
     prof = os.path.join(ROOT, "profiles", f"r01_pmc_k_paths_{args.sampler}_{args.filter}.json")
-    if args.kernel == "persistent" and n == 1024 and S == 16 and os.path.exists(prof):
+    if args.kernel == "persistent" and args.medium == "grid" and n == 1024 and S == 16 and os.path.exists(prof):
         pm = json.load(open(prof))
         traffic = round(pm["hbm_traffic_bytes_per_launch"] / 1e9, 3)
         traffic_src = os.path.relpath(prof, ROOT) + " (GB per launch, PMC FETCH_SIZE x2 + WRITE_SIZE)"
@@ -214,10 +229,13 @@ def main():
     if rank == 0:
         cpu = None
         if not args.no_cpu_baseline and world == 1:
-            host_density = density.cpu().numpy()
-            host_scene = scenes.s_cloud(host_density, width=args.width, height=args.height, sampler=args.sampler,
-                                        spp=spp_total, filter=args.filter)
-            cpu = cpu_baseline(host_scene, S, args.cpu_seconds)
+            if vdb is not None:
+                host_scene = scene
+            else:
+                host_density = density.cpu().numpy()
+                host_scene = scenes.s_cloud(host_density, width=args.width, height=args.height,
+                                            sampler=args.sampler, spp=spp_total, filter=args.filter)
+            cpu = cpu_baseline(host_scene, S, args.cpu_seconds, f"S-cloud-{n} {args.medium}")
         out = {
             "metric": "Msamples/s (whole node) on synthetic S-cloud-1024 720p (disney-cloud stand-in)",
             "value": round(value, 4),
@@ -231,7 +249,7 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (CloudMedium::Density 1024^3 generated on device; disney-cloud assets absent)",
-            "config": {"workload": f"S-cloud-{n} GridMedium, perspective {args.width}x{args.height}, "
+            "config": {"workload": f"S-cloud-{n} {'NanoVDBMedium' if vdb is not None else 'GridMedium'}, perspective {args.width}x{args.height}, "
                                    f"{S} spp/step/GPU, maxdepth {scenes.CLOUD_MAXDEPTH}, {args.sampler} sampler "
                                    f"(pixelsamples {spp_total}), {args.filter} filter",
                        "global_batch": samples // args.steps, "parallelism": f"sample-shard x{world}",

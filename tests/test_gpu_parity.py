@@ -441,28 +441,31 @@ def _vdb_scene(case, W, H):
                         temperatureoffset=20.0, temperaturescale=1.1)
 
 
+@pytest.mark.parametrize("kernel", ["persistent", "wavefront"])
 @pytest.mark.parametrize("case", ["aligned", "rotated", "temperature"])
-def test_nanovdb_medium_replay(case):
+def test_nanovdb_medium_replay(case, kernel):
     """NanoVDBMedium (media.h:602-685): bounds and the 64^3 majorant (media.cpp:556-613)
     bit-exact against the oracle; per-sample replay >= 99.9% bit-identical; film within
-    noise of the platform oracle. NanoVDB's own semantics are restated (parity unpinned,
+    noise of the platform oracle, in both kernel organisations (k_paths<.., kVdb> reads the
+    majorant through L2). NanoVDB's own semantics are restated (parity unpinned,
     tests/test_vdb.py)."""
     from oracle import binding
     W, H, spp = 24, 20, 8
     scene = _vdb_scene(case, W, H)
-    integ = _integrator(scene, maxdepth=8, spp=spp)
+    integ = _integrator(scene, maxdepth=8, spp=spp, kernel=kernel)
     assert integ.ctx.medium_bounds().view(np.uint32).tolist() == scene.medium.bounds.view(np.uint32).tolist()
     canon = binding.OracleRun(scene, max_depth=8, seed=0, libm="canonical")
     got = integ.ctx.majorant(64 ** 3)
     assert got.view(np.uint32).tolist() == canon.majorant.view(np.uint32).tolist()
     assert float(got.max()) > 0
     rgb, w = integ.render()
+    assert (integ.stats()["loop_iterations"] > 0) == (kernel == "persistent")
     frac, _ = _compare_samples(integ, canon, 0, spp)
     ref = binding.OracleRun(scene, max_depth=8, seed=0)
     rgb_o, w_o = ref.render(0, spp, nthreads=8)
     err = _rel_rms(integ.image(rgb, w), integ.image(rgb_o, w_o))
     noise = _oracle_noise(scene, 8, spp, integ, rgb_o, w_o)
-    print(f"nanovdb/{case}: bit-exact samples {frac:.5f}, film rel RMS {err:.3e} (noise {noise:.3e})")
+    print(f"nanovdb/{case}/{kernel}: bit-exact samples {frac:.5f}, film rel RMS {err:.3e} (noise {noise:.3e})")
     assert frac >= 0.999
     assert err <= 0.5 * noise
     integ.close()
