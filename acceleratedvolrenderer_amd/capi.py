@@ -142,6 +142,10 @@ SIGNATURES = {
     "avr_get_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(AvrStats)]),
     "avr_reset_stats": (ctypes.c_int, [ctypes.c_void_p]),
     "avr_film_read": (ctypes.c_int, [ctypes.c_void_p, c_double_p, c_double_p]),
+    "avr_film_spectral": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_float]),
+    "avr_film_read_spectral": (ctypes.c_int, [ctypes.c_void_p, c_double_p, c_double_p]),
+    "avr_film_spectral_device_ptrs": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p),
+                                                     ctypes.POINTER(ctypes.c_void_p)]),
     "avr_film_device_ptrs": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p),
                                             ctypes.POINTER(ctypes.c_void_p)]),
     "avr_film_export_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
@@ -304,6 +308,9 @@ class Context:
         film = scene.film
         _check(self.lib.avr_film(self.h, film.width, film.height, _fp(f32(film.filter_radius)), _fp(f32(film.sensor)),
                                  float(film.imaging_ratio), float(film.max_component_value)))
+        if getattr(film, "nbuckets", 0):
+            _check(self.lib.avr_film_spectral(self.h, int(film.nbuckets), float(film.lambdamin),
+                                              float(film.lambdamax)))
         flt = film.filter
         _check(self.lib.avr_set_filter(self.h, int(flt.type_id), _fp(f32(flt.radius)), float(flt.sigma)))
         _check(self.lib.avr_set_sampler(self.h, int(scene.sampler.type_id), int(scene.sampler.pixelsamples)))
@@ -339,6 +346,13 @@ class Context:
         s = AvrStats()
         _check(self.lib.avr_get_stats(self.h, ctypes.byref(s)))
         return s.as_dict()
+
+    def film_read_spectral(self, npix, nbuckets):
+        """SpectralFilm bucket sums: (bucket_sums, weight_sums), each (npix, nbuckets) fp64."""
+        bs = np.zeros(npix * nbuckets, np.float64)
+        bw = np.zeros(npix * nbuckets, np.float64)
+        _check(self.lib.avr_film_read_spectral(self.h, bs.ctypes.data_as(c_double_p), bw.ctypes.data_as(c_double_p)))
+        return bs.reshape(npix, nbuckets), bw.reshape(npix, nbuckets)
 
     def film_read(self, npix):
         rgb = np.zeros(3 * npix, np.float64)

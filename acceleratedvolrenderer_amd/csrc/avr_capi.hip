@@ -473,6 +473,7 @@ int avr_context_destroy(avr_context *c) {
     for (auto p : fs) if (p) (void)hipFree(p);
     if (c->film.rgb_sum) (void)hipFree(c->film.rgb_sum);
     if (c->film.w_sum) (void)hipFree(c->film.w_sum);
+    if (c->film.bucket_sum) (void)hipFree(c->film.bucket_sum);
     if (c->d_counts) (void)hipFree(c->d_counts);
     if (c->d_heads) (void)hipFree(c->d_heads);
     if (c->d_advance) (void)hipFree(c->d_advance);
@@ -779,6 +780,7 @@ int avr_film(avr_context *c, int width, int height, const float fr[2], const flo
     if (rc) return rc;
     if (c->film.rgb_sum) (void)hipFree(c->film.rgb_sum);
     if (c->film.w_sum) (void)hipFree(c->film.w_sum);
+    if (c->film.bucket_sum) (void)hipFree(c->film.bucket_sum);
     c->film = {};
     c->film.width = width;
     c->film.height = height;
@@ -872,7 +874,31 @@ int avr_film_clear(avr_context *c) {
     const size_t np = (size_t)c->film.width * c->film.height;
     HIP_TRY(hipMemsetAsync(c->film.rgb_sum, 0, 3 * np * sizeof(double), c->stream));
     HIP_TRY(hipMemsetAsync(c->film.w_sum, 0, np * sizeof(double), c->stream));
+    if (c->film.nbuckets > 0)
+        HIP_TRY(hipMemsetAsync(c->film.bucket_sum, 0, 2 * np * c->film.nbuckets * sizeof(double), c->stream));
     return AVR_OK;
+}
+
+// SpectralFilm (film.h:401-530, Create film.cpp:1037-1066): buckets over [lambda_min,
+// lambda_max]; n_buckets = 0 returns to RGBFilm. Both sums live in one allocation.
+int avr_film_spectral(avr_context *c, int n_buckets, float lambda_min, float lambda_max) {
+    if (!c || !c->has_film) return fail(AVR_ERR_STATE, "no film");
+    if (n_buckets < 0) return fail(AVR_ERR_ARG, "n_buckets must be >= 0");
+    if (n_buckets > 0 && !(360.f <= lambda_min && lambda_min < lambda_max && lambda_max <= 830.f))
+        return fail(AVR_ERR_ARG, "SpectralFilm wavelength range must lie within 360..830 nm");
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (c->film.bucket_sum) (void)hipFree(c->film.bucket_sum);
+    c->film.bucket_sum = c->film.bucket_w = nullptr;
+    c->film.nbuckets = n_buckets;
+    c->film.lmin = lambda_min;
+    c->film.lmax = lambda_max;
+    if (n_buckets > 0) {
+        const size_t nb = (size_t)c->film.width * c->film.height * n_buckets;
+        HIP_TRY(dalloc(&c->film.bucket_sum, 2 * nb));
+        c->film.bucket_w = c->film.bucket_sum + nb;
+    }
+    return avr_film_clear(c);
 }
 
 // Stats are resolved lazily so that a render stays asynchronous: every timed interval
@@ -1264,6 +1290,24 @@ int avr_film_read(avr_context *c, double *rgb, double *w) {
     HIP_TRY(hipMemcpyAsync(rgb, c->film.rgb_sum, 3 * np * sizeof(double), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipMemcpyAsync(w, c->film.w_sum, np * sizeof(double), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
+    return AVR_OK;
+}
+
+int avr_film_read_spectral(avr_context *c, double *bucket_sums, double *weight_sums) {
+    if (!c || !c->has_film || c->film.nbuckets <= 0) return fail(AVR_ERR_STATE, "no spectral film");
+    if (!bucket_sums || !weight_sums) return fail(AVR_ERR_ARG, "null buffer");
+    const size_t nb = (size_t)c->film.width * c->film.height * c->film.nbuckets;
+    HIP_TRY(hipMemcpyAsync(bucket_sums, c->film.bucket_sum, nb * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(weight_sums, c->film.bucket_w, nb * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return AVR_OK;
+}
+
+int avr_film_spectral_device_ptrs(avr_context *c, void **bucket_sums, void **weight_sums) {
+    if (!c || !c->has_film || c->film.nbuckets <= 0 || !bucket_sums || !weight_sums)
+        return fail(AVR_ERR_STATE, "no spectral film");
+    *bucket_sums = c->film.bucket_sum;
+    *weight_sums = c->film.bucket_w;
     return AVR_OK;
 }
 

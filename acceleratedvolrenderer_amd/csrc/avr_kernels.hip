@@ -108,7 +108,20 @@ struct DevFilm {
     float max_component;
     double *rgb_sum;                  // W*H*3
     double *w_sum;                    // W*H
+    // SpectralFilm (film.h:401-530): nbuckets > 0 — uniform wavelengths over [lmin, lmax] and
+    // per-pixel bucket sums next to the RGB sums (pixel-major: [pixel * nbuckets + b])
+    int nbuckets;
+    float lmin, lmax;
+    double *bucket_sum, *bucket_w;
 };
+// Film::SampleWavelengths: RGBFilm SampleVisible (spectrum.h:334-347), SpectralFilm
+// SampleUniform (spectrum.h:287-306)
+__device__ __forceinline__ Spec film_sample_lambda(const DevFilm &f, float u) {
+    return f.nbuckets > 0 ? sample_uniform_lambda(u, f.lmin, f.lmax) : sample_visible_lambda(u);
+}
+__device__ __forceinline__ float film_lambda_pdf(const DevFilm &f, float l) {
+    return f.nbuckets > 0 ? 1 / (f.lmax - f.lmin) : visible_wavelength_pdf(l);
+}
 
 struct PathSoA {
     float4 *o, *d, *lambda, *pdf, *beta, *r_u, *r_l, *L;
@@ -660,7 +673,10 @@ __global__ void __launch_bounds__(256) k_camera(Params P) {
         PathSampler<kZSobol> smp;
         smp.start(P, px, py, sampleIndex);
         const float lu = smp.get1d(P);
-        Lambda lam = sample_visible(lu);
+        Lambda lam;
+        lam.l = film_sample_lambda(P.film, lu);
+        lam.pdf = {film_lambda_pdf(P.film, lam.l.v0), film_lambda_pdf(P.film, lam.l.v1),
+                   film_lambda_pdf(P.film, lam.l.v2), film_lambda_pdf(P.film, lam.l.v3)};
         float pFilmX, pFilmY, fweight;
         camera_sample(P, smp, px, py, &pFilmX, &pFilmY, &fweight);
         if (P.film.filter_type != 0) P.ps.weight[id] = fweight;
@@ -992,12 +1008,15 @@ struct DdaL {
     float dx, dy, dz;      // deltaT, negated when the step along that axis is -1
     int vidx;              // x + rx * (y + ry * z)
     int rem;               // cells left: x bits 0-7, y 8-15, z 16-23
+    int pidx;              // cell whose majorant mcur holds (vidx, clamped into the grid)
+    float mcur;            // majorant of cell pidx, loaded one step ahead (software pipelining):
+                           // the caller reloads it (ddal_prefetch) unconditionally every iteration
 };
-__device__ __forceinline__ void ddal_init(DdaL &q, const DevMedium &m, Ray ray, float raytMax) {
+__device__ __forceinline__ void ddal_init(DdaL &q, const DevMedium &m, Ray ray, float raytMax, const float *maj) {
     Dda it;
     if (!dda_init(it, m, ray, raytMax)) {
         q.tMin = kInf; q.tMax = -kInf;
-        q.nx = q.ny = q.nz = q.dx = q.dy = q.dz = 0; q.vidx = 0; q.rem = 0;
+        q.nx = q.ny = q.nz = q.dx = q.dy = q.dz = 0; q.vidx = 0; q.rem = 0; q.pidx = 0; q.mcur = 0;
         return;
     }
     q.tMin = it.tMin; q.tMax = it.tMax;
@@ -1010,9 +1029,15 @@ __device__ __forceinline__ void ddal_init(DdaL &q, const DevMedium &m, Ray ray, 
     const int cy = it.sy > 0 ? m.mres[1] - 1 - it.vy : it.vy;
     const int cz = it.sz > 0 ? m.mres[2] - 1 - it.vz : it.vz;
     q.rem = cx | (cy << 8) | (cz << 16);
+    q.pidx = q.vidx;
+    q.mcur = maj[q.vidx];
 }
+// Reload mcur from pidx: one load per loop iteration into the loop-carried register, so the
+// wait for it lands at the next ddal_next (a load inside ddal_next's predicated block is
+// followed by a phi copy that waits right away).
+__device__ __forceinline__ void ddal_prefetch(DdaL &q, const float *maj) { q.mcur = maj[q.pidx]; }
 // Next(): false when exhausted. `maj` is the LDS copy; sy/sz the linear strides of y and z.
-__device__ __forceinline__ bool ddal_next(DdaL &q, const float *maj, int sy, int sz, float *s0, float *s1,
+__device__ __forceinline__ bool ddal_next(DdaL &q, const float *maj, int sy, int sz, int ncells, float *s0, float *s1,
                                           float *mval) {
     // fields are copied to values first: a select between struct members invites the
     // compiler to turn the struct into a scratch array indexed by the axis
@@ -1027,14 +1052,18 @@ __device__ __forceinline__ bool ddal_next(DdaL &q, const float *maj, int sy, int
     const float dA = ax0 ? dx : (ax1 ? dy : dz);
     const int shift = ax0 ? 0 : (ax1 ? 8 : 16);
     const int stride = ax0 ? 1 : (ax1 ? sy : sz);
-    *mval = maj[vidx];
+    *mval = q.mcur;
     *s0 = tMin;
     const float tExit = fminf_(tMax, nextA);
     *s1 = tExit;
     const bool last = ((rem >> shift) & 0xff) == 0;   // voxel + step == voxelLimit
     q.tMin = (nextA > tMax || last) ? tMax : tExit;
     q.rem = rem - (1 << shift);
-    q.vidx = vidx + (__builtin_signbit(dA) ? -stride : stride);
+    const int nv = vidx + (__builtin_signbit(dA) ? -stride : stride);
+    q.vidx = nv;
+    // the next cell's majorant is loaded by ddal_prefetch so its latency (L2 for NanoVDB's
+    // 64^3 grid) hides behind this step's work; past the last cell the index is clamped
+    q.pidx = min(max(nv, 0), ncells - 1);
     const float nn = nextA + __builtin_fabsf(dA);
     q.nx = ax0 ? nn : nx;
     q.ny = ax1 ? nn : ny;
@@ -1139,7 +1168,7 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
 
     int mode = M_FETCH, ev = EV_NONE;
     int g = 0;
-    const int maj_sy = m.mres[0], maj_sz = m.mres[0] * m.mres[1];
+    const int maj_sy = m.mres[0], maj_sz = m.mres[0] * m.mres[1], maj_n = maj_sz * m.mres[2];
     // path state (Li, integrators.cpp:966-971)
     Spec L{}, lam{}, Le_l{};
     S beta{}, r_u{}, r_l{}, sig_a{}, sig_s{};
@@ -1164,7 +1193,7 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
         tMax *= length(d);
         d = normalize(d);
         sd = d;
-        ddal_init(it, m, Ray{o, d}, tMax);
+        ddal_init(it, m, Ray{o, d}, tMax, majp);
         T_maj = sconst<S>(1.f);
         needNext = true;
     };
@@ -1328,7 +1357,7 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
                         // == rng.Advance((sample_base + sIdx) * 65536) (rng.h:132-146), precomputed
                         smp.rng.state = P.advance[2 * sIdx] * smp.rng.state + smp.rng.inc * P.advance[2 * sIdx + 1];
                     }
-                    lam = sample_visible_lambda(smp.get1d(P));   // pdf: recomputed by k_film
+                    lam = film_sample_lambda(P.film, smp.get1d(P));   // pdf: recomputed by k_film
                     float pFilmX, pFilmY, fweight;
                     camera_sample(P, smp, px, py, &pFilmX, &pFilmY, &fweight);
                     if (P.film.filter_type != 0) P.ps.weight[g] = fweight;
@@ -1406,7 +1435,7 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
             for (int b = 0; b < P.dda_budget; ++b) {
                 if (walk == 0 && needNext) {
                     float s0, s1;
-                    if (!ddal_next(it, majp, maj_sy, maj_sz, &s0, &s1, &mv)) {
+                    if (!ddal_next(it, majp, maj_sy, maj_sz, maj_n, &s0, &s1, &mv)) {
                         walk = 2;
                     } else {
                         ++nSteps;
@@ -1426,6 +1455,8 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
                         }
                     }
                 }
+                // unconditional (all busy lanes): in flight during the candidate test below
+                ddal_prefetch(it, majp);
                 if (walk == 0 && !needNext) {
                     // Fast reject: the candidate t = tMin - log(1-u)/sigma_maj is decided against
                     // segMax from the hardware log2 (v_log_f32, ~1 ulp) when it lies outside an
@@ -1569,8 +1600,8 @@ __global__ void __launch_bounds__(256) k_film(Params P) {
             const int id = s * npix + pix;
             Spec L = spec4(P.ps.L[id]);
             const Spec lam = spec4(P.ps.lambda[id]);
-            const Spec pdf = {visible_wavelength_pdf(lam.v0), visible_wavelength_pdf(lam.v1),
-                              visible_wavelength_pdf(lam.v2), visible_wavelength_pdf(lam.v3)};
+            const Spec pdf = {film_lambda_pdf(P.film, lam.v0), film_lambda_pdf(P.film, lam.v1),
+                              film_lambda_pdf(P.film, lam.v2), film_lambda_pdf(P.film, lam.v3)};
             const LambdaIdx li = lambda_index(lam);
             bool bad = __builtin_isnan(L.v0) || __builtin_isnan(L.v1) || __builtin_isnan(L.v2) || __builtin_isnan(L.v3);
             if (!bad) {
@@ -1590,6 +1621,22 @@ __global__ void __launch_bounds__(256) k_film(Params P) {
             s1 += (double)(w * rgb[1]);
             s2 += (double)(w * rgb[2]);
             ws += (double)w;
+            if (P.film.nbuckets > 0) {
+                // SpectralFilm::AddSample (film.h:436-454): clamp by the max component, scale by
+                // weight * CIE_Y_integral, one bucket per wavelength (LambdaToBucket, 500-504)
+                const float lm = fmaxf_(fmaxf_(fmaxf_(L.v0, L.v1), L.v2), L.v3);
+                if (lm > P.film.max_component) L = L * (P.film.max_component / lm);
+                L = L * (w * 106.856895f);
+                const int nb = P.film.nbuckets;
+                double *bs = P.film.bucket_sum + (size_t)pix * nb, *bw = P.film.bucket_w + (size_t)pix * nb;
+                const float lv[4] = {lam.v0, lam.v1, lam.v2, lam.v3}, Lv[4] = {L.v0, L.v1, L.v2, L.v3};
+                _Pragma("unroll") for (int i = 0; i < 4; ++i) {
+                    int b = (int)((float)nb * (lv[i] - P.film.lmin) / (P.film.lmax - P.film.lmin));
+                    b = b < 0 ? 0 : (b > nb - 1 ? nb - 1 : b);
+                    bs[b] += (double)Lv[i];
+                    bw[b] += (double)w;
+                }
+            }
         }
         P.film.rgb_sum[3 * (size_t)pix] = s0;
         P.film.rgb_sum[3 * (size_t)pix + 1] = s1;

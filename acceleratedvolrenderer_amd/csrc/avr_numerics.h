@@ -222,6 +222,20 @@ AVR_HD Spec sample_visible_lambda(float u) {
     l.v3 = sample_visible_wavelength(visible_up(u, 3));
     return l;
 }
+// SampledWavelengths::SampleUniform (spectrum.h:287-306): Lerp(u, min, max), then steps of
+// (max - min) / 4 wrapped into the range; pdf 1 / (max - min)
+AVR_HD Spec sample_uniform_lambda(float u, float lmin, float lmax) {
+    Spec l;
+    l.v0 = (1 - u) * lmin + u * lmax;
+    const float delta = (lmax - lmin) / 4;
+    l.v1 = l.v0 + delta;
+    if (l.v1 > lmax) l.v1 = lmin + (l.v1 - lmax);
+    l.v2 = l.v1 + delta;
+    if (l.v2 > lmax) l.v2 = lmin + (l.v2 - lmax);
+    l.v3 = l.v2 + delta;
+    if (l.v3 > lmax) l.v3 = lmin + (l.v3 - lmax);
+    return l;
+}
 AVR_HD Lambda sample_visible(float u) {
     Lambda w;
     w.l = sample_visible_lambda(u);

@@ -78,6 +78,20 @@ class VolPathIntegrator:
         f = self.scene.film
         return self.ctx.film_read(f.width * f.height)
 
+    def spectral_sums(self):
+        """SpectralFilm Pixel::bucketSums / weightSums, (W*H, nbuckets) fp64 each."""
+        f = self.scene.film
+        if not getattr(f, "nbuckets", 0):
+            raise ValueError("the scene's film is not a SpectralFilm")
+        return self.ctx.film_read_spectral(f.width * f.height, f.nbuckets)
+
+    def spectral_image(self, fp16=True):
+        """SpectralFilm::GetImage: (H, W, 3 + nbuckets), channels film.channel_names()."""
+        from .scene import spectral_image
+        rgb, w = self.film_sums()
+        bs, bw = self.spectral_sums()
+        return spectral_image(self.scene.film, rgb, w, bs, bw, fp16=fp16)
+
     def image(self, rgb_sum=None, w_sum=None):
         if rgb_sum is None:
             rgb_sum, w_sum = self.film_sums()
@@ -95,7 +109,20 @@ class VolPathIntegrator:
         return img
 
     def write_image(self, path, rgb_sum=None, w_sum=None, spp=None, render_time=None, mse=None, fp16=True):
-        """RGBFilm::WriteImage -> Image::Write: EXR (pbrt's attributes, ZIP) or PFM by extension."""
+        """RGBFilm::WriteImage -> Image::Write: EXR (pbrt's attributes, ZIP) or PFM by extension.
+        SpectralFilm (film.cpp:955-1028): EXR only, R G B + S0.<lambda>nm channels and the
+        spectral layout strings."""
+        f = self.scene.film
+        if getattr(f, "nbuckets", 0):
+            if not str(path).lower().endswith(".exr"):
+                raise ValueError(f"{path}: EXR is the only output format supported by the SpectralFilm.")
+            img = self.spectral_image(fp16)
+            if fp16:
+                img = img.astype(np.float16).astype(np.float32)
+            imageio.write_exr(path, img, channels=f.channel_names(), half=fp16,
+                              samples_per_pixel=spp if spp is not None else self.spp, render_time_seconds=render_time,
+                              mse=mse, strings={"spectralLayoutVersion": "1.0", "emissiveUnits": "W.m^-2.sr^-1"})
+            return img
         img = self.get_image(rgb_sum, w_sum, fp16)
         if str(path).lower().endswith(".pfm"):
             imageio.write_pfm(path, img)

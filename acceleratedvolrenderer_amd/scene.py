@@ -450,6 +450,48 @@ class RGBFilm:
         self.output_from_sensor = spectra.TABLES["srgb_rgb_from_xyz"].astype(np.float32)
 
 
+class SpectralFilm(RGBFilm):
+    """SpectralFilm (film.h:401-530, film.cpp:849-1066): the RGB sums of RGBFilm plus
+    `nbuckets` (default 16) per-pixel spectral buckets over [lambdamin, lambdamax] (default
+    360-830 nm); wavelengths sampled uniformly (SampledWavelengths::SampleUniform). Here the
+    range must lie within 360-830 nm (the densely sampled tables' domain)."""
+    nbuckets_default = 16
+
+    def __init__(self, xresolution=1280, yresolution=720, nbuckets=16, lambdamin=360.0, lambdamax=830.0, **kw):
+        super().__init__(xresolution, yresolution, **kw)
+        if int(nbuckets) < 1:
+            raise ValueError("nbuckets must be positive")
+        if not (360.0 <= float(lambdamin) < float(lambdamax) <= 830.0):
+            raise ValueError("SpectralFilm wavelength range must lie within 360..830 nm")
+        self.nbuckets = int(nbuckets)
+        self.lambdamin = np.float32(lambdamin)
+        self.lambdamax = np.float32(lambdamax)
+
+    def bucket_centers(self):
+        """Channel wavelengths of GetImage: Lerp((i + 0.5) / nBuckets, min, max) (film.cpp:969)."""
+        t = ((np.arange(self.nbuckets, dtype=np.float32) + np.float32(0.5)) / np.float32(self.nbuckets)).astype(
+            np.float32)
+        return ((np.float32(1) - t) * self.lambdamin + t * self.lambdamax).astype(np.float32)
+
+    def channel_names(self):
+        """R, G, B, then S0.<lambda>nm with ',' for '.' (film.cpp:963-973)."""
+        return ["R", "G", "B"] + ["S0." + ("%.3fnm" % float(l)).replace(".", ",") for l in self.bucket_centers()]
+
+
+def spectral_image(film, rgb_sum, w_sum, bucket_sums, weight_sums, fp16=True):
+    """SpectralFilm::GetImage (film.cpp:961-1028), no splats: (H, W, 3 + nbuckets) float32."""
+    rgb = film_rgb(film, rgb_sum, w_sum)
+    if fp16:
+        rgb = np.minimum(rgb, np.float32(65504))
+    bs = np.asarray(bucket_sums, np.float64).reshape(film.height, film.width, film.nbuckets)
+    bw = np.asarray(weight_sums, np.float64).reshape(film.height, film.width, film.nbuckets)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        c = np.where(bw > 0, (bs / np.where(bw > 0, bw, 1)).astype(np.float32), np.float32(0))
+    if fp16:
+        c = np.minimum(c, np.float32(65504))
+    return np.concatenate([rgb, c.astype(np.float32)], axis=2)
+
+
 def _bounding_sphere_radius(pmin, pmax):
     """Bounds3::BoundingSphere (vecmath.h:1335-1338) in float32."""
     pmin = pmin.astype(np.float32)

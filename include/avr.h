@@ -236,6 +236,15 @@ int avr_reset_stats(avr_context *ctx);
 
 /* Film readback: rgb_sum[W*H*3] and w_sum[W*H] (fp64 RGBFilm::Pixel sums). */
 int avr_film_read(avr_context *ctx, double *rgb_sum, double *w_sum);
+/* SpectralFilm (film.h:401-530; SpectralFilm::Create film.cpp:1037-1066 "nbuckets",
+ * "lambdamin", "lambdamax"): after avr_film, n_buckets > 0 switches the film to uniform
+ * wavelength sampling (SampledWavelengths::SampleUniform) over [lambda_min, lambda_max]
+ * (within 360..830 nm here) and per-pixel bucket sums next to the RGB sums
+ * (SpectralFilm::AddSample, film.h:413-455); 0 returns to RGBFilm. Readback: the fp64
+ * Pixel::bucketSums / weightSums, [pixel * n_buckets + bucket]. */
+int avr_film_spectral(avr_context *ctx, int n_buckets, float lambda_min, float lambda_max);
+int avr_film_read_spectral(avr_context *ctx, double *bucket_sums, double *weight_sums);
+int avr_film_spectral_device_ptrs(avr_context *ctx, void **d_bucket_sums, void **d_weight_sums);
 /* Device pointers of the film sums (for an RCCL reduce across GPUs). */
 int avr_film_device_ptrs(avr_context *ctx, void **d_rgb_sum, void **d_w_sum);
 /* Device-to-device copy of the film sums into caller memory on the same GPU, laid out

@@ -76,6 +76,7 @@ class OracleScene(ctypes.Structure):
         ("light_img", c_float_p * 8), ("light_res", ctypes.c_int * 8), ("light_dist", c_float_p * 8),
         ("light_rfl", (ctypes.c_float * 9) * 8), ("light_lfr", (ctypes.c_float * 9) * 8),
         ("light_illuminant", c_float_p),
+        ("film_nbuckets", ctypes.c_int), ("film_lambda_min", ctypes.c_float), ("film_lambda_max", ctypes.c_float),
     ]
 
 
@@ -136,6 +137,10 @@ def lib():
         L.oracle_sample_discrete3.restype = ctypes.c_int
         L.oracle_sample_discrete3.argtypes = [c_float_p, ctypes.c_float]
         L.oracle_sample_visible.argtypes = [ctypes.c_float, c_float_p, c_float_p]
+        L.oracle_sample_uniform.argtypes = [ctypes.c_float, ctypes.c_float, ctypes.c_float, c_float_p, c_float_p]
+        L.oracle_render_spectral.restype = ctypes.c_longlong
+        L.oracle_render_spectral.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int] + [
+            ctypes.POINTER(ctypes.c_double)] * 4
         L.oracle_hg_sample.argtypes = [c_float_p, ctypes.c_float, ctypes.c_float, ctypes.c_float, c_float_p,
                                        c_float_p]
         L.oracle_intersectp.restype = ctypes.c_int
@@ -395,6 +400,9 @@ class OracleRun:
         s.imaging_ratio = float(f.imaging_ratio)
         s.output_from_sensor[:] = [float(v) for v in f.output_from_sensor.reshape(-1)]
         s.max_component_value = float(f.max_component_value)
+        s.film_nbuckets = int(getattr(f, "nbuckets", 0))
+        s.film_lambda_min = float(getattr(f, "lambdamin", 360.0))
+        s.film_lambda_max = float(getattr(f, "lambdamax", 830.0))
         s.max_depth = int(max_depth)
         s.seed = int(seed)
         smp = scene.sampler
@@ -427,6 +435,22 @@ class OracleRun:
                                      w.ctypes.data_as(c_double_p))
         self.last_events = events
         return rgb, w
+
+    def render_spectral(self, spp0, spp1, nthreads=1):
+        """SpectralFilm render: (rgb_sum, w_sum, bucket_sums, weight_sums), buckets (W*H, nb)."""
+        f = self.scene.film
+        npix, nb = f.width * f.height, int(self.s.film_nbuckets)
+        if nb <= 0:
+            raise ValueError("scene film is not a SpectralFilm")
+        rgb = np.zeros(3 * npix, np.float64)
+        w = np.zeros(npix, np.float64)
+        bs = np.zeros(npix * nb, np.float64)
+        bw = np.zeros(npix * nb, np.float64)
+        set_libm(self.libm)
+        dp = lambda a: a.ctypes.data_as(c_double_p)
+        self.last_events = lib().oracle_render_spectral(ctypes.byref(self.s), spp0, spp1, nthreads, dp(rgb), dp(w),
+                                                        dp(bs), dp(bw))
+        return rgb, w, bs.reshape(npix, nb), bw.reshape(npix, nb)
 
     def render_list(self, pixels, spp0, spp1, nthreads=1):
         pixels = np.ascontiguousarray(pixels, np.int32)

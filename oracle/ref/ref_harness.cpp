@@ -203,6 +203,25 @@ int main(int argc, char **argv) {
         printf("]");
     }
 
+    // SampledWavelengths::SampleUniform (spectrum.h:287-306): SpectralFilm::SampleWavelengths
+    {
+        j.key("sample_uniform");
+        printf("[");
+        const float ranges[][2] = {{360.f, 830.f}, {400.f, 700.f}, {380.f, 780.f}, {361.5f, 829.25f}};
+        bool f = true;
+        for (auto &r : ranges)
+            for (int i = 0; i <= 32; ++i) {
+                float u = i / 32.f;
+                if (i == 32) u = 0.99999994f;
+                SampledWavelengths l = SampledWavelengths::SampleUniform(u, r[0], r[1]);
+                SampledSpectrum pdf = l.PDF();
+                printf("%s[%u,%u,%u,%u,%u,%u,%u,%u,%u,%u,%u]", f ? "" : ",", fb(u), fb(r[0]), fb(r[1]), fb(l[0]),
+                       fb(l[1]), fb(l[2]), fb(l[3]), fb(pdf[0]), fb(pdf[1]), fb(pdf[2]), fb(pdf[3]));
+                f = false;
+            }
+        printf("]");
+    }
+
     // ---- Henyey-Greenstein --------------------------------------------------
     {
         j.key("hg_eval");

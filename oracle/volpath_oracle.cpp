@@ -449,6 +449,19 @@ static inline Lambda SampleVisible(float u) {
     }
     return w;
 }
+// SampledWavelengths::SampleUniform — spectrum.h:287-306 (SpectralFilm::SampleWavelengths,
+// film.h:408-410): Lerp(u, min, max) then steps of (max - min) / 4 wrapped into the range
+static inline Lambda SampleUniform(float u, float lmin, float lmax) {
+    Lambda w;
+    w.lambda[0] = (1 - u) * lmin + u * lmax;   // Lerp, util/math.h
+    const float delta = (lmax - lmin) / NS;
+    for (int i = 1; i < NS; ++i) {
+        w.lambda[i] = w.lambda[i - 1] + delta;
+        if (w.lambda[i] > lmax) w.lambda[i] = lmin + (w.lambda[i] - lmax);
+    }
+    for (int i = 0; i < NS; ++i) w.pdf[i] = 1 / (lmax - lmin);
+    return w;
+}
 // DenselySampledSpectrum::Sample — spectrum.h:390-400 (table over 360..830 nm)
 static inline Spec SampleDense(const float *table, const Lambda &l) {
     Spec s;
@@ -794,6 +807,10 @@ typedef struct OracleScene {
     const float *light_dist[8];
     float light_rfl[8][9], light_lfr[8][9];
     const float *light_illuminant;
+    // SpectralFilm (film.h:401-530): nbuckets > 0 selects it — uniform wavelengths over
+    // [lambda_min, lambda_max] and per-pixel spectral buckets next to the RGB sums
+    int film_nbuckets;
+    float film_lambda_min, film_lambda_max;
 } OracleScene;
 
 }  // extern "C"
@@ -1583,7 +1600,8 @@ static SampleResult EvaluatePixelSample(const SceneView &sv, int px, int py, int
     Sampler sampler;
     sampler.Start(s, px, py, sampleIndex);
     float lu = sampler.Get1D();
-    Lambda l = SampleVisible(lu);
+    // Film::SampleWavelengths: RGBFilm SampleVisible, SpectralFilm SampleUniform
+    Lambda l = s.film_nbuckets > 0 ? SampleUniform(lu, s.film_lambda_min, s.film_lambda_max) : SampleVisible(lu);
     float fu0, fu1;
     sampler.Get2D(&fu0, &fu1);            // GetPixel2D
     float fpx, fpy, filterWeight = 1;
@@ -1629,6 +1647,28 @@ static inline void AddSample(const OracleScene &s, double *rgbSum, double *wSum,
         for (int c = 0; c < 3; ++c) rgb[c] *= s.max_component_value / m;
     for (int c = 0; c < 3; ++c) rgbSum[c] += weight * rgb[c];
     *wSum += weight;
+}
+
+// SpectralFilm::AddSample — film.h:413-455: the RGB part as RGBFilm's, then L clamped by
+// its max component, scaled by weight * CIE_Y_integral, and added into the bucket of each
+// wavelength (LambdaToBucket, film.h:500-504) with the weight
+static inline void AddSampleSpectral(const OracleScene &s, double *rgbSum, double *wSum, double *bucketSums,
+                                     double *weightSums, const Spec &Lin, const Lambda &l, float weight) {
+    AddSample(s, rgbSum, wSum, Lin, l, weight);
+    Spec L = Lin;
+    float lm = L.v[0];
+    for (int i = 1; i < NS; ++i) lm = std::max(lm, L.v[i]);
+    if (lm > s.max_component_value)
+        for (int i = 0; i < NS; ++i) L.v[i] *= s.max_component_value / lm;
+    const float k = weight * 106.856895f;   // CIE_Y_integral
+    for (int i = 0; i < NS; ++i) L.v[i] *= k;
+    const int nb = s.film_nbuckets;
+    for (int i = 0; i < NS; ++i) {
+        int b = nb * (l.lambda[i] - s.film_lambda_min) / (s.film_lambda_max - s.film_lambda_min);
+        b = std::min(std::max(b, 0), nb - 1);
+        bucketSums[b] += L.v[i];
+        weightSums[b] += weight;
+    }
 }
 
 }  // namespace oracle
@@ -1939,6 +1979,42 @@ uint64_t oracle_mixbits(uint64_t v) { return MixBits(v); }
 float oracle_fastexp(float x) { return FastExp(x); }
 float oracle_sample_exponential(float u, float a) { return SampleExponential(u, a); }
 int oracle_sample_discrete3(const float *w, float u) { return SampleDiscrete3(w, u); }
+void oracle_sample_uniform(float u, float lmin, float lmax, float *lambda, float *pdf) {
+    Lambda l = SampleUniform(u, lmin, lmax);
+    for (int i = 0; i < NS; ++i) { lambda[i] = l.lambda[i]; pdf[i] = l.pdf[i]; }
+}
+// SpectralFilm render: like oracle_render, plus bucketSums / weightSums [W*H*nbuckets]
+long long oracle_render_spectral(const OracleScene *s, int spp0, int spp1, int nthreads, double *rgbSum,
+                                 double *wSum, double *bucketSums, double *weightSums) {
+    SceneView sv(*s);
+    const int W = s->width, H = s->height, nb = s->film_nbuckets;
+    std::atomic<int> next{0};
+    std::atomic<long long> events{0};
+    auto worker = [&]() {
+        long long ev = 0;
+        while (true) {
+            int py = next.fetch_add(1);
+            if (py >= H) break;
+            for (int px = 0; px < W; ++px)
+                for (int si = spp0; si < spp1; ++si) {
+                    int ne = 0;
+                    SampleResult r = EvaluatePixelSample(sv, px, py, si, &ne);
+                    ev += ne;
+                    size_t pi = (size_t)py * W + px;
+                    AddSampleSpectral(*s, rgbSum + 3 * pi, wSum + pi, bucketSums + pi * nb, weightSums + pi * nb, r.L,
+                                      r.l, r.weight);
+                }
+        }
+        events += ev;
+    };
+    if (nthreads <= 1) worker();
+    else {
+        std::vector<std::thread> th;
+        for (int i = 0; i < nthreads; ++i) th.emplace_back(worker);
+        for (auto &t : th) t.join();
+    }
+    return events.load();
+}
 void oracle_sample_visible(float u, float *lambda, float *pdf) {
     Lambda l = SampleVisible(u);
     for (int i = 0; i < NS; ++i) { lambda[i] = l.lambda[i]; pdf[i] = l.pdf[i]; }

@@ -203,3 +203,15 @@ def test_gaussian_filter_sampling(golden):
         u = rows[:, :2].view(np.float32)
         got = ob.gaussian_filter_samples(rx, ry, sigma, u)
         assert got.view(np.uint32).tolist() == rows[:, 2:].tolist()
+
+
+def test_sample_uniform_wavelengths(golden):
+    """SampledWavelengths::SampleUniform (spectrum.h:287-306), SpectralFilm's sampler."""
+    L = ob.lib()
+    for row in golden["sample_uniform"]:
+        v = f(row)
+        lam = np.zeros(4, np.float32)
+        pdf = np.zeros(4, np.float32)
+        L.oracle_sample_uniform(float(v[0]), float(v[1]), float(v[2]), ob.fp(lam), ob.fp(pdf))
+        assert lam.view(np.uint32).tolist() == v[3:7].view(np.uint32).tolist()
+        assert pdf.view(np.uint32).tolist() == v[7:11].view(np.uint32).tolist()
