@@ -1351,6 +1351,9 @@ int avr_film_export_device(avr_context *c, void *dst) {
     double *d = (double *)dst;
     HIP_TRY(hipMemcpyAsync(d, c->film.rgb_sum, 3 * np * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
     HIP_TRY(hipMemcpyAsync(d + 3 * np, c->film.w_sum, np * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
+    if (c->film.nbuckets > 0)   // SpectralFilm: bucket sums then weights follow
+        HIP_TRY(hipMemcpyAsync(d + 4 * np, c->film.bucket_sum, 2 * np * c->film.nbuckets * sizeof(double),
+                               hipMemcpyDeviceToDevice, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     return AVR_OK;
 }

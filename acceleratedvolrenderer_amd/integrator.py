@@ -30,6 +30,28 @@ def shard_samples(spp, rank, world_size):
     return lo, hi
 
 
+def film_buffer_size(npix, nbuckets=0):
+    """Doubles of the exported film: rgb (3), weight (1) and, for a SpectralFilm, 2 x nbuckets per pixel."""
+    return (4 + 2 * int(nbuckets)) * int(npix)
+
+
+def reduce_film(buf, npix, nbuckets, rank, group=None):
+    """The one exchange step of the multi-GPU path: SUM-reduce of the packed fp64 film
+    (avr_film_export_device layout) to rank 0 over the process group (RCCL on GPUs, gloo in
+    the CPU tests). Rank 0 gets the unpacked sums, other ranks None."""
+    import torch.distributed as dist
+    dist.reduce(buf, dst=0, op=dist.ReduceOp.SUM, group=group)
+    if rank != 0:
+        return None
+    host = buf.cpu().numpy()
+    out = (host[:3 * npix].copy(), host[3 * npix:4 * npix].copy())
+    if nbuckets:
+        k = npix * nbuckets
+        out += (host[4 * npix:4 * npix + k].reshape(npix, nbuckets).copy(),
+                host[4 * npix + k:4 * npix + 2 * k].reshape(npix, nbuckets).copy())
+    return out
+
+
 class VolPathIntegrator:
     def __init__(self, scene, maxdepth=5, spp=16, seed=0, device=0, max_paths=0, lightsampler="bvh",
                  regularize=False, name="volpath", kernel="persistent", grid_layout="fat"):
@@ -172,24 +194,20 @@ class VolPathIntegrator:
     def render_distributed(self, rank, world_size, group=None):
         """Render this rank's sample shard and SUM-reduce the fp64 film to rank 0 (RCCL).
 
-        Returns (rgb_sum, w_sum) on rank 0, None elsewhere.
+        Returns (rgb_sum, w_sum) on rank 0 — (rgb_sum, w_sum, bucket_sums, weight_sums) for a
+        SpectralFilm — and None elsewhere.
         """
         import torch
-        import torch.distributed as dist
 
         lo, hi = shard_samples(self.spp, rank, world_size)
         self.ctx.film_clear()
         if hi > lo:
             self.ctx.render(lo, hi, self.seed, self.maxdepth)
         f = self.scene.film
-        npix = f.width * f.height
-        buf = torch.empty(4 * npix, dtype=torch.float64, device=f"cuda:{self.device}")
+        nb = int(getattr(f, "nbuckets", 0))
+        buf = torch.empty(film_buffer_size(f.width * f.height, nb), dtype=torch.float64, device=f"cuda:{self.device}")
         self.ctx.film_export_device(buf.data_ptr())
-        dist.reduce(buf, dst=0, op=dist.ReduceOp.SUM, group=group)
-        if rank != 0:
-            return None
-        host = buf.cpu().numpy()
-        return host[:3 * npix].copy(), host[3 * npix:].copy()
+        return reduce_film(buf, f.width * f.height, nb, rank, group)
 
     def close(self):
         self.ctx.close()

@@ -248,7 +248,8 @@ int avr_film_spectral_device_ptrs(avr_context *ctx, void **d_bucket_sums, void *
 /* Device pointers of the film sums (for an RCCL reduce across GPUs). */
 int avr_film_device_ptrs(avr_context *ctx, void **d_rgb_sum, void **d_w_sum);
 /* Device-to-device copy of the film sums into caller memory on the same GPU, laid out
- * [rgb_sum (W*H*3) | w_sum (W*H)] as doubles — the buffer handed to the RCCL reduce. */
+ * [rgb_sum (W*H*3) | w_sum (W*H)] as doubles — the buffer handed to the RCCL reduce; a
+ * SpectralFilm appends [bucket_sums (W*H*nb) | weight_sums (W*H*nb)]. */
 int avr_film_export_device(avr_context *ctx, void *d_dst);
 
 /* RGBFilm::GetImage on the device (film.cpp:533-565): per pixel GetPixelRGB (film.h:258-274)
