@@ -57,6 +57,11 @@ def parse():
     return p.parse_args()
 
 
+def log(msg):
+    """Progress on stderr (the JSON line stays the only stdout output)."""
+    print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
 def cpu_baseline(scene_host, spp_per_step, budget_s, label="S-cloud"):
     """Time the CPU oracle (pbrt VolPath restatement, `port`) on a bounded sample of the
     SAME workload: a strided pixel subset across the whole 1280x720 frame, spp_per_step
@@ -64,7 +69,9 @@ def cpu_baseline(scene_host, spp_per_step, budget_s, label="S-cloud"):
     from oracle import binding
     cores = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
     cores = max(1, min(cores, 16, os.cpu_count() or 1))
+    log(f"cpu baseline: building the oracle scene ({label})")
     run = binding.OracleRun(scene_host, max_depth=100, seed=0)
+    log(f"cpu baseline: timing {budget_s:.0f} s on {cores} threads")
     f = scene_host.film
     npix = f.width * f.height
     # a strided pixel subset that spans every row/column band of the frame; samples are
@@ -119,6 +126,7 @@ def main():
     gen.sync()
     gen.close()
     tgen = time.perf_counter() - tgen
+    log(f"density grid {n}^3 generated in {tgen:.2f} s")
     # the sampler's pixelsamples covers every sample index the run renders (ZSobol lays out
     # Morton(pixel) << log2(spp) | index): 256 (config C3) unless more are rendered
     S = args.spp_per_step
@@ -166,6 +174,7 @@ def main():
         base = ((k * world + rank) * S) % spp_total if wrap else (k * world + rank) * S
         integ.ctx.render(base, base + S, 0, scenes.CLOUD_MAXDEPTH)
 
+    log("scene uploaded; warmup")
     for k in range(args.warmup):
         step(k)
     integ.ctx.film_clear()

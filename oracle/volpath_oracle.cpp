@@ -705,7 +705,10 @@ struct VdbTree {
 // NanoVDBMedium ctor's 64^3 majorant (media.cpp:556-613)
 static void VdbMajorant(const VdbTree &g, const float b[6], int rx, int ry, int rz, float *out) {
     const int res[3] = {rx, ry, rz};
-    for (int z = 0; z < rz; ++z)
+    // z-slices on the host's threads (cells are independent; the tree is read-only)
+    std::atomic<int> nextZ{0};
+    auto slice = [&]() {
+    for (int z; (z = nextZ.fetch_add(1)) < rz;)
         for (int y = 0; y < ry; ++y)
             for (int x = 0; x < rx; ++x) {
                 const int c[3] = {x, y, z};
@@ -729,6 +732,11 @@ static void VdbMajorant(const VdbTree &g, const float b[6], int rx, int ry, int 
                         for (int nx = n0[0]; nx <= n1[0]; ++nx) maxValue = std::max(maxValue, g.GetValue(nx, ny, nz));
                 out[x + rx * (y + ry * z)] = maxValue;
             }
+    };
+    const int nt = std::max(1, std::min(16, (int)std::thread::hardware_concurrency()));
+    std::vector<std::thread> th;
+    for (int i = 0; i < nt; ++i) th.emplace_back(slice);
+    for (auto &t : th) t.join();
 }
 
 }  // namespace oracle
