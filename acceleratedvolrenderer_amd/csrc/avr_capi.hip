@@ -1361,3 +1361,14 @@ int avr_film_export_device(avr_context *c, void *dst) {
 }  // extern "C"
 
 #include "avr_graph_capi.hip"
+
+#ifdef AVR_PROFILE_SECTIONS
+// Variant builds only (not part of include/avr.h): read and clear the k_paths section cycles.
+extern "C" int avr_debug_sections(unsigned long long *out) {
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(avr::g_sections), 8 * sizeof(unsigned long long)));
+    unsigned long long z[8] = {};
+    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(avr::g_sections), z, sizeof(z)));
+    return AVR_OK;
+}
+#endif

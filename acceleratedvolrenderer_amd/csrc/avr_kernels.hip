@@ -1133,6 +1133,38 @@ template <> __device__ __forceinline__ Spec sfrom<Spec>(const Spec &x) { return 
 __device__ __forceinline__ Spec smul(const Spec &a, float b) { return a * b; }
 __device__ __forceinline__ Spec smul(const Spec &a, const Spec &b) { return a * b; }
 
+// Section profiling (variant builds with -DAVR_PROFILE_SECTIONS only; tools/section_profile.py):
+// per wave, s_memtime cycles spent in {event handlers, refill, segment starts, DDA walk,
+// collision (exact candidate, fetch, callback)} summed into g_sections.
+#ifdef AVR_PROFILE_SECTIONS
+__device__ unsigned long long g_sections[8];
+struct SecProf {
+    unsigned long long acc[5] = {0, 0, 0, 0, 0};
+    unsigned long long last = 0;
+    int cur = 0;
+    __device__ __forceinline__ void mark(int next) {
+        const unsigned long long t = clock64();
+        const unsigned long long d = t - last;
+        if (cur == 0) acc[0] += d; else if (cur == 1) acc[1] += d; else if (cur == 2) acc[2] += d;
+        else if (cur == 3) acc[3] += d; else acc[4] += d;
+        last = t;
+        cur = next;
+    }
+    __device__ __forceinline__ void flush() {
+        mark(0);
+        if (lane_id() == 0)
+            for (int i = 0; i < 5; ++i) atomicAdd(&g_sections[i], acc[i]);
+    }
+};
+#define AVR_SEC_INIT SecProf secp; secp.last = clock64();
+#define AVR_SEC(i) secp.mark(i);
+#define AVR_SEC_FLUSH secp.flush();
+#else
+#define AVR_SEC_INIT
+#define AVR_SEC(i)
+#define AVR_SEC_FLUSH
+#endif
+
 // NanoVDBMedium (kVdb, media.h:602-685): the same loop over the sparse tree. Its 64^3
 // majorant (1 MiB) does not fit LDS and is read through L2 (per-XCD 4 MiB); the density
 // fetch is NanoVDB's index-space trilinear sampler (avr_vdb.h) and emission comes from the
@@ -1198,7 +1230,9 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
         needNext = true;
     };
 
+    AVR_SEC_INIT
     while (true) {
+        AVR_SEC(0)
         // =================== batched event handlers (each runs once per batch) ===========
         if (__ballot(ev == EV_SCATTER)) {
             if (ev == EV_SCATTER) {
@@ -1314,6 +1348,7 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
             }
         }
 
+        AVR_SEC(1)
         // =================== refill idle lanes: one atomic per wave on a per-XCD head ======
         const uint64_t needMask = __ballot(mode == M_FETCH);
         const uint64_t busyMask = __ballot(mode == M_MEDIUM || mode == M_SHADOW);
@@ -1396,6 +1431,7 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
                 }
             }
         }
+        AVR_SEC(2)
         // =================== segment starts, shared by the NEE shadow ray, the phase-sampled
         // continuation and the camera ray: RNG(seqA, seqB), then SampleT_maj's prologue
         // (medium-space ray, clip, DDA setup) once per batch for every lane that needs one
@@ -1412,6 +1448,7 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
         // =================== tracking: advance every busy lane collision by collision ======
         // until a batch of lanes needs service (events or refill) or none is busy.
         while (true) {
+            AVR_SEC(3)
             const bool busy = (mode == M_MEDIUM || mode == M_SHADOW) && ev == EV_NONE;
             const uint64_t busyNow = __ballot(busy);
             const uint64_t service = __ballot(mode != M_DONE && !busy);
@@ -1480,6 +1517,7 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
                 }
                 if (__ballot(walk == 0) == 0) break;
             }
+            AVR_SEC(4)
             const bool segEnd = walk == 2, pend = walk == 1;
             if (segEnd) {
                 if (mode == M_MEDIUM) ev = EV_ESCAPE;
@@ -1579,6 +1617,7 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
             }
         }
     }
+    AVR_SEC_FLUSH
     flush_stat(P.stats, 0, nLookup);
     flush_stat(P.stats, 1, nPaths);
     flush_stat(P.stats, 3, nShadowLookup);

@@ -1,0 +1,83 @@
+"""k_paths time split by section on the bench workload (profiling variant build).
+
+Builds variants/libavr_prof.so with -DAVR_PROFILE_SECTIONS (here, on the CPU: `--build`), then
+on the GPU runs S-cloud passes through it and prints, per section, the share of wave cycles
+(s_memtime, summed over waves): event handlers, refill + camera rays, segment starts, DDA
+walk, collision (exact candidate + density fetch + callbacks).
+
+usage: python tools/section_profile.py --build            (CPU, before gpurun)
+       python tools/section_profile.py [--res 1024] [--medium grid|nanovdb] [--steps 3]
+"""
+import argparse
+import ctypes
+import json
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+VARIANT = os.path.join(ROOT, "variants", "libavr_prof.so")
+NAMES = ["events", "refill+camera", "segment starts", "dda walk", "collision"]
+
+
+def build():
+    sys.path.insert(0, ROOT)
+    from acceleratedvolrenderer_amd import build as b
+    cmd = [b.HIPCC] + b.FLAGS + ["-DAVR_PROFILE_SECTIONS", b.SRC, "-o", VARIANT]
+    subprocess.check_call(cmd)
+    print(VARIANT)
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--build", action="store_true")
+    p.add_argument("--res", type=int, default=1024)
+    p.add_argument("--medium", default="grid", choices=["grid", "nanovdb"])
+    p.add_argument("--steps", type=int, default=3)
+    p.add_argument("--sampler", default="zsobol")
+    p.add_argument("--filter", default="gaussian")
+    a = p.parse_args()
+    if a.build:
+        return build()
+    os.environ["AVR_LIB"] = VARIANT
+    sys.path.insert(0, ROOT)
+    import torch
+    from acceleratedvolrenderer_amd import VolPathIntegrator, scenes, capi
+    n = a.res
+    density = torch.empty((n, n, n), dtype=torch.float32, device="cuda:0")
+    gen = capi.Context(0)
+    slab = n * n * 64
+    for first in range(0, n ** 3, slab):
+        gen.generate_cloud(density.data_ptr() + 4 * first, n, first, min(slab, n ** 3 - first))
+    gen.sync()
+    gen.close()
+    if a.medium == "nanovdb":
+        scene = scenes.s_cloud_vdb(scenes.vdb_grid(density.cpu().numpy()), sampler=a.sampler, spp=256, filter=a.filter)
+        del density
+    else:
+        scene = scenes.s_cloud(density, sampler=a.sampler, spp=256, filter=a.filter)
+    integ = VolPathIntegrator(scene, maxdepth=scenes.CLOUD_MAXDEPTH, spp=16, device=0)
+    lib = capi.load()
+    lib.avr_debug_sections.argtypes = [ctypes.POINTER(ctypes.c_ulonglong)]
+    out = (ctypes.c_ulonglong * 8)()
+    integ.ctx.render(0, 16, 0, scenes.CLOUD_MAXDEPTH)   # warmup (pixel tables)
+    integ.ctx.sync()
+    lib.avr_debug_sections(out)
+    t0 = time.perf_counter()
+    for k in range(1, 1 + a.steps):
+        integ.ctx.render(16 * k, 16 * (k + 1), 0, scenes.CLOUD_MAXDEPTH)
+    integ.ctx.sync()
+    dt = time.perf_counter() - t0
+    lib.avr_debug_sections(out)
+    tot = sum(out[i] for i in range(5))
+    res = {NAMES[i]: round(out[i] / tot, 4) for i in range(5)}
+    st = integ.stats()
+    print(json.dumps({"medium": a.medium, "res": n, "Msamples_per_s": 1280 * 720 * 16 * a.steps / dt / 1e6,
+                      "section_share": res, "wave_cycles": tot, "loop_iterations": st.get("loop_iterations"),
+                      "dda_steps": st.get("medium_dda_steps")}))
+    integ.close()
+
+
+if __name__ == "__main__":
+    main()
