@@ -55,15 +55,47 @@ AVR_HD void world_to_index(const Grid &g, float x, float y, float z, float *ix, 
 
 AVR_HD float lerp_vdb(float a, float b, float w) { return a + w * (b - a); }
 
-// SampleFromVoxels<Tree, 1, false> at index-space xyz
+// One axis of the 2-voxel stencil: block index, in-leaf offset and validity of voxels r, r+1
+struct StencilAxis {
+    int b0, b1, l0, l1;
+    bool v0, v1;
+};
+AVR_HD StencilAxis stencil_axis(int r, int nblocks, int shift) {
+    StencilAxis a;
+    a.b0 = r >> 3;
+    a.b1 = (r + 1) >> 3;
+    a.l0 = (r & 7) << shift;
+    a.l1 = ((r + 1) & 7) << shift;
+    a.v0 = r >= 0 && a.b0 < nblocks;
+    a.v1 = r + 1 >= 0 && a.b1 < nblocks;
+    return a;
+}
+// getValue for one stencil tap from the shared per-axis terms (same value as get_value)
+AVR_HD float stencil_value(const Grid &g, bool valid, int bx, int by, int bz, int off) {
+    if (!valid) return g.background;
+    const int s = g.slot[((long long)bz * g.lny + by) * g.lnx + bx];
+    if (s >= 0) return g.leaves[(long long)s * 512 + off];
+    if (s == kBackgroundSlot) return g.background;
+    return g.tiles[-s - 1];
+}
+
+// SampleFromVoxels<Tree, 1, false> at index-space xyz. The eight getValue calls share their
+// per-axis block / offset / bounds terms (the stencil crosses a block face on an axis only
+// when the voxel's local coordinate is 7); every tap reads the value get_value would.
 AVR_HD float sample_trilinear(const Grid &g, float x, float y, float z) {
     const float fx = __builtin_floorf(x), fy = __builtin_floorf(y), fz = __builtin_floorf(z);
     const int i = (int)fx, j = (int)fy, k = (int)fz;
     const float u = x - fx, v = y - fy, w = z - fz;
-    const float v000 = get_value(g, i, j, k), v001 = get_value(g, i, j, k + 1);
-    const float v010 = get_value(g, i, j + 1, k), v011 = get_value(g, i, j + 1, k + 1);
-    const float v100 = get_value(g, i + 1, j, k), v101 = get_value(g, i + 1, j, k + 1);
-    const float v110 = get_value(g, i + 1, j + 1, k), v111 = get_value(g, i + 1, j + 1, k + 1);
+    const StencilAxis ax = stencil_axis(i - g.ox, g.lnx, 6), ay = stencil_axis(j - g.oy, g.lny, 3),
+                      az = stencil_axis(k - g.oz, g.lnz, 0);
+    const float v000 = stencil_value(g, ax.v0 && ay.v0 && az.v0, ax.b0, ay.b0, az.b0, ax.l0 | ay.l0 | az.l0);
+    const float v001 = stencil_value(g, ax.v0 && ay.v0 && az.v1, ax.b0, ay.b0, az.b1, ax.l0 | ay.l0 | az.l1);
+    const float v010 = stencil_value(g, ax.v0 && ay.v1 && az.v0, ax.b0, ay.b1, az.b0, ax.l0 | ay.l1 | az.l0);
+    const float v011 = stencil_value(g, ax.v0 && ay.v1 && az.v1, ax.b0, ay.b1, az.b1, ax.l0 | ay.l1 | az.l1);
+    const float v100 = stencil_value(g, ax.v1 && ay.v0 && az.v0, ax.b1, ay.b0, az.b0, ax.l1 | ay.l0 | az.l0);
+    const float v101 = stencil_value(g, ax.v1 && ay.v0 && az.v1, ax.b1, ay.b0, az.b1, ax.l1 | ay.l0 | az.l1);
+    const float v110 = stencil_value(g, ax.v1 && ay.v1 && az.v0, ax.b1, ay.b1, az.b0, ax.l1 | ay.l1 | az.l0);
+    const float v111 = stencil_value(g, ax.v1 && ay.v1 && az.v1, ax.b1, ay.b1, az.b1, ax.l1 | ay.l1 | az.l1);
     return lerp_vdb(lerp_vdb(lerp_vdb(v000, v001, w), lerp_vdb(v010, v011, w), v),
                     lerp_vdb(lerp_vdb(v100, v101, w), lerp_vdb(v110, v111, w), v), u);
 }
