@@ -154,6 +154,16 @@ SIGNATURES = {
     "avr_graph_walks": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(AvrGraphSampling), ctypes.c_longlong, c_float_p,
                                        c_float_p, c_float_p, ctypes.POINTER(ctypes.c_longlong), ctypes.c_int,
                                        ctypes.c_int, ctypes.c_int, c_float_p, c_int_p]),
+    "avr_graph_walks_from": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(AvrGraphSampling), ctypes.c_longlong,
+                                            c_float_p, c_float_p, c_float_p, ctypes.POINTER(ctypes.c_longlong),
+                                            ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_float_p, c_int_p]),
+    "avr_graph_reinforce_rays": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(AvrGraphSampling), ctypes.c_int,
+                                                c_int_p, c_float_p, ctypes.c_float, ctypes.c_int, ctypes.c_int,
+                                                c_float_p, c_float_p, c_float_p, c_int_p]),
+    "avr_graph_add_walks_from": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_longlong, ctypes.c_int, c_float_p, c_int_p,
+                                                c_int_p]),
+    "avr_graph_out_degrees": (ctypes.c_int, [ctypes.c_void_p, c_int_p]),
+    "avr_graph_count_in_radius": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, c_int_p, ctypes.c_float, c_int_p]),
     "avr_graph_light": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(AvrGraphSampling), ctypes.c_int, c_float_p,
                                        c_float_p, ctypes.c_float, ctypes.c_int, ctypes.c_int, ctypes.c_float,
                                        c_float_p]),
@@ -386,7 +396,7 @@ class Context:
         return out
 
     # ---- lighting graph (src/graph) ----
-    def graph_walks(self, sampling, o, d, t_first, index0, iterations, sample_index, max_depth):
+    def graph_walks(self, sampling, o, d, t_first, index0, iterations, sample_index, max_depth, skip_dims=0):
         """FreeGraphBuilder::TracePath walks: (points (n_rays*iterations, max_depth, 3), counts)."""
         o = np.ascontiguousarray(o, np.float32).reshape(-1, 3)
         d = np.ascontiguousarray(d, np.float32).reshape(-1, 3)
@@ -395,11 +405,25 @@ class Context:
         n = len(o) * int(iterations)
         pts = np.zeros((n, max(1, int(max_depth)), 3), np.float32)
         counts = np.zeros(n, np.int32)
-        _check(self.lib.avr_graph_walks(self.h, ctypes.byref(sampling), len(o), _fp(o), _fp(d), _fp(t_first),
-                                        index0.ctypes.data_as(ctypes.POINTER(ctypes.c_longlong)), int(iterations),
-                                        int(sample_index), int(max_depth), _fp(pts),
-                                        counts.ctypes.data_as(c_int_p)))
+        _check(self.lib.avr_graph_walks_from(self.h, ctypes.byref(sampling), len(o), _fp(o), _fp(d), _fp(t_first),
+                                             index0.ctypes.data_as(ctypes.POINTER(ctypes.c_longlong)),
+                                             int(iterations), int(sample_index), int(skip_dims), int(max_depth),
+                                             _fp(pts), counts.ctypes.data_as(c_int_p)))
         return pts, counts
+
+    def graph_reinforce_rays(self, sampling, ids, points, radius, n_rays, cycle):
+        """ReinforceSparseVertices' rays: (o, d (n, n_rays, 3), t_first, valid (n, n_rays))."""
+        ids = np.ascontiguousarray(ids, np.int32)
+        pts = np.ascontiguousarray(points, np.float32).reshape(-1, 3)
+        n, k = len(ids), int(n_rays)
+        o = np.zeros((n, k, 3), np.float32)
+        d = np.zeros((n, k, 3), np.float32)
+        t = np.zeros((n, k), np.float32)
+        valid = np.zeros((n, k), np.int32)
+        _check(self.lib.avr_graph_reinforce_rays(self.h, ctypes.byref(sampling), n, ids.ctypes.data_as(c_int_p),
+                                                 _fp(pts), float(radius), k, int(cycle), _fp(o), _fp(d), _fp(t),
+                                                 valid.ctypes.data_as(c_int_p)))
+        return o, d, t, valid
 
     def graph_light(self, sampling, vertices, in_dir, radius, points_on_radius, iterations, max_dist_to_center):
         """LightingCalculator::GetLightVector: per-vertex light (Inv4Pi applied)."""
@@ -487,6 +511,26 @@ class Graph:
         counts = np.ascontiguousarray(counts, np.int32)
         _check(self.lib.avr_graph_add_walks(self.h, len(counts), int(max_depth), _fp(points),
                                             counts.ctypes.data_as(c_int_p)))
+
+    def add_walks_from(self, points, counts, max_depth, start_vertex):
+        points = np.ascontiguousarray(points, np.float32)
+        counts = np.ascontiguousarray(counts, np.int32)
+        sv = np.ascontiguousarray(start_vertex, np.int32)
+        _check(self.lib.avr_graph_add_walks_from(self.h, len(counts), int(max_depth), _fp(points),
+                                                 counts.ctypes.data_as(c_int_p), sv.ctypes.data_as(c_int_p)))
+
+    def out_degrees(self):
+        nv, _ = self.size()
+        out = np.zeros(nv, np.int32)
+        _check(self.lib.avr_graph_out_degrees(self.h, out.ctypes.data_as(c_int_p)))
+        return out
+
+    def count_in_radius(self, ids, radius):
+        ids = np.ascontiguousarray(ids, np.int32)
+        out = np.zeros(len(ids), np.int32)
+        _check(self.lib.avr_graph_count_in_radius(self.h, len(ids), ids.ctypes.data_as(c_int_p), float(radius),
+                                                  out.ctypes.data_as(c_int_p)))
+        return out
 
     def size(self):
         nv, ne = ctypes.c_longlong(), ctypes.c_longlong()

@@ -142,11 +142,14 @@ struct DiskRec {
 
 }  // namespace graph
 
+// skipDims: sampler dimensions already drawn after StartPixelSample before TracePath (the
+// reinforcement rays' phase sample, free_graph_builder.cpp:448-451)
 template <bool kZSobol>
 __global__ void __launch_bounds__(256) k_graph_walks(Params P, long long nPaths, int iterations, const float *__restrict__ o,
                                                      const float *__restrict__ d, const float *__restrict__ tFirst,
-                                                     const long long *__restrict__ index0, int sampleIndex, int resX,
-                                                     int maxDepth, float *__restrict__ points, int *__restrict__ counts) {
+                                                     const long long *__restrict__ index0, int sampleIndex, int skipDims,
+                                                     int resX, int maxDepth, float *__restrict__ points,
+                                                     int *__restrict__ counts) {
     __shared__ float s_maj[4096];
     const float *maj = stage_majorant(P.med, s_maj);
     const Lambda lw = sample_visible(0.f);   // mediumData.defaultLambda = film.SampleWavelengths(0)
@@ -162,6 +165,7 @@ __global__ void __launch_bounds__(256) k_graph_walks(Params P, long long nPaths,
         graph::index_pixel((unsigned long long)(index0[r] + i), resX, &px, &py);
         PathSampler<kZSobol> smp;
         smp.start(P, px, py, sampleIndex);
+        for (int k = 0; k < skipDims; ++k) (void)smp.get1d(P);
         V3 ro = {o[3 * r], o[3 * r + 1], o[3 * r + 2]}, rd = {d[3 * r], d[3 * r + 1], d[3 * r + 2]};
         bool usedTHit = false;
         int k = 0;
@@ -214,6 +218,61 @@ __global__ void __launch_bounds__(256) k_graph_walks(Params P, long long nPaths,
     flush_stat(P.stats, 3, nLookup);
     flush_stat(P.stats, 4, nIn);
     flush_stat(P.stats, 6, nSteps);
+}
+
+// FreeGraphBuilder::ReinforceSparseVertices' rays (free_graph_builder.cpp:434-475), one lane
+// per listed vertex: StartPixelSample({0, 0}, cycle) on a copy of the sampler, then
+// GetSphereVolumePointsRandom (util.h:238-252: rejection sampling in the cube; the three
+// Get1D of one Point3f are GCC-evaluated right to left, so the first draw is z; the
+// arithmetic is (double(u) - 0.5) * 2 * radius), then per point StartPixelSample(pixel(id *
+// nRays + point), cycle), the medium's HG Sample_p((1, 0, 0), Get2D()), GetHits(box) and
+// SkipIntersection. valid = RayEntersVolume (OutsideTwoHits or InsideOneHit).
+template <bool kZSobol>
+__global__ void __launch_bounds__(256) k_graph_reinforce_rays(Params P, int n, const int *__restrict__ ids,
+                                                              const float *__restrict__ pts, float radius, int nRays,
+                                                              int cycle, int resX, float *__restrict__ o,
+                                                              float *__restrict__ d, float *__restrict__ tFirst,
+                                                              int *__restrict__ valid) {
+    const int v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= n) return;
+    const V3 c = {pts[3 * v], pts[3 * v + 1], pts[3 * v + 2]};
+    PathSampler<kZSobol> cube;
+    cube.start(P, 0, 0, cycle);
+    const double r = (double)radius;
+    for (int k = 0; k < nRays;) {
+        const float pz = (float)(((double)cube.get1d(P) - 0.5) * 2 * r);
+        const float py = (float)(((double)cube.get1d(P) - 0.5) * 2 * r);
+        const float px = (float)(((double)cube.get1d(P) - 0.5) * 2 * r);
+        const V3 q = {px, py, pz};
+        if (!(length(q) < radius)) continue;
+        const long long ray = (long long)v * nRays + k;
+        const V3 sp = q + c;
+        int pxl, pyl;
+        graph::index_pixel((unsigned long long)ids[v] * (unsigned long long)nRays + (unsigned long long)k, resX, &pxl,
+                           &pyl);
+        PathSampler<kZSobol> smp;
+        smp.start(P, pxl, pyl, cycle);
+        float u0, u1, pdf;
+        smp.get2d(P, &u0, &u1);
+        const V3 dir = hg_sample(V3{1.f, 0.f, 0.f}, P.med.g, u0, u1, &pdf);
+        const graph::Hits h = graph::box_hits(P.med, sp, dir);
+        V3 og = sp;
+        float t = 0.f;
+        int ok = 0;
+        if (h.type == graph::kOutsideTwoHits) {
+            og = sp + dir * h.t0;
+            t = h.t1 - h.t0;
+            ok = 1;
+        } else if (h.type == graph::kInsideOneHit) {
+            t = h.t0;
+            ok = 1;
+        }
+        o[3 * ray] = og.x; o[3 * ray + 1] = og.y; o[3 * ray + 2] = og.z;
+        d[3 * ray] = dir.x; d[3 * ray + 1] = dir.y; d[3 * ray + 2] = dir.z;
+        tFirst[ray] = t;
+        valid[ray] = ok;
+        ++k;
+    }
 }
 
 // Per vertex: disk points around vertex - inDir * maxDistToCenter * 2 (GetDiskPoints, util.h:179-204,

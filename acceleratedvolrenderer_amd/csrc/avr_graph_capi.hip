@@ -41,7 +41,15 @@ extern "C" {
 int avr_graph_walks(avr_context *c, const avr_graph_sampling *s, long long n_rays, const float *o, const float *d,
                     const float *t_first, const long long *index0, int iterations, int sample_index, int max_depth,
                     float *points, int *counts) {
-    if (!c || n_rays < 0 || iterations < 0 || max_depth < 0) return fail(AVR_ERR_ARG, "bad walk arguments");
+    return avr_graph_walks_from(c, s, n_rays, o, d, t_first, index0, iterations, sample_index, 0, max_depth, points,
+                                counts);
+}
+
+int avr_graph_walks_from(avr_context *c, const avr_graph_sampling *s, long long n_rays, const float *o, const float *d,
+                         const float *t_first, const long long *index0, int iterations, int sample_index,
+                         int skip_dims, int max_depth, float *points, int *counts) {
+    if (!c || n_rays < 0 || iterations < 0 || max_depth < 0 || skip_dims < 0)
+        return fail(AVR_ERR_ARG, "bad walk arguments");
     if (!c->has_medium) return fail(AVR_ERR_STATE, "medium required");
     const long long nPaths = n_rays * (long long)iterations;
     if (nPaths == 0) return AVR_OK;
@@ -73,10 +81,10 @@ int avr_graph_walks(avr_context *c, const avr_graph_sampling *s, long long n_ray
         const int blocks = blocks_for(nPaths, 256, 256 * 64);
         if (p.sampler_kind == 1)
             hipLaunchKernelGGL(avr::k_graph_walks<true>, dim3(blocks), dim3(256), 0, c->stream, p, nPaths, iterations,
-                               dO, dD, dT, dI, sample_index, s->resolution_x, max_depth, dP, dC);
+                               dO, dD, dT, dI, sample_index, skip_dims, s->resolution_x, max_depth, dP, dC);
         else
             hipLaunchKernelGGL(avr::k_graph_walks<false>, dim3(blocks), dim3(256), 0, c->stream, p, nPaths, iterations,
-                               dO, dD, dT, dI, sample_index, s->resolution_x, max_depth, dP, dC);
+                               dO, dD, dT, dI, sample_index, skip_dims, s->resolution_x, max_depth, dP, dC);
         e = hipGetLastError();
     }
     if (e == hipSuccess && max_depth > 0) e = hipMemcpyAsync(points, dP, szP, hipMemcpyDeviceToHost, c->stream);
@@ -85,6 +93,52 @@ int avr_graph_walks(avr_context *c, const avr_graph_sampling *s, long long n_ray
     (void)hipStreamSynchronize(c->stream);
     (void)hipFree(buf);
     if (e != hipSuccess) return fail(AVR_ERR_HIP, std::string("graph walks: ") + hipGetErrorString(e));
+    return AVR_OK;
+}
+
+int avr_graph_reinforce_rays(avr_context *c, const avr_graph_sampling *s, int n, const int *vertex_ids,
+                             const float *points, float vertex_radius, int n_rays, int cycle, float *o, float *d,
+                             float *t_first, int *valid) {
+    if (!c || n < 0 || n_rays < 0 || cycle < 0 || !(vertex_radius > 0)) return fail(AVR_ERR_ARG, "bad reinforce arguments");
+    if (!c->has_medium) return fail(AVR_ERR_STATE, "medium required");
+    const long long nr = (long long)n * n_rays;
+    if (nr == 0) return AVR_OK;
+    if (!vertex_ids || !points || !o || !d || !t_first || !valid) return fail(AVR_ERR_ARG, "null buffer");
+    long long maxId = 0;
+    for (int i = 0; i < n; ++i) {
+        if (vertex_ids[i] < 0) return fail(AVR_ERR_ARG, "negative vertex id");
+        maxId = std::max<long long>(maxId, vertex_ids[i]);
+    }
+    avr::Params p;
+    int rc = graph_params(c, s, (unsigned long long)(maxId + 1) * (unsigned long long)n_rays, cycle, &p);
+    if (rc) return rc;
+    HIP_TRY(hipSetDevice(c->device));
+    char *buf = nullptr;
+    const size_t szI = (size_t)n * 4, szP = (size_t)n * 12, szR = (size_t)nr * 12, szT = (size_t)nr * 4;
+    HIP_TRY(dalloc(&buf, szI + szP + 2 * szR + 2 * szT));
+    int *dId = (int *)buf;
+    float *dPt = (float *)(buf + szI), *dO = (float *)(buf + szI + szP), *dD = (float *)(buf + szI + szP + szR);
+    float *dT = (float *)(buf + szI + szP + 2 * szR);
+    int *dV = (int *)(buf + szI + szP + 2 * szR + szT);
+    hipError_t e = hipMemcpyAsync(dId, vertex_ids, szI, hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(dPt, points, szP, hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) {
+        if (p.sampler_kind == 1)
+            hipLaunchKernelGGL(avr::k_graph_reinforce_rays<true>, dim3((n + 255) / 256), dim3(256), 0, c->stream, p, n,
+                               dId, dPt, vertex_radius, n_rays, cycle, s->resolution_x, dO, dD, dT, dV);
+        else
+            hipLaunchKernelGGL(avr::k_graph_reinforce_rays<false>, dim3((n + 255) / 256), dim3(256), 0, c->stream, p, n,
+                               dId, dPt, vertex_radius, n_rays, cycle, s->resolution_x, dO, dD, dT, dV);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(o, dO, szR, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(d, dD, szR, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(t_first, dT, szT, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(valid, dV, szT, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    (void)hipStreamSynchronize(c->stream);
+    (void)hipFree(buf);
+    if (e != hipSuccess) return fail(AVR_ERR_HIP, std::string("graph reinforce rays: ") + hipGetErrorString(e));
     return AVR_OK;
 }
 
@@ -241,6 +295,36 @@ int avr_graph_add_walks(avr_graph *g, long long n_walks, int max_depth, const fl
         const int k = counts[w];
         if (k < 0 || k > max_depth) return fail(AVR_ERR_ARG, "walk count out of range");
         g->b.AddWalk(points + (size_t)w * max_depth * 3, k, k == max_depth);
+    }
+    return AVR_OK;
+}
+int avr_graph_add_walks_from(avr_graph *g, long long n_walks, int max_depth, const float *points, const int *counts,
+                             const int *start_vertex) {
+    if (!g || n_walks < 0 || max_depth < 0) return fail(AVR_ERR_ARG, "bad walks");
+    if (n_walks > 0 && (!counts || !start_vertex || (max_depth > 0 && !points))) return fail(AVR_ERR_ARG, "null buffer");
+    for (long long w = 0; w < n_walks; ++w) {
+        const int k = counts[w], sv = start_vertex[w];
+        if (k < 0 || k > max_depth) return fail(AVR_ERR_ARG, "walk count out of range");
+        if (sv < -1 || sv >= (long long)g->b.NumVertices()) return fail(AVR_ERR_ARG, "start vertex out of range");
+        // with a starting vertex the path holds one vertex before the first scatter, so the
+        // walk was traced with max_depth - 1 scatters
+        const int cap = sv >= 0 ? max_depth - 1 : max_depth;
+        if (k > cap) return fail(AVR_ERR_ARG, "walk count out of range");
+        g->b.AddWalk(points + (size_t)w * max_depth * 3, k, k == cap, sv);
+    }
+    return AVR_OK;
+}
+int avr_graph_out_degrees(avr_graph *g, int *out) {
+    if (!g || !out) return fail(AVR_ERR_ARG, "null buffer");
+    g->b.OutDegrees(out);
+    return AVR_OK;
+}
+int avr_graph_count_in_radius(avr_graph *g, int n, const int *vertex_ids, float radius, int *counts) {
+    if (!g || n < 0 || !(radius > 0)) return fail(AVR_ERR_ARG, "bad radius query");
+    if (n > 0 && (!vertex_ids || !counts)) return fail(AVR_ERR_ARG, "null buffer");
+    for (int i = 0; i < n; ++i) {
+        if (vertex_ids[i] < 0 || vertex_ids[i] >= (long long)g->b.NumVertices()) return fail(AVR_ERR_ARG, "vertex id");
+        counts[i] = g->b.CountInRadius(vertex_ids[i], radius);
     }
     return AVR_OK;
 }

@@ -23,9 +23,12 @@ class Builder {
   public:
     explicit Builder(float radius) : r_(radius), r2_(radius * radius) {}   // Sqr(nodeRadius), :14
 
-    // One walk: k scatter points; forced = the walk stopped at maxDepth (PathData::forcedEnd)
-    void AddWalk(const float *pts, int k, bool forced) {
+    // One walk: k scatter points; forced = the walk stopped at maxDepth (PathData::forcedEnd);
+    // start >= 0: TracePath's startingVertex (free_graph_builder.cpp:24-25), the path's
+    // first vertex before any scatter (the reinforcement walks)
+    void AddWalk(const float *pts, int k, bool forced, int start = -1) {
         path_.clear();
+        if (start >= 0) path_.push_back(start);
         for (int j = 0; j < k; ++j) {
             const float p[3] = {pts[3 * j], pts[3 * j + 1], pts[3 * j + 2]};
             // HandlePotentialPathEnd after the segment that produced this scatter
@@ -40,6 +43,33 @@ class Builder {
         // when the walk was cut at maxDepth
         if (!forced && !path_.empty()) ++vsamples_[path_.back()];
         PathInfo(forced);
+    }
+
+    // Vertex::outEdges.size(): distinct targets per vertex
+    void OutDegrees(int *out) const {
+        for (size_t v = 0; v < NumVertices(); ++v) out[v] = 0;
+        for (int f : efrom_) ++out[f];
+    }
+    // CountInRadius (free_graph_builder.cpp:229-236): vertices with squared distance strictly
+    // below Sqr(radius) (nanoflann RadiusResultSet), the vertex itself included
+    int CountInRadius(int v, float radius) const {
+        const float r2 = radius * radius;
+        const float *p = &vxyz_[3 * (size_t)v];
+        const int reach = (int)std::ceil(radius / r_);
+        const int64_t cx = Cell(p[0]), cy = Cell(p[1]), cz = Cell(p[2]);
+        int n = 0;
+        if ((int64_t)reach * 2 + 1 > 64) {   // wide query: scan every vertex
+            for (size_t u = 0; u < NumVertices(); ++u) n += DistSq(&vxyz_[3 * u], p) < r2;
+            return n;
+        }
+        for (int64_t z = cz - reach; z <= cz + reach; ++z)
+            for (int64_t y = cy - reach; y <= cy + reach; ++y)
+                for (int64_t x = cx - reach; x <= cx + reach; ++x) {
+                    auto it = grid_.find(Key(x, y, z));
+                    if (it == grid_.end()) continue;
+                    for (int u : it->second) n += DistSq(&vxyz_[3 * (size_t)u], p) < r2;
+                }
+        return n;
     }
 
     size_t NumVertices() const { return vsamples_.size(); }

@@ -18,8 +18,8 @@ through include/avr.h; the order-dependent vertex merge runs in C++ on the host
 geometry is in the scene's render space; the medium's boundary primitive is its bounds box
 (DESIGN.md §9).
 
-Not mirrored: ReinforceSparseVertices (:280-462, host kd-tree loops that re-use TracePath;
-`active` reinforcement raises NotImplementedError) and the graph's text file format.
+ReinforceSparseVertices (:280-475) runs its rays and walks on the GPU and its sparse-vertex
+checks on the host graph. Not mirrored: the graph's text file format.
 """
 import json
 import math
@@ -261,17 +261,87 @@ class FreeGraphBuilder:
 
     def build_graph(self):
         c = self.config
-        if c.edge_reinforcement.get("active") or c.neighbour_reinforcement.get("active"):
-            raise NotImplementedError("sparse-vertex reinforcement is not implemented")
         o, d, t, idx = self.start_rays()
         pts, counts = self.ctx.graph_walks(self.sampling.struct(), o, d, t, idx, c.iterations_per_step,
                                            self.sample_index_offset, c.max_depth)
         g = capi.Graph(self.radius)
         g.add_walks(pts, counts, c.max_depth)
+        self.reinforce_cycles = self.reinforce_sparse_vertices(g)
         graph = FreeGraph(g, self.radius)
         if c.render_search_range.get("active"):
             graph.search_range = compute_search_ranges(graph.points, int(c.render_search_range["neighboursToUse"]))
         return graph
+
+
+    def _reinforce(self, g, ids, cfg, cycle):
+        """ReinforceSparseVertices(graph, sparseVertices, ...) (:434-475): every listed
+        vertex's sphere rays in one device call, their walks in a second (the rays never
+        depend on the graph), merged in vertex then point order as the reference's loop."""
+        if not len(ids):
+            return
+        md = self.config.max_depth
+        k = int(cfg["reinforcementRays"])
+        ids = np.asarray(ids, np.int32)
+        xyz, _ = g.vertices()
+        smp = self.sampling.struct()
+        o, d, t, valid = self.ctx.graph_reinforce_rays(smp, ids, xyz[ids], self.radius, k, cycle)
+        sel = valid.ravel() != 0
+        if not sel.any():
+            return
+        index0 = (ids.astype(np.int64)[:, None] * k + np.arange(k)[None, :]).ravel()[sel]
+        pts, counts = self.ctx.graph_walks(smp, o.reshape(-1, 3)[sel], d.reshape(-1, 3)[sel], t.ravel()[sel], index0,
+                                           1, cycle, md - 1, skip_dims=2)
+        padded = np.zeros((len(counts), md, 3), np.float32)   # avr_graph_add_walks_from: stride max_depth
+        padded[:, :md - 1] = pts[:, :md - 1]
+        g.add_walks_from(padded, counts, md, np.repeat(ids, k)[sel])
+
+    def reinforce_sparse_vertices(self, g):
+        """FreeGraphBuilder::ReinforceSparseVertices (free_graph_builder.cpp:280-432): until the
+        fraction of initial vertices with fewer than `edgesForNotSparse` out-edges (and / or
+        fewer than `neighboursForNotSparse` vertices within radius x neighbourRangeModifier)
+        drops below `unsatisfiedAllowedRatio`, walks from `reinforcementRays` random points in
+        each sparse vertex's sphere are added, one sampler cycle per round. The sparse lists are
+        re-checked after every pass (the reference skips the re-check when quiet, :392-408,
+        which never terminates). Returns the cycles run."""
+        c = self.config
+        ec, nc = c.edge_reinforcement, c.neighbour_reinforcement
+        ea, na = bool(ec.get("active")), bool(nc.get("active"))
+        if not (ea or na):
+            return 0
+        if c.max_depth == 1:
+            raise ValueError("Unable to reinforce with max depth of 1")
+        n0 = g.size()[0]
+        initial = np.arange(n0, dtype=np.int32)
+        r_sq = f32(self.radius * self.radius)
+        n_radius = f32(f32(np.sqrt(r_sq)) * f32(nc.get("neighbourRangeModifier", 1.0)))
+        state = {"e": initial, "n": initial}
+
+        def check_e():
+            deg = g.out_degrees()
+            state["e"] = state["e"][deg[state["e"]] < int(ec["edgesForNotSparse"])]
+            return len(state["e"]) / n0 < float(ec["unsatisfiedAllowedRatio"])
+
+        def check_n():
+            cnt = g.count_in_radius(state["n"], n_radius)
+            state["n"] = state["n"][cnt < int(nc["neighboursForNotSparse"])]
+            return len(state["n"]) / n0 < float(nc["unsatisfiedAllowedRatio"])
+
+        sat_e = check_e() if ea else True
+        sat_n = check_n() if na else True
+        cycle = 0
+        while not (sat_e and sat_n):
+            if cycle >= self.max_reinforce_cycles:
+                raise RuntimeError(f"graph reinforcement not satisfied after {cycle} cycles")
+            if ea and not sat_e:
+                self._reinforce(g, state["e"], ec, cycle)
+                sat_e = check_e()
+            if na and not sat_n:
+                self._reinforce(g, state["n"], nc, cycle)
+                sat_n = check_n()
+            cycle += 1
+        return cycle
+
+    max_reinforce_cycles = 64
 
 
 def compute_search_ranges(points, n_closest):

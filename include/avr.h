@@ -296,6 +296,23 @@ int avr_graph_walks(avr_context *ctx, const avr_graph_sampling *smp, long long n
                     const float *t_first, const long long *index0, int iterations, int sample_index, int max_depth,
                     float *points, int *counts);
 
+/* avr_graph_walks with skip_dims sampler dimensions drawn after StartPixelSample before the
+ * walk (the reinforcement walks continue the stream their ray's phase sample started). */
+int avr_graph_walks_from(avr_context *ctx, const avr_graph_sampling *smp, long long n_rays, const float *o,
+                         const float *d, const float *t_first, const long long *index0, int iterations,
+                         int sample_index, int skip_dims, int max_depth, float *points, int *counts);
+
+/* FreeGraphBuilder::ReinforceSparseVertices' rays (free_graph_builder.cpp:434-475): for each of
+ * n vertices (ids, points n*3), GetSphereVolumePointsRandom(vertex_radius, point, n_rays) with
+ * the sampler at StartPixelSample({0, 0}, cycle), then per sphere point p the medium's HG
+ * Sample_p((1,0,0), Get2D()) at StartPixelSample(pixel(id * n_rays + p), cycle) and the medium
+ * box crossing: o/d (n*n_rays*3), t_first (medium exit after SkipIntersection), valid
+ * (RayEntersVolume). The walk from each valid ray: avr_graph_walks_from(.., index0 =
+ * id * n_rays + p, iterations 1, sample_index cycle, skip_dims 2, max_depth - 1). */
+int avr_graph_reinforce_rays(avr_context *ctx, const avr_graph_sampling *smp, int n, const int *vertex_ids,
+                             const float *points, float vertex_radius, int n_rays, int cycle, float *o, float *d,
+                             float *t_first, int *valid);
+
 /* LightingCalculator::GetLightVector (lighting_calculator.cpp:84-155) with
  * ComputeRaysToSphere (graph/util.h:814-840) and SampleTransmittance (util.h:344-366):
  * light[v] = Inv4Pi * average over the disk points of vertex v (GetDiskPoints(vertex -
@@ -330,6 +347,13 @@ typedef struct avr_graph avr_graph;
 int avr_graph_create(float vertex_radius, avr_graph **out);
 int avr_graph_destroy(avr_graph *g);
 int avr_graph_add_walks(avr_graph *g, long long n_walks, int max_depth, const float *points, const int *counts);
+/* Walks that start at an existing vertex (TracePath's startingVertex; -1 = none), traced with
+ * max_depth - 1 scatters when a start vertex is given (max_depth counts path vertices). */
+int avr_graph_add_walks_from(avr_graph *g, long long n_walks, int max_depth, const float *points, const int *counts,
+                             const int *start_vertex);
+/* Vertex::outEdges.size() per vertex; CountInRadius (squared distance < radius^2, self included) */
+int avr_graph_out_degrees(avr_graph *g, int *out);
+int avr_graph_count_in_radius(avr_graph *g, int n, const int *vertex_ids, float radius, int *counts);
 int avr_graph_size(avr_graph *g, long long *n_vertices, long long *n_edges);
 int avr_graph_vertices(avr_graph *g, float *xyz, int *samples);
 int avr_graph_edges(avr_graph *g, int *from, int *to, int *samples);

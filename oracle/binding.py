@@ -180,8 +180,11 @@ def lib():
                                          ctypes.c_float, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float,
                                          c_float_p]
         L.oracle_graph_walks.argtypes = [ctypes.POINTER(OracleScene), ctypes.c_int, c_float_p, c_float_p, c_float_p,
-                                         c_ll_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_float_p,
-                                         c_int_p]
+                                         c_ll_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                         c_float_p, c_int_p]
+        L.oracle_graph_reinforce_rays.argtypes = [ctypes.POINTER(OracleScene), ctypes.c_int, c_int_p, c_float_p,
+                                                  ctypes.c_float, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_float_p,
+                                                  c_float_p, c_float_p, c_int_p]
         L.oracle_graph_propagate.restype = ctypes.c_int
         L.oracle_graph_propagate.argtypes = [ctypes.c_int, c_int_p, c_int_p, c_float_p, c_float_p, ctypes.c_int,
                                              c_float_p]
@@ -484,7 +487,23 @@ class OracleRun:
                                      fp(out))
         return out
 
-    def graph_walks(self, o, d, t_first, index0, iterations, sample_index, res_x, max_depth, sampler=None):
+    def graph_reinforce_rays(self, ids, points, radius, n_rays, cycle, res_x, sampler=None):
+        """ReinforceSparseVertices' rays: (o, d (n, n_rays, 3), t_first, valid (n, n_rays))."""
+        ids = np.ascontiguousarray(ids, np.int32)
+        pts = np.ascontiguousarray(points, np.float32)
+        n, k = len(ids), int(n_rays)
+        o = np.zeros((n, k, 3), np.float32)
+        d = np.zeros((n, k, 3), np.float32)
+        t = np.zeros((n, k), np.float32)
+        valid = np.zeros((n, k), np.int32)
+        set_libm(self.libm)
+        with self._graph_sampler(sampler) as s:
+            lib().oracle_graph_reinforce_rays(ctypes.byref(s), n, _ip(ids), fp(pts), float(radius), k, int(cycle),
+                                              int(res_x), fp(o), fp(d), fp(t), _ip(valid))
+        return o, d, t, valid
+
+    def graph_walks(self, o, d, t_first, index0, iterations, sample_index, res_x, max_depth, sampler=None,
+                    skip_dims=0):
         """FreeGraphBuilder::TracePath walks: (points[nrays*iterations, max_depth, 3], counts)."""
         o = np.ascontiguousarray(o, np.float32)
         d = np.ascontiguousarray(d, np.float32)
@@ -497,7 +516,8 @@ class OracleRun:
         with self._graph_sampler(sampler) as s:
             lib().oracle_graph_walks(ctypes.byref(s), len(o), fp(o), fp(d), fp(t_first),
                                      index0.ctypes.data_as(ctypes.POINTER(ctypes.c_longlong)), int(iterations),
-                                     int(sample_index), int(res_x), int(max_depth), fp(pts), _ip(counts))
+                                     int(sample_index), int(skip_dims), int(res_x), int(max_depth), fp(pts),
+                                     _ip(counts))
         return pts, counts
 
     def graph_box_hits(self, o, d):

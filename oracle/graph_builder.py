@@ -44,8 +44,8 @@ class OracleGraph:
                 best, best_d = v, d
         return best
 
-    def add_walk(self, pts, forced):
-        path = []
+    def add_walk(self, pts, forced, start=-1):
+        path = [start] if start >= 0 else []   # TracePath's startingVertex (:24-25)
         for p in pts:
             p = tuple(np.float32(c) for c in p)
             if path:
@@ -91,9 +91,72 @@ class OracleGraph:
         for w, k in enumerate(counts):
             self.add_walk(points[w, :k], int(k) == max_depth)
 
+    def out_degrees(self):
+        deg = np.zeros(len(self.xyz), np.int32)
+        for (f, _t) in self.edges:
+            deg[f] += 1
+        return deg
+
+    def count_in_radius(self, v, radius):
+        """CountInRadius (:229-236): squared distance strictly below radius^2, self included."""
+        r2 = np.float32(radius) * np.float32(radius)
+        return sum(1 for q in self.xyz if self._d2(q, self.xyz[v]) < r2)
+
     def transport_dense(self):
         n = len(self.xyz)
         T = np.zeros((n, n), np.float32)
         for (f, t), s in self.edges.items():
             T[f, t] = np.float32(s) / np.float32(self.samples[f])
         return T
+
+
+def reinforce(graph, run, sampling, radius, max_depth, edge_cfg, neighbour_cfg, max_cycles=64):
+    """FreeGraphBuilder::ReinforceSparseVertices (free_graph_builder.cpp:280-475) over the
+    oracle's rays and walks. The sparse lists are re-checked after every reinforcement pass
+    (the reference re-checks only when not quiet: :392-408). Returns the cycles run."""
+    if max_depth == 1:
+        raise ValueError("Unable to reinforce with max depth of 1")
+    ea, na = bool(edge_cfg.get("active")), bool(neighbour_cfg.get("active"))
+    initial = list(range(len(graph.xyz)))
+    few_e, few_n = list(initial), list(initial)
+    # Sqr(sqrt(squaredSearchRadius) * neighbourRangeModifier) (:287), squared again in the count
+    r_sq = np.float32(np.float32(radius) * np.float32(radius))
+    n_radius = np.float32(np.float32(np.sqrt(r_sq)) * np.float32(neighbour_cfg.get("neighbourRangeModifier", 1.0)))
+
+    def check_e():
+        nonlocal few_e
+        deg = graph.out_degrees()
+        few_e = [v for v in few_e if deg[v] < edge_cfg["edgesForNotSparse"]]
+        return len(few_e) / len(initial) < edge_cfg["unsatisfiedAllowedRatio"]
+
+    def check_n():
+        nonlocal few_n
+        few_n = [v for v in few_n if graph.count_in_radius(v, n_radius) < neighbour_cfg["neighboursForNotSparse"]]
+        return len(few_n) / len(initial) < neighbour_cfg["unsatisfiedAllowedRatio"]
+
+    sat_e = check_e() if ea else True
+    sat_n = check_n() if na else True
+    res_x = sampling[3]
+    cycle = 0
+    while (not sat_e or not sat_n) and cycle < max_cycles:
+        for active, sat, lst, cfg, chk in ((ea, sat_e, few_e, edge_cfg, check_e), (na, sat_n, few_n, neighbour_cfg,
+                                                                                   check_n)):
+            if not active or sat:
+                continue
+            for v in list(lst):
+                k = int(cfg["reinforcementRays"])
+                o, d, t, valid = run.graph_reinforce_rays([v], [graph.xyz[v]], radius, k, cycle, res_x,
+                                                          sampler=sampling)
+                sel = np.nonzero(valid[0])[0]
+                if len(sel) == 0:
+                    continue
+                pts, counts = run.graph_walks(o[0][sel], d[0][sel], t[0][sel], v * k + sel, 1, cycle, res_x,
+                                              max_depth - 1, sampler=sampling, skip_dims=2)
+                for w in range(len(sel)):
+                    graph.add_walk(pts[w, :counts[w]], int(counts[w]) == max_depth - 1, start=v)
+            if chk is check_e:
+                sat_e = check_e()
+            else:
+                sat_n = check_n()
+        cycle += 1
+    return cycle

@@ -2314,9 +2314,11 @@ void oracle_graph_light(const OracleScene *s, int nv, const float *verts, const 
 // tracking with absorb / scatter / null choice; the first segment ends at tFirst, later ones
 // at the box crossing; a real scatter records its point and, below maxDepth, samples the HG
 // phase function (Get2D) for the next direction. Writes up to maxDepth points per walk.
+// skipDims: sampler dimensions drawn after StartPixelSample before TracePath (the
+// reinforcement rays' phase sample, free_graph_builder.cpp:448-451)
 void oracle_graph_walks(const OracleScene *s, int nrays, const float *o, const float *d, const float *tFirst,
-                        const long long *index0, int iterations, int sampleIndex, int resX, int maxDepth,
-                        float *points, int *counts) {
+                        const long long *index0, int iterations, int sampleIndex, int skipDims, int resX,
+                        int maxDepth, float *points, int *counts) {
     using namespace graphm;
     SceneView sv(*s);
     Lambda l = SampleVisible(0.f);
@@ -2327,6 +2329,7 @@ void oracle_graph_walks(const OracleScene *s, int nrays, const float *o, const f
             int px, py;
             IndexPixel((uint64_t)(index0[r] + i), resX, &px, &py);
             smp.Start(*s, px, py, sampleIndex);
+            for (int k = 0; k < skipDims; ++k) (void)smp.Get1D();
             V3 ro = {o[3 * r], o[3 * r + 1], o[3 * r + 2]}, rd = {d[3 * r], d[3 * r + 1], d[3 * r + 2]};
             bool usedTHit = false;
             int k = 0;
@@ -2363,6 +2366,51 @@ void oracle_graph_walks(const OracleScene *s, int nrays, const float *o, const f
             }
             counts[path] = k;
         }
+}
+
+// FreeGraphBuilder::ReinforceSparseVertices' rays (free_graph_builder.cpp:434-475):
+// `sampler.StartPixelSample(Point2i(0, 0), cycle)`, then GetSphereVolumePointsRandom
+// (util.h:238-252) on the sampler copy it receives: Point3f((Get1D() - 0.5) * 2 * radius, x3)
+// in double arithmetic, the constructor's arguments evaluated right to left by GCC (the first
+// draw is z), kept when Length < radius, plus the center; then for each point
+// StartPixelSample(pixel(vertexId * nRays + p), cycle), the medium's phase
+// Sample_p(Vector3f(1, 0, 0), Get2D()), GetHits(primitive) and SkipIntersection.
+void oracle_graph_reinforce_rays(const OracleScene *s, int n, const int *ids, const float *pts, float radius, int nRays,
+                                 int cycle, int resX, float *o, float *d, float *tFirst, int *valid) {
+    using namespace graphm;
+    SceneView sv(*s);
+    for (int v = 0; v < n; ++v) {
+        Sampler cube;
+        cube.Start(*s, 0, 0, cycle);
+        const V3 c = {pts[3 * v], pts[3 * v + 1], pts[3 * v + 2]};
+        std::vector<V3> sp;
+        while ((int)sp.size() < nRays) {
+            const double uz = cube.Get1D(), uy = cube.Get1D(), ux = cube.Get1D();
+            const V3 q = {(float)((ux - 0.5) * 2 * radius), (float)((uy - 0.5) * 2 * radius),
+                          (float)((uz - 0.5) * 2 * radius)};
+            if (Length(q) < radius) sp.push_back(q + c);
+        }
+        for (int k = 0; k < nRays; ++k) {
+            const long long ray = (long long)v * nRays + k;
+            int px, py;
+            IndexPixel((uint64_t)ids[v] * (uint64_t)nRays + (uint64_t)k, resX, &px, &py);
+            Sampler smp;
+            smp.Start(*s, px, py, cycle);
+            float u0, u1, pdf;
+            smp.Get2D(&u0, &u1);
+            const V3 dir = SampleHenyeyGreenstein(V3{1.f, 0.f, 0.f}, s->g, u0, u1, &pdf);
+            const Hits h = BoxHits(sv, sp[k], dir);
+            V3 og = sp[k];
+            float t = 0.f;
+            int ok = 0;
+            if (h.type == OutsideTwoHits) { og = sp[k] + dir * h.t[0]; t = h.t[1] - h.t[0]; ok = 1; }
+            else if (h.type == InsideOneHit) { t = h.t[0]; ok = 1; }
+            o[3 * ray] = og.x; o[3 * ray + 1] = og.y; o[3 * ray + 2] = og.z;
+            d[3 * ray] = dir.x; d[3 * ray + 1] = dir.y; d[3 * ray + 2] = dir.z;
+            tFirst[ray] = t;
+            valid[ray] = ok;
+        }
+    }
 }
 
 // LightingCalculator::ComputeFinalLight (lighting_calculator.cpp:23-59) with Eigen's

@@ -111,6 +111,40 @@ def test_graph_assembly_matches_restatement(seed):
     assert avg == pytest.approx(ref.pl_sum / ref.pl_count, rel=1e-6)
 
 
+def test_graph_assembly_with_start_vertices_matches_restatement():
+    """Reinforcement walks (TracePath's startingVertex, free_graph_builder.cpp:24-25): the
+    start vertex heads the path, takes the first segment's sample and the first edge; out
+    degrees and radius counts (CountInRadius, :229-236) against the restatement."""
+    from acceleratedvolrenderer_amd import capi
+    from oracle.graph_builder import OracleGraph
+    rng = np.random.default_rng(7)
+    radius, md = 0.04, 6
+    pts, counts = _synthetic_walks(rng, 200, md, radius)
+    g, ref = capi.Graph(radius), OracleGraph(radius)
+    g.add_walks(pts, counts, md)
+    ref.add_walks(pts, counts, md)
+    nv = g.size()[0]
+    p2, c2 = _synthetic_walks(rng, 150, md - 1, radius)
+    padded = np.zeros((150, md, 3), np.float32)
+    padded[:, :md - 1] = p2
+    start = rng.integers(0, nv, 150).astype(np.int32)
+    g.add_walks_from(padded, c2, md, start)
+    for w in range(150):
+        ref.add_walk(p2[w, :c2[w]], int(c2[w]) == md - 1, start=int(start[w]))
+    xyz, smp = g.vertices()
+    assert np.array_equal(xyz, np.array(ref.xyz, np.float32)) and smp.tolist() == ref.samples
+    fr, to, es = g.edges()
+    assert list(zip(fr.tolist(), to.tolist(), es.tolist())) == [(a, b, s) for (a, b), s in ref.edges.items()]
+    assert g.out_degrees().tolist() == ref.out_degrees().tolist()
+    ids = np.arange(len(xyz), dtype=np.int32)
+    for r in (0.03, 0.1, 0.5):
+        assert g.count_in_radius(ids, r).tolist() == [ref.count_in_radius(v, r) for v in ids]
+    avg, cnt = g.in_node_path_length()
+    assert cnt == ref.pl_count and avg == pytest.approx(ref.pl_sum / ref.pl_count, rel=1e-6)
+    with pytest.raises(RuntimeError, match="start vertex"):
+        g.add_walks_from(padded[:1], c2[:1], md, np.array([len(xyz) + 5], np.int32))
+
+
 def test_graph_assembly_argument_errors():
     from acceleratedvolrenderer_amd import capi
     with pytest.raises(RuntimeError, match="radius"):
@@ -316,3 +350,55 @@ def test_graph_pipeline_end_to_end(gpu_ctx):
     assert it_o == 6
     assert np.allclose(lc.light_scalar, total, rtol=1e-5)
     print(f"graph: {g.num_vertices} vertices, {len(g.edge_from)} edges, light total mean {total.mean():.4e}")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", [0, 1], ids=["independent", "zsobol"])
+def test_graph_reinforce_rays_replay(gpu_ctx, kind):
+    """ReinforceSparseVertices' sphere rays (free_graph_builder.cpp:434-475) bit-exact."""
+    from acceleratedvolrenderer_amd import graph
+    from oracle import binding
+    scene, ctx = gpu_ctx
+    md = graph.MediumData(scene)
+    rng = np.random.default_rng(5)
+    pts = (md.pmin - 0.02 + rng.random((40, 3), dtype=np.float32) * (md.pmax - md.pmin + 0.04)).astype(np.float32)
+    ids = rng.permutation(200)[:40].astype(np.int32)
+    s = _sampling(kind)
+    o, d, t, valid = ctx.graph_reinforce_rays(s.struct(), ids, pts, 0.03, 7, 2)
+    ro, rd, rt, rv = binding.OracleRun(scene, libm="canonical").graph_reinforce_rays(
+        ids, pts, 0.03, 7, 2, s.resolution[0], sampler=_oracle_sampler(s))
+    assert np.array_equal(valid, rv) and valid.mean() > 0.5
+    for a, b in ((o, ro), (d, rd), (t, rt)):
+        assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
+@pytest.mark.gpu
+def test_graph_build_with_reinforcement_end_to_end(gpu_ctx):
+    """BuildGraph with edge and neighbour reinforcement active on the GPU against the oracle
+    restatement of the same loop (oracle/graph_builder.reinforce): identical vertices,
+    samples and edges."""
+    from oracle import binding
+    from oracle.graph_builder import OracleGraph, reinforce
+    scene, ctx = gpu_ctx
+    b = _builder(scene, ctx, 0, steps=5, iters=3, max_depth=6)
+    ecfg = {"active": True, "unsatisfiedAllowedRatio": 0.3, "reinforcementRays": 4, "edgesForNotSparse": 3}
+    ncfg = {"active": True, "unsatisfiedAllowedRatio": 0.3, "reinforcementRays": 3, "neighboursForNotSparse": 3,
+            "neighbourRangeModifier": 2.0}
+    b.config.edge_reinforcement, b.config.neighbour_reinforcement = ecfg, ncfg
+    g = b.build_graph()
+    run = binding.OracleRun(scene, libm="canonical")
+    o, d, t, idx = b.start_rays()
+    c = b.config
+    smp = _oracle_sampler(b.sampling)
+    pts, counts = run.graph_walks(o, d, t, idx, c.iterations_per_step, 0, b.sampling.resolution[0], c.max_depth,
+                                  sampler=smp)
+    og = OracleGraph(b.radius)
+    og.add_walks(pts, counts, c.max_depth)
+    n_before = len(og.xyz)
+    cycles = reinforce(og, run, smp, b.radius, c.max_depth, ecfg, ncfg)
+    print(f"reinforcement: {cycles} cycles, vertices {n_before} -> {len(og.xyz)}")
+    assert cycles == b.reinforce_cycles >= 1
+    assert np.array_equal(g.points, np.array(og.xyz, np.float32))
+    assert g.samples.tolist() == og.samples
+    assert list(zip(g.edge_from.tolist(), g.edge_to.tolist(), g.edge_samples.tolist())) == [
+        (a, b_, s) for (a, b_), s in og.edges.items()]
