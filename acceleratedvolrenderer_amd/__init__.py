@@ -7,7 +7,7 @@ queues with wave64 ballot compaction, RGBFilm accumulation — behind the C-ABI 
 include/avr.h. See DESIGN.md.
 """
 from . import spectra, transform
-from .scene import (GridMedium, DistantLight, UniformInfiniteLight, ImageInfiniteLight, OrthographicCamera, PerspectiveCamera, RGBFilm, SpectralFilm, spectral_image,
+from .scene import (GridMedium, DistantLight, UniformInfiniteLight, ImageInfiniteLight, OrthographicCamera, PerspectiveCamera, RGBFilm, SpectralFilm, spectral_image, GBufferFilm, gbuffer_image,
                     Scene, film_rgb, HomogeneousMedium, CloudMedium, NanoVDBMedium, RGBGridMedium, BoxFilter, GaussianFilter,
                     IndependentSampler, ZSobolSampler)
 from .vdb import NanoVDBGrid
@@ -19,4 +19,4 @@ from . import scenes
 __all__ = ["spectra", "transform", "GridMedium", "DistantLight", "UniformInfiniteLight", "OrthographicCamera",
            "PerspectiveCamera", "RGBFilm", "Scene", "film_rgb", "VolPathIntegrator", "shard_samples",
            "INTEGRATOR_NAMES", "capi", "scenes", "HomogeneousMedium", "CloudMedium", "NanoVDBMedium", "NanoVDBGrid", "RGBGridMedium", "RGBToSpectrumTable",
-           "SpectralFilm", "spectral_image", "ImageInfiniteLight", "BoxFilter", "GaussianFilter", "IndependentSampler", "ZSobolSampler"]
+           "SpectralFilm", "spectral_image", "GBufferFilm", "gbuffer_image", "ImageInfiniteLight", "BoxFilter", "GaussianFilter", "IndependentSampler", "ZSobolSampler"]

@@ -18,7 +18,7 @@ import numpy as np
 
 from . import capi, imageio
 from .imgtool import channel_average
-from .scene import film_rgb
+from .scene import film_rgb, GBufferFilm, gbuffer_image
 
 INTEGRATOR_NAMES = ("volpath", "volpathcustom", "volpath_mi355x")
 
@@ -144,6 +144,16 @@ class VolPathIntegrator:
             imageio.write_exr(path, img, channels=f.channel_names(), half=fp16,
                               samples_per_pixel=spp if spp is not None else self.spp, render_time_seconds=render_time,
                               mse=mse, strings={"spectralLayoutVersion": "1.0", "emissiveUnits": "W.m^-2.sr^-1"})
+            return img
+        if isinstance(f, GBufferFilm):
+            if rgb_sum is None:
+                rgb_sum, w_sum = self.film_sums()
+            img = gbuffer_image(f, rgb_sum, w_sum, fp16)
+            if fp16:
+                img = img.astype(np.float16).astype(np.float32)
+            imageio.write_exr(path, img, channels=f.channel_names(), half=fp16,
+                              samples_per_pixel=spp if spp is not None else self.spp, render_time_seconds=render_time,
+                              mse=mse)
             return img
         img = self.get_image(rgb_sum, w_sum, fp16)
         if str(path).lower().endswith(".pfm"):

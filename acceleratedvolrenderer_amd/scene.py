@@ -478,6 +478,32 @@ class SpectralFilm(RGBFilm):
         return ["R", "G", "B"] + ["S0." + ("%.3fnm" % float(l)).replace(".", ",") for l in self.bucket_centers()]
 
 
+class GBufferFilm(RGBFilm):
+    """GBufferFilm (film.h:319-400, film.cpp:588-800). Its geometric channels (albedo, P,
+    dzdx/dzdy, N, Ns, uv) and the RGB variance estimators are fed only by a VisibleSurface,
+    which VolPathIntegrator::Li sets at the first intersection whose material has a BSDF
+    (cpu/integrators.cpp:1124-1151); the medium boundaries this path renders are interface
+    shapes (no BSDF), so those channels stay at their zero initial values and the radiance
+    part is RGBFilm's (same AddSample sums: the device film is shared)."""
+    CHANNELS = ["R", "G", "B", "Albedo.R", "Albedo.G", "Albedo.B", "P.X", "P.Y", "P.Z", "dzdx", "dzdy", "N.X",
+                "N.Y", "N.Z", "Ns.X", "Ns.Y", "Ns.Z", "u", "v", "Variance.R", "Variance.G", "Variance.B",
+                "RelativeVariance.R", "RelativeVariance.G", "RelativeVariance.B"]
+
+    def channel_names(self):
+        return list(self.CHANNELS)
+
+
+def gbuffer_image(film, rgb_sum, w_sum, fp16=True):
+    """GBufferFilm::GetImage (film.cpp:688-800), no splats and no visible surfaces:
+    (H, W, 25) float32 in GBufferFilm.CHANNELS order."""
+    rgb = film_rgb(film, rgb_sum, w_sum)
+    if fp16:
+        rgb = np.minimum(rgb, np.float32(65504))
+    out = np.zeros((film.height, film.width, len(GBufferFilm.CHANNELS)), np.float32)
+    out[:, :, :3] = rgb
+    return out
+
+
 def spectral_image(film, rgb_sum, w_sum, bucket_sums, weight_sums, fp16=True):
     """SpectralFilm::GetImage (film.cpp:961-1028), no splats: (H, W, 3 + nbuckets) float32."""
     rgb = film_rgb(film, rgb_sum, w_sum)
