@@ -1169,8 +1169,12 @@ struct SecProf {
 // majorant (1 MiB) does not fit LDS and is read through L2 (per-XCD 4 MiB); the density
 // fetch is NanoVDB's index-space trilinear sampler (avr_vdb.h) and emission comes from the
 // temperature grid. GridMedium (!kVdb) keeps its 16^3 majorant in LDS.
-template <bool kEmissive, bool kGray, bool kZSobol, bool kVdb>
+// RGBGridMedium (kMed 4, media.h:355-427): per-voxel RGB spectra (never gray), 16^3 majorant
+// in LDS, sigma and Le from GridMedium-style trilinear sigmoid lookups (sample_point).
+template <bool kEmissive, bool kGray, bool kZSobol, int kMed>
 __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_WAVES_SPEC) k_paths(Params P) {
+    constexpr bool kVdb = kMed == 3, kRgb = kMed == 4;
+    static_assert(!(kRgb && kGray), "RGB grids carry per-voxel spectra");
     using S = typename std::conditional<kGray, float, Spec>::type;
     // LDS: majorant grid (16 KiB at pbrt's 16^3) + the 471-entry spectral tables the path
     // samples at path start, NEE and escape (sigma_a, sigma_s, up to 4 light spectra).
@@ -1415,7 +1419,7 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
                         const LambdaIdx li = lambda_index(lam);
                         sig_a = sfrom<S>(sample_table(tab_sa, li));
                         sig_s = sfrom<S>(sample_table(tab_ss, li));
-                        if (kEmissive && !kVdb) Le_l = sample_table(m.Le, li);
+                        if (kEmissive && kMed == 0) Le_l = sample_table(m.Le, li);
                     }
                     // first medium segment: RNG from two sampler dims, u from a third (984-989)
                     const float h0 = smp.get1d(P);
@@ -1542,14 +1546,26 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
             // GridMedium::SamplePoint (media.h:287-319) / NanoVDBMedium::SamplePoint (624-637);
             // k_paths runs these two (the host sends the other media to the wavefront kernels)
             V3 pm = xf_point_pair(m.medium_from_render, pc);
-            float dens;
-            if constexpr (kVdb) {
-                dens = vdb::sample_world(m.vdb, pm.x, pm.y, pm.z);
+            S ms_a, ms_s;
+            Spec rgbLe{};
+            if constexpr (kRgb) {
+                // RGBGridMedium::SamplePoint (media.h:377-403), as the wavefront kernels do it
+                const MediumSample rs = sample_point(m, pc, Spec::c(1.f), Spec::c(0.f), Spec::c(0.f), lam, kEmissive);
+                ms_a = sfrom<S>(rs.sigma_a);
+                ms_s = sfrom<S>(rs.sigma_s);
+                rgbLe = rs.Le;
             } else {
-                pm = m.unit_box ? V3{pm.x - m.bmin[0], pm.y - m.bmin[1], pm.z - m.bmin[2]} : box_offset(m.bmin, m.bmax, pm);
-                dens = m.fat ? fat_lookup(m.fat, m.density, m.nx, m.ny, m.nz, pm) : grid_lookup(m.density, m.nx, m.ny, m.nz, pm);
+                float dens;
+                if constexpr (kVdb) {
+                    dens = vdb::sample_world(m.vdb, pm.x, pm.y, pm.z);
+                } else {
+                    pm = m.unit_box ? V3{pm.x - m.bmin[0], pm.y - m.bmin[1], pm.z - m.bmin[2]} : box_offset(m.bmin, m.bmax, pm);
+                    dens = m.fat ? fat_lookup(m.fat, m.density, m.nx, m.ny, m.nz, pm)
+                                 : grid_lookup(m.density, m.nx, m.ny, m.nz, pm);
+                }
+                ms_a = sig_a * dens;
+                ms_s = sig_s * dens;
             }
-            const S ms_a = sig_a * dens, ms_s = sig_s * dens;
             bool stop = false;
             if (mode == M_MEDIUM) {
                 ++nLookup;
@@ -1559,7 +1575,7 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
                     ev = EV_END;
                 } else {
                     if (kEmissive && depth < P.max_depth) {
-                        const Spec Le = kVdb ? vdb_emission(m, pm, lam) : grid_emission(m, pm, lam, Le_l);
+                        const Spec Le = kRgb ? rgbLe : (kVdb ? vdb_emission(m, pm, lam) : grid_emission(m, pm, lam, Le_l));
                         if (Le.nonzero()) {
                             float pdf = sv0(sigma_maj) * sv0(T_maj);
                             S betap = beta * T_maj / pdf;
