@@ -77,8 +77,8 @@ struct avr_context {
     int kernel_mode = 0;      // 0: persistent k_paths (default), 1: wavefront k_medium/k_shadow
     bool last_persistent = false;   // which organisation the last avr_render ran
     int *d_heads = nullptr;   // 8 per-XCD work counters of k_paths
-    int paths_grid[24] = {};  // k_paths<emissive, gray, zsobol, medium> at 8*(0 grid, 1 vdb, 2 rgb) + 4*zsobol + 2*emissive + gray
-    void (*kpaths[24])(avr::Params) = {};
+    int paths_grid[48] = {};  // k_paths<emissive, gray, zsobol, medium, image> at 24*image + 8*(0 grid, 1 vdb, 2 rgb) + 4*zsobol + 2*emissive + gray
+    void (*kpaths[48])(avr::Params) = {};
     // pixel sampler (avr_set_sampler) and filter (avr_set_filter)
     int sampler_kind = 0;     // 0 IndependentSampler, 1 ZSobolSampler
     int sampler_spp = 16;     // samplesPerPixel of the sampler (ZSobol's Morton layout)
@@ -413,21 +413,18 @@ int avr_context_create(int device, long long max_paths, avr_context **out) {
             delete c;
             return fail(AVR_ERR_HIP, "device query failed");
         }
-        // RGB grids (never gray): slots 16 + 4*zsobol + 2*emissive hold the 4-wavelength kernel
-        void (*kerns[24])(avr::Params) = {
-            avr::k_paths<false, false, false, 0>, avr::k_paths<false, true, false, 0>,
-            avr::k_paths<true, false, false, 0>,  avr::k_paths<true, true, false, 0>,
-            avr::k_paths<false, false, true, 0>,  avr::k_paths<false, true, true, 0>,
-            avr::k_paths<true, false, true, 0>,   avr::k_paths<true, true, true, 0>,
-            avr::k_paths<false, false, false, 3>, avr::k_paths<false, true, false, 3>,
-            avr::k_paths<true, false, false, 3>,  avr::k_paths<true, true, false, 3>,
-            avr::k_paths<false, false, true, 3>,  avr::k_paths<false, true, true, 3>,
-            avr::k_paths<true, false, true, 3>,   avr::k_paths<true, true, true, 3>,
-            avr::k_paths<false, false, false, 4>, avr::k_paths<false, false, false, 4>,
-            avr::k_paths<true, false, false, 4>,  avr::k_paths<true, false, false, 4>,
-            avr::k_paths<false, false, true, 4>,  avr::k_paths<false, false, true, 4>,
-            avr::k_paths<true, false, true, 4>,   avr::k_paths<true, false, true, 4>};
-        for (int k = 0; k < 24; ++k) {
+        // slot 24*image + 8*medium(0 grid, 1 vdb, 2 rgb) + 4*zsobol + 2*emissive + gray; RGB grids
+        // are never gray (their gray slots hold the 4-wavelength kernel)
+#define AVR_KP(em, gr, zs, med, im) avr::k_paths<em, (med == 4 ? false : gr), zs, med, im>
+#define AVR_KP8(med, im)                                                                                   \
+    AVR_KP(false, false, false, med, im), AVR_KP(false, true, false, med, im), AVR_KP(true, false, false, med, im), \
+        AVR_KP(true, true, false, med, im), AVR_KP(false, false, true, med, im), AVR_KP(false, true, true, med, im), \
+        AVR_KP(true, false, true, med, im), AVR_KP(true, true, true, med, im)
+        void (*kerns[48])(avr::Params) = {AVR_KP8(0, false), AVR_KP8(3, false), AVR_KP8(4, false),
+                                          AVR_KP8(0, true),  AVR_KP8(3, true),  AVR_KP8(4, true)};
+#undef AVR_KP8
+#undef AVR_KP
+        for (int k = 0; k < 48; ++k) {
             int blocksPerCU = 0;
             if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocksPerCU, kerns[k], 256, 0) != hipSuccess) {
                 delete c;
@@ -1028,10 +1025,10 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
         const long long n0 = P * S;
         // k_paths runs GridMedium and RGBGridMedium (majorant in LDS: at most 4096 cells =
         // pbrt's 16^3; larger grids take the wavefront kernels) and NanoVDBMedium (64^3
-        // majorant through L2); homogeneous and cloud media and image infinite lights
-        // (non-delta, MIS-weighted) run wavefront
+        // majorant through L2), with every light type; homogeneous and cloud media run
+        // wavefront
         const int mcells = c->med.mres[0] * c->med.mres[1] * c->med.mres[2];
-        const bool persistent = c->kernel_mode == 0 && c->n_image_lights == 0 &&
+        const bool persistent = c->kernel_mode == 0 &&
                                 (((c->med.type == 0 || c->med.type == 4) && mcells <= 4096) || c->med.type == 3) &&
                                 c->med.mres[0] <= 255 && c->med.mres[1] <= 255 && c->med.mres[2] <= 255;
         c->last_persistent = persistent;
@@ -1053,8 +1050,8 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
             HIP_TRY(hipMemsetAsync(c->d_heads, 0, 8 * sizeof(int), c->stream));
             EV_MARK(e0);
             // gray medium: sigma_a and sigma_s tables constant over all 471 wavelengths
-            const int kv = 8 * (c->med.type == 3 ? 1 : (c->med.type == 4 ? 2 : 0)) + 4 * c->sampler_kind +
-                           2 * (c->med.emissive ? 1 : 0) + (c->gray && c->med.type != 4 ? 1 : 0);
+            const int kv = 24 * (c->n_image_lights > 0 ? 1 : 0) + 8 * (c->med.type == 3 ? 1 : (c->med.type == 4 ? 2 : 0)) +
+                           4 * c->sampler_kind + 2 * (c->med.emissive ? 1 : 0) + (c->gray && c->med.type != 4 ? 1 : 0);
             hipLaunchKernelGGL(c->kpaths[kv], dim3(c->paths_grid[kv]), dim3(256), 0, c->stream, p);
             HIP_TRY(hipGetLastError());
             EV_MARK(e1);

@@ -1171,7 +1171,9 @@ struct SecProf {
 // temperature grid. GridMedium (!kVdb) keeps its 16^3 majorant in LDS.
 // RGBGridMedium (kMed 4, media.h:355-427): per-voxel RGB spectra (never gray), 16^3 majorant
 // in LDS, sigma and Le from GridMedium-style trilinear sigmoid lookups (sample_point).
-template <bool kEmissive, bool kGray, bool kZSobol, int kMed>
+// kImage: the scene holds an ImageInfiniteLight (non-delta NEE with MIS, MIS-weighted
+// escapes); a separate instantiation so the other kernels keep their register budget.
+template <bool kEmissive, bool kGray, bool kZSobol, int kMed, bool kImage>
 __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_WAVES_SPEC) k_paths(Params P) {
     constexpr bool kVdb = kMed == 3, kRgb = kMed == 4;
     static_assert(!(kRgb && kGray), "RGB grids carry per-voxel spectra");
@@ -1180,6 +1182,9 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
     // samples at path start, NEE and escape (sigma_a, sigma_s, up to 4 light spectra).
     __shared__ float s_maj[kVdb ? 1 : 4096];
     __shared__ float s_tab[(2 + 4) * kNTable];
+    // ImageInfiniteLight shadow rays (non-delta NEE): the sampled (u, v), p_l and the phase
+    // value per lane, parked here while the lane traces its shadow ray (off the VGPR budget)
+    __shared__ float4 s_img[kImage ? 256 : 1];
     // the host routes GridMedium majorant grids of more than 4096 cells to the wavefront kernels
     if constexpr (!kVdb) stage_majorant(P.med, s_maj);
     const float *__restrict__ majp = kVdb ? P.med.majorant : s_maj;
@@ -1187,7 +1192,8 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
     for (int i = threadIdx.x; i < kNTable; i += blockDim.x) {
         s_tab[i] = P.med.sigma_a[i];
         s_tab[kNTable + i] = P.med.sigma_s[i];
-        for (int k = 0; k < nlds; ++k) s_tab[(2 + k) * kNTable + i] = P.lights.list[k].L[i];
+        for (int k = 0; k < nlds; ++k)
+            if (P.lights.list[k].type != 2) s_tab[(2 + k) * kNTable + i] = P.lights.list[k].L[i];
     }
     __syncthreads();
     const float *tab_sa = s_tab, *tab_ss = s_tab + kNTable;
@@ -1254,7 +1260,34 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
                         int idx = (int)(ul / pInf * nl);
                         idx = idx < nl - 1 ? idx : nl - 1;
                         const DevLight &lt = P.lights.list[idx];
-                        if (lt.type == 0) {
+                        if (kImage && lt.type == 2) {
+                            // ImageInfiniteLight::SampleLi with the compensated distribution
+                            // (lights.h:588-613), shadow ray to 2 x sceneRadius (integrators.cpp:1311-1338)
+                            float su, sv, lsPdf;
+                            env::distrib_sample(lt.dist, uL0, uL1, &su, &sv, &lsPdf);
+                            if (lsPdf != 0) {
+                                V3 wl;
+                                env::square_to_sphere(su, sv, &wl.x, &wl.y, &wl.z);
+                                const V3 wi = xf_vec3(lt.rfl, wl);
+                                lsPdf = lsPdf / (4 * kPi);
+                                const Spec Ls = image_le(lt, su, sv, lam);
+                                const float fval = hg_eval(dot(wo, wi), m.g);
+                                if (Ls.nonzero() && fval != 0) {
+                                    const V3 pOut = po + wi * (2 * P.lights.scene_radius);
+                                    const V3 d = pOut - po;
+                                    light = idx;
+                                    T_ray = sr_l = sr_u = sconst<S>(1.f);
+                                    s_img[threadIdx.x] = make_float4(su, sv, (pInf / nl) * lsPdf, fval);
+                                    seqA = hash_3u32(f2u(po.x), f2u(po.y), f2u(po.z));
+                                    seqB = hash_3u32(f2u(d.x), f2u(d.y), f2u(d.z));
+                                    sd = d;
+                                    segPending = true;
+                                    mode = M_SHADOW;
+                                    ev = EV_NONE;
+                                    ++nShadow;
+                                }
+                            }
+                        } else if (lt.type == 0) {
                             const V3 wi = {lt.w[0], lt.w[1], lt.w[2]};
                             const Spec Ls = sample_table(light_table(idx), lambda_index(lam)) * lt.scale;
                             if (Ls.nonzero() && hg_eval(dot(wo, wi), m.g) != 0) {
@@ -1286,13 +1319,23 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
                 Spec contrib = Spec::c(0.f);
                 if (snz(T_ray)) {
                     const DevLight &lt = P.lights.list[light];
-                    const V3 wi = {lt.w[0], lt.w[1], lt.w[2]};
-                    const float pInf = float(P.lights.n) / float(P.lights.n + 0);
-                    const float p_l = pInf / P.lights.n * 1.f;
-                    const S f_hat = sconst<S>(hg_eval(dot(-pd, wi), m.g));
-                    const Spec Ls = sample_table(light_table(light), lambda_index(lam)) * lt.scale;
-                    sr_l = sr_l * (r_u * p_l);
-                    contrib = smul(Ls, beta * f_hat * T_ray) / savg(sr_l);
+                    if (kImage && lt.type == 2) {
+                        // non-delta light: r_l *= r_p * p_l, r_u *= r_p * scatterPDF (1391-1398)
+                        const float4 im = s_img[threadIdx.x];
+                        const S f_hat = sconst<S>(im.w);
+                        const Spec Ls = image_le(lt, im.x, im.y, lam);
+                        sr_l = sr_l * (r_u * im.z);
+                        sr_u = sr_u * (r_u * im.w);
+                        contrib = smul(Ls, beta * f_hat * T_ray) / savg(sr_l + sr_u);
+                    } else {
+                        const V3 wi = {lt.w[0], lt.w[1], lt.w[2]};
+                        const float pInf = float(P.lights.n) / float(P.lights.n + 0);
+                        const float p_l = pInf / P.lights.n * 1.f;
+                        const S f_hat = sconst<S>(hg_eval(dot(-pd, wi), m.g));
+                        const Spec Ls = sample_table(light_table(light), lambda_index(lam)) * lt.scale;
+                        sr_l = sr_l * (r_u * p_l);
+                        contrib = smul(Ls, beta * f_hat * T_ray) / savg(sr_l);
+                    }
                 }
                 L = L + contrib;
                 ev = EV_PHASE;
@@ -1331,12 +1374,21 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
                 r_l = r_l * (T_maj / sv0(T_maj));
                 for (int k = 0; k < P.lights.n; ++k) {
                     const DevLight &lt = P.lights.list[k];
-                    if (lt.type != 1) continue;
-                    const Spec Le = sample_table(light_table(k), lambda_index(lam)) * lt.scale;
+                    if (lt.type == 0 || (!kImage && lt.type == 2)) continue;
+                    Spec Le;
+                    float pdfLi = 0.f;
+                    if (kImage && lt.type == 2) {
+                        float eu = 0, evv = 0;
+                        Le = image_le_dir(lt, pd, lam, &eu, &evv);
+                        if (Le.nonzero() && depth != 0) pdfLi = image_pdf_li(lt, pd);
+                    } else {
+                        Le = sample_table(light_table(k), lambda_index(lam)) * lt.scale;
+                    }
                     if (!Le.nonzero()) continue;
                     if (depth == 0) L = L + smul(Le, beta) / savg(r_u);
                     else {
-                        r_l = r_l * ((1.f / (P.lights.n + 0)) * 0.f);
+                        // lightSampler.PMF * PDF_Li(prevIntrContext, ray.d, true): 0 for the uniform light
+                        r_l = r_l * ((1.f / (P.lights.n + 0)) * pdfLi);
                         L = L + smul(Le, beta) / savg(r_u + r_l);
                     }
                 }

@@ -612,7 +612,9 @@ def test_zsobol_pixel_table_identical(kernel):
 
 
 @pytest.mark.parametrize("with_distant", [False, True])
-def test_image_infinite_light_replay(with_distant):
+@pytest.mark.parametrize("kernel", ["persistent", "wavefront"])
+@pytest.mark.parametrize("variant", ["chromatic", "scatter"])
+def test_image_infinite_light_replay(with_distant, variant, kernel):
     """ImageInfiniteLight (lights.h:552-640): compensated-distribution NEE with MIS
     (integrators.cpp:1282-1399) and MIS-weighted escapes (1090-1107) through a rotated
     equal-area map with a bright spot; with a distant light too, the escape loop's r_l
@@ -636,18 +638,20 @@ def test_image_infinite_light_replay(with_distant):
     rot[:3, :3] = [[c, 0, s], [0, 1, 0], [-s, 0, c]]
     light = ImageInfiniteLight(image=img, rgb_table=table, world_from_light=rot, scale=2.0)
     W, H, spp = 24, 20, 8
-    base = scenes.s_uniform(n=6, width=W, height=H, variant="chromatic")
+    base = scenes.s_uniform(n=6, width=W, height=H, variant=variant,
+                            density=(0.2 + np.random.default_rng(2).random((6, 6, 6), dtype=np.float32)))
     lights = ([DistantLight(from_=(1, 1, -1), to=(0, 0, 0), scale=1.5)] if with_distant else []) + [light]
     scene = Scene(base.camera, base.film, base.medium, lights)
-    integ = _integrator(scene, maxdepth=6, spp=spp)
+    integ = _integrator(scene, maxdepth=6, spp=spp, kernel=kernel)
     rgb, w = integ.render()
+    assert (integ.stats()["loop_iterations"] > 0) == (kernel == "persistent")
     canon = binding.OracleRun(scene, max_depth=6, seed=0, libm="canonical")
     frac, _ = _compare_samples(integ, canon, 0, spp)
     ref = binding.OracleRun(scene, max_depth=6, seed=0)
     rgb_o, w_o = ref.render(0, spp, nthreads=8)
     err = _rel_rms(integ.image(rgb, w), integ.image(rgb_o, w_o))
     noise = _oracle_noise(scene, 6, spp, integ, rgb_o, w_o)
-    print(f"image light (distant={with_distant}): bit-exact {frac:.5f}, film rel RMS {err:.3e} (noise {noise:.3e})")
+    print(f"image light ({variant}/{kernel}, distant={with_distant}): bit-exact {frac:.5f}, film rel RMS {err:.3e} (noise {noise:.3e})")
     assert frac >= 0.999
     assert err <= 0.5 * noise
     integ.close()

@@ -1,7 +1,9 @@
-"""Persistent vs wavefront throughput on a non-GridMedium input (GPU): an RGBGridMedium of
-random sigmoid coefficients (n^3) under the S-cloud camera and lights, zsobol + gaussian.
+"""Persistent vs wavefront throughput on inputs beyond the default bench (GPU): an
+RGBGridMedium of random sigmoid coefficients (n^3), or the S-cloud grid (n^3, CloudMedium
+density) lit by an ImageInfiniteLight sky plus the distant sun; S-cloud camera, zsobol +
+gaussian.
 
-usage: python tools/medium_bench.py [--n 128] [--steps 4] [--kernel persistent|wavefront]
+usage: python tools/medium_bench.py [--scene rgb|image] [--n 128] [--steps 4] [--kernel persistent|wavefront]
 """
 import argparse
 import json
@@ -21,8 +23,9 @@ def main():
     p.add_argument("--steps", type=int, default=4)
     p.add_argument("--kernel", default="persistent")
     p.add_argument("--emissive", action="store_true")
+    p.add_argument("--scene", default="rgb", choices=["rgb", "image"])
     a = p.parse_args()
-    import torch  # noqa: F401
+    import torch
     from acceleratedvolrenderer_amd import VolPathIntegrator, scenes, RGBGridMedium
     from acceleratedvolrenderer_amd.scene import Scene
     rng = np.random.default_rng(0)
@@ -36,11 +39,27 @@ def main():
         c[..., 3] = rng.uniform(0.0, hi, shape)
         return c
     base = scenes.s_cloud(np.zeros((1, 1, 1), np.float32), sampler="zsobol", spp=256, filter="gaussian")
-    kw = dict(sigma_a_coeffs=coeffs(0.3), sigma_s_coeffs=coeffs(4.0), g=0.877)
-    if a.emissive:
-        kw.update(Le_coeffs=coeffs(1.0), Lescale=0.5)
-    med = RGBGridMedium(**kw)
-    scene = Scene(base.camera, base.film, med, base.lights, sampler=base.sampler)
+    if a.scene == "image":
+        from acceleratedvolrenderer_amd import ImageInfiniteLight, RGBToSpectrumTable, capi
+        density = torch.empty((a.n, a.n, a.n), dtype=torch.float32, device="cuda:0")
+        gen = capi.Context(0)
+        gen.generate_cloud(density.data_ptr(), a.n, 0, a.n ** 3)
+        gen.sync()
+        gen.close()
+        table = RGBToSpectrumTable.load(os.path.join(ROOT, "oracle", "_ref", "srgb_table.npz"))
+        res = 256
+        y, x = np.mgrid[0:res, 0:res] / res
+        sky = np.stack([0.35 + 0.2 * y, 0.5 + 0.2 * y, 0.9 - 0.1 * x], 2).astype(np.float32)
+        sky[40:48, 180:188] = [40, 36, 30]
+        cloud = scenes.s_cloud(density, sampler="zsobol", spp=256, filter="gaussian")
+        lights = [cloud.lights[0], ImageInfiniteLight(image=sky, rgb_table=table, scale=0.3)]
+        scene = Scene(cloud.camera, cloud.film, cloud.medium, lights, sampler=cloud.sampler)
+    else:
+        kw = dict(sigma_a_coeffs=coeffs(0.3), sigma_s_coeffs=coeffs(4.0), g=0.877)
+        if a.emissive:
+            kw.update(Le_coeffs=coeffs(1.0), Lescale=0.5)
+        med = RGBGridMedium(**kw)
+        scene = Scene(base.camera, base.film, med, base.lights, sampler=base.sampler)
     integ = VolPathIntegrator(scene, maxdepth=scenes.CLOUD_MAXDEPTH, spp=16, device=0, kernel=a.kernel)
     integ.ctx.render(0, 16, 0, scenes.CLOUD_MAXDEPTH)
     integ.ctx.sync()
@@ -49,7 +68,8 @@ def main():
         integ.ctx.render(16 * k, 16 * (k + 1), 0, scenes.CLOUD_MAXDEPTH)
     integ.ctx.sync()
     dt = time.perf_counter() - t0
-    print(json.dumps({"medium": f"RGBGridMedium {a.n}^3", "kernel": a.kernel, "emissive": a.emissive,
+    name = f"S-cloud-{a.n} grid + ImageInfiniteLight" if a.scene == "image" else f"RGBGridMedium {a.n}^3"
+    print(json.dumps({"scene": name, "kernel": a.kernel, "emissive": a.emissive,
                       "Msamples_per_s": round(1280 * 720 * 16 * a.steps / dt / 1e6, 2)}))
     integ.close()
 
