@@ -77,8 +77,8 @@ struct avr_context {
     int kernel_mode = 0;      // 0: persistent k_paths (default), 1: wavefront k_medium/k_shadow
     bool last_persistent = false;   // which organisation the last avr_render ran
     int *d_heads = nullptr;   // 8 per-XCD work counters of k_paths
-    int paths_grid[48] = {};  // k_paths<emissive, gray, zsobol, medium, image> at 24*image + 8*(0 grid, 1 vdb, 2 rgb) + 4*zsobol + 2*emissive + gray
-    void (*kpaths[48])(avr::Params) = {};
+    int paths_grid[64] = {};  // k_paths<emissive, gray, zsobol, medium, image> at 32*image + 8*(0 grid, 1 vdb, 2 rgb, 3 homogeneous/cloud) + 4*zsobol + 2*emissive + gray
+    void (*kpaths[64])(avr::Params) = {};
     // pixel sampler (avr_set_sampler) and filter (avr_set_filter)
     int sampler_kind = 0;     // 0 IndependentSampler, 1 ZSobolSampler
     int sampler_spp = 16;     // samplesPerPixel of the sampler (ZSobol's Morton layout)
@@ -413,18 +413,18 @@ int avr_context_create(int device, long long max_paths, avr_context **out) {
             delete c;
             return fail(AVR_ERR_HIP, "device query failed");
         }
-        // slot 24*image + 8*medium(0 grid, 1 vdb, 2 rgb) + 4*zsobol + 2*emissive + gray; RGB grids
+        // slot 32*image + 8*medium(0 grid, 1 vdb, 2 rgb, 3 homogeneous/cloud) + 4*zsobol + 2*emissive + gray; RGB grids
         // are never gray (their gray slots hold the 4-wavelength kernel)
 #define AVR_KP(em, gr, zs, med, im) avr::k_paths<em, (med == 4 ? false : gr), zs, med, im>
 #define AVR_KP8(med, im)                                                                                   \
     AVR_KP(false, false, false, med, im), AVR_KP(false, true, false, med, im), AVR_KP(true, false, false, med, im), \
         AVR_KP(true, true, false, med, im), AVR_KP(false, false, true, med, im), AVR_KP(false, true, true, med, im), \
         AVR_KP(true, false, true, med, im), AVR_KP(true, true, true, med, im)
-        void (*kerns[48])(avr::Params) = {AVR_KP8(0, false), AVR_KP8(3, false), AVR_KP8(4, false),
-                                          AVR_KP8(0, true),  AVR_KP8(3, true),  AVR_KP8(4, true)};
+        void (*kerns[64])(avr::Params) = {AVR_KP8(0, false), AVR_KP8(3, false), AVR_KP8(4, false), AVR_KP8(1, false),
+                                          AVR_KP8(0, true),  AVR_KP8(3, true),  AVR_KP8(4, true),  AVR_KP8(1, true)};
 #undef AVR_KP8
 #undef AVR_KP
-        for (int k = 0; k < 48; ++k) {
+        for (int k = 0; k < 64; ++k) {
             int blocksPerCU = 0;
             if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocksPerCU, kerns[k], 256, 0) != hipSuccess) {
                 delete c;
@@ -1023,13 +1023,13 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
         p.sample_base = (int)base;
         p.stats = c->d_stats;
         const long long n0 = P * S;
-        // k_paths runs GridMedium and RGBGridMedium (majorant in LDS: at most 4096 cells =
-        // pbrt's 16^3; larger grids take the wavefront kernels) and NanoVDBMedium (64^3
-        // majorant through L2), with every light type; homogeneous and cloud media run
-        // wavefront
+        // k_paths runs every medium type with every light type: GridMedium, RGBGridMedium and
+        // the single-segment Homogeneous/CloudMedium keep the majorant in LDS (at most 4096
+        // cells = pbrt's 16^3; larger grids take the wavefront kernels), NanoVDBMedium reads
+        // its 64^3 majorant through L2
         const int mcells = c->med.mres[0] * c->med.mres[1] * c->med.mres[2];
         const bool persistent = c->kernel_mode == 0 &&
-                                (((c->med.type == 0 || c->med.type == 4) && mcells <= 4096) || c->med.type == 3) &&
+                                (((c->med.type != 3) && mcells <= 4096) || c->med.type == 3) &&
                                 c->med.mres[0] <= 255 && c->med.mres[1] <= 255 && c->med.mres[2] <= 255;
         c->last_persistent = persistent;
         if (persistent) {
@@ -1050,8 +1050,9 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
             HIP_TRY(hipMemsetAsync(c->d_heads, 0, 8 * sizeof(int), c->stream));
             EV_MARK(e0);
             // gray medium: sigma_a and sigma_s tables constant over all 471 wavelengths
-            const int kv = 24 * (c->n_image_lights > 0 ? 1 : 0) + 8 * (c->med.type == 3 ? 1 : (c->med.type == 4 ? 2 : 0)) +
-                           4 * c->sampler_kind + 2 * (c->med.emissive ? 1 : 0) + (c->gray && c->med.type != 4 ? 1 : 0);
+            const int mk = c->med.type == 3 ? 1 : (c->med.type == 4 ? 2 : (c->med.type == 1 || c->med.type == 2 ? 3 : 0));
+            const int kv = 32 * (c->n_image_lights > 0 ? 1 : 0) + 8 * mk + 4 * c->sampler_kind +
+                           2 * (c->med.emissive ? 1 : 0) + (c->gray && c->med.type != 4 ? 1 : 0);
             hipLaunchKernelGGL(c->kpaths[kv], dim3(c->paths_grid[kv]), dim3(256), 0, c->stream, p);
             HIP_TRY(hipGetLastError());
             EV_MARK(e1);

@@ -1126,6 +1126,8 @@ __device__ __forceinline__ Spec sexp(const Spec &x) { return fast_exp(x); }
 template <typename S> __device__ __forceinline__ S sconst(float a);
 template <> __device__ __forceinline__ float sconst<float>(float a) { return a; }
 template <> __device__ __forceinline__ Spec sconst<Spec>(float a) { return Spec::c(a); }
+__device__ __forceinline__ Spec to_spec(float x) { return Spec::c(x); }
+__device__ __forceinline__ Spec to_spec(const Spec &x) { return x; }
 template <typename S> __device__ __forceinline__ S sfrom(const Spec &x);
 template <> __device__ __forceinline__ float sfrom<float>(const Spec &x) { return x.v0; }
 template <> __device__ __forceinline__ Spec sfrom<Spec>(const Spec &x) { return x; }
@@ -1175,7 +1177,9 @@ struct SecProf {
 // escapes); a separate instantiation so the other kernels keep their register budget.
 template <bool kEmissive, bool kGray, bool kZSobol, int kMed, bool kImage>
 __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_WAVES_SPEC) k_paths(Params P) {
-    constexpr bool kVdb = kMed == 3, kRgb = kMed == 4;
+    // kMed 1: HomogeneousMedium or CloudMedium — dda_init gives their single
+    // HomogeneousMajorantIterator segment over a 1^3 majorant of 1.0; properties from sample_point
+    constexpr bool kVdb = kMed == 3, kRgb = kMed == 4, kAnalytic = kMed == 1;
     static_assert(!(kRgb && kGray), "RGB grids carry per-voxel spectra");
     using S = typename std::conditional<kGray, float, Spec>::type;
     // LDS: majorant grid (16 KiB at pbrt's 16^3) + the 471-entry spectral tables the path
@@ -1471,7 +1475,7 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
                         const LambdaIdx li = lambda_index(lam);
                         sig_a = sfrom<S>(sample_table(tab_sa, li));
                         sig_s = sfrom<S>(sample_table(tab_ss, li));
-                        if (kEmissive && kMed == 0) Le_l = sample_table(m.Le, li);
+                        if (kEmissive && (kMed == 0 || kMed == 1)) Le_l = sample_table(m.Le, li);
                     }
                     // first medium segment: RNG from two sampler dims, u from a third (984-989)
                     const float h0 = smp.get1d(P);
@@ -1606,6 +1610,12 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
                 ms_a = sfrom<S>(rs.sigma_a);
                 ms_s = sfrom<S>(rs.sigma_s);
                 rgbLe = rs.Le;
+            } else if constexpr (kAnalytic) {
+                // HomogeneousMedium / CloudMedium::SamplePoint (media.h:230-238, 478-489)
+                const MediumSample rs = sample_point(m, pc, to_spec(sig_a), to_spec(sig_s), Le_l, lam, kEmissive);
+                ms_a = sfrom<S>(rs.sigma_a);
+                ms_s = sfrom<S>(rs.sigma_s);
+                rgbLe = rs.Le;
             } else {
                 float dens;
                 if constexpr (kVdb) {
@@ -1627,7 +1637,7 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
                     ev = EV_END;
                 } else {
                     if (kEmissive && depth < P.max_depth) {
-                        const Spec Le = kRgb ? rgbLe : (kVdb ? vdb_emission(m, pm, lam) : grid_emission(m, pm, lam, Le_l));
+                        const Spec Le = (kRgb || kAnalytic) ? rgbLe : (kVdb ? vdb_emission(m, pm, lam) : grid_emission(m, pm, lam, Le_l));
                         if (Le.nonzero()) {
                             float pdf = sv0(sigma_maj) * sv0(T_maj);
                             S betap = beta * T_maj / pdf;

@@ -358,11 +358,12 @@ def test_transmittance_matches_oracle_and_beer_lambert():
     ctx.close()
 
 
+@pytest.mark.parametrize("kernel", ["persistent", "wavefront"])
 @pytest.mark.parametrize("kind", ["homogeneous", "homogeneous_emissive", "cloud"])
-def test_homogeneous_and_cloud_media_replay(kind):
+def test_homogeneous_and_cloud_media_replay(kind, kernel):
     """HomogeneousMedium (media.h:217-262) and CloudMedium (media.h:430-528): one majorant
-    segment per ray, constant or procedural density. The persistent organisation is
-    GridMedium-only, so these run the wavefront kernels (chosen by the library)."""
+    segment per ray (HomogeneousMajorantIterator), constant or procedural density, in both
+    kernel organisations."""
     from acceleratedvolrenderer_amd import scenes, HomogeneousMedium, CloudMedium
     from acceleratedvolrenderer_amd.scene import Scene
     from oracle import binding
@@ -373,15 +374,16 @@ def test_homogeneous_and_cloud_media_replay(kind):
                                                      Lescale=2.0),
            "cloud": CloudMedium(sigma_a=0.1, sigma_s=3.0, g=0.6)}[kind]
     scene = Scene(base.camera, base.film, med, base.lights)
-    integ = _integrator(scene, maxdepth=8, spp=spp)
+    integ = _integrator(scene, maxdepth=8, spp=spp, kernel=kernel)
     rgb, w = integ.render()
+    assert (integ.stats()["loop_iterations"] > 0) == (kernel == "persistent")
     canon = binding.OracleRun(scene, max_depth=8, seed=0, libm="canonical")
     frac, _ = _compare_samples(integ, canon, 0, spp)
     ref = binding.OracleRun(scene, max_depth=8, seed=0)
     rgb_o, w_o = ref.render(0, spp, nthreads=8)
     err = _rel_rms(integ.image(rgb, w), integ.image(rgb_o, w_o))
     noise = _oracle_noise(scene, 8, spp, integ, rgb_o, w_o)
-    print(f"{kind}: bit-exact samples {frac:.5f}, film rel RMS {err:.3e} (noise {noise:.3e})")
+    print(f"{kind}/{kernel}: bit-exact samples {frac:.5f}, film rel RMS {err:.3e} (noise {noise:.3e})")
     assert frac >= 0.999
     assert err <= 0.5 * noise
     integ.close()
