@@ -381,6 +381,18 @@ extern "C" {
 
 const char *avr_last_error(void) { return g_err.c_str(); }
 
+
+// Setup calls replace or free device buffers that queued work on the context's stream may
+// still read, and readbacks through hipMemcpy (the null stream) do not order against a
+// non-blocking stream: both first drain the context's stream.
+#define AVR_QUIESCE(c)                                                                              \
+    do {                                                                                            \
+        if ((c) && (c)->stream) {                                                                   \
+            const hipError_t qe_ = hipStreamSynchronize((c)->stream);                               \
+            if (qe_ != hipSuccess) return fail(AVR_ERR_HIP, std::string("stream: ") + hipGetErrorString(qe_)); \
+        }                                                                                           \
+    } while (0)
+
 int avr_context_create(int device, long long max_paths, avr_context **out) {
     if (!out) return fail(AVR_ERR_ARG, "null out");
     int ndev = 0;
@@ -439,6 +451,7 @@ int avr_context_create(int device, long long max_paths, avr_context **out) {
 }
 
 int avr_set_grid_layout(avr_context *c, int layout) {
+    AVR_QUIESCE(c);
     if (!c || (layout != 0 && layout != 1)) return fail(AVR_ERR_ARG, "grid layout must be 0 (linear) or 1 (fat)");
     c->grid_layout = layout;
     return AVR_OK;
@@ -506,6 +519,7 @@ int avr_set_stream(avr_context *c, void *s) {
 int avr_medium_grid(avr_context *c, const float *density, int nx, int ny, int nz, const float bounds[6],
                     const float rfm[16], const float mfr[16], const float *sigma_a, const float *sigma_s, float g,
                     const float *Le, const float *Lescale, int lnx, int lny, int lnz, const int mres[3]) {
+    AVR_QUIESCE(c);
     if (!c || !density || nx < 1 || ny < 1 || nz < 1) return fail(AVR_ERR_ARG, "bad grid");
     HIP_TRY(hipSetDevice(c->device));
     if (c->d_density_owned) { (void)hipFree(c->d_density_owned); c->d_density_owned = nullptr; }
@@ -521,6 +535,7 @@ int avr_medium_grid_device(avr_context *c, const float *d_density, int nx, int n
                            const float rfm[16], const float mfr[16], const float *sigma_a, const float *sigma_s,
                            float g, const float *Le, const float *Lescale, int lnx, int lny, int lnz,
                            const int mres[3]) {
+    AVR_QUIESCE(c);
     if (!c || !d_density || nx < 1 || ny < 1 || nz < 1) return fail(AVR_ERR_ARG, "bad grid");
     if ((size_t)nx * ny * nz > (size_t)INT32_MAX) return fail(AVR_ERR_ARG, "grid too large for int32 indexing");
     HIP_TRY(hipSetDevice(c->device));
@@ -531,6 +546,7 @@ int avr_medium_grid_device(avr_context *c, const float *d_density, int nx, int n
 
 int avr_medium_temperature(avr_context *c, const float *temperature, float temperature_scale,
                            float temperature_offset) {
+    AVR_QUIESCE(c);
     if (!c || !temperature) return fail(AVR_ERR_ARG, "null temperature grid");
     if (!c->has_medium || c->med.type != 0) return fail(AVR_ERR_STATE, "temperature needs a grid medium first");
     if (!c->med.Le || !c->med.lescale) return fail(AVR_ERR_STATE, "medium emission tables missing");
@@ -551,6 +567,7 @@ int avr_medium_temperature(avr_context *c, const float *temperature, float tempe
 
 int avr_medium_homogeneous(avr_context *c, const float bounds[6], const float rfm[16], const float mfr[16],
                            const float *sigma_a, const float *sigma_s, float g, const float *Le) {
+    AVR_QUIESCE(c);
     if (!c || !bounds || !rfm || !mfr) return fail(AVR_ERR_ARG, "null medium argument");
     HIP_TRY(hipSetDevice(c->device));
     static const float one = 1.f;
@@ -562,6 +579,7 @@ int avr_medium_homogeneous(avr_context *c, const float bounds[6], const float rf
 int avr_medium_cloud(avr_context *c, const float bounds[6], const float rfm[16], const float mfr[16],
                      const float *sigma_a, const float *sigma_s, float g, float density, float wispiness,
                      float frequency) {
+    AVR_QUIESCE(c);
     if (!c || !bounds || !rfm || !mfr) return fail(AVR_ERR_ARG, "null medium argument");
     HIP_TRY(hipSetDevice(c->device));
     const int mres[3] = {1, 1, 1};
@@ -573,6 +591,7 @@ int avr_medium_cloud(avr_context *c, const float bounds[6], const float rfm[16],
 int avr_medium_nanovdb(avr_context *c, const avr_vdb_grid *density, const avr_vdb_grid *temperature, const float rfm[16],
                        const float mfr[16], const float *sigma_a, const float *sigma_s, float g, float Lescale,
                        float temperature_offset, float temperature_scale) {
+    AVR_QUIESCE(c);
     if (!c || !density || !rfm || !mfr) return fail(AVR_ERR_ARG, "null medium argument");
     HIP_TRY(hipSetDevice(c->device));
     HIP_TRY(hipStreamSynchronize(c->stream));
@@ -610,6 +629,7 @@ int avr_medium_nanovdb(avr_context *c, const avr_vdb_grid *density, const avr_vd
 int avr_medium_rgbgrid(avr_context *c, int nx, int ny, int nz, const float bounds[6], const float rfm[16],
                        const float mfr[16], const float *sigma_a, const float *sigma_s, float sigma_scale, float g,
                        const float *Le, const float *illuminant, float Le_scale) {
+    AVR_QUIESCE(c);
     if (!c || !bounds || !rfm || !mfr) return fail(AVR_ERR_ARG, "null medium argument");
     if (nx < 1 || ny < 1 || nz < 1) return fail(AVR_ERR_ARG, "bad grid");
     if (!sigma_a && !sigma_s)
@@ -648,6 +668,7 @@ int avr_medium_rgbgrid(avr_context *c, int nx, int ny, int nz, const float bound
 }
 
 int avr_medium_bounds(avr_context *c, float bounds[6]) {
+    AVR_QUIESCE(c);
     if (!c || !c->has_medium || !bounds) return fail(AVR_ERR_STATE, "no medium");
     for (int a = 0; a < 3; ++a) { bounds[a] = c->med.bmin[a]; bounds[3 + a] = c->med.bmax[a]; }
     return AVR_OK;
@@ -664,6 +685,7 @@ int avr_generate_cloud(avr_context *c, float *d_out, int n, long long first, lon
 }
 
 int avr_read_majorant(avr_context *c, float *out) {
+    AVR_QUIESCE(c);
     if (!c || !c->has_medium || !out) return fail(AVR_ERR_STATE, "no medium");
     const int nm = c->med.mres[0] * c->med.mres[1] * c->med.mres[2];
     HIP_TRY(hipMemcpyAsync(out, c->d_majorant, nm * sizeof(float), hipMemcpyDeviceToHost, c->stream));
@@ -675,6 +697,7 @@ static void pc1d_build(const float *f, int n, float mn, float mx, float *cdf, fl
 
 int avr_lights(avr_context *c, int n, const int *types, const float *w3, const float *L, const float *scale,
                float scene_radius) {
+    AVR_QUIESCE(c);
     if (!c || n < 0 || n > avr::kMaxLights) return fail(AVR_ERR_ARG, "0..8 lights supported");
     if (n > 0 && (!types || !w3 || !L || !scale)) return fail(AVR_ERR_ARG, "null light arrays");
     HIP_TRY(hipSetDevice(c->device));
@@ -707,6 +730,7 @@ int avr_lights(avr_context *c, int n, const int *types, const float *w3, const f
 // ImageInfiniteLight: pixel spectra, the compensated PiecewiseConstant2D (lights.cpp:1026-1038)
 int avr_light_image(avr_context *c, int index, int res, const float *pixel_coeffs, const float *distribution,
                     const float *illuminant, const float render_from_light[16], const float light_from_render[16]) {
+    AVR_QUIESCE(c);
     if (!c || index < 0 || index >= c->lights.n || c->h_lights[index].type != 2)
         return fail(AVR_ERR_ARG, "avr_light_image: index must name a type-2 light of the last avr_lights call");
     if (res < 1 || !pixel_coeffs || !distribution || !illuminant || !render_from_light || !light_from_render)
@@ -776,6 +800,7 @@ int avr_camera(avr_context *c, int type, const float cfr[16], const float rfc[16
 
 int avr_film(avr_context *c, int width, int height, const float fr[2], const float *sensor, float imaging_ratio,
              float max_component_value) {
+    AVR_QUIESCE(c);
     if (!c || width < 1 || height < 1 || !fr || !sensor) return fail(AVR_ERR_ARG, "bad film");
     HIP_TRY(hipSetDevice(c->device));
     int rc = upload_table(&c->d_xyz, sensor, 3 * (size_t)avr::kNTable, c->stream);
@@ -815,6 +840,7 @@ static void pc1d_build(const float *f, int n, float mn, float mx, float *cdf, fl
 }
 
 int avr_set_filter(avr_context *c, int type, const float radius[2], float sigma) {
+    AVR_QUIESCE(c);
     if (!c || (type != 0 && type != 1) || !radius || !(radius[0] > 0) || !(radius[1] > 0))
         return fail(AVR_ERR_ARG, "filter: type 0 (box) or 1 (gaussian) with a positive radius");
     HIP_TRY(hipSetDevice(c->device));
@@ -857,6 +883,7 @@ int avr_set_filter(avr_context *c, int type, const float radius[2], float sigma)
 }
 
 int avr_set_sampler_table(avr_context *c, int dims) {
+    AVR_QUIESCE(c);
     if (!c || dims < 0 || dims > 4096) return fail(AVR_ERR_ARG, "sampler table dimensions must be 0..4096");
     c->zs_dims = dims;
     c->zs_key[0] = -1;   // rebuild (or drop) at the next render
@@ -917,6 +944,7 @@ static int fold_stats(avr_context *c) {
     c->timed.clear();
     c->ev_used = 0;
     unsigned long long h[avr::kNumStats];
+    HIP_TRY(hipStreamSynchronize(c->stream));
     HIP_TRY(hipMemcpy(h, c->d_stats, sizeof(h), hipMemcpyDeviceToHost));
     c->stats.medium_lookups = h[0];
     c->stats.medium_items_in = h[1];
@@ -1323,6 +1351,7 @@ int avr_film_device_ptrs(avr_context *c, void **rgb, void **w) {
 
 int avr_last_pass_samples(avr_context *c, float *L, float *lambda, float *pdf, long long n_max, int *first,
                           int *ns) {
+    AVR_QUIESCE(c);
     if (!c || !c->has_film || !L || !lambda || !pdf || !first || !ns) return fail(AVR_ERR_ARG, "null arg");
     const long long n = (long long)c->film.width * c->film.height * c->last_S;
     if (n_max < n) return fail(AVR_ERR_ARG, "buffer too small for the last pass");
@@ -1337,6 +1366,7 @@ int avr_last_pass_samples(avr_context *c, float *L, float *lambda, float *pdf, l
 }
 
 int avr_last_pass_weights(avr_context *c, float *w, long long n_max) {
+    AVR_QUIESCE(c);
     if (!c || !c->has_film || !w) return fail(AVR_ERR_ARG, "null arg");
     const long long n = (long long)c->film.width * c->film.height * c->last_S;
     if (n_max < n) return fail(AVR_ERR_ARG, "buffer too small for the last pass");

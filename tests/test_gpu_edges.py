@@ -111,3 +111,22 @@ def test_zsobol_index_range_is_checked():
     with pytest.raises(RuntimeError, match="2\\^32"):
         integ.ctx.render(0, 1, 0, 1)
     integ.close()
+
+
+@pytest.mark.parametrize("kernel", ["persistent", "wavefront"])
+def test_readback_is_ordered_after_an_asynchronous_render(kernel):
+    """avr_render only enqueues on the context's (non-blocking) stream; the per-sample
+    readback must still see the finished pass (it drains the stream first)."""
+    from acceleratedvolrenderer_amd import VolPathIntegrator, scenes
+    from oracle import binding
+    dens = binding.cloud_grid(16)
+    scene = scenes.s_cloud(dens, width=40, height=24)
+    integ = VolPathIntegrator(scene, device=0, maxdepth=scenes.CLOUD_MAXDEPTH, spp=8, kernel=kernel)
+    integ.ctx.render(8, 16, 0, scenes.CLOUD_MAXDEPTH)        # no sync before the readback
+    _, _, L, _, _ = integ.ctx.last_pass_samples(40 * 24, 8)
+    canon = binding.OracleRun(scene, max_depth=scenes.CLOUD_MAXDEPTH, seed=0, libm="canonical")
+    same = sum(np.array_equal(L[s * 960 + p].view(np.uint32),
+                              canon.pixel_sample(p % 40, p // 40, 8 + s)[0].view(np.uint32))
+               for s in range(8) for p in range(0, 960, 7))
+    assert same == 8 * len(range(0, 960, 7))
+    integ.close()
