@@ -108,7 +108,7 @@ struct avr_context {
     int zs_dims = 256;
     int zs_key[3] = {-1, -1, -1};
     int refill_min = 32;
-    int dda_budget = 12;
+    int dda_budget = 0;       // 0: by majorant resolution (12 cells up to 16^3, 32 for NanoVDB's 64^3)
     int grid_layout = 1;
     bool gray = false;        // sigma_a and sigma_s constant over 360..830 nm      // 1: build the fat (footprint) copy when memory allows, 0: linear only
     float4 *d_fat = nullptr;
@@ -460,7 +460,7 @@ int avr_set_grid_layout(avr_context *c, int layout) {
 int avr_grid_layout_active(avr_context *c) { return (c && c->d_fat) ? 1 : 0; }
 
 int avr_set_dda_budget(avr_context *c, int cells) {
-    if (!c || cells < 1) return fail(AVR_ERR_ARG, "DDA budget must be >= 1 cell");
+    if (!c || cells < 0) return fail(AVR_ERR_ARG, "DDA budget must be >= 1 cell (0: default)");
     c->dda_budget = cells;
     return AVR_OK;
 }
@@ -1073,7 +1073,10 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
             HIP_TRY(hipGetLastError());
             p.advance = c->d_advance;
             p.refill_min = c->refill_min;
-            p.dda_budget = c->dda_budget;
+            {
+                const int mres = std::max(c->med.mres[0], std::max(c->med.mres[1], c->med.mres[2]));
+                p.dda_budget = c->dda_budget > 0 ? c->dda_budget : (mres > 16 ? 32 : 12);
+            }
             p.heads = c->d_heads;
             HIP_TRY(hipMemsetAsync(c->d_heads, 0, 8 * sizeof(int), c->stream));
             EV_MARK(e0);

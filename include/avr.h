@@ -67,7 +67,9 @@ int avr_set_kernel_mode(avr_context *ctx, int mode);
  * are idle (or none is busy); larger values batch the camera-ray setup across lanes. */
 int avr_set_refill_min(avr_context *ctx, int lanes);
 /* k_paths: majorant-grid cells a lane may cross per tracking iteration before yielding to
- * the wave (default 12); bounds the divergence of the DDA walk. No effect on results. */
+ * the wave (0 = default: 12 for majorant grids up to 16^3, 32 for finer ones such as
+ * NanoVDB's 64^3 — measured optima); bounds the divergence of the DDA walk. No effect on
+ * results. */
 int avr_set_dda_budget(avr_context *ctx, int cells);
 /* Density layout for the NEXT avr_medium_grid* call: 1 (default) also builds a "fat"
  * footprint copy — entry (ix,iy,iz) holds the 8 trilinear taps as 32 contiguous bytes,
