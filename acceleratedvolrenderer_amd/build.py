@@ -15,6 +15,8 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 # so a device sample replays the CPU oracle's sample.
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared",
          "-I" + os.path.join(ROOT, "include")]
+# RCCL for avr_film_reduce_rccl (in-process multi-GPU film reduce)
+LIBS = ["-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"]
 
 
 def up_to_date():
@@ -27,7 +29,7 @@ def up_to_date():
 def build(force=False, verbose=False):
     if not force and up_to_date():
         return OUT
-    cmd = [HIPCC] + FLAGS + [SRC, "-o", OUT + ".tmp"]
+    cmd = [HIPCC] + FLAGS + [SRC, "-o", OUT + ".tmp"] + LIBS
     if verbose:
         print(" ".join(cmd))
     subprocess.check_call(cmd)

@@ -149,6 +149,7 @@ SIGNATURES = {
     "avr_film_device_ptrs": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p),
                                             ctypes.POINTER(ctypes.c_void_p)]),
     "avr_film_export_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "avr_film_reduce_rccl": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, ctypes.c_int]),
     "avr_last_pass_samples": (ctypes.c_int, [ctypes.c_void_p, c_float_p, c_float_p, c_float_p, ctypes.c_longlong,
                                              c_int_p, c_int_p]),
     "avr_graph_walks": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(AvrGraphSampling), ctypes.c_longlong, c_float_p,
@@ -564,3 +565,10 @@ class Graph:
         a, n = ctypes.c_float(), ctypes.c_longlong()
         _check(self.lib.avr_graph_in_node_path_length(self.h, ctypes.byref(a), ctypes.byref(n)))
         return a.value, n.value
+
+
+def film_reduce_rccl(contexts, root=0):
+    """avr_film_reduce_rccl: SUM the films of `contexts` (one per GPU) into contexts[root]."""
+    lib = load()
+    arr = (ctypes.c_void_p * len(contexts))(*[c.h.value if hasattr(c.h, "value") else c.h for c in contexts])
+    _check(lib.avr_film_reduce_rccl(arr, len(contexts), int(root)))

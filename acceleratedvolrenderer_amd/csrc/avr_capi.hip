@@ -13,6 +13,7 @@
 #include "avr_graph.hip"
 #include "../../include/avr.h"
 
+#include <rccl/rccl.h>
 #include <climits>
 #include <cmath>
 #include <cstdio>
@@ -1391,6 +1392,51 @@ int avr_film_export_device(avr_context *c, void *dst) {
         HIP_TRY(hipMemcpyAsync(d + 4 * np, c->film.bucket_sum, 2 * np * c->film.nbuckets * sizeof(double),
                                hipMemcpyDeviceToDevice, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
+    return AVR_OK;
+}
+
+// RGBFilm sums of several contexts (one per GPU, one process: pbrt's in-process multi-GPU
+// render) SUM-reduced into the root context's film with RCCL over xGMI: rgb, weights and,
+// for a SpectralFilm, the bucket sums — in place on the root.
+int avr_film_reduce_rccl(avr_context **ctxs, int n, int root) {
+    if (!ctxs || n < 1 || root < 0 || root >= n) return fail(AVR_ERR_ARG, "film reduce: bad context list");
+    for (int i = 0; i < n; ++i) {
+        if (!ctxs[i] || !ctxs[i]->has_film) return fail(AVR_ERR_STATE, "film reduce: context without a film");
+        const avr::DevFilm &a = ctxs[i]->film, &b = ctxs[root]->film;
+        if (a.width != b.width || a.height != b.height || a.nbuckets != b.nbuckets)
+            return fail(AVR_ERR_ARG, "film reduce: films differ in resolution or buckets");
+        for (int j = 0; j < i; ++j)
+            if (ctxs[j]->device == ctxs[i]->device) return fail(AVR_ERR_ARG, "film reduce: one context per GPU");
+    }
+    std::vector<int> devs(n);
+    for (int i = 0; i < n; ++i) {
+        devs[i] = ctxs[i]->device;
+        HIP_TRY(hipSetDevice(devs[i]));
+        HIP_TRY(hipStreamSynchronize(ctxs[i]->stream));
+    }
+    std::vector<ncclComm_t> comms(n);
+    if (ncclCommInitAll(comms.data(), n, devs.data()) != ncclSuccess) return fail(AVR_ERR_HIP, "ncclCommInitAll failed");
+    const size_t np = (size_t)ctxs[root]->film.width * ctxs[root]->film.height;
+    const size_t nb = (size_t)ctxs[root]->film.nbuckets;
+    ncclResult_t r = ncclGroupStart();
+    for (int i = 0; r == ncclSuccess && i < n; ++i) {
+        avr::DevFilm &f = ctxs[i]->film;
+        r = ncclReduce(f.rgb_sum, f.rgb_sum, 3 * np, ncclDouble, ncclSum, root, comms[i], ctxs[i]->stream);
+        if (r == ncclSuccess) r = ncclReduce(f.w_sum, f.w_sum, np, ncclDouble, ncclSum, root, comms[i], ctxs[i]->stream);
+        if (r == ncclSuccess && nb > 0)
+            r = ncclReduce(f.bucket_sum, f.bucket_sum, 2 * np * nb, ncclDouble, ncclSum, root, comms[i], ctxs[i]->stream);
+    }
+    const ncclResult_t re = ncclGroupEnd();
+    if (r == ncclSuccess) r = re;
+    hipError_t e = hipSuccess;
+    for (int i = 0; i < n; ++i) {
+        (void)hipSetDevice(devs[i]);
+        const hipError_t ei = hipStreamSynchronize(ctxs[i]->stream);
+        if (e == hipSuccess) e = ei;
+    }
+    for (auto &cm : comms) (void)ncclCommDestroy(cm);
+    if (r != ncclSuccess) return fail(AVR_ERR_HIP, std::string("film reduce: ") + ncclGetErrorString(r));
+    if (e != hipSuccess) return fail(AVR_ERR_HIP, std::string("film reduce: ") + hipGetErrorString(e));
     return AVR_OK;
 }
 

@@ -247,6 +247,11 @@ int avr_film_read(avr_context *ctx, double *rgb_sum, double *w_sum);
 int avr_film_spectral(avr_context *ctx, int n_buckets, float lambda_min, float lambda_max);
 int avr_film_read_spectral(avr_context *ctx, double *bucket_sums, double *weight_sums);
 int avr_film_spectral_device_ptrs(avr_context *ctx, void **d_bucket_sums, void **d_weight_sums);
+/* In-process multi-GPU render (one context per GPU, e.g. avr_render(ctx_k, k*spp/N,
+ * (k+1)*spp/N, ...)): SUM-reduce the n contexts' film sums (rgb, weights, SpectralFilm
+ * buckets) into ctxs[root]'s film over RCCL (xGMI); the other films are left as they are.
+ * Films must match in resolution and buckets; one context per device. */
+int avr_film_reduce_rccl(avr_context **ctxs, int n, int root);
 /* Device pointers of the film sums (for an RCCL reduce across GPUs). */
 int avr_film_device_ptrs(avr_context *ctx, void **d_rgb_sum, void **d_w_sum);
 /* Device-to-device copy of the film sums into caller memory on the same GPU, laid out

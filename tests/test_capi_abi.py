@@ -41,3 +41,9 @@ def test_errors_are_reported_not_raised():
     assert lib.avr_context_create(0, 0, None) != 0
     assert b"null" in lib.avr_last_error()
     assert lib.avr_render(None, 0, 1, 0, 5) != 0
+
+
+def test_film_reduce_argument_errors_without_a_gpu():
+    lib = capi.load()
+    assert lib.avr_film_reduce_rccl(None, 1, 0) != 0
+    assert b"context list" in lib.avr_last_error()

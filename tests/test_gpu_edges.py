@@ -130,3 +130,22 @@ def test_readback_is_ordered_after_an_asynchronous_render(kernel):
                for s in range(8) for p in range(0, 960, 7))
     assert same == 8 * len(range(0, 960, 7))
     integ.close()
+
+
+def test_film_reduce_rccl_single_gpu():
+    """avr_film_reduce_rccl with one context (the 1-GPU box): the root film is its own sum;
+    a second context on the same device is refused (one context per GPU)."""
+    from acceleratedvolrenderer_amd import VolPathIntegrator, capi
+    dens = np.random.default_rng(4).random((6, 6, 6), dtype=np.float32)
+    a = VolPathIntegrator(_scene(12, 8, dens), device=0, maxdepth=4, spp=4)
+    b = VolPathIntegrator(_scene(12, 8, dens), device=0, maxdepth=4, spp=4)
+    rgb, w = a.render()
+    capi.film_reduce_rccl([a.ctx], root=0)
+    rgb2, w2 = a.film_sums()
+    assert np.array_equal(rgb, rgb2) and np.array_equal(w, w2)
+    with pytest.raises(RuntimeError, match="one context per GPU"):
+        capi.film_reduce_rccl([a.ctx, b.ctx], root=0)
+    with pytest.raises(RuntimeError, match="context list"):
+        capi.film_reduce_rccl([a.ctx], root=1)
+    a.close()
+    b.close()

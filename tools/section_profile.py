@@ -24,7 +24,7 @@ NAMES = ["events", "refill+camera", "segment starts", "dda walk", "collision"]
 def build():
     sys.path.insert(0, ROOT)
     from acceleratedvolrenderer_amd import build as b
-    cmd = [b.HIPCC] + b.FLAGS + ["-DAVR_PROFILE_SECTIONS", b.SRC, "-o", VARIANT]
+    cmd = [b.HIPCC] + b.FLAGS + ["-DAVR_PROFILE_SECTIONS", b.SRC, "-o", VARIANT] + b.LIBS
     subprocess.check_call(cmd)
     print(VARIANT)
 
