@@ -628,7 +628,7 @@ template <> struct PathSampler<true> {
 // time (1D) and lens (2D); returns pFilm and the filter weight.
 template <typename Smp>
 __device__ __forceinline__ void camera_sample(const Params &P, Smp &smp, int px, int py, float *pFilmX, float *pFilmY,
-                                              float *weight) {
+                                              float *weight, const smp::FilterTables *ft = nullptr) {
     float fu0, fu1;
     smp.get2d(P, &fu0, &fu1);
     float fpx, fpy;
@@ -637,7 +637,7 @@ __device__ __forceinline__ void camera_sample(const Params &P, Smp &smp, int px,
         fpx = lerp(fu0, -P.film.filter_rx, P.film.filter_rx);
         fpy = lerp(fu1, -P.film.filter_ry, P.film.filter_ry);
     } else {
-        ::avr::smp::gaussian_filter_sample(P.film.gauss, fu0, fu1, &fpx, &fpy, weight);
+        ::avr::smp::gaussian_filter_sample(ft ? *ft : P.film.gauss, fu0, fu1, &fpx, &fpy, weight);
     }
     *pFilmX = ((float)px + fpx) + 0.5f;
     *pFilmY = ((float)py + fpy) + 0.5f;
@@ -1189,6 +1189,23 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
     // ImageInfiniteLight shadow rays (non-delta NEE): the sampled (u, v), p_l and the phase
     // value per lane, parked here while the lane traces its shadow ray (off the VGPR budget)
     __shared__ float4 s_img[kImage ? 256 : 1];
+    // GaussianFilter's FilterSampler tables (pbrt's default radius 1.5: 48 x 48 function +
+    // CDFs, ~19 KB) staged here when they fit: the camera-ray refill's two binary searches
+    // then run on LDS instead of dependent L2 loads
+    constexpr int kFiltLds = 4864;
+    __shared__ float s_filt[kFiltLds];
+    smp::FilterTables ftab = P.film.gauss;
+    if (P.film.filter_type != 0) {
+        const int nf = smp::filter_table_floats(ftab.nx, ftab.ny);
+        if (nf <= kFiltLds) {
+            const float *base = ftab.f;
+            for (int i = threadIdx.x; i < nf; i += blockDim.x) s_filt[i] = base[i];
+            ftab.f = s_filt;
+            ftab.ccdf = s_filt + (P.film.gauss.ccdf - base);
+            ftab.cint = s_filt + (P.film.gauss.cint - base);
+            ftab.mcdf = s_filt + (P.film.gauss.mcdf - base);
+        }
+    }
     // the host routes GridMedium majorant grids of more than 4096 cells to the wavefront kernels
     if constexpr (!kVdb) stage_majorant(P.med, s_maj);
     const float *__restrict__ majp = kVdb ? P.med.majorant : s_maj;
@@ -1454,7 +1471,7 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
                     }
                     lam = film_sample_lambda(P.film, smp.get1d(P));   // pdf: recomputed by k_film
                     float pFilmX, pFilmY, fweight;
-                    camera_sample(P, smp, px, py, &pFilmX, &pFilmY, &fweight);
+                    camera_sample(P, smp, px, py, &pFilmX, &pFilmY, &fweight, &ftab);
                     if (P.film.filter_type != 0) P.ps.weight[g] = fweight;
                     const float *r = P.cam.raster;
                     V3 pCam = {r[0] * pFilmX + r[1] * pFilmY + r[2] * 0.f + r[3],

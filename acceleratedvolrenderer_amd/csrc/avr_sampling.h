@@ -226,7 +226,7 @@ struct FilterTables {
     const float *f, *ccdf, *cint, *mcdf;
     float mint;
 };
-inline int filter_table_floats(int nx, int ny) { return nx * ny + ny * (nx + 1) + ny + (ny + 1) + 1; }
+AVR_HD int filter_table_floats(int nx, int ny) { return nx * ny + ny * (nx + 1) + ny + (ny + 1) + 1; }
 
 // Sample one PiecewiseConstant1D given as (cdf[n+1], func[n], funcInt) over [mn, mx]
 AVR_HD float pc1d_sample(const float *cdf, const float *func, int n, float funcInt, float mn, float mx, float u,
