@@ -115,9 +115,29 @@ struct avr_context {
     float4 *d_fat = nullptr;
     uint64_t *d_advance = nullptr;  // per-pass PCG advance table {A, H}
     long long advance_cap = 0;
+    // avr_film_reduce_rccl: this context's communicator and the clique (contexts in rank
+    // order) it was created with by ncclCommInitAll; reused while the same clique reduces
+    ncclComm_t comm = nullptr;
+    std::vector<avr_context *> comm_group;
 };
 
 namespace {
+
+// Destroy the communicators of c's RCCL clique (every member's: a clique with one member
+// gone cannot run a collective) and forget the clique on each member.
+void release_comms(avr_context *c) {
+    if (!c || c->comm_group.empty()) return;
+    const std::vector<avr_context *> group = c->comm_group;
+    for (avr_context *m : group) {
+        if (m->comm) {
+            (void)hipSetDevice(m->device);
+            (void)ncclCommDestroy(m->comm);
+        }
+        m->comm = nullptr;
+        m->comm_group.clear();
+    }
+    (void)hipSetDevice(c->device);
+}
 
 void free_paths(avr_context *c) {
     float4 *f4[] = {c->ps.o, c->ps.d, c->ps.lambda, c->ps.pdf, c->ps.beta, c->ps.r_u, c->ps.r_l, c->ps.L,
@@ -396,6 +416,8 @@ const char *avr_last_error(void) { return g_err.c_str(); }
 
 int avr_context_create(int device, long long max_paths, avr_context **out) {
     if (!out) return fail(AVR_ERR_ARG, "null out");
+    // path ids (s * pixels + pixel) are 32-bit in the kernels: passes hold < 2^31 paths
+    if (max_paths > INT_MAX) return fail(AVR_ERR_ARG, "max_paths above 2^31 - 1 (32-bit path ids)");
     int ndev = 0;
     HIP_TRY(hipGetDeviceCount(&ndev));
     if (device < 0 || device >= ndev) return fail(AVR_ERR_ARG, "device index out of range");
@@ -482,6 +504,7 @@ int avr_context_destroy(avr_context *c) {
     if (!c) return AVR_OK;
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
+    release_comms(c);
     free_paths(c);
     float *fs[] = {c->d_density_owned, c->d_sigma_a, c->d_sigma_s, c->d_Le, c->d_lescale, c->d_majorant,
                    c->d_lightL, c->d_xyz};
@@ -992,7 +1015,9 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
         // below the sampler's samplesPerPixel and the Sobol' index below 2^32
         if (spp_end > c->sampler_spp) return fail(AVR_ERR_ARG, "zsobol: sample index beyond samplesPerPixel");
         zs = avr::smp::zsobol_params(c->sampler_spp, c->film.width, c->film.height, seed);
-        if (zs.nBase4Digits > 16) return fail(AVR_ERR_ARG, "zsobol: resolution x spp beyond 2^32 sample indices");
+        // SobolSample takes indices below 2^SobolMatrixSize = 2^52 (lowdiscrepancy.h:170)
+        if (2 * zs.nBase4Digits - (zs.log2spp & 1) > 52)
+            return fail(AVR_ERR_ARG, "zsobol: resolution x spp beyond the 2^52 Sobol' index range");
     }
     HIP_TRY(hipSetDevice(c->device));
     if (c->sampler_kind == 1) {
@@ -1414,8 +1439,23 @@ int avr_film_reduce_rccl(avr_context **ctxs, int n, int root) {
         HIP_TRY(hipSetDevice(devs[i]));
         HIP_TRY(hipStreamSynchronize(ctxs[i]->stream));
     }
+    // communicators are created once per clique (ncclCommInitAll costs a bootstrap) and
+    // cached on the contexts; a different context list releases the old cliques first
+    const std::vector<avr_context *> clique(ctxs, ctxs + n);
+    bool cached = true;
+    for (int i = 0; i < n && cached; ++i) cached = ctxs[i]->comm && ctxs[i]->comm_group == clique;
+    if (!cached) {
+        for (int i = 0; i < n; ++i) release_comms(ctxs[i]);
+        std::vector<ncclComm_t> fresh(n);
+        if (ncclCommInitAll(fresh.data(), n, devs.data()) != ncclSuccess)
+            return fail(AVR_ERR_HIP, "ncclCommInitAll failed");
+        for (int i = 0; i < n; ++i) {
+            ctxs[i]->comm = fresh[i];
+            ctxs[i]->comm_group = clique;
+        }
+    }
     std::vector<ncclComm_t> comms(n);
-    if (ncclCommInitAll(comms.data(), n, devs.data()) != ncclSuccess) return fail(AVR_ERR_HIP, "ncclCommInitAll failed");
+    for (int i = 0; i < n; ++i) comms[i] = ctxs[i]->comm;
     const size_t np = (size_t)ctxs[root]->film.width * ctxs[root]->film.height;
     const size_t nb = (size_t)ctxs[root]->film.nbuckets;
     ncclResult_t r = ncclGroupStart();
@@ -1434,7 +1474,6 @@ int avr_film_reduce_rccl(avr_context **ctxs, int n, int root) {
         const hipError_t ei = hipStreamSynchronize(ctxs[i]->stream);
         if (e == hipSuccess) e = ei;
     }
-    for (auto &cm : comms) (void)ncclCommDestroy(cm);
     if (r != ncclSuccess) return fail(AVR_ERR_HIP, std::string("film reduce: ") + ncclGetErrorString(r));
     if (e != hipSuccess) return fail(AVR_ERR_HIP, std::string("film reduce: ") + hipGetErrorString(e));
     return AVR_OK;

@@ -619,8 +619,16 @@ template <> struct PathSampler<true> {
     }
     __device__ __forceinline__ float get1d(const Params &P) { return z.get1d(P.zs); }
     __device__ __forceinline__ void get2d(const Params &P, float *u0, float *u1) { z.get2d(P.zs, u0, u1); }
-    __device__ __forceinline__ void load(const Params &P, int i) { z.morton = P.ps.smp_state[i]; z.dimension = (uint32_t)P.ps.smp_inc[i]; }
-    __device__ __forceinline__ void save(const Params &P, int i) { P.ps.smp_state[i] = z.morton; P.ps.smp_inc[i] = z.dimension; }
+    __device__ __forceinline__ void load(const Params &P, int i) {
+        const uint64_t st = P.ps.smp_state[i];
+        z.morton = (uint32_t)st;
+        z.hi = (uint32_t)(st >> 32);
+        z.dimension = (uint32_t)P.ps.smp_inc[i];
+    }
+    __device__ __forceinline__ void save(const Params &P, int i) {
+        P.ps.smp_state[i] = ((uint64_t)z.hi << 32) | z.morton;
+        P.ps.smp_inc[i] = z.dimension;
+    }
 };
 
 // GetCameraSample (samplers.h:797-815) after the wavelength draw: pixel 2D through the
@@ -1972,7 +1980,7 @@ __global__ void __launch_bounds__(256) k_zsobol_table(smp::ZSobolParams zp, int 
         const int d = (int)(k % dmax);
         const long long pix = k / dmax;
         const uint32_t pm = (uint32_t)smp::encode_morton2((uint32_t)(pix % width), (uint32_t)(pix / width));
-        table[(size_t)pm * dmax + d] = smp::zsobol_upper(pm << zp.log2spp, (uint32_t)d, zp);
+        table[(size_t)pm * dmax + d] = smp::zsobol_upper(pm, (uint32_t)d, zp);
     }
 }
 

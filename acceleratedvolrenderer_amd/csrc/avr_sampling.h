@@ -107,36 +107,42 @@ struct ZSobolParams {
     int dmax;
 };
 
-// MixBits(x) >> 24 for x < 2^32 (a 40-bit value), as (hi 8 bits, lo 32 bits)
-AVR_HD void mix_hi40(uint32_t x, uint32_t *hi, uint32_t *lo) {
-    uint64_t v = (uint64_t)(x ^ (x >> 31));   // v ^= v >> 31 on a zero-extended 32-bit value
+// Morton(pixel) << log2(spp) | sampleIndex fits 32 bits (nBase4Digits <= 16: e.g. 1024 spp
+// at 1080p); beyond it (4096 spp at 720p ...) the index and the digit prefixes are 64-bit.
+AVR_HD bool zsobol_wide(const ZSobolParams &zp) { return zp.nBase4Digits > 16; }
+
+// (MixBits(x) >> 24) % 24 (util/hash.h:84-92) with the 40-bit quotient split into 32-bit
+// pieces: 2^32 = 16 (mod 24). M = 32-bit: x zero-extended, so v ^= v >> 31 is done in 32 bits.
+template <typename M>
+AVR_HD uint32_t mix_perm24(M x) {
+    uint64_t v = sizeof(M) == 4 ? (uint64_t)(uint32_t)(x ^ (x >> 31)) : ((uint64_t)x ^ ((uint64_t)x >> 31));
     v *= 0x7fb5d329728ea185ull;
     v ^= v >> 27;
     v *= 0x81dadef4bc2dd44dull;
     v ^= v >> 33;
-    *hi = (uint32_t)(v >> 56);
-    *lo = (uint32_t)(v >> 24);
+    return ((uint32_t)(v >> 56) * 16u + (uint32_t)(v >> 24) % 24u) % 24u;
+}
+AVR_HD uint32_t zperm(uint32_t p, uint32_t digit) {
+    const uint64_t w = p < 8 ? kZPermW0 : (p < 16 ? kZPermW1 : kZPermW2);
+    return (uint32_t)(w >> ((p & 7) * 8 + 2 * digit)) & 3u;
 }
 
 // ZSobolSampler::GetSampleIndex (samplers.h:296-355), digits i in [iLo, iHi] (most
-// significant first) of the current dimension. The host guarantees Morton(pixel) <<
-// log2(spp) | index < 2^32 (nBase4Digits <= 16), so the Morton index, every digit prefix and
-// the result fit in 32 bits (the reference's uint64_t values have zero upper halves).
-AVR_HD uint32_t zsobol_digits(uint32_t morton, uint32_t dimension, const ZSobolParams &zp, int iHi, int iLo) {
-    uint32_t sampleIndex = 0;
+// significant first) of the current dimension. M is uint32_t when the whole index fits 32
+// bits (the reference's uint64_t values then have zero upper halves), uint64_t otherwise.
+// 0x55555555u * dimension is a 32-bit product, zero-extended by the XOR.
+template <typename M>
+AVR_HD M zsobol_digits(M morton, uint32_t dimension, const ZSobolParams &zp, int iHi, int iLo) {
+    M sampleIndex = 0;
     const bool pow2 = zp.log2spp & 1;
     const uint32_t dmix = 0x55555555u * dimension;
+    constexpr int kBits = 8 * (int)sizeof(M);
     for (int i = iHi; i >= iLo; --i) {
         const int shift = 2 * i - (pow2 ? 1 : 0);
-        const uint32_t digit = (morton >> shift) & 3u;
-        const uint32_t higher = shift + 2 >= 32 ? 0u : morton >> (shift + 2);
-        uint32_t hi, lo;
-        mix_hi40(higher ^ dmix, &hi, &lo);
-        // (MixBits(..) >> 24) % 24 from 32-bit pieces: 2^32 = 16 (mod 24)
-        const uint32_t p = (hi * 16u + lo % 24u) % 24u;
-        const uint64_t w = p < 8 ? kZPermW0 : (p < 16 ? kZPermW1 : kZPermW2);
-        const uint32_t nd = (uint32_t)(w >> ((p & 7) * 8 + 2 * digit)) & 3u;
-        sampleIndex |= nd << shift;
+        const uint32_t digit = (uint32_t)(morton >> shift) & 3u;
+        const M higher = shift + 2 >= kBits ? M(0) : M(morton >> (shift + 2));
+        const uint32_t p = mix_perm24<M>((M)(higher ^ (M)dmix));
+        sampleIndex |= (M)zperm(p, digit) << shift;
     }
     return sampleIndex;
 }
@@ -145,20 +151,30 @@ AVR_HD uint32_t zsobol_digits(uint32_t morton, uint32_t dimension, const ZSobolP
 AVR_HD int zsobol_split(const ZSobolParams &zp) { return (zp.log2spp + (zp.log2spp & 1)) / 2; }
 
 // The digits that depend on the pixel only (not on the sample index): a function of
-// (Morton(pixel), dimension), shared by every sample of the pixel.
-AVR_HD uint32_t zsobol_upper(uint32_t morton, uint32_t dimension, const ZSobolParams &zp) {
-    return zsobol_digits(morton, dimension, zp, zp.nBase4Digits - 1, zsobol_split(zp));
+// (Morton(pixel), dimension), shared by every sample of the pixel. Returned shifted down by
+// log2(spp) (the lowest of them sits at bit log2spp), so it fits 32 bits for any resolution
+// up to 65536^2; pm = Morton(pixel).
+AVR_HD uint32_t zsobol_upper(uint32_t pm, uint32_t dimension, const ZSobolParams &zp) {
+    if (zsobol_wide(zp)) {
+        const uint64_t m = (uint64_t)pm << zp.log2spp;
+        return (uint32_t)(zsobol_digits<uint64_t>(m, dimension, zp, zp.nBase4Digits - 1, zsobol_split(zp)) >>
+                          zp.log2spp);
+    }
+    const uint32_t m = pm << zp.log2spp;
+    return zsobol_digits<uint32_t>(m, dimension, zp, zp.nBase4Digits - 1, zsobol_split(zp)) >> zp.log2spp;
 }
 
 // The remaining digits and the final base-2 digit of an odd log2(spp)
-AVR_HD uint32_t zsobol_lower(uint32_t morton, uint32_t dimension, const ZSobolParams &zp) {
+template <typename M>
+AVR_HD uint32_t zsobol_lower(M morton, uint32_t dimension, const ZSobolParams &zp) {
     const bool pow2 = zp.log2spp & 1;
-    uint32_t sampleIndex = zsobol_digits(morton, dimension, zp, zsobol_split(zp) - 1, pow2 ? 1 : 0);
+    uint32_t sampleIndex = (uint32_t)zsobol_digits<M>(morton, dimension, zp, zsobol_split(zp) - 1, pow2 ? 1 : 0);
     if (pow2) {
         const uint32_t dmix = 0x55555555u * dimension;
-        const uint32_t digit = morton & 1u;
-        const uint32_t x = (morton >> 1) ^ dmix;
-        uint64_t v = (uint64_t)(x ^ (x >> 31));
+        const uint32_t digit = (uint32_t)morton & 1u;
+        const M x = (M)(morton >> 1) ^ (M)dmix;
+        uint64_t v = (uint64_t)x;
+        v ^= v >> 31;
         v *= 0x7fb5d329728ea185ull;
         v ^= v >> 27;
         v *= 0x81dadef4bc2dd44dull;
@@ -168,35 +184,61 @@ AVR_HD uint32_t zsobol_lower(uint32_t morton, uint32_t dimension, const ZSobolPa
     return sampleIndex;
 }
 
-AVR_HD uint32_t zsobol_index(uint32_t morton, uint32_t dimension, const ZSobolParams &zp) {
+// GetSampleIndex of (morton, dimension): upper digits from the table when present
+template <typename M>
+AVR_HD M zsobol_index(M morton, uint32_t dimension, const ZSobolParams &zp) {
     uint32_t up;
+    const uint32_t pm = (uint32_t)(morton >> zp.log2spp);
     if (zp.upper && (int)dimension < zp.dmax)
-        up = zp.upper[(size_t)(morton >> zp.log2spp) * (size_t)zp.dmax + dimension];
+        up = zp.upper[(size_t)pm * (size_t)zp.dmax + dimension];
     else
-        up = zsobol_upper(morton, dimension, zp);
-    return up | zsobol_lower(morton, dimension, zp);
+        up = zsobol_upper(pm, dimension, zp);
+    return ((M)up << zp.log2spp) | (M)zsobol_lower<M>(morton, dimension, zp);
 }
 
-// ZSobolSampler state of one pixel sample
+// SobolSample bits (lowdiscrepancy.h:168-180) of a 64-bit index: dimension 0's columns
+// 32..51 are zero; dimension 1's repeat columns 0..19 (the Pascal matrix mod 2 has period
+// 32 in 32 bits; sobolmatrices.cpp rows 0 and 1), so its bits XOR over the two halves.
+AVR_HD uint32_t sobol_bits64(uint32_t lo, uint32_t hi, int dim) {
+    return dim == 0 ? sobol_bits(lo, 0) : (sobol_bits(lo, 1) ^ sobol_bits(hi, 1));
+}
+
+// ZSobolSampler state of one pixel sample: the Morton index with the sample index appended
+// (hi = its upper 32 bits, zero unless zsobol_wide) and the dimension
 struct ZSobol {
     uint32_t morton;
+    uint32_t hi;
     uint32_t dimension;
     AVR_HD void start(int px, int py, int sampleIndex, const ZSobolParams &zp) {
-        morton = ((uint32_t)encode_morton2((uint32_t)px, (uint32_t)py) << zp.log2spp) | (uint32_t)sampleIndex;
+        const uint64_t m = (encode_morton2((uint32_t)px, (uint32_t)py) << zp.log2spp) | (uint64_t)(uint32_t)sampleIndex;
+        morton = (uint32_t)m;
+        hi = (uint32_t)(m >> 32);
         dimension = 0;
     }
+    AVR_HD void index(const ZSobolParams &zp, uint32_t *alo, uint32_t *ahi) const {
+        if (zsobol_wide(zp)) {
+            const uint64_t a = zsobol_index<uint64_t>(((uint64_t)hi << 32) | morton, dimension, zp);
+            *alo = (uint32_t)a;
+            *ahi = (uint32_t)(a >> 32);
+        } else {
+            *alo = zsobol_index<uint32_t>(morton, dimension, zp);
+            *ahi = 0;
+        }
+    }
     AVR_HD float get1d(const ZSobolParams &zp) {
-        const uint32_t a = zsobol_index(morton, dimension, zp);
+        uint32_t a, ah;
+        index(zp, &a, &ah);   // dimension 0 reads the low 32 bits only
         ++dimension;
         const uint32_t h = (uint32_t)hash_2u32(dimension, (uint32_t)zp.seed);
         return u32_to_unit(fast_owen(sobol_bits(a, 0), h));
     }
     AVR_HD void get2d(const ZSobolParams &zp, float *u0, float *u1) {
-        const uint32_t a = zsobol_index(morton, dimension, zp);
+        uint32_t a, ah;
+        index(zp, &a, &ah);
         dimension += 2;
         const uint64_t h = hash_2u32(dimension, (uint32_t)zp.seed);
         *u0 = u32_to_unit(fast_owen(sobol_bits(a, 0), (uint32_t)h));
-        *u1 = u32_to_unit(fast_owen(sobol_bits(a, 1), (uint32_t)(h >> 32)));
+        *u1 = u32_to_unit(fast_owen(sobol_bits64(a, ah, 1), (uint32_t)(h >> 32)));
     }
 };
 

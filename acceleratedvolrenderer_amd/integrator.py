@@ -1,7 +1,7 @@
 """VolPathIntegrator on MI355X — the host-side mirror of pbrt-v4's integrator plugin.
 
 pbrt: `Integrator::Create("volpath" | "volpathcustom", ...)` (cpu/integrators.cpp:3658-3709,
-graph/volpath_custom.cpp:736-749) builds a VolPathIntegrator(maxdepth=5, lightsampler="bvh")
+src/graph/volpath_custom.cpp:736-749) builds a VolPathIntegrator(maxdepth=5, lightsampler="bvh")
 whose Render() walks pixel samples (integrators.cpp:72-232). Here Render() drives the
 HIP wavefront through the C-ABI (include/avr.h). Parameter names and defaults follow
 pbrt: maxdepth 5, IndependentSampler seed 0 (pbrt's `--seed`), `--maxdepth` override as
@@ -77,15 +77,29 @@ class VolPathIntegrator:
         self.ctx.set_grid_layout(1 if grid_layout == "fat" else 0)
         self.ctx.set_scene(scene)
 
+    @staticmethod
+    def create_params(name, params, maxdepth_override=None):
+        """Constructor arguments of Integrator::Create(name, parameters) for the volumetric
+        integrators (cpu/integrators.cpp:3658-3709). "volpath": maxdepth from the scene file
+        (default 5), lightsampler, regularize (VolPathIntegrator::Create,
+        integrators.cpp:1408-1418); the command-line --maxdepth does not reach it. The fork's
+        "volpathcustom" (src/graph/volpath_custom.cpp:736-749) takes the --maxdepth option
+        whenever it is given (a std::optional: 0 counts) over the file's value;
+        "volpath_mi355x" (this library's registration) behaves like it.
+        pixelsamples and seed are the sampler's. Unknown names raise as pbrt's ErrorExit."""
+        if name not in INTEGRATOR_NAMES:
+            raise ValueError(f"{name}: integrator type unknown.")
+        maxdepth = int(params.get("maxdepth", 5))
+        if maxdepth_override is not None and name != "volpath":
+            maxdepth = int(maxdepth_override)
+        return dict(maxdepth=maxdepth, spp=int(params.get("pixelsamples", 16)), seed=int(params.get("seed", 0)),
+                    lightsampler=params.get("lightsampler", "bvh"), regularize=bool(params.get("regularize", False)),
+                    name=name)
+
     @classmethod
-    def create(cls, name, params, scene, device=0, maxdepth_override=None):
+    def create(cls, name, params, scene, device=0, maxdepth_override=None, **kw):
         """Integrator::Create-style factory from a pbrt ParameterDictionary-like dict."""
-        maxdepth = params.get("maxdepth", 5)
-        if maxdepth_override is not None:
-            maxdepth = maxdepth_override
-        return cls(scene, maxdepth=maxdepth, spp=params.get("pixelsamples", 16), seed=params.get("seed", 0),
-                   device=device, lightsampler=params.get("lightsampler", "bvh"),
-                   regularize=params.get("regularize", False), name=name)
+        return cls(scene, device=device, **cls.create_params(name, params, maxdepth_override), **kw)
 
     def render(self, spp_begin=0, spp_end=None, clear=True):
         """Render sample indices [spp_begin, spp_end); returns (rgb_sum, w_sum) fp64."""

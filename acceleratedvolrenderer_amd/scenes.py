@@ -116,3 +116,60 @@ def s_cloud_vdb(density, width=1280, height=720, fov=45.0, sampler="independent"
     grid = density if isinstance(density, NanoVDBGrid) else vdb_grid(density)
     base = s_cloud(np.zeros((1, 1, 1), np.float32), width, height, fov, sampler, spp, filter)
     return Scene(base.camera, base.film, cloud_vdb_medium(grid), base.lights, sampler=base.sampler)
+
+
+def explosion_vdb(n=1024, radius=0.36, t_max=3000.0, seed=7):
+    """Synthetic stand-in for BASELINE config C5's emissive explosion (1024^3 NanoVDB; the
+    asset is absent): density and temperature NanoVDBGrids over an n^3 index extent (index i
+    at world i / n), leaves only inside a sphere of `radius` (world units) around the centre.
+    Radial profiles with a deterministic per-leaf perturbation:
+      density     = clamp(1.2 (1 - r/R) + 0.15 w, 0, 1)
+      temperature = t_max (1 - r/R)^2 (1 + 0.1 w)   (K, > 100 K only well inside)
+    where w in [-1, 1) is hashed from the leaf origin. Built leaf-vectorised on the host:
+    (4/3) pi (R n / 8)^3 leaves (~390k, 0.8 GB per grid at n = 1024)."""
+    nb = n // 8
+    R = radius * n
+    c = n / 2.0
+    bz, by, bx = np.meshgrid(np.arange(nb), np.arange(nb), np.arange(nb), indexing="ij")
+    org = np.stack([bx.ravel(), by.ravel(), bz.ravel()], 1).astype(np.int64) * 8
+    centre = org + 4.0
+    keep = np.sqrt(((centre - c) ** 2).sum(1)) < R + 8.0
+    org = org[keep]
+    del bx, by, bz, centre
+    h = (org[:, 0] * 73856093) ^ (org[:, 1] * 19349663) ^ (org[:, 2] * 83492791) ^ seed
+    w = ((h % 2000) / 1000.0 - 1.0).astype(np.float32)[:, None, None, None]
+    l = np.arange(8, dtype=np.float32)
+    # leaf values x-major [x][y][z]
+    lx, ly, lz = np.meshgrid(l, l, l, indexing="ij")
+    dens = np.empty((len(org), 8, 8, 8), np.float32)
+    temp = np.empty((len(org), 8, 8, 8), np.float32)
+    step = 65536
+    for i in range(0, len(org), step):
+        o = org[i:i + step].astype(np.float32)
+        dx = o[:, 0, None, None, None] + lx - np.float32(c)
+        dy = o[:, 1, None, None, None] + ly - np.float32(c)
+        dz = o[:, 2, None, None, None] + lz - np.float32(c)
+        q = np.maximum(np.float32(0), np.float32(1) - np.sqrt(dx * dx + dy * dy + dz * dz) / np.float32(R))
+        ww = w[i:i + step]
+        dens[i:i + step] = np.clip(np.float32(1.2) * q + np.float32(0.15) * ww * (q > 0), 0, 1)
+        temp[i:i + step] = np.float32(t_max) * q * q * (np.float32(1) + np.float32(0.1) * ww)
+    m = np.eye(4)
+    m[0, 0] = m[1, 1] = m[2, 2] = 1.0 / n
+    bb = np.array([0, 0, 0, n - 1, n - 1, n - 1], np.int32)
+    org32 = org.astype(np.int32)
+    return (NanoVDBGrid(org32, dens, 0.0, index_bbox=bb, index_to_world=m),
+            NanoVDBGrid(org32, temp, 0.0, index_bbox=bb, index_to_world=m))
+
+
+def s_explosion(density, temperature, width=1280, height=720, sampler="zsobol", spp=256, nbuckets=16,
+                Lescale=1.0, **medium):
+    """C5 stand-in scene: an emissive NanoVDBMedium (density + temperature grids) seen by a
+    perspective camera on a SpectralFilm (C5 is spectral), a dim sky for scattered light."""
+    from .scene import SpectralFilm
+    med = NanoVDBMedium(density, temperature=temperature, sigma_a=medium.pop("sigma_a", 1.0),
+                        sigma_s=medium.pop("sigma_s", 1.0), scale=medium.pop("scale", 4.0),
+                        g=medium.pop("g", 0.2), Lescale=Lescale, **medium)
+    cam = PerspectiveCamera(fov=45.0, pos=(0.5, 0.5, -0.9), look=(0.5, 0.5, 0.5), up=(0.0, 1.0, 0.0))
+    film = SpectralFilm(width, height, nbuckets=nbuckets, filter=GaussianFilter())
+    smp = ZSobolSampler(spp) if sampler == "zsobol" else IndependentSampler(spp)
+    return Scene(cam, film, med, [UniformInfiniteLight(scale=0.05)], sampler=smp)

@@ -1,21 +1,33 @@
 """Benchmark: Msamples/s of the MI355X volumetric path integrator on the BASELINE.json
 metric workload ("disney-cloud 720p" -> synthetic S-cloud-1024):
 GridMedium 1024^3 f32 (4 GiB) filled on device with CloudMedium::Density, perspective
-1280x720, VolPath maxdepth 100, IndependentSampler seed 0.
+1280x720, VolPath maxdepth 100, ZSobol sampler + Gaussian filter (pbrt's defaults).
 
 A step = one render pass of --spp-per-step sample indices over every pixel (the hot path:
 camera rays -> delta tracking -> ratio-tracked shadow rays -> film). Each rank renders
 its own disjoint sample indices (weak scaling); the fp64 film is SUM-reduced over RCCL
 once at the end of the timed region (T_render ends at the film reduce).
 
-Prints ONE JSON line (rank 0) with roofline (k_paths, the fused delta-tracking /
-ratio-tracking / density-fetch kernel; HIP-event time of its launches on the context stream)
-and cpu_baseline (the oracle restatement on a bounded sample of the same workload).
+`--gpus N` without a launcher starts N rank processes itself (torch.distributed.run as a
+child, acceleratedvolrenderer_amd/launch.py); under a launcher WORLD_SIZE must equal N.
+
+Prints ONE JSON line (rank 0) with
+  * roofline: k_paths (the fused delta-tracking / ratio-tracking / density-fetch kernel),
+    algorithmic bytes per launch / its HIP-event time on the context stream, against the
+    HBM peak; `traffic` and the `limiter` block come from rocprofv3 PMC passes that this
+    script runs as child processes on the same configuration (N=1, --pmc auto);
+  * cpu_baseline: the oracle restatement (`port`) on a bounded sample of the same
+    workload, on every host core this process may use (affinity and cgroup quota).
 """
 import argparse
+import csv
+import glob
 import json
 import os
+import shutil
+import subprocess
 import sys
+import tempfile
 import time
 
 import numpy as np
@@ -24,10 +36,16 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+VALU_SIMDS = 1024       # 256 CUs x 4 SIMDs; a wave64 VALU op issues in 2 cycles (MI355X_MICROARCH.md)
 # SURVEY.md §8d algorithmic bytes: 32 B per trilinear lookup (8 taps x 4 B) and 132 B per
 # work item read / written (ray 24, tMax 4, lambda+pdf 32, beta/r_u/r_l 48, RNG 16, pixel/depth 8).
 BYTES_PER_LOOKUP = 32
 BYTES_PER_ITEM = 132
+BYTES_PER_SAMPLE_RECORD = 32   # k_paths' per-sample record (L, lambda) read later by k_film
+# rocprofv3 passes (one run each; at most 8 SQ, 4 TCC (FETCH_SIZE 3, WRITE_SIZE 2), 2 GRBM)
+PMC_PASSES = (("fetch", ("FETCH_SIZE",)), ("write", ("WRITE_SIZE",)),
+              ("sq", ("SQ_INSTS_VALU", "SQ_WAVE_CYCLES", "SQ_ACTIVE_INST_ANY", "SQ_WAIT_INST_ANY", "SQ_WAIT_ANY",
+                      "SQ_WAVES", "GRBM_GUI_ACTIVE")))
 
 
 def parse():
@@ -42,6 +60,8 @@ def parse():
     p.add_argument("--max-paths", type=int, default=0)
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU-baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--pmc", default="auto", choices=["auto", "on", "off"],
+                   help="rocprofv3 counter passes for traffic / VALU (auto: at N=1 when rocprofv3 exists)")
     p.add_argument("--kernel", default="persistent", choices=["persistent", "wavefront"])
     p.add_argument("--medium", default="grid", choices=["grid", "nanovdb"],
                    help="S-cloud as GridMedium (default) or as a NanoVDBMedium tree (disney-cloud's type)")
@@ -54,6 +74,7 @@ def parse():
                    help="pixel sampler (BASELINE.md S-cloud: zsobol, pbrt's default)")
     p.add_argument("--filter", default="gaussian", choices=["gaussian", "box"],
                    help="pixel filter (pbrt's default: gaussian radius 1.5, sigma 0.5)")
+    p.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     return p.parse_args()
 
 
@@ -62,23 +83,62 @@ def log(msg):
     print(f"[bench] {msg}", file=sys.stderr, flush=True)
 
 
+def host_cpu_info():
+    """Host cores this process may use: the affinity mask, capped by a cgroup CPU quota."""
+    info = {"nproc": os.cpu_count() or 1}
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = info["nproc"]
+    info["affinity"] = aff
+    quota = None
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            q, per = open(path).read().split()[:2]
+            if q != "max":
+                quota = max(1, int(int(q) // int(per)))
+        except (OSError, ValueError):
+            pass
+    if quota is None:
+        try:
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                quota = max(1, q // per)
+        except (OSError, ValueError):
+            pass
+    info["cgroup_quota_cpus"] = quota
+    info["used"] = min(aff, quota) if quota else aff
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.lower().startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    info["model"] = model
+    return info
+
+
 def cpu_baseline(scene_host, spp_per_step, budget_s, label="S-cloud"):
     """Time the CPU oracle (pbrt VolPath restatement, `port`) on a bounded sample of the
-    SAME workload: a strided pixel subset across the whole 1280x720 frame, spp_per_step
-    samples each, on the host cores this process may use."""
+    SAME workload: a strided pixel subset across the whole frame, spp_per_step samples
+    each, threaded over every host core this process may use (the reference's ParallelFor
+    over AvailableCores(), util/parallel.cpp:307-332)."""
     from oracle import binding
-    cores = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
-    cores = max(1, min(cores, 16, os.cpu_count() or 1))
+    info = host_cpu_info()
+    cores = info["used"]
     log(f"cpu baseline: building the oracle scene ({label})")
     run = binding.OracleRun(scene_host, max_depth=100, seed=0)
-    log(f"cpu baseline: timing {budget_s:.0f} s on {cores} threads")
+    log(f"cpu baseline: timing {budget_s:.0f} s on {cores} threads ({info['model']})")
     f = scene_host.film
     npix = f.width * f.height
     # a strided pixel subset that spans every row/column band of the frame; samples are
     # taken in sampleIndex order, sweep after sweep, until the time budget is used
     stride = 61
     order = np.arange(0, npix, stride, dtype=np.int32)
-    chunk = 512
+    chunk = max(512, 32 * cores)   # enough pixels per call to keep every thread busy
     done_s = 0
     swept_spp = 0
     t0 = time.perf_counter()
@@ -91,21 +151,66 @@ def cpu_baseline(scene_host, spp_per_step, budget_s, label="S-cloud"):
                 break
         swept_spp += spp_per_step
     t_used = time.perf_counter() - t0
-    done_px = len(order)
     return {"value": done_s / t_used / 1e6, "unit": "Msamples/s", "cores": cores, "kind": "port",
-            "sample": f"{done_s} samples: pixels every {stride}th of {f.width}x{f.height} ({done_px} px), "
+            "host": info,
+            "sample": f"{done_s} samples: pixels every {stride}th of {f.width}x{f.height} ({len(order)} px), "
                       f"sample indices from 0 in sweeps of {spp_per_step}, same {label} "
                       f"scene, {t_used:.1f} s on {cores} threads"}
 
 
+def pmc_passes(args, kernel_substr="k_paths", timeout_s=240):
+    """rocprofv3 counter passes of this same bench configuration, one child process per
+    pass (--pmc only: no tracing in the same run), each killed after timeout_s. Returns
+    per-launch averages of the dominant kernel's counters, or None."""
+    exe = shutil.which("rocprofv3")
+    if exe is None:
+        return None, "rocprofv3 not found"
+    child = [sys.executable, os.path.join(ROOT, "bench.py"), "--pmc-child", "--no-cpu-baseline", "--pmc", "off",
+             "--steps", "2", "--warmup", "1"]
+    for k in ("res", "width", "height", "spp_per_step", "max_paths", "kernel", "medium", "refill_min", "grid_layout",
+              "dda_budget", "zsobol_table", "sampler", "filter"):
+        child += [f"--{k.replace('_', '-')}", str(getattr(args, k))]
+    out = {}
+    tmp = tempfile.mkdtemp(prefix="avr_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
+    try:
+        for name, counters in PMC_PASSES:
+            d = os.path.join(tmp, name)
+            cmd = [exe, "--pmc", *counters, "-d", d, "-o", "run", "--output-format", "csv", "--"] + child
+            log(f"pmc pass {name}: {' '.join(counters)}")
+            try:
+                r = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, timeout=timeout_s)
+            except subprocess.TimeoutExpired:
+                return None, f"pmc pass {name} timed out"
+            if r.returncode != 0:
+                return None, f"pmc pass {name} exited {r.returncode}: {r.stderr.decode(errors='replace')[-300:]}"
+            files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+            if not files:
+                return None, f"pmc pass {name}: no counter file"
+            per = {}
+            for fn in files:
+                for row in csv.DictReader(open(fn)):
+                    if kernel_substr in row["Kernel_Name"]:
+                        per.setdefault(row["Counter_Name"], {}).setdefault(row.get("Dispatch_Id", ""), 0.0)
+                        per[row["Counter_Name"]][row.get("Dispatch_Id", "")] += float(row["Counter_Value"])
+            for cn, disp in per.items():
+                # the child's first launch is its warmup; average the timed launches
+                vals = [disp[k] for k in sorted(disp, key=lambda x: int(x) if x.isdigit() else 0)]
+                vals = vals[1:] if len(vals) > 1 else vals
+                out[cn] = sum(vals) / len(vals)
+        return out, None
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+
+
 def main():
     args = parse()
+    from acceleratedvolrenderer_amd import launch
+    # one process per GPU: start the N ranks before anything touches a GPU
+    launch.ensure_world(args.gpus, os.path.abspath(__file__), sys.argv[1:])
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    world, rank, local_rank = launch.world_from_env()
     if world > 1:
         dist.init_process_group("nccl", init_method="env://")
     torch.cuda.set_device(local_rank)
@@ -205,35 +310,36 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{dev}")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    if args.pmc_child:
+        integ.close()
+        return
 
     samples = npix * S * args.steps * world
     value = samples / elapsed / 1e6
     # roofline of the dominant kernel: algorithmic bytes / summed device time of its launches
     med_s = agg["ms_medium"] / 1e3
     launches = max(1, agg["medium_launches"])
-    if args.kernel == "persistent":
+    persistent = bool(agg.get("loop_iterations"))   # k_paths counts its wave loop iterations
+    if persistent:
         # k_paths fuses delta tracking and ratio tracking: 32 B per trilinear lookup (both kinds)
-        # + the 32 B per-sample record (L, lambda) it writes; path state never leaves VGPRs.
+        # + the 32 B per-sample record it writes; path state never leaves VGPRs.
         kname = "k_paths (persistent: delta + ratio tracking, density fetch)"
-        med_bytes = BYTES_PER_LOOKUP * (agg["medium_lookups"] + agg["shadow_lookups"]) + 32 * agg["medium_items_in"]
+        med_bytes = (BYTES_PER_LOOKUP * (agg["medium_lookups"] + agg["shadow_lookups"]) +
+                     BYTES_PER_SAMPLE_RECORD * agg["medium_items_in"])
     else:
         kname = "k_medium (wavefront delta tracking + density fetch)"
         med_bytes = BYTES_PER_LOOKUP * agg["medium_lookups"] + BYTES_PER_ITEM * (agg["medium_items_in"] +
                                                                                 agg["medium_items_out"])
     achieved = med_bytes / med_s / 1e9 if med_s > 0 else 0.0
-    # HBM traffic per launch from the committed rocprofv3 PMC passes of this kernel on this
-    # workload (FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md HBM section); bench.py
-    # itself cannot read counters. Null when the profile does not match the run.
-    traffic, traffic_src, valu = None, None, None
-    prof = os.path.join(ROOT, "profiles", f"r01_pmc_k_paths_{args.sampler}_{args.filter}.json")
-    if args.kernel == "persistent" and args.medium == "grid" and n == 1024 and S == 16 and os.path.exists(prof):
-        pm = json.load(open(prof))
-        traffic = round(pm["hbm_traffic_bytes_per_launch"] / 1e9, 3)
-        traffic_src = os.path.relpath(prof, ROOT) + " (GB per launch, PMC FETCH_SIZE x2 + WRITE_SIZE)"
-        # the bound that is actually close: VALU issue (wave64 op = 2 SIMD cycles)
-        valu = {"wave_instructions_per_launch": pm["valu_wave_instructions_per_launch"],
-                "issue_fraction": round(pm["valu_issue_fraction"], 4),
-                "wave_cycle_split": pm["wave_cycle_split"], "source": os.path.relpath(prof, ROOT)}
+    avg_launch_ms = agg["ms_medium"] / launches
+    grid_layout = "fat" if integ.ctx.grid_layout_active() else "linear"
+    host_density = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and vdb is None:
+        host_density = density.cpu().numpy()
+    integ.close()
+    del density
+    torch.cuda.empty_cache()
+
     out = None
     if rank == 0:
         cpu = None
@@ -241,10 +347,40 @@ def main():
             if vdb is not None:
                 host_scene = scene
             else:
-                host_density = density.cpu().numpy()
                 host_scene = scenes.s_cloud(host_density, width=args.width, height=args.height,
                                             sampler=args.sampler, spp=spp_total, filter=args.filter)
             cpu = cpu_baseline(host_scene, S, args.cpu_seconds, f"S-cloud-{n} {args.medium}")
+            host_scene = host_density = None
+        # HBM traffic and the VALU limiter from rocprofv3 counter passes of this same
+        # configuration (child processes; the guide's gfx950 rule: FETCH_SIZE x2 + WRITE_SIZE)
+        traffic, limiter, pmc_note = None, None, "pmc off"
+        want_pmc = args.pmc == "on" or (args.pmc == "auto" and world == 1)
+        if want_pmc and persistent:
+            ctr, err = pmc_passes(args)
+            if ctr is None:
+                pmc_note = err
+                log(f"pmc: {err}")
+            else:
+                pmc_note = "rocprofv3 --pmc child passes of this configuration (bench.py pmc_passes)"
+                if "FETCH_SIZE" in ctr and "WRITE_SIZE" in ctr:
+                    traffic = round((2 * ctr["FETCH_SIZE"] + ctr["WRITE_SIZE"]) * 1024 / 1e9, 4)
+                if "SQ_INSTS_VALU" in ctr and "SQ_WAVE_CYCLES" in ctr:
+                    # effective clock from GRBM_GUI_ACTIVE (summed over 8 XCDs) over the launch time
+                    clk = (ctr["GRBM_GUI_ACTIVE"] / 8 / (avg_launch_ms / 1e3)) if ctr.get("GRBM_GUI_ACTIVE") else 2.4e9
+                    valu_frac = ctr["SQ_INSTS_VALU"] * 2 / (VALU_SIMDS * clk * avg_launch_ms / 1e3)
+                    wc = ctr["SQ_WAVE_CYCLES"]
+                    limiter = {
+                        "kind": "valu-issue + dependent-chain latency" if valu_frac > 4 * achieved / HBM_PEAK_GBPS
+                        else "hbm",
+                        "valu_issue_frac": round(valu_frac, 4),
+                        "valu_wave_insts_per_launch": ctr["SQ_INSTS_VALU"],
+                        "valu_wave_insts_per_sample": round(ctr["SQ_INSTS_VALU"] / (npix * S), 1),
+                        "effective_clock_ghz": round(clk / 1e9, 3),
+                        "waves": ctr.get("SQ_WAVES"),
+                        "wave_cycle_split": {"issuing": round(ctr["SQ_ACTIVE_INST_ANY"] / wc, 4),
+                                             "dependency/issue stall": round(ctr["SQ_WAIT_INST_ANY"] / wc, 4),
+                                             "s_waitcnt (memory/LDS)": round(ctr["SQ_WAIT_ANY"] / wc, 4)},
+                    }
         out = {
             "metric": "Msamples/s (whole node) on synthetic S-cloud-1024 720p (disney-cloud stand-in)",
             "value": round(value, 4),
@@ -265,19 +401,21 @@ def main():
                        "sample_index_wrap": wrap},
             "roofline": {
                 "kernel": kname,
+                # the roof this kernel is priced against (no MFMA work on the path); the
+                # counters' verdict on what actually limits it is `limiter`
                 "bound": "hbm",
                 "achieved": round(achieved, 2),
                 "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBPS, 5),
                 "traffic": traffic,
-                "traffic_source": traffic_src,
+                "traffic_source": pmc_note,
                 "bytes_per_launch": med_bytes / launches,
-                "avg_launch_ms": agg["ms_medium"] / launches,
+                "avg_launch_ms": avg_launch_ms,
                 "launches": launches,
+                "limiter": limiter,
             },
-            "valu": valu,
-            "grid_layout": "fat" if integ.ctx.grid_layout_active() else "linear",
+            "grid_layout": grid_layout,
             "simd_utilisation": (agg["active_lane_iterations"] / (64.0 * agg["loop_iterations"])
                                  if agg.get("loop_iterations") else None),
             "cpu_baseline": cpu,
@@ -289,12 +427,13 @@ def main():
                 "shadow_lookups": agg["shadow_lookups"], "medium_items_in": agg["medium_items_in"],
                 "loop_iterations": agg.get("loop_iterations"), "medium_dda_steps": agg["medium_dda_steps"],
                 "medium_items_out": agg["medium_items_out"], "shadow_items": agg["shadow_items"],
-                "shadow_achieved_GBps": round((BYTES_PER_LOOKUP * agg["shadow_lookups"] + BYTES_PER_ITEM *
-                                               agg["shadow_items"]) / max(1e-9, agg["ms_shadow"] / 1e3) / 1e9, 2),
+                # wavefront organisation only (k_paths has no separate shadow kernel)
+                "shadow_achieved_GBps": (round((BYTES_PER_LOOKUP * agg["shadow_lookups"] + BYTES_PER_ITEM *
+                                                agg["shadow_items"]) / (agg["ms_shadow"] / 1e3) / 1e9, 2)
+                                         if agg["ms_shadow"] > 0 else None),
             },
         }
         print(json.dumps(out), flush=True)
-    integ.close()
     if world > 1:
         dist.destroy_process_group()
 

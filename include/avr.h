@@ -56,7 +56,8 @@ typedef struct avr_stats {
 const char *avr_last_error(void);
 
 /* Context on HIP device `device` (one process per GPU; no implicit peer access).
- * `max_paths` bounds the paths in flight per wavefront pass (0 = default 16M). */
+ * `max_paths` bounds the paths in flight per pass (0 = default 16M; at most 2^31 - 1:
+ * path ids are 32-bit, AVR_ERR_ARG above). */
 int avr_context_create(int device, long long max_paths, avr_context **out);
 int avr_context_destroy(avr_context *ctx);
 /* Kernel organisation: 0 = persistent-wave megakernel k_paths (default: path state in
@@ -250,7 +251,9 @@ int avr_film_spectral_device_ptrs(avr_context *ctx, void **d_bucket_sums, void *
 /* In-process multi-GPU render (one context per GPU, e.g. avr_render(ctx_k, k*spp/N,
  * (k+1)*spp/N, ...)): SUM-reduce the n contexts' film sums (rgb, weights, SpectralFilm
  * buckets) into ctxs[root]'s film over RCCL (xGMI); the other films are left as they are.
- * Films must match in resolution and buckets; one context per device. */
+ * Films must match in resolution and buckets; one context per device. The communicators
+ * are created on the first reduce of a context list (ncclCommInitAll) and cached on the
+ * contexts for later reduces of the same list; avr_context_destroy releases them. */
 int avr_film_reduce_rccl(avr_context **ctxs, int n, int root);
 /* Device pointers of the film sums (for an RCCL reduce across GPUs). */
 int avr_film_device_ptrs(avr_context *ctx, void **d_rgb_sum, void **d_w_sum);

@@ -385,7 +385,11 @@ int main(int argc, char **argv) {
                               {16, 1280, 720, 1279, 719, 15, 0}, {16, 1280, 720, 640, 360, 7, 7},
                               {1, 1280, 720, 100, 200, 0, 0},    {2, 1280, 720, 100, 200, 1, 0},
                               {8, 1280, 720, 33, 44, 5, 3},      {64, 1920, 1080, 1919, 1079, 63, 0},
-                              {256, 1280, 720, 321, 123, 200, 0}, {4, 32, 32, 31, 0, 2, 1}};
+                              {256, 1280, 720, 321, 123, 200, 0}, {4, 32, 32, 31, 0, 2, 1},
+                              // indices past 2^32 (config C5's 4096 spp at 720p and beyond)
+                              {4096, 1280, 720, 1279, 719, 4095, 0}, {4096, 1280, 720, 640, 360, 1234, 0},
+                              {8192, 1280, 720, 77, 700, 5000, 2}, {65536, 1920, 1080, 1500, 1000, 65535, 0},
+                              {4096, 1920, 1080, 3, 1079, 17, 5}};
         const char *pattern = "1212111111221112211122";
         int ci = 0;
         for (const Case &c : cases) {
@@ -406,8 +410,10 @@ int main(int argc, char **argv) {
         j.key("sobol_fastowen");
         printf("[");
         RNG rng(5, 9);
-        for (int i = 0; i < 64; ++i) {
+        for (int i = 0; i < 96; ++i) {
+            // 64 indices below 2^32, then 32 up to the 2^52 table limit (SobolMatrixSize 52)
             uint64_t a = i < 8 ? (uint64_t)i : (uint64_t)rng.Uniform<uint32_t>();
+            if (i >= 64) a |= ((uint64_t)rng.Uniform<uint32_t>() & 0xfffffu) << 32;
             uint32_t seed = rng.Uniform<uint32_t>();
             printf("%s[\"%llu\",%u,%u,%u,%u,%u]", i ? "," : "", (unsigned long long)a, seed,
                    fb(SobolSample(a, 0, FastOwenScrambler(seed))), fb(SobolSample(a, 1, FastOwenScrambler(seed))),

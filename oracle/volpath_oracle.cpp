@@ -835,13 +835,13 @@ namespace oracle {
 // Sobol' generator matrices of dimensions 0 and 1 (sobolmatrices.cpp, first two rows),
 // from their definition: dimension 0 is the van der Corput radical inverse (column i =
 // bit 31-i); dimension 1 is the Pascal matrix mod 2 (direction numbers of x + 1):
-// column i = column i-1 XOR (column i-1 >> 1). Columns >= 32 do not exist in 32 bits and
-// ZSobol indices stay below 2^32 (checked by the host).
+// column i = column i-1 XOR (column i-1 >> 1). The tables hold SobolMatrixSize = 52
+// columns (sobolmatrices.h:16): dimension 0's columns 32..51 are zero, dimension 1's
+// repeat columns 0..19 (the Pascal pattern has period 32 in 32 bits).
 static uint32_t SobolColumn(int dim, int i) {
-    if (i >= 32) return 0;
-    if (dim == 0) return 1u << (31 - i);
+    if (dim == 0) return i < 32 ? 1u << (31 - i) : 0u;
     uint32_t v = 0x80000000u;
-    for (int k = 1; k <= i; ++k) v ^= v >> 1;
+    for (int k = 1; k <= (i & 31); ++k) v ^= v >> 1;
     return v;
 }
 static uint32_t SobolBits(uint64_t a, int dim) {

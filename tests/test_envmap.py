@@ -132,3 +132,18 @@ def test_oracle_image_light_furnace(srgb_table):
     assert np.all(np.isfinite(r))
     m, sd = float(r.mean()), float(r.std() / np.sqrt(r.size))
     assert abs(m - 1) < 5 * sd + 1e-3, (m, sd)
+
+
+def test_srgb_subset_fixture_converts_the_envmap_like_the_full_table(srgb_table):
+    """tests/golden/srgb_table_subset.npz (what the GPU image-light test loads on the box,
+    where the reference sources are absent) gives the same coefficients as the full table
+    generated by the reference's rgb2spec_opt, for the test's environment map."""
+    import os
+    import sys
+    from acceleratedvolrenderer_amd import RGBToSpectrumTable
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "tests", "golden"))
+    from make_srgb_subset import envmap_image
+    sub = RGBToSpectrumTable.load(os.path.join(root, "tests", "golden", "srgb_table_subset.npz"))
+    img = envmap_image()
+    assert np.array_equal(sub.spectrum_coeffs(img).view(np.uint32), srgb_table.spectrum_coeffs(img).view(np.uint32))

@@ -149,3 +149,25 @@ def test_film_reduce_rccl_single_gpu():
         capi.film_reduce_rccl([a.ctx], root=1)
     a.close()
     b.close()
+
+
+def test_volpathcustom_maxdepth_override_renders_the_override_depth():
+    """a21: Integrator::Create("volpathcustom") with pbrt's --maxdepth (src/graph/
+    volpath_custom.cpp:736-749) renders exactly what maxdepth=<override> renders; the
+    scene file's maxdepth is ignored. Bit-identical films, and different from the file's."""
+    from acceleratedvolrenderer_amd import VolPathIntegrator
+    dens = np.full((4, 4, 4), 2.0, np.float32)
+    scene = _scene(8, 6, dens)
+    a = VolPathIntegrator.create("volpathcustom", {"maxdepth": 50, "pixelsamples": 8}, scene, device=0,
+                                 maxdepth_override=2)
+    assert a.maxdepth == 2
+    rgb_a, w_a = a.render()
+    b = VolPathIntegrator(scene, maxdepth=2, spp=8, device=0)
+    rgb_b, w_b = b.render()
+    c = VolPathIntegrator.create("volpath", {"maxdepth": 50, "pixelsamples": 8}, scene, device=0,
+                                 maxdepth_override=2)
+    rgb_c, _ = c.render()
+    assert np.array_equal(rgb_a, rgb_b) and np.array_equal(w_a, w_b)
+    assert not np.array_equal(rgb_a, rgb_c)
+    for x in (a, b, c):
+        x.close()

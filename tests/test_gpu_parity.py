@@ -623,18 +623,16 @@ def test_image_infinite_light_replay(with_distant, variant, kernel):
     accumulation over lights is exercised. Replay >= 99.9 % bit-identical vs the canonical
     oracle, film within noise of the platform oracle."""
     import os
+    import sys
     from acceleratedvolrenderer_amd import scenes, ImageInfiniteLight, DistantLight, RGBToSpectrumTable
     from acceleratedvolrenderer_amd.scene import Scene
     from oracle import binding
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    tab = os.path.join(root, "oracle", "_ref", "srgb_table.npz")
-    if not os.path.exists(tab):
-        pytest.skip("sRGB table not generated (tests/conftest.py srgb_table)")
-    table = RGBToSpectrumTable.load(tab)
-    res = 32
-    y, x = np.mgrid[0:res, 0:res] / res
-    img = np.stack([0.3 + 0.5 * x, 0.2 + 0.6 * y, 0.4 + 0.3 * x * y], 2).astype(np.float32)
-    img[5:8, 20:23] = [30, 25, 18]
+    # the cells of pbrt's sRGB table this image touches (tests/golden/make_srgb_subset.py)
+    table = RGBToSpectrumTable.load(os.path.join(root, "tests", "golden", "srgb_table_subset.npz"))
+    sys.path.insert(0, os.path.join(root, "tests", "golden"))
+    from make_srgb_subset import envmap_image
+    img = envmap_image()
     rot = np.eye(4)
     c, s = np.cos(0.7), np.sin(0.7)
     rot[:3, :3] = [[c, 0, s], [0, 1, 0], [-s, 0, c]]

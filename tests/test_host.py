@@ -127,3 +127,24 @@ def test_gbuffer_film_layout_for_volume_only_scenes(tmp_path):
     imageio.write_exr(p, img, channels=f.channel_names())
     back, names, _ = imageio.read_exr(p)
     assert sorted(names) == sorted(f.channel_names())
+
+
+def test_integrator_create_names_and_maxdepth_override():
+    """Integrator::Create (cpu/integrators.cpp:3658-3709): "volpath" takes maxdepth from the
+    scene file only (VolPathIntegrator::Create, 1408-1418); "volpathcustom"
+    (src/graph/volpath_custom.cpp:736-749) takes pbrt's --maxdepth whenever it is given,
+    0 included (a std::optional); unknown names fail like ErrorExit."""
+    import pytest
+    from acceleratedvolrenderer_amd import VolPathIntegrator
+    cp = VolPathIntegrator.create_params
+    assert cp("volpath", {})["maxdepth"] == 5
+    assert cp("volpath", {"maxdepth": 9}, maxdepth_override=3)["maxdepth"] == 9
+    assert cp("volpathcustom", {"maxdepth": 9})["maxdepth"] == 9
+    assert cp("volpathcustom", {"maxdepth": 9}, maxdepth_override=3)["maxdepth"] == 3
+    assert cp("volpathcustom", {"maxdepth": 9}, maxdepth_override=0)["maxdepth"] == 0
+    assert cp("volpath_mi355x", {}, maxdepth_override=7)["maxdepth"] == 7
+    p = cp("volpathcustom", {"pixelsamples": 64, "seed": 3, "lightsampler": "uniform", "regularize": True})
+    assert (p["spp"], p["seed"], p["lightsampler"], p["regularize"], p["name"]) == (64, 3, "uniform", True,
+                                                                                 "volpathcustom")
+    with pytest.raises(ValueError, match="integrator type unknown"):
+        cp("bdpt", {})

@@ -1,0 +1,48 @@
+"""bench.py's `--gpus N` launcher (acceleratedvolrenderer_amd/launch.py) on CPU with gloo:
+without a launcher environment it starts N ranks itself (torch.distributed.run as a child
+process), each rank renders its sample shard and the fp64 film is SUM-reduced to rank 0;
+under a launcher a world size different from --gpus is refused."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CHILD = os.path.join(ROOT, "tests", "launch_child.py")
+
+
+def _env():
+    e = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        e.pop(k, None)
+    e["OMP_NUM_THREADS"] = "1"
+    return e
+
+
+def _run(args, env):
+    r = subprocess.run([sys.executable, CHILD] + args, capture_output=True, text=True, env=env, timeout=240)
+    return r
+
+
+def test_launcher_starts_the_world_and_reduces_the_film():
+    one = _run(["--gpus", "1"], _env())
+    assert one.returncode == 0, one.stderr
+    ref = json.loads([x for x in one.stdout.splitlines() if x.startswith("{")][-1])
+    assert ref["n_gpus"] == 1
+    two = _run(["--gpus", "2"], _env())
+    assert two.returncode == 0, two.stderr[-2000:]
+    lines = [x for x in two.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1          # rank 0 only
+    got = json.loads(lines[0])
+    assert got["n_gpus"] == 2
+    assert got["w"] == ref["w"]     # every (pixel, sample) exactly once over the shards
+    for a, b in zip(got["rgb"], ref["rgb"]):
+        assert abs(a - b) <= 1e-12 * abs(b)
+
+
+def test_launcher_refuses_a_mismatched_world():
+    e = _env()
+    e.update({"WORLD_SIZE": "3", "RANK": "0", "LOCAL_RANK": "0"})
+    r = _run(["--gpus", "2"], e)
+    assert r.returncode != 0
+    assert "WORLD_SIZE=3" in r.stderr

@@ -25,19 +25,24 @@ def hdr(tmp_path_factory):
         "  ZSobolParams zp = zsobol_params(spp, rx, ry, seed); ZSobol z; z.start(px, py, s, zp);\n"
         "  for (; *pat; ++pat) { if (*pat == '1') *out++ = z.get1d(zp); else { z.get2d(zp, out, out + 1); out += 2; } }\n"
         "}\n"
-        "int zs_split(int spp, int rx, int ry, int dmax, int n, const int *q, unsigned *full, unsigned *tab) {\n"
+        "int zs_split(int spp, int rx, int ry, int dmax, int n, const int *q, unsigned long long *full,\n"
+        "             unsigned long long *tab) {\n"
         "  ZSobolParams zp = zsobol_params(spp, rx, ry, 0);\n"
         "  size_t rows = (size_t)encode_morton2(rx - 1, ry - 1) + 1;\n"
         "  unsigned *t = new unsigned[rows * dmax];\n"
         "  for (int y = 0; y < ry; ++y) for (int x = 0; x < rx; ++x) for (int d = 0; d < dmax; ++d) {\n"
-        "    unsigned pm = (unsigned)encode_morton2(x, y); t[(size_t)pm * dmax + d] = zsobol_upper(pm << zp.log2spp, d, zp); }\n"
+        "    unsigned pm = (unsigned)encode_morton2(x, y); t[(size_t)pm * dmax + d] = zsobol_upper(pm, d, zp); }\n"
         "  for (int i = 0; i < n; ++i) {\n"
-        "    unsigned m = ((unsigned)encode_morton2(q[4 * i], q[4 * i + 1]) << zp.log2spp) | (unsigned)q[4 * i + 2];\n"
-        "    full[i] = zsobol_index(m, q[4 * i + 3], zp);\n"
-        "    ZSobolParams zt = zp; zt.upper = t; zt.dmax = dmax; tab[i] = zsobol_index(m, q[4 * i + 3], zt); }\n"
+        "    unsigned long long m = (encode_morton2(q[4 * i], q[4 * i + 1]) << zp.log2spp) | (unsigned)q[4 * i + 2];\n"
+        "    ZSobolParams zt = zp; zt.upper = t; zt.dmax = dmax;\n"
+        "    if (zsobol_wide(zp)) { full[i] = zsobol_index<unsigned long long>(m, q[4 * i + 3], zp);\n"
+        "      tab[i] = zsobol_index<unsigned long long>(m, q[4 * i + 3], zt); }\n"
+        "    else { full[i] = zsobol_index<unsigned>((unsigned)m, q[4 * i + 3], zp);\n"
+        "      tab[i] = zsobol_index<unsigned>((unsigned)m, q[4 * i + 3], zt); } }\n"
         "  delete[] t; return zsobol_split(zp); }\n"
         "float sob(unsigned long long a, int dim, unsigned seed, int scr) {\n"
-        "  unsigned v = sobol_bits((unsigned)a, dim); return u32_to_unit(scr ? fast_owen(v, seed) : v); }\n"
+        "  unsigned v = sobol_bits64((unsigned)a, (unsigned)(a >> 32), dim);\n"
+        "  return u32_to_unit(scr ? fast_owen(v, seed) : v); }\n"
         "}\n")
     so = d / "shim.so"
     subprocess.check_call(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-shared", "-fPIC", str(src), "-o", str(so)])
@@ -61,23 +66,23 @@ def test_header_zsobol_streams_match_reference(hdr, golden):
 def test_header_sobol_bits_match_reference(hdr, golden):
     for a, seed, f0, f1, p0, p1 in golden["sobol_fastowen"]:
         a = int(a)
-        if a >= 1 << 32:
-            continue
         got = [hdr.sob(a, 0, seed, 1), hdr.sob(a, 1, seed, 1), hdr.sob(a, 0, 0, 0), hdr.sob(a, 1, 0, 0)]
         assert np.array(got, np.float32).view(np.uint32).tolist() == [f0, f1, p0, p1]
 
 
-@pytest.mark.parametrize("spp", [1, 2, 16, 128, 256])
-def test_zsobol_pixel_table_split(hdr, spp):
+@pytest.mark.parametrize("spp,rx,ry", [(1, 37, 21), (2, 37, 21), (16, 37, 21), (128, 37, 21), (256, 37, 21),
+                                        (4096, 1280, 720), (8192, 300, 200), (65536, 1100, 900)])
+def test_zsobol_pixel_table_split(hdr, spp, rx, ry):
     """GetSampleIndex = (pixel-only digits, tabulated per Morton(pixel) x dimension) | (sample
-    digits): identical to the untabulated index, including dimensions past the table."""
+    digits): identical to the untabulated index, including dimensions past the table, for
+    32-bit and (4096 spp at 720p and up) 64-bit indices."""
     rng = np.random.default_rng(spp)
-    rx, ry, dmax, n = 37, 21, 12, 4000
+    dmax, n = 12, 4000
     q = np.stack([rng.integers(0, rx, n), rng.integers(0, ry, n), rng.integers(0, spp, n),
                   rng.integers(0, 2 * dmax, n)], 1).astype(np.int32)
-    full = np.zeros(n, np.uint32)
-    tab = np.zeros(n, np.uint32)
-    U = ctypes.POINTER(ctypes.c_uint)
+    full = np.zeros(n, np.uint64)
+    tab = np.zeros(n, np.uint64)
+    U = ctypes.POINTER(ctypes.c_ulonglong)
     split = hdr.zs_split(spp, rx, ry, dmax, n, q.ctypes.data_as(ctypes.POINTER(ctypes.c_int)),
                          full.ctypes.data_as(U), tab.ctypes.data_as(U))
     assert np.array_equal(full, tab)
