@@ -100,15 +100,42 @@ def test_empty_sample_range_and_argument_errors():
     integ.close()
 
 
-def test_zsobol_index_range_is_checked():
-    """ZSobol's 32-bit device index: Morton(pixel) << log2(spp) | index must fit 2^32
-    (the device's ZSobol index); beyond it the call fails instead of aliasing."""
-    from acceleratedvolrenderer_amd import VolPathIntegrator, scenes, ZSobolSampler
+@pytest.mark.parametrize("kernel", ["persistent", "wavefront"])
+def test_zsobol_64bit_indices_replay_and_range_is_checked(kernel):
+    """ZSobol indices past 2^32 (Morton(pixel) << log2(spp) | index: 4096 spp on a film
+    whose rounded-up resolution is 2048 = 34 bits, config C5's regime) replay the oracle's
+    64-bit GetSampleIndex / SobolSample bit for bit, with and without the pixel table;
+    beyond SobolSample's 2^52 index range (sobolmatrices.h:16) the render fails instead of
+    aliasing."""
+    from acceleratedvolrenderer_amd import VolPathIntegrator, ZSobolSampler
     from acceleratedvolrenderer_amd.scene import Scene
-    base = _scene(4096, 1, np.ones((2, 2, 2), np.float32))
+    from oracle import binding
+    dens = (0.3 + np.random.default_rng(4).random((6, 6, 6), dtype=np.float32)).astype(np.float32)
+    base = _scene(1100, 3, dens)
     scene = Scene(base.camera, base.film, base.medium, base.lights, sampler=ZSobolSampler(1 << 12))
-    integ = VolPathIntegrator(scene, device=0, maxdepth=1, spp=1)
-    with pytest.raises(RuntimeError, match="2\\^32"):
+    canon = binding.OracleRun(scene, max_depth=5, seed=0, libm="canonical")
+    for dims in (256, 0):
+        integ = VolPathIntegrator(scene, device=0, maxdepth=5, spp=4096, kernel=kernel)
+        integ.ctx.set_sampler_table(dims)
+        integ.ctx.film_clear()
+        integ.ctx.render(4090, 4096, 0, 5)
+        npix = 1100 * 3
+        first, ns, L, lam, _ = integ.ctx.last_pass_samples(npix, 6)
+        assert (first, ns) == (4090, 6)
+        exact = 0
+        for s in range(ns):
+            for pix in range(0, npix, 7):
+                Lo, lo, _, _ = canon.pixel_sample(pix % 1100, pix // 1100, first + s)
+                g = s * npix + pix
+                exact += int(np.array_equal(L[g].view(np.uint32), Lo.view(np.uint32)) and
+                             np.array_equal(lam[g].view(np.uint32), lo.view(np.uint32)))
+        total = ns * len(range(0, npix, 7))
+        print(f"zsobol 64-bit ({kernel}, table {dims}): {exact}/{total} bit-identical")
+        assert exact / total >= 0.999
+        integ.close()
+    big = Scene(base.camera, _scene(40000, 1, dens).film, base.medium, base.lights, sampler=ZSobolSampler(1 << 21))
+    integ = VolPathIntegrator(big, device=0, maxdepth=1, spp=1, kernel=kernel)
+    with pytest.raises(RuntimeError, match="2\\^52"):
         integ.ctx.render(0, 1, 0, 1)
     integ.close()
 
