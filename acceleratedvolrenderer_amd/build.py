@@ -1,19 +1,32 @@
 """Build libavr_hip.so in-tree with hipcc for gfx950 (no JIT cache: the .so travels
-with the repository snapshot to the GPU box)."""
+with the repository snapshot to the GPU box).
+
+The persistent path kernel k_paths has 112 instantiations (medium kind x emission x gray
+state x sampler x image light x render mode); they are compiled as eight objects
+(csrc/avr_kpaths.hip, one per medium kind and render mode) in parallel with the C-ABI
+unit (csrc/avr_capi.hip, -DAVR_KP_SPLIT), then linked."""
 import os
 import subprocess
+from concurrent.futures import ThreadPoolExecutor
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
-SRC = os.path.join(HERE, "csrc", "avr_capi.hip")
-DEPS = [os.path.join(HERE, "csrc", f) for f in ("avr_capi.hip", "avr_kernels.hip", "avr_numerics.h", "avr_canon.h", "avr_sampling.h", "avr_vdb.h", "avr_envmap.h", "avr_flip.h", "avr_graph.hip", "avr_graph_capi.hip", "avr_graph_host.h")] + [
-    os.path.join(ROOT, "include", "avr.h")]
+CSRC = os.path.join(HERE, "csrc")
+SRC = os.path.join(CSRC, "avr_capi.hip")
+KPATHS = os.path.join(CSRC, "avr_kpaths.hip")
+DEPS = [os.path.join(CSRC, f) for f in (
+    "avr_capi.hip", "avr_kernels.hip", "avr_kpaths.hip", "avr_kpaths_list.h", "avr_numerics.h", "avr_canon.h",
+    "avr_sampling.h", "avr_vdb.h", "avr_envmap.h", "avr_flip.h", "avr_graph.hip", "avr_graph_capi.hip",
+    "avr_graph_host.h", "avr_boundary.h")] + [os.path.join(ROOT, "include", "avr.h")]
 OUT = os.path.join(HERE, "libavr_hip.so")
+OBJDIR = os.path.join(ROOT, "build", "obj")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+# (medium kind, fast) per k_paths object: 0 GridMedium, 1 Homogeneous/Cloud, 3 NanoVDB, 4 RGB grid
+KP_UNITS = [(m, f) for f in (0, 1) for m in (0, 1, 3, 4)]
 
 # -ffp-contract=off: same float semantics as pbrt's CPU build (CMakeLists.txt:134-137),
 # so a device sample replays the CPU oracle's sample.
-FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared",
+FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC",
          "-I" + os.path.join(ROOT, "include")]
 # RCCL for avr_film_reduce_rccl (in-process multi-GPU film reduce)
 LIBS = ["-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"]
@@ -23,15 +36,32 @@ def up_to_date():
     if not os.path.exists(OUT):
         return False
     t = os.path.getmtime(OUT)
-    return all(os.path.getmtime(d) <= t for d in DEPS)
+    return all(os.path.getmtime(d) <= t for d in DEPS if os.path.exists(d))
 
 
-def build(force=False, verbose=False):
+def _compile(args):
+    src, obj, defs, verbose = args
+    cmd = [HIPCC] + FLAGS + defs + ["-c", src, "-o", obj]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.check_call(cmd)
+    return obj
+
+
+def build(force=False, verbose=False, jobs=None):
     if not force and up_to_date():
         return OUT
-    cmd = [HIPCC] + FLAGS + [SRC, "-o", OUT + ".tmp"] + LIBS
+    os.makedirs(OBJDIR, exist_ok=True)
+    units = [(SRC, os.path.join(OBJDIR, "avr_capi.o"), ["-DAVR_KP_SPLIT"], verbose)]
+    for med, fast in KP_UNITS:
+        units.append((KPATHS, os.path.join(OBJDIR, f"avr_kpaths_m{med}_f{fast}.o"),
+                      [f"-DAVR_KP_MED={med}", f"-DAVR_KP_FAST={fast}"], verbose))
+    jobs = jobs or max(1, min(len(units), int(os.environ.get("MAX_JOBS", os.cpu_count() or 4))))
+    with ThreadPoolExecutor(jobs) as ex:
+        objs = list(ex.map(_compile, units))
+    cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC"] + objs + ["-o", OUT + ".tmp"] + LIBS
     if verbose:
-        print(" ".join(cmd))
+        print(" ".join(cmd), flush=True)
     subprocess.check_call(cmd)
     os.replace(OUT + ".tmp", OUT)
     return OUT

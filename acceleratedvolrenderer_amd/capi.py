@@ -90,6 +90,7 @@ SIGNATURES = {
     "avr_context_destroy": (ctypes.c_int, [ctypes.c_void_p]),
     "avr_set_stream": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "avr_set_kernel_mode": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "avr_set_render_mode": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "avr_set_refill_min": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "avr_set_dda_budget": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "avr_set_grid_layout": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
@@ -233,6 +234,12 @@ class Context:
             self.close()
         except Exception:
             pass
+
+    def set_render_mode(self, mode):
+        """0 / "replay": canonical math, per-sample parity with the CPU oracle; 1 / "fast":
+        hardware transcendentals, statistical parity (avr_set_render_mode)."""
+        m = {"replay": 0, "fast": 1}.get(mode, mode)
+        _check(self.lib.avr_set_render_mode(self.h, int(m)))
 
     def set_kernel_mode(self, mode):
         """0 = persistent megakernel (default), 1 = wavefront queues."""

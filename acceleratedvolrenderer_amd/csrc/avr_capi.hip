@@ -10,6 +10,16 @@
 // Everything is enqueued on one HIP stream; the host reads back one int (the
 // survivor count) per depth iteration to size the next launch and stop early.
 #include "avr_kernels.hip"
+#ifdef AVR_KP_SPLIT
+// k_paths is instantiated in avr_kpaths.hip's translation units (one per medium kind and
+// render mode, compiled in parallel by build.py); declared here, launched from avr_render
+#include "avr_kpaths_list.h"
+namespace avr {
+#define AVR_KP_DECL(em, gr, zs, med, im, fa) extern template __global__ void k_paths<em, gr, zs, med, im, fa>(Params);
+AVR_KP_ALL(AVR_KP_DECL)
+#undef AVR_KP_DECL
+}  // namespace avr
+#endif
 #include "avr_graph.hip"
 #include "../../include/avr.h"
 
@@ -77,9 +87,13 @@ struct avr_context {
     int last_base = 0, last_S = 0;
     int kernel_mode = 0;      // 0: persistent k_paths (default), 1: wavefront k_medium/k_shadow
     bool last_persistent = false;   // which organisation the last avr_render ran
+    bool last_fast = false;         // ... and whether k_paths ran in fast mode
     int *d_heads = nullptr;   // 8 per-XCD work counters of k_paths
-    int paths_grid[64] = {};  // k_paths<emissive, gray, zsobol, medium, image> at 32*image + 8*(0 grid, 1 vdb, 2 rgb, 3 homogeneous/cloud) + 4*zsobol + 2*emissive + gray
-    void (*kpaths[64])(avr::Params) = {};
+    // k_paths<emissive, gray, zsobol, medium, image, fast> at 64*fast + 32*image + 8*(0 grid, 1 vdb,
+    // 2 rgb, 3 homogeneous/cloud) + 4*zsobol + 2*emissive + gray
+    int paths_grid[128] = {};
+    void (*kpaths[128])(avr::Params) = {};
+    int render_mode = 0;      // 0 replay (canonical math, per-sample parity), 1 fast (hardware math)
     // pixel sampler (avr_set_sampler) and filter (avr_set_filter)
     int sampler_kind = 0;     // 0 IndependentSampler, 1 ZSobolSampler
     int sampler_spp = 16;     // samplesPerPixel of the sampler (ZSobol's Morton layout)
@@ -140,7 +154,7 @@ void release_comms(avr_context *c) {
 }
 
 void free_paths(avr_context *c) {
-    float4 *f4[] = {c->ps.o, c->ps.d, c->ps.lambda, c->ps.pdf, c->ps.beta, c->ps.r_u, c->ps.r_l, c->ps.L,
+    float4 *f4[] = {c->ps.o, c->ps.d, c->ps.lambda, c->ps.pdf, c->ps.beta, c->ps.r_u, c->ps.r_l, c->ps.L, c->ps.rec,
                     c->sh.o, c->sh.d, c->sh.bf, c->sh.Ls, c->sh.rp};
     for (auto p : f4) if (p) (void)hipFree(p);
     if (c->ps.smp_state) (void)hipFree(c->ps.smp_state);
@@ -164,6 +178,7 @@ int ensure_paths(avr_context *c, long long n) {
     HIP_TRY(dalloc(&c->ps.r_l, N)); HIP_TRY(dalloc(&c->ps.L, N));
     HIP_TRY(dalloc(&c->ps.smp_state, N)); HIP_TRY(dalloc(&c->ps.smp_inc, N)); HIP_TRY(dalloc(&c->ps.depth, N));
     HIP_TRY(dalloc(&c->ps.weight, N));
+    HIP_TRY(dalloc(&c->ps.rec, 2 * N));   // k_paths: 32-B record per sample
     HIP_TRY(dalloc(&c->sh.path, N)); HIP_TRY(dalloc(&c->sh.o, N)); HIP_TRY(dalloc(&c->sh.d, N));
     HIP_TRY(dalloc(&c->sh.bf, N)); HIP_TRY(dalloc(&c->sh.Ls, N)); HIP_TRY(dalloc(&c->sh.rp, N));
     HIP_TRY(dalloc(&c->sh.pdfs, N));
@@ -450,16 +465,19 @@ int avr_context_create(int device, long long max_paths, avr_context **out) {
         }
         // slot 32*image + 8*medium(0 grid, 1 vdb, 2 rgb, 3 homogeneous/cloud) + 4*zsobol + 2*emissive + gray; RGB grids
         // are never gray (their gray slots hold the 4-wavelength kernel)
-#define AVR_KP(em, gr, zs, med, im) avr::k_paths<em, (med == 4 ? false : gr), zs, med, im>
-#define AVR_KP8(med, im)                                                                                   \
-    AVR_KP(false, false, false, med, im), AVR_KP(false, true, false, med, im), AVR_KP(true, false, false, med, im), \
-        AVR_KP(true, true, false, med, im), AVR_KP(false, false, true, med, im), AVR_KP(false, true, true, med, im), \
-        AVR_KP(true, false, true, med, im), AVR_KP(true, true, true, med, im)
-        void (*kerns[64])(avr::Params) = {AVR_KP8(0, false), AVR_KP8(3, false), AVR_KP8(4, false), AVR_KP8(1, false),
-                                          AVR_KP8(0, true),  AVR_KP8(3, true),  AVR_KP8(4, true),  AVR_KP8(1, true)};
+#define AVR_KP(em, gr, zs, med, im, fa) avr::k_paths<em, (med == 4 ? false : gr), zs, med, im, fa>
+#define AVR_KP8(med, im, fa)                                                                                           \
+    AVR_KP(false, false, false, med, im, fa), AVR_KP(false, true, false, med, im, fa),                                 \
+        AVR_KP(true, false, false, med, im, fa), AVR_KP(true, true, false, med, im, fa),                               \
+        AVR_KP(false, false, true, med, im, fa), AVR_KP(false, true, true, med, im, fa),                               \
+        AVR_KP(true, false, true, med, im, fa), AVR_KP(true, true, true, med, im, fa)
+#define AVR_KP32(im, fa) AVR_KP8(0, im, fa), AVR_KP8(3, im, fa), AVR_KP8(4, im, fa), AVR_KP8(1, im, fa)
+        void (*kerns[128])(avr::Params) = {AVR_KP32(false, false), AVR_KP32(true, false), AVR_KP32(false, true),
+                                           AVR_KP32(true, true)};
+#undef AVR_KP32
 #undef AVR_KP8
 #undef AVR_KP
-        for (int k = 0; k < 64; ++k) {
+        for (int k = 0; k < 128; ++k) {
             int blocksPerCU = 0;
             if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocksPerCU, kerns[k], 256, 0) != hipSuccess) {
                 delete c;
@@ -491,6 +509,13 @@ int avr_set_dda_budget(avr_context *c, int cells) {
 int avr_set_refill_min(avr_context *c, int lanes) {
     if (!c || lanes < 1 || lanes > 64) return fail(AVR_ERR_ARG, "refill threshold must be 1..64 lanes");
     c->refill_min = lanes;
+    return AVR_OK;
+}
+
+int avr_set_render_mode(avr_context *c, int mode) {
+    AVR_QUIESCE(c);
+    if (!c || (mode != 0 && mode != 1)) return fail(AVR_ERR_ARG, "render mode must be 0 (replay) or 1 (fast)");
+    c->render_mode = mode;
     return AVR_OK;
 }
 
@@ -1086,6 +1111,7 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
                                 (((c->med.type != 3) && mcells <= 4096) || c->med.type == 3) &&
                                 c->med.mres[0] <= 255 && c->med.mres[1] <= 255 && c->med.mres[2] <= 255;
         c->last_persistent = persistent;
+        c->last_fast = persistent && c->render_mode == 1;
         if (persistent) {
             // PCG32 Advance(s*65536) as an affine map state' = A*state + inc*H (rng.h:132-146:
             // every step is linear in inc, so H = accPlus computed with inc = 1).
@@ -1108,11 +1134,13 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
             EV_MARK(e0);
             // gray medium: sigma_a and sigma_s tables constant over all 471 wavelengths
             const int mk = c->med.type == 3 ? 1 : (c->med.type == 4 ? 2 : (c->med.type == 1 || c->med.type == 2 ? 3 : 0));
-            const int kv = 32 * (c->n_image_lights > 0 ? 1 : 0) + 8 * mk + 4 * c->sampler_kind +
+            const int kv = 64 * c->render_mode + 32 * (c->n_image_lights > 0 ? 1 : 0) + 8 * mk + 4 * c->sampler_kind +
                            2 * (c->med.emissive ? 1 : 0) + (c->gray && c->med.type != 4 ? 1 : 0);
             hipLaunchKernelGGL(c->kpaths[kv], dim3(c->paths_grid[kv]), dim3(256), 0, c->stream, p);
             HIP_TRY(hipGetLastError());
             EV_MARK(e1);
+            p.rec_mode = 1;   // k_film reads the records k_paths wrote
+            p.fast = c->render_mode;
             hipLaunchKernelGGL(avr::k_film, dim3(blocks_for(P)), dim3(256), 0, c->stream, p);
             HIP_TRY(hipGetLastError());
             EV_MARK(e2);
@@ -1384,7 +1412,26 @@ int avr_last_pass_samples(avr_context *c, float *L, float *lambda, float *pdf, l
     if (!c || !c->has_film || !L || !lambda || !pdf || !first || !ns) return fail(AVR_ERR_ARG, "null arg");
     const long long n = (long long)c->film.width * c->film.height * c->last_S;
     if (n_max < n) return fail(AVR_ERR_ARG, "buffer too small for the last pass");
-    if (n > 0) {
+    if (n > 0 && c->last_persistent) {
+        // k_paths records {L}, {u_lambda, weight}: wavelengths and pdfs re-derived on the host
+        // with the device's functions (canonical math: bit-identical to k_film's; a fast-mode
+        // pass's hardware log is approximated by the host libm)
+        std::vector<float4> rec(2 * (size_t)n);
+        HIP_TRY(hipMemcpy(rec.data(), c->ps.rec, 2 * n * sizeof(float4), hipMemcpyDeviceToHost));
+        const avr::DevFilm &f = c->film;
+        for (long long i = 0; i < n; ++i) {
+            const float4 r0 = rec[2 * i], u = rec[2 * i + 1];
+            const avr::Spec l = f.nbuckets > 0 ? avr::sample_uniform_lambda(u.x, f.lmin, f.lmax)
+                                               : (c->last_fast ? avr::sample_visible_lambda_fast(u.x)
+                                                               : avr::sample_visible_lambda(u.x));
+            const float lv[4] = {l.v0, l.v1, l.v2, l.v3};
+            L[4 * i] = r0.x; L[4 * i + 1] = r0.y; L[4 * i + 2] = r0.z; L[4 * i + 3] = r0.w;
+            for (int k = 0; k < 4; ++k) {
+                lambda[4 * i + k] = lv[k];
+                pdf[4 * i + k] = f.nbuckets > 0 ? 1 / (f.lmax - f.lmin) : avr::visible_wavelength_pdf(lv[k]);
+            }
+        }
+    } else if (n > 0) {
         HIP_TRY(hipMemcpy(L, c->ps.L, n * sizeof(float4), hipMemcpyDeviceToHost));
         HIP_TRY(hipMemcpy(lambda, c->ps.lambda, n * sizeof(float4), hipMemcpyDeviceToHost));
         HIP_TRY(hipMemcpy(pdf, c->ps.pdf, n * sizeof(float4), hipMemcpyDeviceToHost));
@@ -1401,6 +1448,10 @@ int avr_last_pass_weights(avr_context *c, float *w, long long n_max) {
     if (n_max < n) return fail(AVR_ERR_ARG, "buffer too small for the last pass");
     if (c->filter_type == 0) {
         for (long long i = 0; i < n; ++i) w[i] = 1.f;   // BoxFilter::Sample weight
+    } else if (n > 0 && c->last_persistent) {
+        std::vector<float4> rec(2 * (size_t)n);
+        HIP_TRY(hipMemcpy(rec.data(), c->ps.rec, 2 * n * sizeof(float4), hipMemcpyDeviceToHost));
+        for (long long i = 0; i < n; ++i) w[i] = rec[2 * i + 1].y;
     } else if (n > 0) {
         HIP_TRY(hipMemcpy(w, c->ps.weight, n * sizeof(float), hipMemcpyDeviceToHost));
     }

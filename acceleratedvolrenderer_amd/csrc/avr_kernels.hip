@@ -119,6 +119,11 @@ struct DevFilm {
 __device__ __forceinline__ Spec film_sample_lambda(const DevFilm &f, float u) {
     return f.nbuckets > 0 ? sample_uniform_lambda(u, f.lmin, f.lmax) : sample_visible_lambda(u);
 }
+// fast render mode: the visible-wavelength inversion with the hardware log (same u -> same
+// wavelengths in k_paths and k_film, both on the device)
+__device__ __forceinline__ Spec film_sample_lambda_fast(const DevFilm &f, float u) {
+    return f.nbuckets > 0 ? sample_uniform_lambda(u, f.lmin, f.lmax) : sample_visible_lambda_fast(u);
+}
 __device__ __forceinline__ float film_lambda_pdf(const DevFilm &f, float l) {
     return f.nbuckets > 0 ? 1 / (f.lmax - f.lmin) : visible_wavelength_pdf(l);
 }
@@ -128,6 +133,9 @@ struct PathSoA {
     uint64_t *smp_state, *smp_inc;
     int *depth;
     float *weight;                    // per-sample filter weight (GaussianFilter only)
+    // k_paths' per-sample record, 32 B at 2*id: {L[4]} then {u_lambda, filter weight, 0, 0}
+    // (k_film re-derives the wavelengths from u_lambda); one 32-B sector per sample
+    float4 *rec;
 };
 struct ShadowSoA {
     int *path;
@@ -167,6 +175,8 @@ struct Params {
     int refill_min;                   // k_paths: refill a wave once this many lanes are idle
     int dda_budget;                   // k_paths: majorant cells a lane may cross per tracking
                                       //   iteration before yielding (bounds DDA divergence)
+    int rec_mode;                     // k_film: 1 = read k_paths' records (ps.rec), 0 = wavefront SoA
+    int fast;                         // render mode: 0 replay (canonical math), 1 fast (hardware math)
 };
 
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
@@ -225,6 +235,7 @@ __device__ __forceinline__ float fat_lookup(const float4 *__restrict__ fat, cons
     return lerp(dz, lerp(dy, d00, d10), lerp(dy, d01, d11));
 }
 
+#ifndef AVR_KPATHS_TU   // host-launched kernels: compiled in the C-ABI translation unit only
 __global__ void __launch_bounds__(256) k_fatten(const float *__restrict__ v, int nx, int ny, int nz, float4 *fat) {
     const size_t n = (size_t)(nx + 1) * (ny + 1) * (nz + 1);
     for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < n; e += (size_t)gridDim.x * blockDim.x) {
@@ -238,12 +249,14 @@ __global__ void __launch_bounds__(256) k_fatten(const float *__restrict__ v, int
     }
 }
 
+#endif
+
 // ---------------------------------------------------------------------------
 // CloudMedium::Density — the procedural medium (medium type 2) and the generator of the
 // synthetic heterogeneous grid (BASELINE.md S-cloud; k_cloud below): CloudMedium::Density
 // (media.h:496-520; density 1, wispiness 1, frequency 5) at voxel centres, with
 // pbrt's Perlin Noise/DNoise (util/noise.cpp). Only +,-,*,floor,fmod: bit-exact vs CPU.
-__constant__ int c_perm[512] = {
+static __constant__ int c_perm[512] = {
     151, 160, 137, 91, 90, 15, 131, 13, 201, 95, 96, 53, 194, 233, 7, 225, 140, 36, 103, 30, 69, 142,
     8, 99, 37, 240, 21, 10, 23, 190, 6, 148, 247, 120, 234, 75, 0, 26, 197, 62, 94, 252, 219, 203, 117,
     35, 11, 32, 57, 177, 33, 88, 237, 149, 56, 87, 174, 20, 125, 136, 171, 168, 68, 175, 74, 165, 71,
@@ -914,6 +927,7 @@ __global__ void __launch_bounds__(256) k_medium(Params P) {
 // ---------------------------------------------------------------------------
 // Ratio tracking along shadow rays — SampleLd's transmittance loop
 // (cpu/integrators.cpp:1339-1398), incl. Russian roulette at Tr < 0.05, q = 0.75.
+#ifndef AVR_KPATHS_TU
 __global__ void __launch_bounds__(256) k_shadow(Params P) {
     __shared__ float s_maj[4096];
     const float *maj = stage_majorant(P.med, s_maj);
@@ -971,6 +985,7 @@ __global__ void __launch_bounds__(256) k_shadow(Params P) {
     flush_stat(P.stats, 4, nIn);
     flush_stat(P.stats, 6, nSteps);
 }
+#endif
 
 // ---------------------------------------------------------------------------
 // k_paths — persistent-wave megakernel (the default path).
@@ -1083,6 +1098,7 @@ __device__ __forceinline__ bool ddal_next(DdaL &q, const float *maj, int sy, int
 // samplers.h:457-460; rng.h:132-146) as an affine map state' = A * state + inc * H: every
 // step of the log-time loop is linear in inc, so H is the loop's accPlus run with inc = 1.
 // One entry per sample index of a pass; k_paths applies it to each pixel's stream.
+#ifndef AVR_KPATHS_TU
 __global__ void k_advance(uint64_t *adv, long long base, int S) {
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= S) return;
@@ -1100,6 +1116,7 @@ __global__ void k_advance(uint64_t *adv, long long base, int S) {
     adv[2 * s] = accMult;
     adv[2 * s + 1] = accPlus;
 }
+#endif
 
 #ifndef AVR_PATHS_WAVES_GRAY
 #define AVR_PATHS_WAVES_GRAY 3   // 168 VGPRs, no scratch (4 waves -> 128 VGPRs spills ~100 B/lane)
@@ -1131,6 +1148,11 @@ __device__ __forceinline__ float sclamp0(float x) { return fmaxf_(0.f, x); }
 __device__ __forceinline__ Spec sclamp0(const Spec &x) { return clamp_zero(x); }
 __device__ __forceinline__ float sexp(float x) { return fast_exp(x); }
 __device__ __forceinline__ Spec sexp(const Spec &x) { return fast_exp(x); }
+// FastExp (replay) or the hardware exp (fast mode)
+template <bool kFast> __device__ __forceinline__ float sexpm(float x) { return kFast ? hw_exp(x) : fast_exp(x); }
+template <bool kFast> __device__ __forceinline__ Spec sexpm(const Spec &x) {
+    return kFast ? Spec{hw_exp(x.v0), hw_exp(x.v1), hw_exp(x.v2), hw_exp(x.v3)} : fast_exp(x);
+}
 template <typename S> __device__ __forceinline__ S sconst(float a);
 template <> __device__ __forceinline__ float sconst<float>(float a) { return a; }
 template <> __device__ __forceinline__ Spec sconst<Spec>(float a) { return Spec::c(a); }
@@ -1183,7 +1205,8 @@ struct SecProf {
 // in LDS, sigma and Le from GridMedium-style trilinear sigmoid lookups (sample_point).
 // kImage: the scene holds an ImageInfiniteLight (non-delta NEE with MIS, MIS-weighted
 // escapes); a separate instantiation so the other kernels keep their register budget.
-template <bool kEmissive, bool kGray, bool kZSobol, int kMed, bool kImage>
+// kFast: the "fast" render mode (hardware transcendentals, statistical parity); replay otherwise.
+template <bool kEmissive, bool kGray, bool kZSobol, int kMed, bool kImage, bool kFast>
 __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_WAVES_SPEC) k_paths(Params P) {
     // kMed 1: HomogeneousMedium or CloudMedium — dda_init gives their single
     // HomogeneousMajorantIterator segment over a 1^3 majorant of 1.0; properties from sample_point
@@ -1197,6 +1220,9 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
     // ImageInfiniteLight shadow rays (non-delta NEE): the sampled (u, v), p_l and the phase
     // value per lane, parked here while the lane traces its shadow ray (off the VGPR budget)
     __shared__ float4 s_img[kImage ? 256 : 1];
+    // per lane: the camera sample's wavelength u and filter weight, parked here until the
+    // path ends and its 32-B record is written (off the VGPR budget)
+    __shared__ float2 s_rec[256];
     // GaussianFilter's FilterSampler tables (pbrt's default radius 1.5: 48 x 48 function +
     // CDFs, ~19 KB) staged here when they fit: the camera-ray refill's two binary searches
     // then run on LDS instead of dependent L2 loads
@@ -1376,7 +1402,7 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
                 float up0, up1;
                 smp.get2d(P, &up0, &up1);
                 float phPdf;
-                const V3 wi = hg_sample(-pd, m.g, up0, up1, &phPdf);
+                const V3 wi = hg_sample<kFast>(-pd, m.g, up0, up1, &phPdf);
                 if (phPdf == 0) {
                     ev = EV_END;
                 } else {
@@ -1426,8 +1452,11 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
         }
         if (__ballot(ev == EV_END)) {
             if (ev == EV_END) {
-                P.ps.L[g] = to4(L);
-                P.ps.lambda[g] = to4(lam);
+                // the 32-B per-sample record: L, then {u_lambda, filter weight}
+                float4 *rp = P.ps.rec + 2 * (size_t)g;
+                const float2 q = s_rec[threadIdx.x];
+                rp[0] = to4(L);
+                rp[1] = make_float4(q.x, q.y, 0.f, 0.f);
                 mode = M_FETCH;
                 ev = EV_NONE;
             }
@@ -1477,10 +1506,12 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
                         // == rng.Advance((sample_base + sIdx) * 65536) (rng.h:132-146), precomputed
                         smp.rng.state = P.advance[2 * sIdx] * smp.rng.state + smp.rng.inc * P.advance[2 * sIdx + 1];
                     }
-                    lam = film_sample_lambda(P.film, smp.get1d(P));   // pdf: recomputed by k_film
+                    const float ulam = smp.get1d(P);
+                    // wavelengths (pdf: recomputed by k_film from the record's u_lambda)
+                    lam = kFast ? film_sample_lambda_fast(P.film, ulam) : film_sample_lambda(P.film, ulam);
                     float pFilmX, pFilmY, fweight;
                     camera_sample(P, smp, px, py, &pFilmX, &pFilmY, &fweight, &ftab);
-                    if (P.film.filter_type != 0) P.ps.weight[g] = fweight;
+                    s_rec[threadIdx.x] = make_float2(ulam, fweight);
                     const float *r = P.cam.raster;
                     V3 pCam = {r[0] * pFilmX + r[1] * pFilmY + r[2] * 0.f + r[3],
                                r[4] * pFilmX + r[5] * pFilmY + r[6] * 0.f + r[7],
@@ -1568,7 +1599,7 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
                             if (!kGray) {
                                 float dt = s1 - s0;
                                 if (__builtin_isinf(dt)) dt = kFloatMax;
-                                T_maj = T_maj * sexp(-(sigma_maj * dt));
+                                T_maj = T_maj * sexpm<kFast>(-(sigma_maj * dt));
                             }
                         } else {
                             tMin = s0;
@@ -1586,17 +1617,24 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
                     // an absolute one for log2 near 1); accepted and ambiguous candidates stay
                     // "pending" and are decided exactly, once per wave, after the walk.
                     const float sm0 = st0 * mv;
-                    const float rs = __builtin_amdgcn_rcpf(sm0);
-                    const float eFast = -__builtin_amdgcn_logf(1 - u) * (kLn2 * rs);
-                    const float tFast = tMin + eFast;
-                    const float margin = 1e-5f * eFast + 4.8e-7f * __builtin_fabsf(segMax) + 1e-6f * rs + 1e-30f;
-                    if (!(tFast > segMax + margin)) {
+                    bool pending;
+                    if constexpr (kFast) {
+                        // fast mode: the hardware candidate is the candidate (decided once)
+                        pending = tMin + m_exp_dist<true>(u, sm0) < segMax;
+                    } else {
+                        const float rs = __builtin_amdgcn_rcpf(sm0);
+                        const float eFast = -__builtin_amdgcn_logf(1 - u) * (kLn2 * rs);
+                        const float tFast = tMin + eFast;
+                        const float margin = 1e-5f * eFast + 4.8e-7f * __builtin_fabsf(segMax) + 1e-6f * rs + 1e-30f;
+                        pending = !(tFast > segMax + margin);
+                    }
+                    if (pending) {
                         walk = 1;
                     } else {
                         u = rng.uniform();
                         float dt = segMax - tMin;
                         if (__builtin_isinf(dt)) dt = kFloatMax;
-                        T_maj = T_maj * sexp(-((sig_t * mv) * dt));
+                        T_maj = T_maj * sexpm<kFast>(-((sig_t * mv) * dt));
                         needNext = true;
                     }
                 }
@@ -1611,18 +1649,18 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
             }
             if (!pend) continue;   // walk budget used up: resume the DDA next iteration
             // exact candidate (media.h:770-777): t = tMin + SampleExponential(u, sigma_maj[0])
-            t = tMin + sample_exponential(u, st0 * mv);
+            t = tMin + m_exp_dist<kFast>(u, st0 * mv);
             u = rng.uniform();
             if (!(t < segMax)) {   // rejected after all: close the segment (media.h:790-801)
                 float dt = segMax - tMin;
                 if (__builtin_isinf(dt)) dt = kFloatMax;
-                T_maj = T_maj * sexp(-((sig_t * mv) * dt));
+                T_maj = T_maj * sexpm<kFast>(-((sig_t * mv) * dt));
                 needNext = true;
                 continue;
             }
             // ---- collision: density fetch for every lane that reached one ----
             const S sigma_maj = sig_t * mv;
-            T_maj = T_maj * sexp(-(sigma_maj * (t - tMin)));
+            T_maj = T_maj * sexpm<kFast>(-(sigma_maj * (t - tMin)));
             const V3 pc = po + sd * t;
             // GridMedium::SamplePoint (media.h:287-319) / NanoVDBMedium::SamplePoint (624-637);
             // k_paths runs these two (the host sends the other media to the wavefront kernels)
@@ -1730,6 +1768,7 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
     flush_stat(P.stats, 9, nActive);
 }
 
+#ifndef AVR_KPATHS_TU
 // ---------------------------------------------------------------------------
 // Film — NaN/Inf guard (integrators.cpp:272-282), PixelSensor::ToSensorRGB (film.h:95-100),
 // RGBFilm::AddSample (film.h:239-255): per pixel, the pass's samples in sampleIndex order.
@@ -1739,9 +1778,22 @@ __global__ void __launch_bounds__(256) k_film(Params P) {
         double s0 = P.film.rgb_sum[3 * (size_t)pix], s1 = P.film.rgb_sum[3 * (size_t)pix + 1],
                s2 = P.film.rgb_sum[3 * (size_t)pix + 2], ws = P.film.w_sum[pix];
         for (int s = 0; s < P.pass_samples; ++s) {
-            const int id = s * npix + pix;
-            Spec L = spec4(P.ps.L[id]);
-            const Spec lam = spec4(P.ps.lambda[id]);
+            const size_t id = (size_t)s * npix + pix;
+            Spec L;
+            Spec lam;
+            float w = 1.f;   // CameraSample::filterWeight
+            if (P.rec_mode) {
+                // k_paths' 32-B record: L, {u_lambda, weight}; the wavelengths are re-derived
+                // from u_lambda with the function k_paths sampled them with
+                const float4 r0 = P.ps.rec[2 * id], r1 = P.ps.rec[2 * id + 1];
+                L = spec4(r0);
+                lam = P.fast ? film_sample_lambda_fast(P.film, r1.x) : film_sample_lambda(P.film, r1.x);
+                if (P.film.filter_type != 0) w = r1.y;
+            } else {
+                L = spec4(P.ps.L[id]);
+                lam = spec4(P.ps.lambda[id]);
+                if (P.film.filter_type != 0) w = P.ps.weight[id];
+            }
             const Spec pdf = {film_lambda_pdf(P.film, lam.v0), film_lambda_pdf(P.film, lam.v1),
                               film_lambda_pdf(P.film, lam.v2), film_lambda_pdf(P.film, lam.v3)};
             const LambdaIdx li = lambda_index(lam);
@@ -1758,7 +1810,6 @@ __global__ void __launch_bounds__(256) k_film(Params P) {
             float mx = fmaxf_(fmaxf_(rgb[0], rgb[1]), rgb[2]);
             if (mx > P.film.max_component)
                 for (int c = 0; c < 3; ++c) rgb[c] *= P.film.max_component / mx;
-            const float w = P.film.filter_type != 0 ? P.ps.weight[id] : 1.f;   // CameraSample::filterWeight
             s0 += (double)(w * rgb[0]);
             s1 += (double)(w * rgb[1]);
             s2 += (double)(w * rgb[2]);
@@ -2087,4 +2138,5 @@ __global__ void __launch_bounds__(256) k_cloud(float *out, int n, long long firs
     }
 }
 
+#endif  // AVR_KPATHS_TU
 }  // namespace avr

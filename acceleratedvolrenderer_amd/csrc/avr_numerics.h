@@ -181,6 +181,35 @@ AVR_HD float cr_cosh(float x) { return coshf(x); }
 AVR_HD void cr_sincos(float x, float *s, float *c) { *s = sinf(x); *c = cosf(x); }
 #endif
 
+// "fast" render mode (avr_set_render_mode 1; SURVEY §7: replay / fast): the hardware
+// transcendentals (v_log_f32, v_exp_f32, v_sin/cos_f32 — about 1 ulp) replace the canonical
+// f64 sequences and pbrt's CPU FastExp polynomial. The estimator is unchanged; sample paths
+// differ in their last bits, so parity is statistical (tests/test_gpu_fast.py). The host
+// versions exist only so that shared code compiles; fast mode is a device path.
+#if defined(__HIP_DEVICE_COMPILE__)
+AVR_HD float hw_log(float x) { return __builtin_amdgcn_logf(x) * 0.693147181f; }
+AVR_HD float hw_exp(float x) { return __builtin_amdgcn_exp2f(x * 1.442695041f); }
+AVR_HD float hw_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
+// sin / cos of 2*pi*t (the hardware takes its argument in turns)
+AVR_HD void hw_sincos_turns(float t, float *s, float *c) {
+    *s = __builtin_amdgcn_sinf(t);
+    *c = __builtin_amdgcn_cosf(t);
+}
+#else   // host compilation pass (and host-side callers such as the C-ABI readback)
+AVR_HD float hw_log(float x) { return logf(x); }
+AVR_HD float hw_exp(float x) { return expf(x); }
+AVR_HD float hw_rcp(float x) { return 1.f / x; }
+AVR_HD void hw_sincos_turns(float t, float *s, float *c) {
+    *s = sinf(6.28318531f * t);
+    *c = cosf(6.28318531f * t);
+}
+#endif
+// exponential free-flight distance -log(1 - u) / a (SampleExponential, sampling.h:222-225)
+template <bool kFast> AVR_HD float m_exp_dist(float u, float a) {
+    if (kFast) return -hw_log(1 - u) * hw_rcp(a);
+    return -cr_log(1 - u) / a;
+}
+
 // Blackbody (spectrum.h:69-80) with FastExp, and BlackbodySpectrum's normalisation
 // 1 / Blackbody(lambdaMax, T), lambdaMax = 2.8977721e-3 / T (spectrum.h:500-530)
 AVR_HD float blackbody(float lambda, float T) {
@@ -194,6 +223,11 @@ AVR_HD float blackbody_norm(float T) { return 1 / blackbody((2.8977721e-3f / T) 
 
 // Wavelength sampling — sampling.h:163-171, spectrum.h:334-347
 AVR_HD float sample_visible_wavelength(float u) { return 538 - 138.888889f * cr_atanh(0.85691062f - 1.82750197f * u); }
+// fast mode: atanh(x) = log((1 + x) / (1 - x)) / 2 with the hardware log
+AVR_HD float sample_visible_wavelength_fast(float u) {
+    const float x = 0.85691062f - 1.82750197f * u;
+    return 538 - 138.888889f * (0.5f * hw_log((1 + x) / (1 - x)));
+}
 AVR_HD float visible_wavelength_pdf(float l) {
     if (l < 360 || l > 830) return 0;
     return 0.0039398042f / sqr(cr_cosh(0.0072f * (l - 538)));
@@ -210,6 +244,10 @@ AVR_HD float visible_up(float u, int i) {
     float up = u + float(i) / 4;
     if (up > 1) up -= 1;
     return up;
+}
+AVR_HD Spec sample_visible_lambda_fast(float u) {
+    return {sample_visible_wavelength_fast(visible_up(u, 0)), sample_visible_wavelength_fast(visible_up(u, 1)),
+            sample_visible_wavelength_fast(visible_up(u, 2)), sample_visible_wavelength_fast(visible_up(u, 3))};
 }
 AVR_HD Spec sample_visible_lambda(float u) {
     Spec l;
@@ -272,6 +310,7 @@ AVR_HD float hg_eval(float cosTheta, float g) {
     float denom = 1 + sqr(g) + 2 * g * cosTheta;
     return kInv4Pi * (1 - sqr(g)) / (denom * __builtin_sqrtf(fmaxf_(0.f, denom)));
 }
+template <bool kFast = false>
 AVR_HD V3 hg_sample(V3 wo, float g, float u0, float u1, float *pdf) {
     g = clampf(g, -.99f, .99f);
     float cosTheta;
@@ -286,7 +325,8 @@ AVR_HD V3 hg_sample(V3 wo, float g, float u0, float u1, float *pdf) {
     V3 fy = {b, sign + sqr(wo.y) * a, -wo.y};
     float st = clampf(sinTheta, -1, 1);
     float sinPhi, cosPhi;
-    cr_sincos(phi, &sinPhi, &cosPhi);
+    if (kFast) hw_sincos_turns(u1, &sinPhi, &cosPhi);   // sin / cos of 2 pi u1 in hardware
+    else cr_sincos(phi, &sinPhi, &cosPhi);
     V3 s = {st * cosPhi, st * sinPhi, clampf(cosTheta, -1, 1)};
     V3 wi = s.x * fx + s.y * fy + s.z * wo;
     *pdf = hg_eval(cosTheta, g);

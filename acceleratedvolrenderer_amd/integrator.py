@@ -54,7 +54,7 @@ def reduce_film(buf, npix, nbuckets, rank, group=None):
 
 class VolPathIntegrator:
     def __init__(self, scene, maxdepth=5, spp=16, seed=0, device=0, max_paths=0, lightsampler="bvh",
-                 regularize=False, name="volpath", kernel="persistent", grid_layout="fat"):
+                 regularize=False, name="volpath", kernel="persistent", grid_layout="fat", mode="replay"):
         if name not in INTEGRATOR_NAMES:
             raise ValueError(f"unknown integrator {name!r}")
         if lightsampler not in ("bvh", "uniform", "power"):
@@ -75,6 +75,10 @@ class VolPathIntegrator:
         if grid_layout not in ("fat", "linear"):
             raise ValueError("grid_layout must be 'fat' or 'linear'")
         self.ctx.set_grid_layout(1 if grid_layout == "fat" else 0)
+        if mode not in ("replay", "fast"):
+            raise ValueError("mode must be 'replay' (per-sample parity) or 'fast' (statistical parity)")
+        self.mode = mode
+        self.ctx.set_render_mode(mode)
         self.ctx.set_scene(scene)
 
     @staticmethod

@@ -74,6 +74,9 @@ def parse():
                    help="pixel sampler (BASELINE.md S-cloud: zsobol, pbrt's default)")
     p.add_argument("--filter", default="gaussian", choices=["gaussian", "box"],
                    help="pixel filter (pbrt's default: gaussian radius 1.5, sigma 0.5)")
+    p.add_argument("--mode", default="replay", choices=["replay", "fast"],
+                   help="render mode: replay (canonical math, per-sample CPU parity; the headline) or fast "
+                        "(hardware transcendentals, statistical parity)")
     p.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     return p.parse_args()
 
@@ -168,7 +171,7 @@ def pmc_passes(args, kernel_substr="k_paths", timeout_s=240):
     child = [sys.executable, os.path.join(ROOT, "bench.py"), "--pmc-child", "--no-cpu-baseline", "--pmc", "off",
              "--steps", "2", "--warmup", "1"]
     for k in ("res", "width", "height", "spp_per_step", "max_paths", "kernel", "medium", "refill_min", "grid_layout",
-              "dda_budget", "zsobol_table", "sampler", "filter"):
+              "dda_budget", "zsobol_table", "sampler", "filter", "mode"):
         child += [f"--{k.replace('_', '-')}", str(getattr(args, k))]
     out = {}
     tmp = tempfile.mkdtemp(prefix="avr_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
@@ -267,7 +270,8 @@ def main():
         scene = scenes.s_cloud(density, width=args.width, height=args.height, sampler=args.sampler, spp=spp_total,
                                filter=args.filter)
     integ = VolPathIntegrator(scene, maxdepth=scenes.CLOUD_MAXDEPTH, spp=args.spp_per_step, seed=0, device=dev,
-                              max_paths=args.max_paths, kernel=args.kernel, grid_layout=args.grid_layout)
+                              max_paths=args.max_paths, kernel=args.kernel, grid_layout=args.grid_layout,
+                              mode=args.mode)
     if args.refill_min:
         integ.ctx.set_refill_min(args.refill_min)
     if args.dda_budget:
@@ -396,7 +400,7 @@ def main():
             "data": "synthetic (CloudMedium::Density 1024^3 generated on device; disney-cloud assets absent)",
             "config": {"workload": f"S-cloud-{n} {'NanoVDBMedium' if vdb is not None else 'GridMedium'}, perspective {args.width}x{args.height}, "
                                    f"{S} spp/step/GPU, maxdepth {scenes.CLOUD_MAXDEPTH}, {args.sampler} sampler "
-                                   f"(pixelsamples {spp_total}), {args.filter} filter",
+                                   f"(pixelsamples {spp_total}), {args.filter} filter, {args.mode} mode",
                        "global_batch": samples // args.steps, "parallelism": f"sample-shard x{world}",
                        "sample_index_wrap": wrap},
             "roofline": {

@@ -64,6 +64,14 @@ int avr_context_destroy(avr_context *ctx);
  * VGPRs, ballot-based lane refill), 1 = wavefront kernels k_camera/k_medium/k_shadow with
  * compacted SoA queues between events (pbrt wavefront decomposition). Same estimator. */
 int avr_set_kernel_mode(avr_context *ctx, int mode);
+/* Render mode for later renders (SURVEY.md §7 "replay / fast"): 0 = replay (default) — the
+ * device evaluates log/atanh/cosh/sin/cos by the canonical f64 sequences and FastExp by pbrt's
+ * CPU polynomial (util/math.h:450-471), so every sample replays the CPU VolPathIntegrator's bit
+ * for bit; 1 = fast — the hardware v_log/v_exp/v_sin/v_cos (about 1 ulp) and a single
+ * free-flight decision per candidate: the same estimator with different last bits, so parity
+ * is statistical (film error within the Monte Carlo noise). Applies to the persistent kernel
+ * (kernel mode 0); the wavefront kernels always replay. */
+int avr_set_render_mode(avr_context *ctx, int mode);
 /* k_paths: refill a wave's idle lanes with new samples once at least `lanes` (1..64)
  * are idle (or none is busy); larger values batch the camera-ray setup across lanes. */
 int avr_set_refill_min(avr_context *ctx, int lanes);

@@ -1,0 +1,98 @@
+"""The "fast" render mode (avr_set_render_mode 1; SURVEY.md §7 "replay / fast").
+
+Fast mode evaluates log / exp / sin / cos with the hardware instructions (about 1 ulp) and
+decides each free-flight candidate once, instead of the canonical f64 sequences and pbrt's
+CPU FastExp polynomial that replay uses. The estimator (VolPathIntegrator::Li,
+cpu/integrators.cpp:962-1280) is the same, so parity is statistical. Tolerances:
+  * correlated: at the same seed the fast film may differ from the platform CPU oracle's
+    film by at most 0.5 x the Monte Carlo noise (relative RMS between two oracle films at
+    different seeds) — the sample streams are the same and only last bits differ;
+  * unbiased: the frame mean of a fast render at many more samples lies within 4 standard
+    errors of the oracle's frame mean;
+  * counts: every (pixel, sample) path is traced exactly once (weights bit-exact).
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    torch.cuda.init()
+
+
+def _rel_rms(a, b):
+    return float(np.sqrt(np.mean((a - b) ** 2)) / max(1e-12, np.sqrt(np.mean(b ** 2))))
+
+
+def _scene(kind):
+    from acceleratedvolrenderer_amd import scenes
+    from oracle import binding
+    if kind == "uniform":   # C2's scene type: uniform GridMedium cube, orthographic
+        n = 16
+        dens = np.full((n, n, n), 0.75, np.float32)
+        return scenes.s_uniform(n=n, width=32, height=32, variant="scatter", density=dens), 5
+    if kind == "cloud":     # C3's stand-in: the S-cloud, perspective, ZSobol + Gaussian
+        dens = binding.cloud_grid(32)
+        return scenes.s_cloud(dens, width=48, height=27, sampler="zsobol", spp=1024,
+                              filter="gaussian"), scenes.CLOUD_MAXDEPTH
+    raise ValueError(kind)
+
+
+@pytest.mark.parametrize("kind", ["uniform", "cloud"])
+def test_fast_mode_statistical_parity(kind):
+    from acceleratedvolrenderer_amd import VolPathIntegrator
+    from oracle import binding
+    scene, maxdepth = _scene(kind)
+    spp = 16
+    fast = VolPathIntegrator(scene, maxdepth=maxdepth, spp=spp, seed=0, device=0, mode="fast")
+    rgb_f, w_f = fast.render()
+    ref = binding.OracleRun(scene, max_depth=maxdepth, seed=0)
+    rgb_o, w_o = ref.render(0, spp, nthreads=8)
+    assert np.array_equal(w_f, w_o), "every (pixel, sample) path traced once, same filter weights"
+    rgb_1, w_1 = binding.OracleRun(scene, max_depth=maxdepth, seed=1).render(0, spp, nthreads=8)
+    img_f, img_o, img_1 = fast.image(rgb_f, w_f), fast.image(rgb_o, w_o), fast.image(rgb_1, w_1)
+    err, noise = _rel_rms(img_f, img_o), _rel_rms(img_1, img_o)
+
+    # unbiasedness: 64x the samples on the device vs the oracle's frame mean
+    rgb_big, w_big = fast.render(0, 64 * spp if kind == "uniform" else 1024)
+    img_big = fast.image(rgb_big, w_big)
+    o_mean = 0.5 * (img_o.mean() + img_1.mean())
+    # standard error of the oracle's two-seed frame mean from the per-pixel seed difference
+    # (var of (o + o1) / 2 over N pixels = var(o - o1) / (4 N)); the device mean adds ~1/32 of it
+    se = 1.02 * float(np.std(img_o - img_1)) / (2 * np.sqrt(img_o.size))
+    print(f"fast/{kind}: film rel RMS vs platform oracle {err:.3e} (MC noise {noise:.3e}); frame mean "
+          f"{img_big.mean():.6f} vs oracle {o_mean:.6f} (se {se:.2e})")
+    assert err <= 0.5 * noise
+    assert abs(img_big.mean() - o_mean) <= 4 * se + 1e-6 * abs(o_mean)
+    fast.close()
+
+
+def test_fast_and_replay_modes_switch_on_one_context():
+    """The mode is a per-render switch: replay after fast is bit-identical to replay alone."""
+    from acceleratedvolrenderer_amd import VolPathIntegrator
+    scene, maxdepth = _scene("uniform")
+    a = VolPathIntegrator(scene, maxdepth=maxdepth, spp=8, seed=0, device=0)
+    rgb_a, w_a = a.render()
+    a.ctx.set_render_mode("fast")
+    rgb_f, _ = a.render()
+    a.ctx.set_render_mode("replay")
+    rgb_b, w_b = a.render()
+    assert np.array_equal(rgb_a, rgb_b) and np.array_equal(w_a, w_b)
+    assert not np.array_equal(rgb_a, rgb_f)   # the fast pass really ran other arithmetic
+    a.close()
+
+
+def test_render_mode_argument_errors():
+    from acceleratedvolrenderer_amd import capi
+    lib = capi.load()
+    assert lib.avr_set_render_mode(None, 0) != 0
+    ctx = capi.Context(0)
+    with pytest.raises(RuntimeError):
+        ctx.set_render_mode(2)
+    ctx.close()
