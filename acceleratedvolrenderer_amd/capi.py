@@ -91,6 +91,10 @@ SIGNATURES = {
     "avr_set_stream": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "avr_set_kernel_mode": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "avr_set_render_mode": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "avr_set_majorant_res": (ctypes.c_int, [ctypes.c_void_p, c_int_p]),
+    "avr_medium_boundary_sphere": (ctypes.c_int, [ctypes.c_void_p, c_float_p, ctypes.c_float]),
+    "avr_tune_majorant": (ctypes.c_int, [ctypes.c_void_p, c_int_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                         ctypes.c_int, ctypes.c_int, c_int_p, c_float_p]),
     "avr_set_refill_min": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "avr_set_dda_budget": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "avr_set_grid_layout": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
@@ -241,6 +245,20 @@ class Context:
         m = {"replay": 0, "fast": 1}.get(mode, mode)
         _check(self.lib.avr_set_render_mode(self.h, int(m)))
 
+    def set_majorant_res(self, res):
+        r = np.asarray(res, np.int32).reshape(3)
+        _check(self.lib.avr_set_majorant_res(self.h, r.ctypes.data_as(c_int_p)))
+
+    def tune_majorant(self, candidates, spp_begin, spp_end, seed, max_depth):
+        """avr_tune_majorant: returns (chosen (x, y, z), per-candidate probe ms)."""
+        cand = np.ascontiguousarray(np.asarray(candidates, np.int32).reshape(-1, 3))
+        chosen = np.zeros(3, np.int32)
+        ms = np.zeros(len(cand), np.float32)
+        _check(self.lib.avr_tune_majorant(self.h, cand.ctypes.data_as(c_int_p), len(cand), int(spp_begin),
+                                          int(spp_end), int(seed), int(max_depth), chosen.ctypes.data_as(c_int_p),
+                                          ms.ctypes.data_as(c_float_p)))
+        return tuple(int(v) for v in chosen), ms
+
     def set_kernel_mode(self, mode):
         """0 = persistent megakernel (default), 1 = wavefront queues."""
         _check(self.lib.avr_set_kernel_mode(self.h, int(mode)))
@@ -304,6 +322,11 @@ class Context:
                 self.h, _fp(med.density), med.nx, med.ny, med.nz, _fp(args[0]), _fp(args[1]), _fp(args[2]),
                 _fp(args[3]), _fp(args[4]), float(med.g), _fp(Le), _fp(ls), ls.shape[2], ls.shape[1], ls.shape[0],
                 mres.ctypes.data_as(c_int_p)))
+        sph = getattr(scene, "interface_sphere_render", None)
+        if sph is not None:
+            c3 = f32(sph[:3])
+            self._keep.append(c3)
+            _check(self.lib.avr_medium_boundary_sphere(self.h, _fp(c3), float(sph[3])))
         temp = getattr(med, "temperature", None)
         if temp is not None:
             self._keep.append(temp)

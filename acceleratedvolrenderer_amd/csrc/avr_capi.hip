@@ -318,6 +318,41 @@ int upload_vdb(avr_context *c, const avr_vdb_grid *G, int k, avr::vdb::Grid &g) 
     return AVR_OK;
 }
 
+// (Re)build the current medium's majorant grid at resolution mres on the device:
+// GridMedium MaxValue per cell (media.cpp:229-246), RGBGridMedium's sigma scale x (max
+// sigma_a + max sigma_s) (media.cpp:339-378), NanoVDBMedium's slop-widened cell maxima
+// (media.cpp:585-613); Homogeneous / Cloud: one segment with majorant 1.
+int build_majorant(avr_context *c, const int mres[3]) {
+    avr::DevMedium &m = c->med;
+    const int type = m.type;
+    if (c->d_majorant) (void)hipFree(c->d_majorant);
+    c->d_majorant = nullptr;
+    const int nm = mres[0] * mres[1] * mres[2];
+    HIP_TRY(dalloc(&c->d_majorant, (size_t)nm));
+    for (int i = 0; i < 3; ++i) m.mres[i] = mres[i];
+    if (type == 0) {
+        hipLaunchKernelGGL(avr::k_majorant, dim3(nm), dim3(256), 0, c->stream, m.density, m.nx, m.ny, m.nz, mres[0],
+                           mres[1], mres[2], c->d_majorant);
+        HIP_TRY(hipGetLastError());
+    } else if (type == 4) {
+        hipLaunchKernelGGL(avr::k_majorant_rgb, dim3(nm), dim3(256), 0, c->stream, m.rgb_a, m.rgb_s, m.nx, m.ny, m.nz,
+                           mres[0], mres[1], mres[2], m.rgb_sigma_scale, c->d_majorant);
+        HIP_TRY(hipGetLastError());
+    } else if (type == 3) {
+        const int *b = c->vdb_ibbox;
+        hipLaunchKernelGGL(avr::k_majorant_vdb, dim3(nm), dim3(256), 0, c->stream, m.vdb,
+                           make_float3(m.bmin[0], m.bmin[1], m.bmin[2]), make_float3(m.bmax[0], m.bmax[1], m.bmax[2]),
+                           make_int4(b[0], b[1], b[2], 0), make_int4(b[3], b[4], b[5], 0), mres[0], mres[1], mres[2],
+                           c->d_majorant);
+        HIP_TRY(hipGetLastError());
+    } else {   // single segment, sigma_maj = sigma_t * 1 (density <= 1 for the cloud)
+        const float one = 1.f;
+        HIP_TRY(hipMemcpyAsync(c->d_majorant, &one, sizeof(float), hipMemcpyHostToDevice, c->stream));
+    }
+    m.majorant = c->d_majorant;
+    return AVR_OK;
+}
+
 int medium_common(avr_context *c, const float *d_density, int nx, int ny, int nz, const float bounds[6],
                   const float rfm[16], const float mfr[16], const float *sigma_a, const float *sigma_s, float g,
                   const float *Le, const float *Lescale, int lnx, int lny, int lnz, const int mres[3],
@@ -345,6 +380,7 @@ int medium_common(avr_context *c, const float *d_density, int nx, int ny, int nz
     m.temp_scale = 1.f;
     m.temp_offset = 0.f;
     m.type = type;
+    m.boundary = 0;   // the bounds box until avr_medium_boundary_sphere
     m.cloud_density = cloud ? cloud[0] : 0.f;
     m.cloud_wispiness = cloud ? cloud[1] : 0.f;
     m.cloud_frequency = cloud ? cloud[2] : 0.f;
@@ -366,29 +402,7 @@ int medium_common(avr_context *c, const float *d_density, int nx, int ny, int nz
     m.Le = c->d_Le;
     m.lescale = c->d_lescale;
     m.lnx = lnx; m.lny = lny; m.lnz = lnz;
-    if (c->d_majorant) (void)hipFree(c->d_majorant);
-    const int nm = mres[0] * mres[1] * mres[2];
-    HIP_TRY(dalloc(&c->d_majorant, (size_t)nm));
-    if (type == 0) {
-        hipLaunchKernelGGL(avr::k_majorant, dim3(nm), dim3(256), 0, c->stream, d_density, nx, ny, nz, mres[0], mres[1],
-                           mres[2], c->d_majorant);
-        HIP_TRY(hipGetLastError());
-    } else if (type == 4) {
-        hipLaunchKernelGGL(avr::k_majorant_rgb, dim3(nm), dim3(256), 0, c->stream, m.rgb_a, m.rgb_s, nx, ny, nz,
-                           mres[0], mres[1], mres[2], m.rgb_sigma_scale, c->d_majorant);
-        HIP_TRY(hipGetLastError());
-    } else if (type == 3) {
-        const int *b = c->vdb_ibbox;
-        hipLaunchKernelGGL(avr::k_majorant_vdb, dim3(nm), dim3(256), 0, c->stream, m.vdb,
-                           make_float3(bounds[0], bounds[1], bounds[2]), make_float3(bounds[3], bounds[4], bounds[5]),
-                           make_int4(b[0], b[1], b[2], 0), make_int4(b[3], b[4], b[5], 0), mres[0], mres[1], mres[2],
-                           c->d_majorant);
-        HIP_TRY(hipGetLastError());
-    } else {   // single segment, sigma_maj = sigma_t * 1 (density <= 1 for the cloud)
-        const float one = 1.f;
-        HIP_TRY(hipMemcpyAsync(c->d_majorant, &one, sizeof(float), hipMemcpyHostToDevice, c->stream));
-    }
-    m.majorant = c->d_majorant;
+    if ((rc = build_majorant(c, mres))) return rc;
     if (c->d_fat) { (void)hipFree(c->d_fat); c->d_fat = nullptr; }
     m.fat = nullptr;
     if (c->grid_layout == 1 && type == 0) {
@@ -740,6 +754,85 @@ int avr_read_majorant(avr_context *c, float *out) {
     HIP_TRY(hipMemcpyAsync(out, c->d_majorant, nm * sizeof(float), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     return AVR_OK;
+}
+
+int avr_medium_boundary_sphere(avr_context *c, const float center[3], float radius) {
+    AVR_QUIESCE(c);
+    if (!c || !c->has_medium) return fail(AVR_ERR_STATE, "no medium");
+    if (radius > 0 && !center) return fail(AVR_ERR_ARG, "null sphere centre");
+    if (!(radius <= 0 || std::isfinite(radius))) return fail(AVR_ERR_ARG, "sphere radius must be finite");
+    c->med.boundary = radius > 0 ? 1 : 0;
+    for (int i = 0; i < 3; ++i) c->med.sph[i] = radius > 0 ? center[i] : 0.f;
+    c->med.sph[3] = radius > 0 ? radius : 0.f;
+    return AVR_OK;
+}
+
+int avr_set_majorant_res(avr_context *c, const int res[3]) {
+    AVR_QUIESCE(c);
+    if (!c || !c->has_medium || !res) return fail(AVR_ERR_STATE, "no medium");
+    if (c->med.type == 1 || c->med.type == 2)
+        return fail(AVR_ERR_ARG, "homogeneous / cloud media have a single majorant segment");
+    if (res[0] < 1 || res[1] < 1 || res[2] < 1 || res[0] > 255 || res[1] > 255 || res[2] > 255)
+        return fail(AVR_ERR_ARG, "majorant resolution must be 1..255 per axis");
+    HIP_TRY(hipSetDevice(c->device));
+    int rc = build_majorant(c, res);
+    if (rc) return rc;
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return AVR_OK;
+}
+
+int avr_tune_majorant(avr_context *c, const int *candidates, int n, int spp_begin, int spp_end, int seed,
+                      int max_depth, int chosen[3], float *ms) {
+    AVR_QUIESCE(c);
+    if (!c || !candidates || n < 1 || !chosen) return fail(AVR_ERR_ARG, "null argument");
+    if (!c->has_medium || !c->has_film || !c->has_camera) return fail(AVR_ERR_STATE, "scene incomplete");
+    if (spp_end <= spp_begin) return fail(AVR_ERR_ARG, "empty probe sample range");
+    for (int k = 0; k < 3 * n; ++k)
+        if (candidates[k] < 1 || candidates[k] > 255) return fail(AVR_ERR_ARG, "majorant resolution must be 1..255");
+    HIP_TRY(hipSetDevice(c->device));
+    // the probes render into the film: keep its sums and put them back afterwards
+    const size_t np = (size_t)c->film.width * c->film.height;
+    const size_t nd = (4 + 2 * (size_t)std::max(0, c->film.nbuckets)) * np;
+    double *saved = nullptr;
+    HIP_TRY(dalloc(&saved, nd));
+    int rc = avr_film_export_device(c, saved);
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (!rc && (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess)) rc = fail(AVR_ERR_HIP, "event");
+    float best = -1.f;
+    int bestk = 0;
+    // one untimed probe first: the first render after a scene change builds one-off tables
+    for (int k = -1; k < n && !rc; ++k) {
+        const int *r = candidates + 3 * (k < 0 ? 0 : k);
+        if ((rc = build_majorant(c, r))) break;
+        if (hipEventRecord(e0, c->stream) != hipSuccess) { rc = fail(AVR_ERR_HIP, "event record"); break; }
+        if ((rc = avr_render(c, spp_begin, spp_end, seed, max_depth))) break;
+        if (hipEventRecord(e1, c->stream) != hipSuccess || hipEventSynchronize(e1) != hipSuccess) {
+            rc = fail(AVR_ERR_HIP, "event sync");
+            break;
+        }
+        float t = 0.f;
+        (void)hipEventElapsedTime(&t, e0, e1);
+        if (k < 0) continue;
+        if (ms) ms[k] = t;
+        if (best < 0 || t < best) { best = t; bestk = k; }
+    }
+    if (!rc) rc = build_majorant(c, candidates + 3 * bestk);
+    if (!rc) {
+        // restore the film sums
+        double *d = saved;
+        HIP_TRY(hipMemcpyAsync(c->film.rgb_sum, d, 3 * np * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
+        HIP_TRY(hipMemcpyAsync(c->film.w_sum, d + 3 * np, np * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
+        if (c->film.nbuckets > 0)
+            HIP_TRY(hipMemcpyAsync(c->film.bucket_sum, d + 4 * np, 2 * np * c->film.nbuckets * sizeof(double),
+                                   hipMemcpyDeviceToDevice, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        for (int i = 0; i < 3; ++i) chosen[i] = candidates[3 * bestk + i];
+    }
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    (void)hipFree(saved);
+    if (!rc) rc = avr_reset_stats(c);
+    return rc;
 }
 
 static void pc1d_build(const float *f, int n, float mn, float mx, float *cdf, float *funcInt);

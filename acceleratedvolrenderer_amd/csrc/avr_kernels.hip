@@ -21,6 +21,7 @@
 #include "avr_vdb.h"
 #include "avr_envmap.h"
 #include "avr_flip.h"
+#include "avr_boundary.h"
 
 #include <type_traits>
 
@@ -45,6 +46,11 @@ struct DevMedium {
     // lookup is ONE 32-B-aligned access inside one cache line instead of 8 scattered taps
     // in 2-4 lines. 8x the grid's memory ((n+1)^3 x 32 B; 34 GB at 1024^3 of the 288 GB).
     const float4 *fat;
+    // medium interface (f3): 0 = the bounds box (the default scene model), 1 = a sphere
+    // {cx, cy, cz, r} in render space (a shape with no material and MediumInterface(inside =
+    // this medium, outside = none): interaction.cpp:91-97 SkipIntersection)
+    int boundary;
+    float sph[4];
     int unit_box;          // bounds extent exactly 1 on every axis: Offset's divisions are by 1.0f
     // medium type: 0 GridMedium (media.h:265-352), 1 HomogeneousMedium (media.h:217-262),
     // 2 CloudMedium (media.h:430-528). Types 1 and 2 have one majorant segment (the
@@ -126,6 +132,23 @@ __device__ __forceinline__ Spec film_sample_lambda_fast(const DevFilm &f, float 
 }
 __device__ __forceinline__ float film_lambda_pdf(const DevFilm &f, float l) {
     return f.nbuckets > 0 ? 1 / (f.lmax - f.lmin) : visible_wavelength_pdf(l);
+}
+
+// Interface sphere (DevMedium::boundary 1). Model, shared with the oracle: the medium lives
+// inside the sphere; a camera ray that crosses it starts its first medium segment at the
+// entry point o + t0 d (pbrt: no medium outside, so no SampleT_maj before the entry and
+// SkipIntersection there, integrators.cpp:1118-1122); every medium segment and shadow ray
+// ends at the sphere exit computed from its own origin (pbrt re-intersects from the spawned
+// point); a ray that does not cross the sphere sees no medium. Sphere::BasicIntersect's
+// interval quadric (avr_boundary.h); origins are not offset by intersection error bounds,
+// so paths match pbrt's statistically, the oracle's bit for bit.
+__device__ __forceinline__ float interface_exit(const DevMedium &m, V3 o, V3 d) {
+    const shape::Hits h = shape::sphere_hits(V3{m.sph[0], m.sph[1], m.sph[2]}, m.sph[3], o, d);
+    return h.type == shape::kInsideOneHit ? h.t0 : (h.type == shape::kOutsideTwoHits ? h.t1 : 0.f);
+}
+__device__ __forceinline__ V3 interface_entry(const DevMedium &m, V3 o, V3 d) {
+    const shape::Hits h = shape::sphere_hits(V3{m.sph[0], m.sph[1], m.sph[2]}, m.sph[3], o, d);
+    return h.type == shape::kOutsideTwoHits ? o + d * h.t0 : o;
 }
 
 struct PathSoA {
@@ -712,6 +735,7 @@ __global__ void __launch_bounds__(256) k_camera(Params P) {
         if (P.cam.type == 0) ray = {pCam, {0.f, 0.f, 1.f}};
         else ray = {{0.f, 0.f, 0.f}, normalize(pCam)};
         ray = xf_ray(P.cam.render_from_camera, ray, nullptr, /*forward=*/true);
+        if (P.med.boundary) ray.o = interface_entry(P.med, ray.o, ray.d);
         P.ps.o[id] = to4(ray.o);
         P.ps.d[id] = to4(ray.d);
         P.ps.lambda[id] = to4(lam.l);
@@ -802,7 +826,8 @@ __global__ void __launch_bounds__(256) k_medium(Params P) {
                 r_l = r_l * (T_maj * sigma_maj / pdf);
                 return beta.nonzero() && r_u.nonzero();
             };
-            Spec T_maj = sample_t_maj(P.med, maj, Ray{o, d}, kInf, u0, rng, sig_a, sig_s, Le_l, lamv, nLookup, nSteps, cb);
+            const float tMax = P.med.boundary ? interface_exit(P.med, o, d) : kInf;
+            Spec T_maj = sample_t_maj(P.med, maj, Ray{o, d}, tMax, u0, rng, sig_a, sig_s, Le_l, lamv, nLookup, nSteps, cb);
 
             if (scattered) {
                 // ---- SampleLd for the medium interaction (integrators.cpp:1282-1338) ----
@@ -961,7 +986,8 @@ __global__ void __launch_bounds__(256) k_shadow(Params P) {
             }
             return T_ray.nonzero();
         };
-        Spec T_maj = sample_t_maj(P.med, maj, Ray{o, d}, 1 - kShadowEpsilon, u, rng, sig_a, sig_s, Le_l, lamv,
+        const float tMax = P.med.boundary ? fminf_(1 - kShadowEpsilon, interface_exit(P.med, o, d)) : 1 - kShadowEpsilon;
+        Spec T_maj = sample_t_maj(P.med, maj, Ray{o, d}, tMax, u, rng, sig_a, sig_s, Le_l, lamv,
                                   nLookup, nSteps, cb);
         T_ray = T_ray * (T_maj / T_maj.v0);
         r_l = r_l * (T_maj / T_maj.v0);
@@ -1522,7 +1548,7 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
                     if (P.cam.type == 0) ray = {pCam, {0.f, 0.f, 1.f}};
                     else ray = {{0.f, 0.f, 0.f}, normalize(pCam)};
                     ray = xf_ray(P.cam.render_from_camera, ray, nullptr, /*forward=*/true);
-                    po = ray.o;
+                    po = m.boundary ? interface_entry(m, ray.o, ray.d) : ray.o;
                     pd = ray.d;
                     L = Spec::c(0.f);
                     beta = r_u = r_l = sconst<S>(1.f);
@@ -1555,7 +1581,9 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
             if (segPending) {
                 rng.set_sequence(seqA, seqB);
                 if (mode == M_SHADOW) u = rng.uniform();
-                seg_start(po, sd, mode == M_SHADOW ? 1 - kShadowEpsilon : kInf);
+                float tMax = mode == M_SHADOW ? 1 - kShadowEpsilon : kInf;
+                if (m.boundary) tMax = fminf_(tMax, interface_exit(m, po, sd));
+                seg_start(po, sd, tMax);
                 segPending = false;
             }
         }

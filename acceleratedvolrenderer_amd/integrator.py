@@ -105,6 +105,16 @@ class VolPathIntegrator:
         """Integrator::Create-style factory from a pbrt ParameterDictionary-like dict."""
         return cls(scene, device=device, **cls.create_params(name, params, maxdepth_override), **kw)
 
+    def tune_majorant(self, candidates=(1, 2, 4, 8, 16), probe=(0, 1)):
+        """The fast mode's tuned majorant: time one probe render of sample
+        indices [probe[0], probe[1]) per candidate majorant resolution (r^3) on the device and
+        keep the fastest (avr_tune_majorant; the film is left as it was). Any conservative
+        majorant gives the same estimator in expectation; only pbrt's own resolution (16^3
+        grids, 64^3 NanoVDB) replays pbrt's sample streams. Returns (chosen, {r: probe ms})."""
+        cands = [(int(r),) * 3 for r in candidates]
+        chosen, ms = self.ctx.tune_majorant(cands, probe[0], probe[1], self.seed, self.maxdepth)
+        return chosen, {c[0]: float(t) for c, t in zip(cands, ms)}
+
     def render(self, spp_begin=0, spp_end=None, clear=True):
         """Render sample indices [spp_begin, spp_end); returns (rgb_sum, w_sum) fp64."""
         if spp_end is None:

@@ -533,8 +533,12 @@ def _bounding_sphere_radius(pmin, pmax):
 class Scene:
     """Resolved render-space scene (CameraWorld rendering space, cameras.cpp:35-41)."""
 
-    def __init__(self, camera, film, medium, lights, sampler=None):
+    def __init__(self, camera, film, medium, lights, sampler=None, interface_sphere=None):
+        """interface_sphere: None (the medium's bounds box is its interface shape) or
+        (world-space centre, radius) of a sphere without material whose MediumInterface holds
+        the medium inside (pbrt's `AttributeBegin MediumInterface "cloud" "" Shape "sphere"`)."""
         self.camera, self.film, self.medium, self.lights = camera, film, medium, list(lights)
+        self.interface_sphere = interface_sphere
         self.sampler = sampler if sampler is not None else IndependentSampler()
         if len(self.lights) > 8:
             raise ValueError("at most 8 lights")
@@ -551,6 +555,17 @@ class Scene:
                       for z in (medium.p0[2], medium.p1[2])])
         rc = (rfm @ c.T).T[:, :3]
         self.scene_radius = _bounding_sphere_radius(rc.min(axis=0), rc.max(axis=0))
+        self.interface_sphere_render = None
+        if interface_sphere is not None:
+            cw, r = interface_sphere
+            if not float(r) > 0:
+                raise ValueError("interface sphere radius must be > 0")
+            cr = (self.render_from_world @ np.array([*map(float, cw), 1.0]))[:3].astype(np.float32)
+            self.interface_sphere_render = np.array([*cr, np.float32(r)], np.float32)
+            # the sphere is then the scene's only shape: Sphere::Bounds (shapes.cpp) -> sceneRadius
+            lo = cr.astype(np.float64) - float(r)
+            hi = cr.astype(np.float64) + float(r)
+            self.scene_radius = _bounding_sphere_radius(lo, hi)
         self.light_types = np.array([l.type_id for l in self.lights], np.int32)
         self.light_w = np.stack([l.render_direction(self.render_from_world) for l in self.lights]).astype(
             np.float32) if self.lights else np.zeros((0, 3), np.float32)

@@ -10,6 +10,9 @@ S-uniform  (config C2): GridMedium n^3 of 1.0 on [0,1]^3, orthographic camera lo
 S-cloud    (metric input): GridMedium n^3 filled with CloudMedium::Density (media.h:496-520,
            density 1, wispiness 1, frequency 5) at voxel centres; sigma_a=0, sigma_s=1,
            scale 4 (albedo 1), g 0.877, distant light + dim sky, perspective 1280x720, maxdepth 100.
+S-sphere   (SURVEY §8f row 3, medium interfaces) S-uniform's medium and variants bounded by an
+           interface sphere (a shape with no material, MediumInterface inside = the medium),
+           centre and radius in world space; by default inscribed in the [0,1]^3 grid box.
 S-vdb      NanoVDBMedium over a sparse copy of a dense grid (index i at world i / n, so the
            world bbox of an n^3 grid is [0, 1]^3), S-uniform's camera and light variants.
 """
@@ -59,6 +62,17 @@ def s_uniform(n=256, width=512, height=512, variant="absorber", density=None):
                              screenwindow=(-0.5, 0.5, -0.5, 0.5))
     film = RGBFilm(width, height)
     return Scene(cam, film, med, lights)
+
+
+def s_sphere(n=32, width=64, height=64, variant="scatter", density=None, center=(0.5, 0.5, 0.5), radius=0.45,
+             camera="orthographic"):
+    """S-uniform's scene with the medium bounded by an interface sphere instead of its box."""
+    base = s_uniform(n=n, width=width, height=height, variant=variant, density=density)
+    cam = base.camera
+    if camera == "perspective":
+        cam = PerspectiveCamera(fov=50.0, pos=(0.9, 0.7, -1.1), look=(0.5, 0.5, 0.5), up=(0.0, 1.0, 0.0))
+    return Scene(cam, base.film, base.medium, base.lights, sampler=base.sampler,
+                 interface_sphere=(tuple(float(v) for v in center), float(radius)))
 
 
 def vdb_grid(density, index_to_world=None, index_min=(0, 0, 0), background=0.0):

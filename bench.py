@@ -77,6 +77,9 @@ def parse():
     p.add_argument("--mode", default="replay", choices=["replay", "fast"],
                    help="render mode: replay (canonical math, per-sample CPU parity; the headline) or fast "
                         "(hardware transcendentals, statistical parity)")
+    p.add_argument("--majorant-res", type=int, default=None,
+                   help="GridMedium majorant resolution per axis: 0 = pbrt's 16^3 (replay default), -1 = tuned "
+                        "on the device among 1,2,4,8,16 (fast-mode default, outside the timed region)")
     p.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     return p.parse_args()
 
@@ -171,8 +174,9 @@ def pmc_passes(args, kernel_substr="k_paths", timeout_s=240):
     child = [sys.executable, os.path.join(ROOT, "bench.py"), "--pmc-child", "--no-cpu-baseline", "--pmc", "off",
              "--steps", "2", "--warmup", "1"]
     for k in ("res", "width", "height", "spp_per_step", "max_paths", "kernel", "medium", "refill_min", "grid_layout",
-              "dda_budget", "zsobol_table", "sampler", "filter", "mode"):
-        child += [f"--{k.replace('_', '-')}", str(getattr(args, k))]
+              "dda_budget", "zsobol_table", "sampler", "filter", "mode", "majorant_res"):
+        if getattr(args, k) is not None:
+            child += [f"--{k.replace('_', '-')}", str(getattr(args, k))]
     out = {}
     tmp = tempfile.mkdtemp(prefix="avr_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
     try:
@@ -269,6 +273,8 @@ def main():
     else:
         scene = scenes.s_cloud(density, width=args.width, height=args.height, sampler=args.sampler, spp=spp_total,
                                filter=args.filter)
+        if args.majorant_res and args.majorant_res > 0:
+            scene.medium.majorant_res = (args.majorant_res,) * 3
     integ = VolPathIntegrator(scene, maxdepth=scenes.CLOUD_MAXDEPTH, spp=args.spp_per_step, seed=0, device=dev,
                               max_paths=args.max_paths, kernel=args.kernel, grid_layout=args.grid_layout,
                               mode=args.mode)
@@ -277,6 +283,12 @@ def main():
     if args.dda_budget:
         integ.ctx.set_dda_budget(args.dda_budget)
     integ.ctx.set_sampler_table(args.zsobol_table)
+    maj_res = tuple(scene.medium.majorant_res)
+    tune_ms = None
+    if args.majorant_res == -1 or (args.majorant_res is None and args.mode == "fast" and vdb is None):
+        maj_res, tune_ms = integ.tune_majorant(probe=(0, 1))
+        log(f"tuned majorant {maj_res} (probe ms {tune_ms})")
+        args.majorant_res = maj_res[0]   # the counter passes (child processes) render the same majorant
 
     def step(k):
         # asynchronous on the context stream: steps queue back to back
@@ -401,6 +413,7 @@ def main():
             "config": {"workload": f"S-cloud-{n} {'NanoVDBMedium' if vdb is not None else 'GridMedium'}, perspective {args.width}x{args.height}, "
                                    f"{S} spp/step/GPU, maxdepth {scenes.CLOUD_MAXDEPTH}, {args.sampler} sampler "
                                    f"(pixelsamples {spp_total}), {args.filter} filter, {args.mode} mode",
+                       "majorant_res": list(maj_res), "majorant_tuning_ms": tune_ms,
                        "global_batch": samples // args.steps, "parallelism": f"sample-shard x{world}",
                        "sample_index_wrap": wrap},
             "roofline": {

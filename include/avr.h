@@ -174,6 +174,15 @@ int avr_medium_rgbgrid(avr_context *ctx, int nx, int ny, int nz, const float bou
                        const float render_from_medium[16], const float medium_from_render[16],
                        const float *sigma_a, const float *sigma_s, float sigma_scale, float g, const float *Le,
                        const float *illuminant, float Le_scale);
+/* Medium interface of the current medium (pbrt: a shape with no material
+ * whose MediumInterface has this medium inside and none outside, interaction.cpp:91-97
+ * SkipIntersection, shapes.h:152-200 Sphere). radius > 0: a sphere of that radius at `center`
+ * (render space) bounds the medium — camera rays start their first segment where they enter
+ * it, every segment and shadow ray ends at its exit, rays that miss it see no medium (the
+ * medium's SampleT_maj still clips to its bounds box, media.h:325-328); radius <= 0 returns
+ * to the default model (the bounds box is the interface). Reset by every avr_medium_* call.
+ * Both kernel organisations. */
+int avr_medium_boundary_sphere(avr_context *ctx, const float center[3], float radius);
 /* The medium bounds the last avr_medium_* call set (medium space, min xyz then max xyz). */
 int avr_medium_bounds(avr_context *ctx, float bounds[6]);
 /* Fill d_out[first .. first+count) of an n^3 grid with CloudMedium::Density
@@ -182,6 +191,19 @@ int avr_generate_cloud(avr_context *ctx, float *d_out, int n, long long first, l
                        float wispiness, float frequency);
 /* Copy the device majorant grid to host (mres product floats). */
 int avr_read_majorant(avr_context *ctx, float *out);
+/* Rebuild the current medium's majorant grid at res[3] cells (1..255 per axis) from the
+ * medium's own data (GridMedium / RGBGridMedium / NanoVDBMedium; the single-segment media
+ * refuse). pbrt fixes 16^3 for grids (media.cpp:229) and 64^3 for NanoVDB (media.cpp:521):
+ * replay parity with pbrt assumes those; any conservative majorant gives the same estimator
+ * in expectation (SURVEY §7 "fast": tuned majorant, statistical parity). The persistent
+ * kernel keeps grids of up to 4096 cells in LDS; finer grid majorants run the wavefront kernels. */
+int avr_set_majorant_res(avr_context *ctx, const int res[3]);
+/* The "tuned majorant": render the probe sample range [spp_begin, spp_end) once per
+ * candidate resolution (n triples in `candidates`), timed with HIP events on the context
+ * stream, keep the fastest (chosen[3]; per-candidate times in ms[n] when non-null). The
+ * film sums are restored and the work counters reset afterwards. */
+int avr_tune_majorant(avr_context *ctx, const int *candidates, int n, int spp_begin, int spp_end, int seed,
+                      int max_depth, int chosen[3], float *ms);
 
 /* Lights (lights.h:244-305 DistantLight, lights.cpp:950-972 UniformInfiniteLight).
  * type 0 = distant: w = render-space unit vector towards the light

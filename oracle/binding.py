@@ -77,6 +77,7 @@ class OracleScene(ctypes.Structure):
         ("light_rfl", (ctypes.c_float * 9) * 8), ("light_lfr", (ctypes.c_float * 9) * 8),
         ("light_illuminant", c_float_p),
         ("film_nbuckets", ctypes.c_int), ("film_lambda_min", ctypes.c_float), ("film_lambda_max", ctypes.c_float),
+        ("boundary", ctypes.c_int), ("sphere", ctypes.c_float * 4),
     ]
 
 
@@ -406,6 +407,10 @@ class OracleRun:
         s.film_nbuckets = int(getattr(f, "nbuckets", 0))
         s.film_lambda_min = float(getattr(f, "lambdamin", 360.0))
         s.film_lambda_max = float(getattr(f, "lambdamax", 830.0))
+        sph = getattr(scene, "interface_sphere_render", None)
+        s.boundary = 1 if sph is not None else 0
+        if sph is not None:
+            s.sphere[:] = [float(v) for v in sph]
         s.max_depth = int(max_depth)
         s.seed = int(seed)
         smp = scene.sampler

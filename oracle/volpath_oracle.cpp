@@ -819,6 +819,9 @@ typedef struct OracleScene {
     // [lambda_min, lambda_max] and per-pixel spectral buckets next to the RGB sums
     int film_nbuckets;
     float film_lambda_min, film_lambda_max;
+    // medium interface: 0 the bounds box, 1 a sphere {cx, cy, cz, r} in render space
+    int boundary;
+    float sphere[4];
 } OracleScene;
 
 }  // extern "C"
@@ -1425,6 +1428,16 @@ static Spec SampleT_maj(const SceneView &sv, Ray ray, float tMax, float u, RNG &
     return Spec::Const(1.f);
 }
 
+// Interface sphere (OracleScene::boundary 1; defined after the graph section's SphereHits).
+// The medium is inside the sphere (a shape without material whose MediumInterface is
+// (inside = medium, outside = none)): a camera ray moves to its entry point before its first
+// medium segment — pbrt samples no medium before it and calls SkipIntersection there
+// (integrators.cpp:1118-1122) — and every segment / shadow ray ends at the sphere exit seen
+// from its own origin (pbrt re-intersects from the spawned point). Origins are not offset by
+// the intersection's error bounds (the same model as the device).
+static float InterfaceExit(const OracleScene &s, V3 o, V3 d);
+static V3 InterfaceEntry(const OracleScene &s, V3 o, V3 d);
+
 // VolPathIntegrator::SampleLd for a medium interaction — integrators.cpp:1282-1399
 static Spec SampleLd(const SceneView &sv, V3 p, V3 wo, const Lambda &l, Sampler &sampler, Spec beta, Spec r_p) {
     const OracleScene &s = sv.s;
@@ -1468,8 +1481,10 @@ static Spec SampleLd(const SceneView &sv, V3 p, V3 wo, const Lambda &l, Sampler 
     Ray lightRay = {p, pOutside - p};
     Spec T_ray = Spec::Const(1.f), r_l = Spec::Const(1.f), r_u = Spec::Const(1.f);
     RNG rng(HashBytes(&lightRay.o, 12), HashBytes(&lightRay.d, 12));
-    // The box boundary only toggles the medium; SampleT_maj clips to the same bounds.
+    // The box boundary only toggles the medium; SampleT_maj clips to the same bounds. An
+    // interface sphere ends the medium part at its exit (Intersect(lightRay, 1 - eps)->tHit).
     float tMax = 1 - ShadowEpsilon;
+    if (s.boundary) tMax = std::min<float>(tMax, InterfaceExit(s, lightRay.o, lightRay.d));
     float uu = rng.Uniform();
     Spec T_maj = SampleT_maj(sv, lightRay, tMax, uu, rng, l, [&](V3, const MediumProps &mp, Spec sigma_maj, Spec Tm) {
         Spec sigma_n = ClampZero(sigma_maj - mp.sigma_a - mp.sigma_s);
@@ -1503,10 +1518,11 @@ static Spec Li(const SceneView &sv, Ray ray, Lambda &l, Sampler &sampler, int *n
     bool specularBounce = false;
     int depth = 0;
     const int maxDepth = s.max_depth;
+    if (s.boundary) ray.o = InterfaceEntry(s, ray.o, ray.d);
     while (true) {
         // ray.medium is the grid medium (see header: the interface box only toggles it)
         bool scattered = false, terminated = false;
-        float tMax = Infinity;
+        float tMax = s.boundary ? InterfaceExit(s, ray.o, ray.d) : Infinity;
         uint64_t hash0 = HashFloat(sampler.Get1D());
         uint64_t hash1 = HashFloat(sampler.Get1D());
         RNG rng(hash0, hash1);
@@ -2261,6 +2277,7 @@ static inline float Average(const std::vector<float> &v) {
 }
 }  // namespace graphm
 
+
 // LightingCalculator::GetLightVector (lighting_calculator.cpp:84-155) with
 // ComputeRaysToSphere(rayInSphere = nullopt) (util.h:814-840): per vertex (list index =
 // vertex id), disk points around vertex - inDir * maxDistToCenter * 2, a ray along inDir
@@ -2467,3 +2484,15 @@ void oracle_cloud_grid(int n, int z0, int z1, float *out) {
 }
 
 }  // extern "C"
+
+// Interface sphere helpers (declared before SampleLd / Li), C++ linkage
+namespace oracle {
+static float InterfaceExit(const OracleScene &s, V3 o, V3 d) {
+    const graphm::Hits h = graphm::SphereHits(V3{s.sphere[0], s.sphere[1], s.sphere[2]}, s.sphere[3], o, d);
+    return h.type == graphm::InsideOneHit ? h.t[0] : (h.type == graphm::OutsideTwoHits ? h.t[1] : 0.f);
+}
+static V3 InterfaceEntry(const OracleScene &s, V3 o, V3 d) {
+    const graphm::Hits h = graphm::SphereHits(V3{s.sphere[0], s.sphere[1], s.sphere[2]}, s.sphere[3], o, d);
+    return h.type == graphm::OutsideTwoHits ? o + d * h.t[0] : o;
+}
+}  // namespace oracle

@@ -171,3 +171,54 @@ def test_libm_modes_agree_statistically_and_mostly_per_sample():
     rc, _ = c.render(0, spp, nthreads=4)
     noise = np.sqrt(np.mean((rc - ra) ** 2))
     assert np.sqrt(np.mean((rb - ra) ** 2)) <= 0.25 * noise
+
+
+def _sphere_absorber_expectation(W, H, R, sub=64):
+    """Per-pixel E[exp(-chord)] of the orthographic S-sphere absorber (sigma_t = 1, density 1
+    inside the sphere): the box filter (radius 0.5) spreads a pixel's samples uniformly over
+    the pixel square; chord = 2 sqrt(R^2 - rho^2) of the ray at distance rho from the centre."""
+    out = np.empty((H, W))
+    o = (np.arange(sub) + 0.5) / sub
+    for py in range(H):
+        for px in range(W):
+            x = (px + o[None, :]) / W - 0.5
+            y = (py + o[:, None]) / H - 0.5
+            chord = 2 * np.sqrt(np.maximum(0.0, R * R - x * x - y * y))
+            out[py, px] = np.exp(-chord).mean()
+    return out
+
+
+def test_interface_sphere_absorber_chord_transmittance():
+    """f3 interface sphere (interaction.cpp:91-97 SkipIntersection, shapes.h:152-200): an
+    absorbing medium bounded by a sphere inscribed in its box transmits exp(-chord) per ray
+    (Beer-Lambert along the sphere chord), and pixels whose rays all miss the sphere see no
+    medium at all (every sample exactly 1, where the box interface would attenuate)."""
+    n, W, H, R, spp = 16, 8, 8, 0.45, 256
+    sc = scenes.s_sphere(n=n, width=W, height=H, variant="absorber", radius=R)
+    run = ob.OracleRun(sc, max_depth=5)
+    want = _sphere_absorber_expectation(W, H, R)
+    got = np.zeros((H, W))
+    for py in range(H):
+        for px in range(W):
+            Ls = np.array([run.pixel_sample(px, py, s)[0][0] for s in range(spp)])
+            assert set(np.unique(Ls)).issubset({0.0, 1.0})
+            got[py, px] = Ls.mean()
+    # the corner pixels' rays never cross the sphere: no attenuation at all
+    for px, py in ((0, 0), (W - 1, 0), (0, H - 1), (W - 1, H - 1)):
+        assert got[py, px] == 1.0 and want[py, px] == 1.0
+    var = np.sum(want * (1 - want)) / spp
+    assert abs(got.sum() - want.sum()) < 4 * np.sqrt(var)
+    # per pixel, within 5 binomial standard deviations (plus one sample of slack)
+    assert np.all(np.abs(got - want) <= 5 * np.sqrt(want * (1 - want) / spp) + 1.0 / spp)
+
+
+def test_interface_sphere_box_clips_a_larger_sphere():
+    """A sphere larger than the medium box: SampleT_maj still clips to the bounds
+    (media.h:325-328), so rays through the box see the box's Beer-Lambert answer."""
+    n, spp = 8, 512
+    sc = scenes.s_sphere(n=n, width=8, height=8, variant="absorber", radius=2.0)
+    run = ob.OracleRun(sc, max_depth=5)
+    Ls = np.array([run.pixel_sample(px, py, s)[0][0] for px in range(2, 6) for py in range(2, 6)
+                   for s in range(spp // 16)])
+    want = np.exp(-(1 - 0.25 / n))
+    assert abs(Ls.mean() - want) < 4 * np.sqrt(want * (1 - want) / len(Ls))
