@@ -36,6 +36,7 @@ class AvrStats(ctypes.Structure):
         ("ms_film", ctypes.c_double),
         ("ms_total", ctypes.c_double),
         ("ms_setup", ctypes.c_double),
+        ("ms_binning", ctypes.c_double),
     ]
 
     def as_dict(self):
@@ -91,6 +92,7 @@ SIGNATURES = {
     "avr_set_stream": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "avr_set_kernel_mode": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "avr_set_render_mode": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "avr_set_ray_binning": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "avr_set_majorant_res": (ctypes.c_int, [ctypes.c_void_p, c_int_p]),
     "avr_medium_boundary_sphere": (ctypes.c_int, [ctypes.c_void_p, c_float_p, ctypes.c_float]),
     "avr_tune_majorant": (ctypes.c_int, [ctypes.c_void_p, c_int_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
@@ -258,6 +260,9 @@ class Context:
                                           int(spp_end), int(seed), int(max_depth), chosen.ctypes.data_as(c_int_p),
                                           ms.ctypes.data_as(c_float_p)))
         return tuple(int(v) for v in chosen), ms
+
+    def set_ray_binning(self, on):
+        _check(self.lib.avr_set_ray_binning(self.h, 1 if on else 0))
 
     def set_kernel_mode(self, mode):
         """0 = persistent megakernel (default), 1 = wavefront queues."""

@@ -94,6 +94,9 @@ struct avr_context {
     int paths_grid[128] = {};
     void (*kpaths[128])(avr::Params) = {};
     int render_mode = 0;      // 0 replay (canonical math, per-sample parity), 1 fast (hardware math)
+    int ray_binning = 0;      // wavefront organisation: counting-sort queues by (majorant cell, octant)
+    int *d_bin_keys = nullptr, *d_bin_out = nullptr, *d_bin_hist = nullptr;
+    long long bin_cap = 0;
     // pixel sampler (avr_set_sampler) and filter (avr_set_filter)
     int sampler_kind = 0;     // 0 IndependentSampler, 1 ZSobolSampler
     int sampler_spp = 16;     // samplesPerPixel of the sampler (ZSobol's Morton layout)
@@ -533,6 +536,13 @@ int avr_set_render_mode(avr_context *c, int mode) {
     return AVR_OK;
 }
 
+int avr_set_ray_binning(avr_context *c, int on) {
+    AVR_QUIESCE(c);
+    if (!c || (on != 0 && on != 1)) return fail(AVR_ERR_ARG, "ray binning must be 0 or 1");
+    c->ray_binning = on;
+    return AVR_OK;
+}
+
 int avr_set_kernel_mode(avr_context *c, int mode) {
     if (!c || (mode != 0 && mode != 1)) return fail(AVR_ERR_ARG, "kernel mode must be 0 (persistent) or 1 (wavefront)");
     c->kernel_mode = mode;
@@ -554,6 +564,7 @@ int avr_context_destroy(avr_context *c) {
     if (c->film.bucket_sum) (void)hipFree(c->film.bucket_sum);
     if (c->d_counts) (void)hipFree(c->d_counts);
     if (c->d_heads) (void)hipFree(c->d_heads);
+    for (int *b : {c->d_bin_keys, c->d_bin_out, c->d_bin_hist}) if (b) (void)hipFree(b);
     if (c->d_advance) (void)hipFree(c->d_advance);
     if (c->d_filter) (void)hipFree(c->d_filter);
     if (c->d_temperature) (void)hipFree(c->d_temperature);
@@ -1260,6 +1271,37 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
             HIP_TRY(hipMemsetAsync(c->d_counts + 2, 0, sizeof(int), c->stream));
             p.queue_in = first ? nullptr : c->d_queue[cur];
             p.count_in = c->d_counts + cur;
+            const int nbins = 8 * c->med.mres[0] * c->med.mres[1] * c->med.mres[2];
+            const bool bin = c->ray_binning && nbins <= 8 * 4096;
+            if (bin && c->bin_cap < n0) {
+                for (int **b : {&c->d_bin_keys, &c->d_bin_out}) {
+                    if (*b) (void)hipFree(*b);
+                    HIP_TRY(dalloc(b, (size_t)n0));
+                }
+                if (!c->d_bin_hist) HIP_TRY(dalloc(&c->d_bin_hist, (size_t)8 * 4096));
+                c->bin_cap = n0;
+            }
+            auto bin_queue = [&](const int *queue, const int *count_p, const float4 *o, const float4 *d) -> int {
+                HIP_TRY(hipMemsetAsync(c->d_bin_hist, 0, nbins * sizeof(int), c->stream));
+                const int nbk = blocks_for(count);
+                hipLaunchKernelGGL(avr::k_bin_count, dim3(nbk), dim3(256), 0, c->stream, c->med, queue, count_p, o, d,
+                                   c->d_bin_keys, c->d_bin_hist);
+                hipLaunchKernelGGL(avr::k_bin_scan, dim3(1), dim3(1024), 0, c->stream, c->d_bin_hist, nbins);
+                hipLaunchKernelGGL(avr::k_bin_scatter, dim3(nbk), dim3(256), 0, c->stream, queue, count_p,
+                                   c->d_bin_keys, c->d_bin_hist, c->d_bin_out);
+                HIP_TRY(hipGetLastError());
+                return AVR_OK;
+            };
+            // camera rays keep their pixel order (already coherent); later depths are binned
+            if (bin && !first) {
+                EV_MARK(s0);
+                int rc = bin_queue(c->d_queue[cur], c->d_counts + cur, c->ps.o, c->ps.d);
+                if (rc) return rc;
+                EV_MARK(s1);
+                c->timed.push_back({s0, s1, &avr_stats::ms_binning, false});
+                HIP_TRY(hipMemcpyAsync(c->d_queue[cur], c->d_bin_out, (size_t)count * sizeof(int),
+                                       hipMemcpyDeviceToDevice, c->stream));
+            }
             p.queue_out = c->d_queue[nxt];
             p.count_out = c->d_counts + nxt;
             p.shadow_count = c->d_counts + 2;
@@ -1269,11 +1311,22 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
             else hipLaunchKernelGGL(avr::k_medium<false>, dim3(nb), dim3(256), 0, c->stream, p);
             HIP_TRY(hipGetLastError());
             EV_MARK(m1);
+            p.sh_perm = nullptr;
+            if (bin) {
+                // the shadow rays k_medium just pushed, binned the same way (read through sh_perm)
+                EV_MARK(s2);
+                int rc = bin_queue(nullptr, c->d_counts + 2, c->sh.o, c->sh.d);
+                if (rc) return rc;
+                EV_MARK(s3);
+                c->timed.push_back({s2, s3, &avr_stats::ms_binning, false});
+                p.sh_perm = c->d_bin_out;
+            }
+            EV_MARK(m15);
             hipLaunchKernelGGL(avr::k_shadow, dim3(nb), dim3(256), 0, c->stream, p);
             HIP_TRY(hipGetLastError());
             EV_MARK(m2);
             c->timed.push_back({m0, m1, &avr_stats::ms_medium, true});
-            c->timed.push_back({m1, m2, &avr_stats::ms_shadow, false});
+            c->timed.push_back({m15, m2, &avr_stats::ms_shadow, false});
             // the queue length decides the next launch: the wavefront organisation syncs here
             HIP_TRY(hipMemcpyAsync(c->h_count, c->d_counts + nxt, sizeof(int), hipMemcpyDeviceToHost, c->stream));
             HIP_TRY(hipStreamSynchronize(c->stream));

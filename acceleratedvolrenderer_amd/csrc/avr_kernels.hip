@@ -199,6 +199,7 @@ struct Params {
     int dda_budget;                   // k_paths: majorant cells a lane may cross per tracking
                                       //   iteration before yielding (bounds DDA divergence)
     int rec_mode;                     // k_film: 1 = read k_paths' records (ps.rec), 0 = wavefront SoA
+    const int *sh_perm;               // k_shadow: processing order of the shadow queue (ray binning), or null
     int fast;                         // render mode: 0 replay (canonical math), 1 fast (hardware math)
 };
 
@@ -958,8 +959,9 @@ __global__ void __launch_bounds__(256) k_shadow(Params P) {
     const float *maj = stage_majorant(P.med, s_maj);
     const int count = *P.shadow_count;
     unsigned long long nLookup = 0, nIn = 0, nSteps = 0;
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < count; i += gridDim.x * blockDim.x) {
+    for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < count; k += gridDim.x * blockDim.x) {
         ++nIn;
+        const int i = P.sh_perm ? P.sh_perm[k] : k;   // binned order (avr_set_ray_binning)
         const int path = P.sh.path[i];
         const V3 o = from4(P.sh.o[i]);
         const V3 d = from4(P.sh.d[i]);
@@ -1141,6 +1143,70 @@ __global__ void k_advance(uint64_t *adv, long long base, int S) {
     }
     adv[2 * s] = accMult;
     adv[2 * s + 1] = accPlus;
+}
+#endif
+
+// ---------------------------------------------------------------------------
+// Ray binning for the wavefront organisation (north star: "density-grid fetches coalesced
+// along sorted ray packets"): before a k_medium / k_shadow launch the
+// queue is counting-sorted by key = (majorant cell of the ray origin, direction octant), so
+// the 64 lanes of a wave start in the same majorant cell heading the same way and their
+// trilinear gathers share cache lines. Order only: every path's result is unchanged.
+#ifndef AVR_KPATHS_TU
+__device__ __forceinline__ int ray_bin(const DevMedium &m, V3 o, V3 d) {
+    const V3 pm = xf_point_lr(m.medium_from_render, o);
+    int c[3];
+    const float pv[3] = {pm.x, pm.y, pm.z};
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const float u = (pv[a] - m.bmin[a]) / (m.bmax[a] - m.bmin[a]);
+        int k = (int)(u * (float)m.mres[a]);
+        c[a] = k < 0 ? 0 : (k >= m.mres[a] ? m.mres[a] - 1 : k);
+    }
+    const int oct = (d.x < 0 ? 1 : 0) | (d.y < 0 ? 2 : 0) | (d.z < 0 ? 4 : 0);
+    return ((c[2] * m.mres[1] + c[1]) * m.mres[0] + c[0]) * 8 + oct;
+}
+// pass 1: key per item (queue entry or identity) and the bin histogram
+__global__ void __launch_bounds__(256) k_bin_count(DevMedium m, const int *__restrict__ queue, const int *count_p,
+                                                   const float4 *__restrict__ o, const float4 *__restrict__ d,
+                                                   int *__restrict__ keys, int *__restrict__ hist) {
+    const int count = *count_p;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < count; i += gridDim.x * blockDim.x) {
+        const int j = queue ? queue[i] : i;
+        const int k = ray_bin(m, from4(o[j]), from4(d[j]));
+        keys[i] = k;
+        atomicAdd(hist + k, 1);
+    }
+}
+// pass 2: exclusive scan of the histogram in place (one workgroup; nbins <= 8 * 4096)
+__global__ void __launch_bounds__(1024) k_bin_scan(int *hist, int nbins) {
+    __shared__ int s_part[1024];
+    const int per = (nbins + 1023) / 1024;
+    const int lo = threadIdx.x * per, hi = lo + per < nbins ? lo + per : nbins;
+    int sum = 0;
+    for (int i = lo; i < hi; ++i) sum += hist[i];
+    s_part[threadIdx.x] = sum;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {   // Hillis-Steele inclusive scan of the parts
+        const int v = threadIdx.x >= off ? s_part[threadIdx.x - off] : 0;
+        __syncthreads();
+        s_part[threadIdx.x] += v;
+        __syncthreads();
+    }
+    int run = s_part[threadIdx.x] - sum;
+    for (int i = lo; i < hi; ++i) {
+        const int h = hist[i];
+        hist[i] = run;
+        run += h;
+    }
+}
+// pass 3: scatter the items (queue entries or indices) to their bins
+__global__ void __launch_bounds__(256) k_bin_scatter(const int *__restrict__ queue, const int *count_p,
+                                                     const int *__restrict__ keys, int *__restrict__ offs,
+                                                     int *__restrict__ out) {
+    const int count = *count_p;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < count; i += gridDim.x * blockDim.x)
+        out[atomicAdd(offs + keys[i], 1)] = queue ? queue[i] : i;
 }
 #endif
 

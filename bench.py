@@ -43,7 +43,7 @@ BYTES_PER_LOOKUP = 32
 BYTES_PER_ITEM = 132
 BYTES_PER_SAMPLE_RECORD = 32   # k_paths' per-sample record (L, lambda) read later by k_film
 # rocprofv3 passes (one run each; at most 8 SQ, 4 TCC (FETCH_SIZE 3, WRITE_SIZE 2), 2 GRBM)
-PMC_PASSES = (("fetch", ("FETCH_SIZE",)), ("write", ("WRITE_SIZE",)),
+PMC_PASSES = (("fetch", ("FETCH_SIZE",)), ("write", ("WRITE_SIZE",)), ("tcc", ("TCC_HIT_sum", "TCC_MISS_sum")),
               ("sq", ("SQ_INSTS_VALU", "SQ_WAVE_CYCLES", "SQ_ACTIVE_INST_ANY", "SQ_WAIT_INST_ANY", "SQ_WAIT_ANY",
                       "SQ_WAVES", "GRBM_GUI_ACTIVE")))
 
@@ -80,6 +80,8 @@ def parse():
     p.add_argument("--majorant-res", type=int, default=None,
                    help="GridMedium majorant resolution per axis: 0 = pbrt's 16^3 (replay default), -1 = tuned "
                         "on the device among 1,2,4,8,16 (fast-mode default, outside the timed region)")
+    p.add_argument("--ray-binning", type=int, default=0,
+                   help="wavefront kernels: counting-sort the queues by (majorant cell, octant) before each launch")
     p.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     return p.parse_args()
 
@@ -174,7 +176,7 @@ def pmc_passes(args, kernel_substr="k_paths", timeout_s=240):
     child = [sys.executable, os.path.join(ROOT, "bench.py"), "--pmc-child", "--no-cpu-baseline", "--pmc", "off",
              "--steps", "2", "--warmup", "1"]
     for k in ("res", "width", "height", "spp_per_step", "max_paths", "kernel", "medium", "refill_min", "grid_layout",
-              "dda_budget", "zsobol_table", "sampler", "filter", "mode", "majorant_res"):
+              "dda_budget", "zsobol_table", "sampler", "filter", "mode", "majorant_res", "ray_binning"):
         if getattr(args, k) is not None:
             child += [f"--{k.replace('_', '-')}", str(getattr(args, k))]
     out = {}
@@ -283,6 +285,8 @@ def main():
     if args.dda_budget:
         integ.ctx.set_dda_budget(args.dda_budget)
     integ.ctx.set_sampler_table(args.zsobol_table)
+    if args.ray_binning:
+        integ.ctx.set_ray_binning(1)
     maj_res = tuple(scene.medium.majorant_res)
     tune_ms = None
     if args.majorant_res == -1 or (args.majorant_res is None and args.mode == "fast" and vdb is None):
@@ -369,10 +373,10 @@ def main():
             host_scene = host_density = None
         # HBM traffic and the VALU limiter from rocprofv3 counter passes of this same
         # configuration (child processes; the guide's gfx950 rule: FETCH_SIZE x2 + WRITE_SIZE)
-        traffic, limiter, pmc_note = None, None, "pmc off"
+        traffic, limiter, pmc_note, cache = None, None, "pmc off", None
         want_pmc = args.pmc == "on" or (args.pmc == "auto" and world == 1)
-        if want_pmc and persistent:
-            ctr, err = pmc_passes(args)
+        if want_pmc:
+            ctr, err = pmc_passes(args, kernel_substr="k_paths" if persistent else "k_medium")
             if ctr is None:
                 pmc_note = err
                 log(f"pmc: {err}")
@@ -380,7 +384,14 @@ def main():
                 pmc_note = "rocprofv3 --pmc child passes of this configuration (bench.py pmc_passes)"
                 if "FETCH_SIZE" in ctr and "WRITE_SIZE" in ctr:
                     traffic = round((2 * ctr["FETCH_SIZE"] + ctr["WRITE_SIZE"]) * 1024 / 1e9, 4)
-                if "SQ_INSTS_VALU" in ctr and "SQ_WAVE_CYCLES" in ctr:
+                lookups_pl = (agg["medium_lookups"] + (agg["shadow_lookups"] if persistent else 0)) / launches
+                cache = {
+                    "fetch_bytes_per_lookup": (round(2 * ctr["FETCH_SIZE"] * 1024 / lookups_pl, 2)
+                                               if "FETCH_SIZE" in ctr and lookups_pl else None),
+                    "tcc_hit_rate": (round(ctr["TCC_HIT_sum"] / (ctr["TCC_HIT_sum"] + ctr["TCC_MISS_sum"]), 4)
+                                     if ctr.get("TCC_HIT_sum") is not None and ctr.get("TCC_MISS_sum") else None),
+                }
+                if persistent and "SQ_INSTS_VALU" in ctr and "SQ_WAVE_CYCLES" in ctr:
                     # effective clock from GRBM_GUI_ACTIVE (summed over 8 XCDs) over the launch time
                     clk = (ctr["GRBM_GUI_ACTIVE"] / 8 / (avg_launch_ms / 1e3)) if ctr.get("GRBM_GUI_ACTIVE") else 2.4e9
                     valu_frac = ctr["SQ_INSTS_VALU"] * 2 / (VALU_SIMDS * clk * avg_launch_ms / 1e3)
@@ -431,6 +442,7 @@ def main():
                 "avg_launch_ms": avg_launch_ms,
                 "launches": launches,
                 "limiter": limiter,
+                "cache": cache,
             },
             "grid_layout": grid_layout,
             "simd_utilisation": (agg["active_lane_iterations"] / (64.0 * agg["loop_iterations"])

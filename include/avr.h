@@ -50,6 +50,7 @@ typedef struct avr_stats {
     double ms_camera, ms_medium, ms_shadow, ms_film; /* summed hipEvent times      */
     double ms_total;                                  /* first launch .. film done  */
     double ms_setup;   /* one-off device tables built by avr_render (ZSobol pixel table) */
+    double ms_binning; /* wavefront ray binning (avr_set_ray_binning): key, scan, scatter passes */
 } avr_stats;
 
 /* Last error message of the calling thread ("" if none). */
@@ -72,6 +73,11 @@ int avr_set_kernel_mode(avr_context *ctx, int mode);
  * is statistical (film error within the Monte Carlo noise). Applies to the persistent kernel
  * (kernel mode 0); the wavefront kernels always replay. */
 int avr_set_render_mode(avr_context *ctx, int mode);
+/* Wavefront organisation (kernel mode 1) only: 1 = counting-sort the medium queue (depths
+ * after the camera rays) and the shadow queue by (majorant cell of the ray origin, direction
+ * octant) before each k_medium / k_shadow launch, so a wave's lanes gather from nearby voxels
+ * (north star "density fetches coalesced along sorted ray packets"). Results unchanged. */
+int avr_set_ray_binning(avr_context *ctx, int on);
 /* k_paths: refill a wave's idle lanes with new samples once at least `lanes` (1..64)
  * are idle (or none is busy); larger values batch the camera-ray setup across lanes. */
 int avr_set_refill_min(avr_context *ctx, int lanes);

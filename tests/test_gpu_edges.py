@@ -198,3 +198,27 @@ def test_volpathcustom_maxdepth_override_renders_the_override_depth():
     assert not np.array_equal(rgb_a, rgb_c)
     for x in (a, b, c):
         x.close()
+
+
+def test_wavefront_ray_binning_changes_order_not_results():
+    """N1 ray binning (avr_set_ray_binning): the medium and shadow queues are counting-sorted
+    by (majorant cell, octant) before each launch; every path's arithmetic is unchanged, so the
+    film and the work counters are identical to the unsorted wavefront run (and to k_paths)."""
+    from acceleratedvolrenderer_amd import VolPathIntegrator, scenes
+    from oracle import binding
+    dens = binding.cloud_grid(32)
+    scene = scenes.s_cloud(dens, width=48, height=27)
+    runs = []
+    for kernel, binning in (("wavefront", 0), ("wavefront", 1), ("persistent", 0)):
+        integ = VolPathIntegrator(scene, maxdepth=scenes.CLOUD_MAXDEPTH, spp=8, seed=0, device=0, kernel=kernel)
+        integ.ctx.set_ray_binning(binning)
+        rgb, w = integ.render()
+        st = integ.stats()
+        runs.append((rgb, w, st))
+        integ.close()
+    (r0, w0, s0), (r1, w1, s1), (r2, w2, _) = runs
+    assert np.array_equal(r0, r1) and np.array_equal(w0, w1)
+    assert np.array_equal(r0, r2) and np.array_equal(w0, w2)
+    for k in ("medium_lookups", "shadow_lookups", "shadow_items", "medium_items_in"):
+        assert s0[k] == s1[k], k
+    assert s1["ms_binning"] > 0 and s0["ms_binning"] == 0
