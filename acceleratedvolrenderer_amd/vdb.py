@@ -150,6 +150,17 @@ class NanoVDBGrid:
         p0, p1 = self.world_bbox()
         return vals, p0, p1
 
+    @classmethod
+    def read_nvdb(cls, path, name=None):
+        """NanoVDBMedium::Create's readGrid (media.cpp:487-509): the FloatGrid `name` (first grid
+        when None) of an uncompressed .nvdb file (acceleratedvolrenderer_amd/nvdb.py)."""
+        from .nvdb import read_nvdb
+        return read_nvdb(path, name)
+
+    def write_nvdb(self, path, name="density"):
+        from .nvdb import write_nvdb
+        write_nvdb(path, {name: self})
+
     def save(self, path):
         np.savez(path, leaf_origins=self.leaf_origins, leaf_values=self.leaf_values, tile_origins=self.tile_origins,
                  tile_sizes=self.tile_sizes, tile_values=self.tile_values, background=self.background,

@@ -82,6 +82,9 @@ def parse():
                         "on the device among 1,2,4,8,16 (fast-mode default, outside the timed region)")
     p.add_argument("--ray-binning", type=int, default=0,
                    help="wavefront kernels: counting-sort the queues by (majorant cell, octant) before each launch")
+    p.add_argument("--nvdb", default=None,
+                   help="NanoVDBMedium from this .nvdb file's density grid (needs --medium nanovdb); 'roundtrip' "
+                        "writes the synthetic cloud's tree to a temporary .nvdb and reads it back")
     p.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     return p.parse_args()
 
@@ -176,7 +179,7 @@ def pmc_passes(args, kernel_substr="k_paths", timeout_s=240):
     child = [sys.executable, os.path.join(ROOT, "bench.py"), "--pmc-child", "--no-cpu-baseline", "--pmc", "off",
              "--steps", "2", "--warmup", "1"]
     for k in ("res", "width", "height", "spp_per_step", "max_paths", "kernel", "medium", "refill_min", "grid_layout",
-              "dda_budget", "zsobol_table", "sampler", "filter", "mode", "majorant_res", "ray_binning"):
+              "dda_budget", "zsobol_table", "sampler", "filter", "mode", "majorant_res", "ray_binning", "nvdb"):
         if getattr(args, k) is not None:
             child += [f"--{k.replace('_', '-')}", str(getattr(args, k))]
     out = {}
@@ -265,7 +268,19 @@ def main():
         # sparse tree of the same cloud (leaf blocks where the density is nonzero), built on
         # the host; outside the timed region like the grid generation
         tvdb = time.perf_counter()
-        vdb = scenes.vdb_grid(density.cpu().numpy())
+        if args.nvdb and args.nvdb != "roundtrip":
+            from acceleratedvolrenderer_amd.vdb import NanoVDBGrid
+            vdb = NanoVDBGrid.read_nvdb(args.nvdb)
+        else:
+            vdb = scenes.vdb_grid(density.cpu().numpy())
+            if args.nvdb == "roundtrip":
+                from acceleratedvolrenderer_amd.vdb import NanoVDBGrid
+                tmpf = os.path.join(tempfile.mkdtemp(prefix="avr_nvdb_", dir=os.environ.get("TMPDIR", "/tmp")),
+                                    "cloud.nvdb")
+                vdb.write_nvdb(tmpf)
+                vdb = NanoVDBGrid.read_nvdb(tmpf)
+                shutil.rmtree(os.path.dirname(tmpf), ignore_errors=True)
+                log(f"NanoVDB grid written to and read back from an .nvdb file ({len(vdb.leaf_origins)} leaves)")
         del density
         density = None
         torch.cuda.empty_cache()

@@ -222,3 +222,23 @@ def test_wavefront_ray_binning_changes_order_not_results():
     for k in ("medium_lookups", "shadow_lookups", "shadow_items", "medium_items_in"):
         assert s0[k] == s1[k], k
     assert s1["ms_binning"] > 0 and s0["ms_binning"] == 0
+
+
+def test_nanovdb_medium_from_nvdb_file_renders_identically(tmp_path):
+    """f1: a NanoVDBMedium read back from an .nvdb file (NanoVDBMedium::Create's readGrid,
+    media.cpp:487-509) renders bit-identically to the tree it was written from."""
+    from acceleratedvolrenderer_amd import VolPathIntegrator, scenes
+    from acceleratedvolrenderer_amd.vdb import NanoVDBGrid
+    from oracle import binding
+    dens = binding.cloud_grid(32)
+    g = scenes.vdb_grid(dens)
+    p = tmp_path / "cloud.nvdb"
+    g.write_nvdb(p)
+    r = NanoVDBGrid.read_nvdb(p)
+    films = []
+    for grid in (g, r):
+        scene = scenes.s_cloud_vdb(grid, width=40, height=24)
+        integ = VolPathIntegrator(scene, maxdepth=scenes.CLOUD_MAXDEPTH, spp=4, seed=0, device=0)
+        films.append(integ.render())
+        integ.close()
+    assert np.array_equal(films[0][0], films[1][0]) and np.array_equal(films[0][1], films[1][1])
