@@ -125,7 +125,7 @@ struct avr_context {
     uint32_t *d_zs_table = nullptr;
     int zs_dims = 256;
     int zs_key[3] = {-1, -1, -1};
-    int refill_min = 32;
+    int refill_min = 0;       // 0: by render mode (32 replay, 40 fast: measured optima)
     int dda_budget = 0;       // 0: by majorant resolution (12 cells up to 16^3, 32 for NanoVDB's 64^3)
     int grid_layout = 1;
     bool gray = false;        // sigma_a and sigma_s constant over 360..830 nm      // 1: build the fat (footprint) copy when memory allows, 0: linear only
@@ -524,7 +524,7 @@ int avr_set_dda_budget(avr_context *c, int cells) {
 }
 
 int avr_set_refill_min(avr_context *c, int lanes) {
-    if (!c || lanes < 1 || lanes > 64) return fail(AVR_ERR_ARG, "refill threshold must be 1..64 lanes");
+    if (!c || lanes < 0 || lanes > 64) return fail(AVR_ERR_ARG, "refill threshold must be 1..64 lanes (0: default)");
     c->refill_min = lanes;
     return AVR_OK;
 }
@@ -1228,7 +1228,7 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
                                (long long)base, S);
             HIP_TRY(hipGetLastError());
             p.advance = c->d_advance;
-            p.refill_min = c->refill_min;
+            p.refill_min = c->refill_min > 0 ? c->refill_min : (c->render_mode == 1 ? 40 : 32);
             {
                 const int mres = std::max(c->med.mres[0], std::max(c->med.mres[1], c->med.mres[2]));
                 p.dda_budget = c->dda_budget > 0 ? c->dda_budget : (mres > 16 ? 32 : 12);

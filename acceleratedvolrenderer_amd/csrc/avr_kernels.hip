@@ -1352,7 +1352,9 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
     const long long N = (long long)npix * P.pass_samples;
     const int lane = lane_id();
     const int xcc = xcc_id();
-    unsigned long long nLookup = 0, nSteps = 0, nPaths = 0, nShadow = 0, nShadowLookup = 0;
+    // work counters: per lane in 32 bits (a lane traces at most a few thousand segments per
+    // launch), the wave-loop counters wave-uniform (scalar registers)
+    uint32_t nLookup = 0, nSteps = 0, nPaths = 0, nShadow = 0, nShadowLookup = 0;
     unsigned long long nIter = 0, nActive = 0;
 
     int mode = M_FETCH, ev = EV_NONE;
@@ -1663,7 +1665,8 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
             const uint64_t busyNow = __ballot(busy);
             const uint64_t service = __ballot(mode != M_DONE && !busy);
             if (busyNow == 0 || __popcll(service) >= P.refill_min) break;
-            if (lane == 0) { ++nIter; nActive += __popcll(busyNow); }
+            ++nIter;
+            nActive += __popcll(busyNow);
             if (!busy) continue;
             // ---- advance to the next tentative collision (media.h:754-802) ----
             // Hot loop: on the S-cloud input a path crosses ~20 majorant cells per density
@@ -1858,8 +1861,10 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
     flush_stat(P.stats, 3, nShadowLookup);
     flush_stat(P.stats, 4, nShadow);
     flush_stat(P.stats, 5, nSteps);
-    flush_stat(P.stats, 8, nIter);
-    flush_stat(P.stats, 9, nActive);
+    if (lane == 0) {   // wave-uniform counters: one add per wave
+        if (nIter) atomicAdd(P.stats + 8, nIter);
+        if (nActive) atomicAdd(P.stats + 9, nActive);
+    }
 }
 
 #ifndef AVR_KPATHS_TU

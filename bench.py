@@ -85,6 +85,8 @@ def parse():
     p.add_argument("--nvdb", default=None,
                    help="NanoVDBMedium from this .nvdb file's density grid (needs --medium nanovdb); 'roundtrip' "
                         "writes the synthetic cloud's tree to a temporary .nvdb and reads it back")
+    p.add_argument("--fast-leg", type=int, default=1,
+                   help="after the replay measurement, time the same steps in fast mode (reported as fast_mode)")
     p.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     return p.parse_args()
 
@@ -351,6 +353,44 @@ def main():
 
     samples = npix * S * args.steps * world
     value = samples / elapsed / 1e6
+
+    # Second leg, after the headline (replay) measurement: the same steps in the "fast" render
+    # mode (hardware transcendentals, majorant tuned on the device; statistical parity,
+    # tests/test_gpu_fast.py), timed the same way. Not the headline value.
+    fast_line = None
+    if args.mode == "replay" and args.fast_leg and args.kernel == "persistent":
+        integ.ctx.set_render_mode("fast")
+        cands = (1, 2, 4, 8, 16) + ((32, 64) if vdb is not None else ())
+        fres, fms = integ.tune_majorant(candidates=cands, probe=(0, 1))
+        integ.ctx.film_clear()
+        for k in range(args.warmup):
+            step(k)
+        integ.ctx.film_clear()
+        integ.ctx.sync()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        tf = time.perf_counter()
+        for k in range(args.warmup, args.warmup + args.steps):
+            step(k)
+        integ.ctx.film_export_device(buf.data_ptr())
+        if world > 1:
+            dist.reduce(buf, dst=0, op=dist.ReduceOp.SUM)
+        integ.ctx.sync()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        ef = time.perf_counter() - tf
+        if world > 1:
+            t = torch.tensor([ef], dtype=torch.float64, device=f"cuda:{dev}")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            ef = float(t.item())
+        fast_line = {"value": round(samples / ef / 1e6, 4), "unit": "Msamples/s", "ms_per_step": round(1e3 * ef / args.steps, 3),
+                     "majorant_res": list(fres), "majorant_probe_ms": {str(k): round(v, 4) for k, v in fms.items()},
+                     "parity": "statistical (hardware log/exp/sin/cos, tuned majorant): tests/test_gpu_fast.py"}
+        log(f"fast mode: {fast_line['value']} Msamples/s (majorant {fres})")
     # roofline of the dominant kernel: algorithmic bytes / summed device time of its launches
     med_s = agg["ms_medium"] / 1e3
     launches = max(1, agg["medium_launches"])
@@ -459,6 +499,7 @@ def main():
                 "limiter": limiter,
                 "cache": cache,
             },
+            "fast_mode": fast_line,
             "grid_layout": grid_layout,
             "simd_utilisation": (agg["active_lane_iterations"] / (64.0 * agg["loop_iterations"])
                                  if agg.get("loop_iterations") else None),

@@ -20,7 +20,7 @@ run_bench() {
 }
 if [ $# -gt 0 ]; then
   for a in "$@"; do
-    if [ "$a" = "--" ]; then run_bench; else args+=("$a"); fi
+    if [ "$a" = "--" ]; then run_bench; elif [ -n "$a" ]; then args+=("$a"); fi
   done
   run_bench
 fi
