@@ -691,6 +691,7 @@ __device__ __forceinline__ void camera_sample(const Params &P, Smp &smp, int px,
     smp.get2d(P, &l0, &l1);       // lens
 }
 
+__device__ __forceinline__ const float *base_of(const smp::FilterTables &t) { return t.f; }
 __device__ __forceinline__ float4 to4(V3 v) { return make_float4(v.x, v.y, v.z, 0.f); }
 __device__ __forceinline__ V3 from4(float4 v) { return {v.x, v.y, v.z}; }
 __device__ __forceinline__ float4 to4(Spec s) { return make_float4(s.v0, s.v1, s.v2, s.v3); }
@@ -1315,21 +1316,33 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
     // per lane: the camera sample's wavelength u and filter weight, parked here until the
     // path ends and its 32-B record is written (off the VGPR budget)
     __shared__ float2 s_rec[256];
+    // the camera (cameraFromRaster, renderFromCamera: 28 floats used only by the refill), read
+    // from LDS there instead of occupying kernel-argument SGPRs for the whole kernel
+    __shared__ DevCamera s_cam;
+    if (threadIdx.x == 0) s_cam = P.cam;
     // GaussianFilter's FilterSampler tables (pbrt's default radius 1.5: 48 x 48 function +
     // CDFs, ~19 KB) staged here when they fit: the camera-ray refill's two binary searches
     // then run on LDS instead of dependent L2 loads
     constexpr int kFiltLds = 4864;
     __shared__ float s_filt[kFiltLds];
-    smp::FilterTables ftab = P.film.gauss;
+    // the table descriptor itself also lives in LDS (read by the refill only)
+    __shared__ smp::FilterTables s_ftab;
     if (P.film.filter_type != 0) {
-        const int nf = smp::filter_table_floats(ftab.nx, ftab.ny);
+        const smp::FilterTables &g = P.film.gauss;
+        const int nf = smp::filter_table_floats(g.nx, g.ny);
         if (nf <= kFiltLds) {
-            const float *base = ftab.f;
+            const float *base = g.f;
             for (int i = threadIdx.x; i < nf; i += blockDim.x) s_filt[i] = base[i];
-            ftab.f = s_filt;
-            ftab.ccdf = s_filt + (P.film.gauss.ccdf - base);
-            ftab.cint = s_filt + (P.film.gauss.cint - base);
-            ftab.mcdf = s_filt + (P.film.gauss.mcdf - base);
+        }
+        if (threadIdx.x == 0) {
+            smp::FilterTables t = g;
+            if (nf <= kFiltLds) {
+                t.f = s_filt;
+                t.ccdf = s_filt + (g.ccdf - base_of(g));
+                t.cint = s_filt + (g.cint - base_of(g));
+                t.mcdf = s_filt + (g.mcdf - base_of(g));
+            }
+            s_ftab = t;
         }
     }
     // the host routes GridMedium majorant grids of more than 4096 cells to the wavefront kernels
@@ -1604,18 +1617,19 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
                     // wavelengths (pdf: recomputed by k_film from the record's u_lambda)
                     lam = kFast ? film_sample_lambda_fast(P.film, ulam) : film_sample_lambda(P.film, ulam);
                     float pFilmX, pFilmY, fweight;
-                    camera_sample(P, smp, px, py, &pFilmX, &pFilmY, &fweight, &ftab);
+                    camera_sample(P, smp, px, py, &pFilmX, &pFilmY, &fweight, &s_ftab);
                     s_rec[threadIdx.x] = make_float2(ulam, fweight);
-                    const float *r = P.cam.raster;
+                    const DevCamera &cam = s_cam;
+                    const float *r = cam.raster;
                     V3 pCam = {r[0] * pFilmX + r[1] * pFilmY + r[2] * 0.f + r[3],
                                r[4] * pFilmX + r[5] * pFilmY + r[6] * 0.f + r[7],
                                r[8] * pFilmX + r[9] * pFilmY + r[10] * 0.f + r[11]};
                     const float wp = r[12] * pFilmX + r[13] * pFilmY + r[14] * 0.f + r[15];
                     if (wp != 1) pCam = pCam / wp;
                     Ray ray;
-                    if (P.cam.type == 0) ray = {pCam, {0.f, 0.f, 1.f}};
+                    if (cam.type == 0) ray = {pCam, {0.f, 0.f, 1.f}};
                     else ray = {{0.f, 0.f, 0.f}, normalize(pCam)};
-                    ray = xf_ray(P.cam.render_from_camera, ray, nullptr, /*forward=*/true);
+                    ray = xf_ray(cam.render_from_camera, ray, nullptr, /*forward=*/true);
                     po = m.boundary ? interface_entry(m, ray.o, ray.d) : ray.o;
                     pd = ray.d;
                     L = Spec::c(0.f);

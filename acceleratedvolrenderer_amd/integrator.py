@@ -105,7 +105,7 @@ class VolPathIntegrator:
         """Integrator::Create-style factory from a pbrt ParameterDictionary-like dict."""
         return cls(scene, device=device, **cls.create_params(name, params, maxdepth_override), **kw)
 
-    def tune_majorant(self, candidates=(1, 2, 4, 8, 16), probe=(0, 1)):
+    def tune_majorant(self, candidates=(1, 2, 4, 8, 16), probe=(0, 4)):
         """The fast mode's tuned majorant: time one probe render of sample
         indices [probe[0], probe[1]) per candidate majorant resolution (r^3) on the device and
         keep the fastest (avr_tune_majorant; the film is left as it was). Any conservative

@@ -307,7 +307,7 @@ def main():
     maj_res = tuple(scene.medium.majorant_res)
     tune_ms = None
     if args.majorant_res == -1 or (args.majorant_res is None and args.mode == "fast" and vdb is None):
-        maj_res, tune_ms = integ.tune_majorant(probe=(0, 1))
+        maj_res, tune_ms = integ.tune_majorant(probe=(0, 4))
         log(f"tuned majorant {maj_res} (probe ms {tune_ms})")
         args.majorant_res = maj_res[0]   # the counter passes (child processes) render the same majorant
 
@@ -361,7 +361,7 @@ def main():
     if args.mode == "replay" and args.fast_leg and args.kernel == "persistent":
         integ.ctx.set_render_mode("fast")
         cands = (1, 2, 4, 8, 16) + ((32, 64) if vdb is not None else ())
-        fres, fms = integ.tune_majorant(candidates=cands, probe=(0, 1))
+        fres, fms = integ.tune_majorant(candidates=cands, probe=(0, 4))
         integ.ctx.film_clear()
         for k in range(args.warmup):
             step(k)
