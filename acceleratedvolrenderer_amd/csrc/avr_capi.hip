@@ -89,10 +89,12 @@ struct avr_context {
     bool last_persistent = false;   // which organisation the last avr_render ran
     bool last_fast = false;         // ... and whether k_paths ran in fast mode
     int *d_heads = nullptr;   // 8 per-XCD work counters of k_paths
-    // k_paths<emissive, gray, zsobol, medium, image, fast> at 64*fast + 32*image + 8*(0 grid, 1 vdb,
-    // 2 rgb, 3 homogeneous/cloud) + 4*zsobol + 2*emissive + gray
-    int paths_grid[128] = {};
-    void (*kpaths[128])(avr::Params) = {};
+    // k_paths<emissive, gray, sampler, medium, image, fast> at slot
+    // ((((fast*2 + image)*4 + medium(0 grid, 1 vdb, 2 rgb, 3 homogeneous/cloud))*3 + sampler(0
+    // independent, 1 zsobol 32-bit, 2 zsobol 64-bit))*2 + emissive)*2 + gray
+    static constexpr int kNumPaths = 192;
+    int paths_grid[kNumPaths] = {};
+    void (*kpaths[kNumPaths])(avr::Params) = {};
     int render_mode = 0;      // 0 replay (canonical math, per-sample parity), 1 fast (hardware math)
     int ray_binning = 0;      // wavefront organisation: counting-sort queues by (majorant cell, octant)
     int *d_bin_keys = nullptr, *d_bin_out = nullptr, *d_bin_hist = nullptr;
@@ -483,18 +485,18 @@ int avr_context_create(int device, long long max_paths, avr_context **out) {
         // slot 32*image + 8*medium(0 grid, 1 vdb, 2 rgb, 3 homogeneous/cloud) + 4*zsobol + 2*emissive + gray; RGB grids
         // are never gray (their gray slots hold the 4-wavelength kernel)
 #define AVR_KP(em, gr, zs, med, im, fa) avr::k_paths<em, (med == 4 ? false : gr), zs, med, im, fa>
-#define AVR_KP8(med, im, fa)                                                                                           \
-    AVR_KP(false, false, false, med, im, fa), AVR_KP(false, true, false, med, im, fa),                                 \
-        AVR_KP(true, false, false, med, im, fa), AVR_KP(true, true, false, med, im, fa),                               \
-        AVR_KP(false, false, true, med, im, fa), AVR_KP(false, true, true, med, im, fa),                               \
-        AVR_KP(true, false, true, med, im, fa), AVR_KP(true, true, true, med, im, fa)
-#define AVR_KP32(im, fa) AVR_KP8(0, im, fa), AVR_KP8(3, im, fa), AVR_KP8(4, im, fa), AVR_KP8(1, im, fa)
-        void (*kerns[128])(avr::Params) = {AVR_KP32(false, false), AVR_KP32(true, false), AVR_KP32(false, true),
-                                           AVR_KP32(true, true)};
-#undef AVR_KP32
-#undef AVR_KP8
+#define AVR_KP4(zs, med, im, fa)                                                                                      \
+    AVR_KP(false, false, zs, med, im, fa), AVR_KP(false, true, zs, med, im, fa), AVR_KP(true, false, zs, med, im, fa), \
+        AVR_KP(true, true, zs, med, im, fa)
+#define AVR_KP12(med, im, fa) AVR_KP4(0, med, im, fa), AVR_KP4(2, med, im, fa), AVR_KP4(3, med, im, fa)
+#define AVR_KP48(im, fa) AVR_KP12(0, im, fa), AVR_KP12(3, im, fa), AVR_KP12(4, im, fa), AVR_KP12(1, im, fa)
+        void (*kerns[avr_context::kNumPaths])(avr::Params) = {AVR_KP48(false, false), AVR_KP48(true, false),
+                                                              AVR_KP48(false, true), AVR_KP48(true, true)};
+#undef AVR_KP48
+#undef AVR_KP12
+#undef AVR_KP4
 #undef AVR_KP
-        for (int k = 0; k < 128; ++k) {
+        for (int k = 0; k < avr_context::kNumPaths; ++k) {
             int blocksPerCU = 0;
             if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocksPerCU, kerns[k], 256, 0) != hipSuccess) {
                 delete c;
@@ -1238,8 +1240,9 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
             EV_MARK(e0);
             // gray medium: sigma_a and sigma_s tables constant over all 471 wavelengths
             const int mk = c->med.type == 3 ? 1 : (c->med.type == 4 ? 2 : (c->med.type == 1 || c->med.type == 2 ? 3 : 0));
-            const int kv = 64 * c->render_mode + 32 * (c->n_image_lights > 0 ? 1 : 0) + 8 * mk + 4 * c->sampler_kind +
-                           2 * (c->med.emissive ? 1 : 0) + (c->gray && c->med.type != 4 ? 1 : 0);
+            const int sv = c->sampler_kind == 0 ? 0 : (avr::smp::zsobol_wide(p.zs) ? 2 : 1);
+            const int kv = ((((c->render_mode * 2 + (c->n_image_lights > 0 ? 1 : 0)) * 4 + mk) * 3 + sv) * 2 +
+                            (c->med.emissive ? 1 : 0)) * 2 + (c->gray && c->med.type != 4 ? 1 : 0);
             hipLaunchKernelGGL(c->kpaths[kv], dim3(c->paths_grid[kv]), dim3(256), 0, c->stream, p);
             HIP_TRY(hipGetLastError());
             EV_MARK(e1);

@@ -633,8 +633,11 @@ __device__ __forceinline__ Spec sample_t_maj(const DevMedium &m, const float *ma
 // rng.h:43-45) advanced by sampleIndex * 65536; Get2D = two Get1D, left to right.
 // ZSobolSampler — samplers.h:225-330 (avr_sampling.h). In the wavefront SoA the state
 // lives in smp_state / smp_inc (PCG state / increment, or Morton index / dimension).
-template <bool kZSobol> struct PathSampler;
-template <> struct PathSampler<false> {
+// PathSampler<K>: K = 0 IndependentSampler; K = 1 ZSobolSampler (index width decided per
+// call); K = 2 / 3 ZSobolSampler with a 32-bit / 64-bit sample index fixed at compile time
+// (k_paths instantiations: one code path per kernel; the host picks by zsobol_wide).
+template <int K> struct PathSampler;
+template <> struct PathSampler<0> {
     Pcg32 rng;
     __device__ __forceinline__ void start(const Params &P, int px, int py, int sampleIndex) {
         const uint64_t seq = hash_3u32((uint32_t)px, (uint32_t)py, (uint32_t)P.seed);
@@ -649,13 +652,17 @@ template <> struct PathSampler<false> {
     __device__ __forceinline__ void load(const Params &P, int i) { rng.state = P.ps.smp_state[i]; rng.inc = P.ps.smp_inc[i]; }
     __device__ __forceinline__ void save(const Params &P, int i) { P.ps.smp_state[i] = rng.state; P.ps.smp_inc[i] = rng.inc; }
 };
-template <> struct PathSampler<true> {
+template <int K> struct PathSampler {
+    static_assert(K >= 1 && K <= 3, "ZSobol sampler variants");
+    static constexpr int kW = K - 1;   // 0 run-time width, 1 32-bit, 2 64-bit
     smp::ZSobol z;
     __device__ __forceinline__ void start(const Params &P, int px, int py, int sampleIndex) {
         z.start(px, py, sampleIndex, P.zs);
     }
-    __device__ __forceinline__ float get1d(const Params &P) { return z.get1d(P.zs); }
-    __device__ __forceinline__ void get2d(const Params &P, float *u0, float *u1) { z.get2d(P.zs, u0, u1); }
+    __device__ __forceinline__ float get1d(const Params &P) { return z.template get1d<kW>(P.zs); }
+    __device__ __forceinline__ void get2d(const Params &P, float *u0, float *u1) {
+        z.template get2d<kW>(P.zs, u0, u1);
+    }
     __device__ __forceinline__ void load(const Params &P, int i) {
         const uint64_t st = P.ps.smp_state[i];
         z.morton = (uint32_t)st;
@@ -1299,7 +1306,7 @@ struct SecProf {
 // kImage: the scene holds an ImageInfiniteLight (non-delta NEE with MIS, MIS-weighted
 // escapes); a separate instantiation so the other kernels keep their register budget.
 // kFast: the "fast" render mode (hardware transcendentals, statistical parity); replay otherwise.
-template <bool kEmissive, bool kGray, bool kZSobol, int kMed, bool kImage, bool kFast>
+template <bool kEmissive, bool kGray, int kSmp, int kMed, bool kImage, bool kFast>
 __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_WAVES_SPEC) k_paths(Params P) {
     // kMed 1: HomogeneousMedium or CloudMedium — dda_init gives their single
     // HomogeneousMajorantIterator segment over a 1^3 majorant of 1.0; properties from sample_point
@@ -1376,7 +1383,8 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
     // path state (Li, integrators.cpp:966-971)
     Spec L{}, lam{}, Le_l{};
     S beta{}, r_u{}, r_l{}, sig_a{}, sig_s{};
-    PathSampler<kZSobol> smp{};
+    constexpr bool kZSobol = kSmp != 0;   // kSmp: 0 Independent, 2 / 3 ZSobol with 32 / 64-bit index
+    PathSampler<kSmp> smp{};
     int depth = 0;
     V3 po{}, pd{};         // segment origin (== the path vertex) and the path's ray direction
     // segment state (SampleT_maj)

@@ -215,8 +215,12 @@ struct ZSobol {
         hi = (uint32_t)(m >> 32);
         dimension = 0;
     }
+    // kW: 0 = index width decided at run time, 1 = 32-bit (Morton(pixel) << log2 spp fits 32
+    // bits; the caller guarantees !zsobol_wide), 2 = 64-bit (the caller guarantees zsobol_wide).
+    // The fixed widths let a kernel instantiation carry one code path only.
+    template <int kW = 0>
     AVR_HD void index(const ZSobolParams &zp, uint32_t *alo, uint32_t *ahi) const {
-        if (zsobol_wide(zp)) {
+        if (kW == 2 || (kW == 0 && zsobol_wide(zp))) {
             const uint64_t a = zsobol_index<uint64_t>(((uint64_t)hi << 32) | morton, dimension, zp);
             *alo = (uint32_t)a;
             *ahi = (uint32_t)(a >> 32);
@@ -225,16 +229,18 @@ struct ZSobol {
             *ahi = 0;
         }
     }
+    template <int kW = 0>
     AVR_HD float get1d(const ZSobolParams &zp) {
         uint32_t a, ah;
-        index(zp, &a, &ah);   // dimension 0 reads the low 32 bits only
+        index<kW>(zp, &a, &ah);   // dimension 0 reads the low 32 bits only
         ++dimension;
         const uint32_t h = (uint32_t)hash_2u32(dimension, (uint32_t)zp.seed);
         return u32_to_unit(fast_owen(sobol_bits(a, 0), h));
     }
+    template <int kW = 0>
     AVR_HD void get2d(const ZSobolParams &zp, float *u0, float *u1) {
         uint32_t a, ah;
-        index(zp, &a, &ah);
+        index<kW>(zp, &a, &ah);
         dimension += 2;
         const uint64_t h = hash_2u32(dimension, (uint32_t)zp.seed);
         *u0 = u32_to_unit(fast_owen(sobol_bits(a, 0), (uint32_t)h));
