@@ -362,6 +362,11 @@ def main():
         integ.ctx.set_render_mode("fast")
         cands = (1, 2, 4, 8, 16) + ((32, 64) if vdb is not None else ())
         fres, fms = integ.tune_majorant(candidates=cands, probe=(0, 4))
+        if world > 1:   # every rank renders with rank 0's choice
+            t = torch.tensor(list(fres), dtype=torch.int64, device=f"cuda:{dev}")
+            dist.broadcast(t, src=0)
+            fres = tuple(int(v) for v in t.tolist())
+            integ.ctx.set_majorant_res(fres)
         integ.ctx.film_clear()
         for k in range(args.warmup):
             step(k)

@@ -6,8 +6,9 @@
 tag=$1; shift
 mkdir -p gpurun_out
 if [ "${SKIP_TESTS:-0}" != 1 ]; then
+  kargs=(); [ -n "${KEXPR:-}" ] && kargs=(-k "$KEXPR")
   timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ${TESTS:-} \
-    > gpurun_out/${tag}_tests.log 2>&1
+    "${kargs[@]}" > gpurun_out/${tag}_tests.log 2>&1
   rc=$?; echo "tests rc=$rc"; tail -3 gpurun_out/${tag}_tests.log
   [ $rc -eq 0 ] || [ $rc -eq 1 ] || [ $rc -eq 5 ] || exit $rc
 fi
