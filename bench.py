@@ -87,6 +87,10 @@ def parse():
                         "writes the synthetic cloud's tree to a temporary .nvdb and reads it back")
     p.add_argument("--fast-leg", type=int, default=1,
                    help="after the replay measurement, time the same steps in fast mode (reported as fast_mode)")
+    p.add_argument("--scene", default="cloud", choices=["cloud", "uniform", "explosion"],
+                   help="cloud: the metric workload (S-cloud); uniform: BASELINE C2's uniform cube (orthographic, "
+                        "use --res 256 --width 512 --height 512); explosion: C5's emissive NanoVDB stand-in with a "
+                        "SpectralFilm (pixelsamples >= 4096)")
     p.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     return p.parse_args()
 
@@ -181,7 +185,8 @@ def pmc_passes(args, kernel_substr="k_paths", timeout_s=240):
     child = [sys.executable, os.path.join(ROOT, "bench.py"), "--pmc-child", "--no-cpu-baseline", "--pmc", "off",
              "--steps", "2", "--warmup", "1"]
     for k in ("res", "width", "height", "spp_per_step", "max_paths", "kernel", "medium", "refill_min", "grid_layout",
-              "dda_budget", "zsobol_table", "sampler", "filter", "mode", "majorant_res", "ray_binning", "nvdb"):
+              "dda_budget", "zsobol_table", "sampler", "filter", "mode", "majorant_res", "ray_binning", "nvdb",
+              "scene"):
         if getattr(args, k) is not None:
             child += [f"--{k.replace('_', '-')}", str(getattr(args, k))]
     out = {}
@@ -266,7 +271,29 @@ def main():
         if spp_total % S:
             raise SystemExit(f"--spp-per-step {S} must divide the ZSobol index range {spp_total} for this run length")
     vdb = None
-    if args.medium == "nanovdb":
+    maxdepth = scenes.CLOUD_MAXDEPTH
+    workload_name = {"cloud": f"S-cloud-{n}", "uniform": f"S-uniform-{n} (C2)",
+                     "explosion": f"S-explosion-{n} emissive spectral (C5 stand-in)"}[args.scene]
+    if args.scene == "explosion":
+        spp_total = max(spp_total, 4096)   # C5: 4096 spp (64-bit ZSobol indices at 720p)
+    if args.scene == "uniform":
+        # C2: GridMedium n^3 of 1.0, orthographic; S-uniform's "scatter" variant (distant light + sky)
+        density.fill_(1.0)
+        scene = scenes.s_uniform(n=n, width=args.width, height=args.height, variant="scatter", density=density)
+        from acceleratedvolrenderer_amd.scene import ZSobolSampler, IndependentSampler
+        scene.sampler = ZSobolSampler(spp_total) if args.sampler == "zsobol" else IndependentSampler(spp_total)
+        maxdepth = 100
+    elif args.scene == "explosion":
+        tvdb = time.perf_counter()
+        del density
+        density = None
+        torch.cuda.empty_cache()
+        vdb, vtemp = scenes.explosion_vdb(n=n)
+        scene = scenes.s_explosion(vdb, vtemp, width=args.width, height=args.height, sampler=args.sampler,
+                                   spp=spp_total)
+        tgen += time.perf_counter() - tvdb
+        maxdepth = 100
+    elif args.medium == "nanovdb":
         # sparse tree of the same cloud (leaf blocks where the density is nonzero), built on
         # the host; outside the timed region like the grid generation
         tvdb = time.perf_counter()
@@ -294,7 +321,7 @@ def main():
                                filter=args.filter)
         if args.majorant_res and args.majorant_res > 0:
             scene.medium.majorant_res = (args.majorant_res,) * 3
-    integ = VolPathIntegrator(scene, maxdepth=scenes.CLOUD_MAXDEPTH, spp=args.spp_per_step, seed=0, device=dev,
+    integ = VolPathIntegrator(scene, maxdepth=maxdepth, spp=args.spp_per_step, seed=0, device=dev,
                               max_paths=args.max_paths, kernel=args.kernel, grid_layout=args.grid_layout,
                               mode=args.mode)
     if args.refill_min:
@@ -314,7 +341,7 @@ def main():
     def step(k):
         # asynchronous on the context stream: steps queue back to back
         base = ((k * world + rank) * S) % spp_total if wrap else (k * world + rank) * S
-        integ.ctx.render(base, base + S, 0, scenes.CLOUD_MAXDEPTH)
+        integ.ctx.render(base, base + S, 0, maxdepth)
 
     log("scene uploaded; warmup")
     for k in range(args.warmup):
@@ -332,7 +359,9 @@ def main():
         step(k)
     # final film reduce over RCCL (part of T_render)
     npix = args.width * args.height
-    buf = torch.empty(4 * npix, dtype=torch.float64, device=f"cuda:{dev}")
+    from acceleratedvolrenderer_amd.integrator import film_buffer_size
+    buf = torch.empty(film_buffer_size(npix, getattr(scene.film, "nbuckets", 0)), dtype=torch.float64,
+                      device=f"cuda:{dev}")
     integ.ctx.film_export_device(buf.data_ptr())
     if world > 1:
         dist.reduce(buf, dst=0, op=dist.ReduceOp.SUM)
@@ -426,10 +455,14 @@ def main():
         if not args.no_cpu_baseline and world == 1:
             if vdb is not None:
                 host_scene = scene
+            elif args.scene == "uniform":
+                host_scene = scenes.s_uniform(n=n, width=args.width, height=args.height, variant="scatter",
+                                              density=host_density)
+                host_scene.sampler = scene.sampler
             else:
                 host_scene = scenes.s_cloud(host_density, width=args.width, height=args.height,
                                             sampler=args.sampler, spp=spp_total, filter=args.filter)
-            cpu = cpu_baseline(host_scene, S, args.cpu_seconds, f"S-cloud-{n} {args.medium}")
+            cpu = cpu_baseline(host_scene, S, args.cpu_seconds, f"{workload_name} {args.medium}")
             host_scene = host_density = None
         # HBM traffic and the VALU limiter from rocprofv3 counter passes of this same
         # configuration (child processes; the guide's gfx950 rule: FETCH_SIZE x2 + WRITE_SIZE)
@@ -480,9 +513,11 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (CloudMedium::Density 1024^3 generated on device; disney-cloud assets absent)",
-            "config": {"workload": f"S-cloud-{n} {'NanoVDBMedium' if vdb is not None else 'GridMedium'}, perspective {args.width}x{args.height}, "
-                                   f"{S} spp/step/GPU, maxdepth {scenes.CLOUD_MAXDEPTH}, {args.sampler} sampler "
+            "data": {"cloud": f"synthetic (CloudMedium::Density {n}^3 generated on device; disney-cloud assets absent)",
+                     "uniform": f"synthetic (uniform density {n}^3)",
+                     "explosion": f"synthetic (radial density + temperature NanoVDB grids over {n}^3; explosion asset absent)"}[args.scene],
+            "config": {"workload": f"{workload_name} {'NanoVDBMedium' if vdb is not None else 'GridMedium'}, {'orthographic' if args.scene == 'uniform' else 'perspective'} {args.width}x{args.height}, "
+                                   f"{S} spp/step/GPU, maxdepth {maxdepth}, {args.sampler} sampler "
                                    f"(pixelsamples {spp_total}), {args.filter} filter, {args.mode} mode",
                        "majorant_res": list(maj_res), "majorant_tuning_ms": tune_ms,
                        "global_batch": samples // args.steps, "parallelism": f"sample-shard x{world}",
