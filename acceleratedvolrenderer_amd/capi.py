@@ -95,6 +95,7 @@ SIGNATURES = {
     "avr_set_ray_binning": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "avr_set_majorant_res": (ctypes.c_int, [ctypes.c_void_p, c_int_p]),
     "avr_medium_boundary_sphere": (ctypes.c_int, [ctypes.c_void_p, c_float_p, ctypes.c_float]),
+    "avr_medium_boundary_convex": (ctypes.c_int, [ctypes.c_void_p, c_float_p, ctypes.c_int]),
     "avr_tune_majorant": (ctypes.c_int, [ctypes.c_void_p, c_int_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                          ctypes.c_int, ctypes.c_int, c_int_p, c_float_p]),
     "avr_set_refill_min": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
@@ -332,6 +333,11 @@ class Context:
             c3 = f32(sph[:3])
             self._keep.append(c3)
             _check(self.lib.avr_medium_boundary_sphere(self.h, _fp(c3), float(sph[3])))
+        planes = getattr(scene, "interface_planes_render", None)
+        if planes is not None:
+            pl = f32(planes.reshape(-1))
+            self._keep.append(pl)
+            _check(self.lib.avr_medium_boundary_convex(self.h, _fp(pl), len(planes)))
         temp = getattr(med, "temperature", None)
         if temp is not None:
             self._keep.append(temp)

@@ -95,5 +95,30 @@ __device__ __forceinline__ Hits sphere_hits(V3 c, float r, V3 o, V3 d) {
     return {kOutsideTwoHits, mid(t0), mid(t1)};
 }
 
+// Convex polyhedron as the intersection of half-spaces n.p <= h (outward normals; e.g. the
+// face planes of a convex triangle mesh): the ray's parametric slab clip, the generalisation
+// of Bounds3::IntersectP (vecmath.h:1547-1571) to arbitrary planes. Same hit kinds as above:
+// InsideOneHit {exit} for an origin inside, OutsideTwoHits {entry, exit}, else no hit.
+// Float operation order fixed (dot products left to right, -ffp-contract=off): the oracle's
+// restatement is bit-identical.
+__host__ __device__ __forceinline__ Hits convex_hits(const float4 *planes, int n, V3 o, V3 d) {
+    float t0 = -kInf, t1 = kInf;
+    for (int i = 0; i < n; ++i) {
+        const float4 pl = planes[i];
+        const float denom = (pl.x * d.x + pl.y * d.y) + pl.z * d.z;
+        const float num = pl.w - ((pl.x * o.x + pl.y * o.y) + pl.z * o.z);
+        if (denom == 0.f) {
+            if (num < 0.f) return {kOutsideZeroHits, 0.f, 0.f};   // parallel and outside this plane
+        } else {
+            const float t = num / denom;
+            if (denom > 0.f) t1 = t < t1 ? t : t1;   // leaving through this plane
+            else t0 = t > t0 ? t : t0;                // entering through this plane
+        }
+    }
+    if (!(t0 <= t1) || t1 <= 0.f) return {kOutsideZeroHits, 0.f, 0.f};
+    if (t0 <= 0.f) return {kInsideOneHit, t1, 0.f};
+    return {kOutsideTwoHits, t0, t1};
+}
+
 }  // namespace shape
 }  // namespace avr

@@ -97,6 +97,7 @@ struct avr_context {
     void (*kpaths[kNumPaths])(avr::Params) = {};
     int render_mode = 0;      // 0 replay (canonical math, per-sample parity), 1 fast (hardware math)
     int ray_binning = 0;      // wavefront organisation: counting-sort queues by (majorant cell, octant)
+    float4 *d_planes = nullptr;   // convex interface half-spaces (avr_medium_boundary_convex)
     int *d_bin_keys = nullptr, *d_bin_out = nullptr, *d_bin_hist = nullptr;
     long long bin_cap = 0;
     // pixel sampler (avr_set_sampler) and filter (avr_set_filter)
@@ -567,6 +568,7 @@ int avr_context_destroy(avr_context *c) {
     if (c->d_counts) (void)hipFree(c->d_counts);
     if (c->d_heads) (void)hipFree(c->d_heads);
     for (int *b : {c->d_bin_keys, c->d_bin_out, c->d_bin_hist}) if (b) (void)hipFree(b);
+    if (c->d_planes) (void)hipFree(c->d_planes);
     if (c->d_advance) (void)hipFree(c->d_advance);
     if (c->d_filter) (void)hipFree(c->d_filter);
     if (c->d_temperature) (void)hipFree(c->d_temperature);
@@ -777,6 +779,30 @@ int avr_medium_boundary_sphere(avr_context *c, const float center[3], float radi
     c->med.boundary = radius > 0 ? 1 : 0;
     for (int i = 0; i < 3; ++i) c->med.sph[i] = radius > 0 ? center[i] : 0.f;
     c->med.sph[3] = radius > 0 ? radius : 0.f;
+    return AVR_OK;
+}
+
+int avr_medium_boundary_convex(avr_context *c, const float *planes, int n_planes) {
+    AVR_QUIESCE(c);
+    if (!c || !c->has_medium) return fail(AVR_ERR_STATE, "no medium");
+    if (n_planes < 0 || n_planes > 256 || (n_planes > 0 && !planes))
+        return fail(AVR_ERR_ARG, "convex interface: 0..256 planes {nx, ny, nz, h}");
+    for (int i = 0; i < 4 * n_planes; ++i)
+        if (!std::isfinite(planes[i])) return fail(AVR_ERR_ARG, "convex interface planes must be finite");
+    HIP_TRY(hipSetDevice(c->device));
+    if (c->d_planes) { (void)hipFree(c->d_planes); c->d_planes = nullptr; }
+    c->med.planes = nullptr;
+    c->med.n_planes = 0;
+    if (n_planes == 0) {
+        if (c->med.boundary == 2) c->med.boundary = 0;
+        return AVR_OK;
+    }
+    HIP_TRY(dalloc(&c->d_planes, (size_t)n_planes));
+    HIP_TRY(hipMemcpyAsync(c->d_planes, planes, 4 * sizeof(float) * n_planes, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    c->med.planes = c->d_planes;
+    c->med.n_planes = n_planes;
+    c->med.boundary = 2;
     return AVR_OK;
 }
 

@@ -47,10 +47,13 @@ struct DevMedium {
     // in 2-4 lines. 8x the grid's memory ((n+1)^3 x 32 B; 34 GB at 1024^3 of the 288 GB).
     const float4 *fat;
     // medium interface (f3): 0 = the bounds box (the default scene model), 1 = a sphere
-    // {cx, cy, cz, r} in render space (a shape with no material and MediumInterface(inside =
-    // this medium, outside = none): interaction.cpp:91-97 SkipIntersection)
+    // {cx, cy, cz, r} in render space, 2 = a convex polyhedron (n_planes half-spaces
+    // {nx, ny, nz, h}: n.p <= h inside; a convex triangle mesh's face planes) — shapes with no
+    // material and MediumInterface(inside = this medium, outside = none): interaction.cpp:91-97
     int boundary;
     float sph[4];
+    const float4 *planes;
+    int n_planes;
     int unit_box;          // bounds extent exactly 1 on every axis: Offset's divisions are by 1.0f
     // medium type: 0 GridMedium (media.h:265-352), 1 HomogeneousMedium (media.h:217-262),
     // 2 CloudMedium (media.h:430-528). Types 1 and 2 have one majorant segment (the
@@ -142,12 +145,16 @@ __device__ __forceinline__ float film_lambda_pdf(const DevFilm &f, float l) {
 // point); a ray that does not cross the sphere sees no medium. Sphere::BasicIntersect's
 // interval quadric (avr_boundary.h); origins are not offset by intersection error bounds,
 // so paths match pbrt's statistically, the oracle's bit for bit.
+__device__ __forceinline__ shape::Hits interface_hits(const DevMedium &m, V3 o, V3 d) {
+    if (m.boundary == 2) return shape::convex_hits(m.planes, m.n_planes, o, d);
+    return shape::sphere_hits(V3{m.sph[0], m.sph[1], m.sph[2]}, m.sph[3], o, d);
+}
 __device__ __forceinline__ float interface_exit(const DevMedium &m, V3 o, V3 d) {
-    const shape::Hits h = shape::sphere_hits(V3{m.sph[0], m.sph[1], m.sph[2]}, m.sph[3], o, d);
+    const shape::Hits h = interface_hits(m, o, d);
     return h.type == shape::kInsideOneHit ? h.t0 : (h.type == shape::kOutsideTwoHits ? h.t1 : 0.f);
 }
 __device__ __forceinline__ V3 interface_entry(const DevMedium &m, V3 o, V3 d) {
-    const shape::Hits h = shape::sphere_hits(V3{m.sph[0], m.sph[1], m.sph[2]}, m.sph[3], o, d);
+    const shape::Hits h = interface_hits(m, o, d);
     return h.type == shape::kOutsideTwoHits ? o + d * h.t0 : o;
 }
 

@@ -518,6 +518,32 @@ def spectral_image(film, rgb_sum, w_sum, bucket_sums, weight_sums, fp16=True):
     return np.concatenate([rgb, c.astype(np.float32)], axis=2)
 
 
+def convex_mesh_planes(vertices, triangles):
+    """Outward face planes {nx, ny, nz, h} (inside: n.p <= h) of a closed convex triangle mesh,
+    coplanar faces merged; f64."""
+    v = np.asarray(vertices, np.float64).reshape(-1, 3)
+    t = np.asarray(triangles, np.int64).reshape(-1, 3)
+    c = v.mean(axis=0)
+    out = []
+    for a, b, d in t:
+        n = np.cross(v[b] - v[a], v[d] - v[a])
+        ln = np.linalg.norm(n)
+        if ln == 0:
+            continue
+        n = n / ln
+        h = float(n @ v[a])
+        if n @ c > h:
+            n, h = -n, -h
+        if not any(np.allclose(n, q[:3], atol=1e-9) and abs(h - q[3]) < 1e-9 for q in out):
+            out.append(np.array([*n, h]))
+    if len(out) < 4:
+        raise ValueError("interface mesh must be a closed convex polyhedron")
+    planes = np.array(out)
+    if np.any(v @ planes[:, :3].T > planes[:, 3] + 1e-6 * (1 + np.abs(planes[:, 3]))):
+        raise ValueError("interface mesh is not convex")
+    return planes
+
+
 def _bounding_sphere_radius(pmin, pmax):
     """Bounds3::BoundingSphere (vecmath.h:1335-1338) in float32."""
     pmin = pmin.astype(np.float32)
@@ -533,10 +559,12 @@ def _bounding_sphere_radius(pmin, pmax):
 class Scene:
     """Resolved render-space scene (CameraWorld rendering space, cameras.cpp:35-41)."""
 
-    def __init__(self, camera, film, medium, lights, sampler=None, interface_sphere=None):
+    def __init__(self, camera, film, medium, lights, sampler=None, interface_sphere=None, interface_mesh=None):
         """interface_sphere: None (the medium's bounds box is its interface shape) or
         (world-space centre, radius) of a sphere without material whose MediumInterface holds
-        the medium inside (pbrt's `AttributeBegin MediumInterface "cloud" "" Shape "sphere"`)."""
+        the medium inside (pbrt's `AttributeBegin MediumInterface "cloud" "" Shape "sphere"`).
+        interface_mesh: (vertices, triangles) of a closed CONVEX triangle mesh in world space
+        (e.g. pbrt's `Shape "trianglemesh"` cube around a medium) bounding the medium instead."""
         self.camera, self.film, self.medium, self.lights = camera, film, medium, list(lights)
         self.interface_sphere = interface_sphere
         self.sampler = sampler if sampler is not None else IndependentSampler()
@@ -556,6 +584,16 @@ class Scene:
         rc = (rfm @ c.T).T[:, :3]
         self.scene_radius = _bounding_sphere_radius(rc.min(axis=0), rc.max(axis=0))
         self.interface_sphere_render = None
+        self.interface_planes_render = None
+        if interface_mesh is not None:
+            verts, tris = interface_mesh
+            pw = convex_mesh_planes(verts, tris)
+            off = np.asarray(self.render_from_world, np.float64)[:3, 3]   # CameraWorld: a translation
+            pr = pw.copy()
+            pr[:, 3] = pw[:, 3] + pw[:, :3] @ off
+            self.interface_planes_render = pr.astype(np.float32)
+            vr = np.asarray(verts, np.float64) + off
+            self.scene_radius = _bounding_sphere_radius(vr.min(axis=0), vr.max(axis=0))
         if interface_sphere is not None:
             cw, r = interface_sphere
             if not float(r) > 0:

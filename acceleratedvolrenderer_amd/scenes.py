@@ -75,6 +75,33 @@ def s_sphere(n=32, width=64, height=64, variant="scatter", density=None, center=
                  interface_sphere=(tuple(float(v) for v in center), float(radius)))
 
 
+def box_mesh(p0, p1, rotate_deg=0.0):
+    """A closed box triangle mesh (pbrt `Shape "trianglemesh"`) from p0 to p1, optionally rotated
+    about the y axis through its centre: (vertices (8, 3), triangles (12, 3))."""
+    p0, p1 = np.asarray(p0, np.float64), np.asarray(p1, np.float64)
+    v = np.array([[x, y, z] for z in (p0[2], p1[2]) for y in (p0[1], p1[1]) for x in (p0[0], p1[0])])
+    if rotate_deg:
+        c = (p0 + p1) / 2
+        a = np.radians(rotate_deg)
+        r = np.array([[np.cos(a), 0, np.sin(a)], [0, 1, 0], [-np.sin(a), 0, np.cos(a)]])
+        v = (v - c) @ r.T + c
+    t = np.array([[0, 2, 1], [1, 2, 3], [4, 5, 6], [5, 7, 6], [0, 1, 4], [1, 5, 4], [2, 6, 3], [3, 6, 7],
+                  [0, 4, 2], [2, 4, 6], [1, 3, 5], [3, 7, 5]])
+    return v, t
+
+
+def s_mesh_interface(n=32, width=64, height=64, variant="scatter", density=None, mesh=None, camera="orthographic"):
+    """S-uniform's medium bounded by a convex triangle-mesh interface (default: a box rotated by
+    30 degrees inside the grid box)."""
+    base = s_uniform(n=n, width=width, height=height, variant=variant, density=density)
+    if mesh is None:
+        mesh = box_mesh((0.2, 0.15, 0.2), (0.8, 0.85, 0.8), rotate_deg=30.0)
+    cam = base.camera
+    if camera == "perspective":
+        cam = PerspectiveCamera(fov=50.0, pos=(0.9, 0.7, -1.1), look=(0.5, 0.5, 0.5), up=(0.0, 1.0, 0.0))
+    return Scene(cam, base.film, base.medium, base.lights, sampler=base.sampler, interface_mesh=mesh)
+
+
 def vdb_grid(density, index_to_world=None, index_min=(0, 0, 0), background=0.0):
     """Sparse NanoVDB-style copy of a dense (nz, ny, nx) grid; default map: index i at world
     i / n per axis."""

@@ -190,6 +190,12 @@ int avr_medium_rgbgrid(avr_context *ctx, int nx, int ny, int nz, const float bou
  * to the default model (the bounds box is the interface). Reset by every avr_medium_* call.
  * Both kernel organisations. */
 int avr_medium_boundary_sphere(avr_context *ctx, const float center[3], float radius);
+/* A convex polyhedral medium interface (e.g. a convex triangle mesh — a box mesh, a prism —
+ * given by its face planes): n_planes half-spaces {nx, ny, nz, h} in render space, the
+ * medium inside every n.p <= h (outward normals, 1..256 planes; 0 returns to the box). Same
+ * semantics as the sphere; crossings by the parametric slab clip (vecmath.h:1547-1571
+ * generalised), not pbrt's watertight triangle test, so paths match pbrt statistically. */
+int avr_medium_boundary_convex(avr_context *ctx, const float *planes, int n_planes);
 /* The medium bounds the last avr_medium_* call set (medium space, min xyz then max xyz). */
 int avr_medium_bounds(avr_context *ctx, float bounds[6]);
 /* Fill d_out[first .. first+count) of an n^3 grid with CloudMedium::Density

@@ -77,7 +77,7 @@ class OracleScene(ctypes.Structure):
         ("light_rfl", (ctypes.c_float * 9) * 8), ("light_lfr", (ctypes.c_float * 9) * 8),
         ("light_illuminant", c_float_p),
         ("film_nbuckets", ctypes.c_int), ("film_lambda_min", ctypes.c_float), ("film_lambda_max", ctypes.c_float),
-        ("boundary", ctypes.c_int), ("sphere", ctypes.c_float * 4),
+        ("boundary", ctypes.c_int), ("sphere", ctypes.c_float * 4), ("n_planes", ctypes.c_int), ("planes", c_float_p),
     ]
 
 
@@ -411,6 +411,11 @@ class OracleRun:
         s.boundary = 1 if sph is not None else 0
         if sph is not None:
             s.sphere[:] = [float(v) for v in sph]
+        planes = getattr(scene, "interface_planes_render", None)
+        if planes is not None:
+            s.boundary = 2
+            s.n_planes = len(planes)
+            s.planes = arr(np.ascontiguousarray(planes, np.float32).reshape(-1))
         s.max_depth = int(max_depth)
         s.seed = int(seed)
         smp = scene.sampler

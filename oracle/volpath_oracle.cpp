@@ -819,9 +819,12 @@ typedef struct OracleScene {
     // [lambda_min, lambda_max] and per-pixel spectral buckets next to the RGB sums
     int film_nbuckets;
     float film_lambda_min, film_lambda_max;
-    // medium interface: 0 the bounds box, 1 a sphere {cx, cy, cz, r} in render space
+    // medium interface: 0 the bounds box, 1 a sphere {cx, cy, cz, r} in render space,
+    // 2 a convex polyhedron: n_planes half-spaces {nx, ny, nz, h}, inside n.p <= h
     int boundary;
     float sphere[4];
+    int n_planes;
+    const float *planes;
 } OracleScene;
 
 }  // extern "C"
@@ -2487,12 +2490,36 @@ void oracle_cloud_grid(int n, int z0, int z1, float *out) {
 
 // Interface sphere helpers (declared before SampleLd / Li), C++ linkage
 namespace oracle {
+// Convex polyhedron = intersection of half-spaces n.p <= h: the parametric slab clip of
+// Bounds3::IntersectP (vecmath.h:1547-1571) over arbitrary planes; dot products left to right.
+static graphm::Hits ConvexHits(const float *pl, int n, V3 o, V3 d) {
+    float t0 = -Infinity, t1 = Infinity;
+    for (int i = 0; i < n; ++i) {
+        const float nx = pl[4 * i], ny = pl[4 * i + 1], nz = pl[4 * i + 2], h = pl[4 * i + 3];
+        const float denom = (nx * d.x + ny * d.y) + nz * d.z;
+        const float num = h - ((nx * o.x + ny * o.y) + nz * o.z);
+        if (denom == 0.f) {
+            if (num < 0.f) return {graphm::OutsideZeroHits, {0, 0}};
+        } else {
+            const float t = num / denom;
+            if (denom > 0.f) t1 = std::min(t1, t);
+            else t0 = std::max(t0, t);
+        }
+    }
+    if (!(t0 <= t1) || t1 <= 0.f) return {graphm::OutsideZeroHits, {0, 0}};
+    if (t0 <= 0.f) return {graphm::InsideOneHit, {t1, 0}};
+    return {graphm::OutsideTwoHits, {t0, t1}};
+}
+static graphm::Hits InterfaceHits(const OracleScene &s, V3 o, V3 d) {
+    if (s.boundary == 2) return ConvexHits(s.planes, s.n_planes, o, d);
+    return graphm::SphereHits(V3{s.sphere[0], s.sphere[1], s.sphere[2]}, s.sphere[3], o, d);
+}
 static float InterfaceExit(const OracleScene &s, V3 o, V3 d) {
-    const graphm::Hits h = graphm::SphereHits(V3{s.sphere[0], s.sphere[1], s.sphere[2]}, s.sphere[3], o, d);
+    const graphm::Hits h = InterfaceHits(s, o, d);
     return h.type == graphm::InsideOneHit ? h.t[0] : (h.type == graphm::OutsideTwoHits ? h.t[1] : 0.f);
 }
 static V3 InterfaceEntry(const OracleScene &s, V3 o, V3 d) {
-    const graphm::Hits h = graphm::SphereHits(V3{s.sphere[0], s.sphere[1], s.sphere[2]}, s.sphere[3], o, d);
+    const graphm::Hits h = InterfaceHits(s, o, d);
     return h.type == graphm::OutsideTwoHits ? o + d * h.t[0] : o;
 }
 }  // namespace oracle

@@ -1,4 +1,5 @@
-"""f3 medium interfaces on the GPU: media bounded by an interface sphere (a shape without
+"""f3 medium interfaces on the GPU: media bounded by an interface sphere or a convex triangle
+mesh (a box mesh, rotated: its face planes) — shapes without
 material whose MediumInterface holds the medium inside; interaction.cpp:91-97
 SkipIntersection, shapes.h:152-200 Sphere::BasicIntersect) in both kernel organisations.
 
@@ -42,7 +43,8 @@ def _exact_fraction(integ, ref, ns):
 
 
 @pytest.mark.parametrize("kernel", ["persistent", "wavefront"])
-@pytest.mark.parametrize("case", ["inscribed_ortho", "offset_perspective", "chromatic_perspective"])
+@pytest.mark.parametrize("case", ["inscribed_ortho", "offset_perspective", "chromatic_perspective", "convex_mesh_ortho",
+                                  "convex_mesh_perspective"])
 def test_sphere_interface_replay(case, kernel):
     from acceleratedvolrenderer_amd import VolPathIntegrator, scenes
     from oracle import binding
@@ -54,9 +56,15 @@ def test_sphere_interface_replay(case, kernel):
     elif case == "offset_perspective":   # sphere partly outside the medium box: the box clips
         scene = scenes.s_sphere(n=n, width=32, height=24, variant="scatter", density=dens, center=(0.3, 0.6, 0.55),
                                 radius=0.5, camera="perspective")
-    else:
+    elif case == "chromatic_perspective":
         scene = scenes.s_sphere(n=n, width=32, height=24, variant="emissive_chromatic", density=dens,
                                 center=(0.5, 0.45, 0.5), radius=0.4, camera="perspective")
+    elif case == "convex_mesh_ortho":   # a box mesh rotated by 30 degrees (convex triangle mesh)
+        scene = scenes.s_mesh_interface(n=n, width=24, height=24, variant="scatter", density=dens)
+    else:                               # a rotated box mesh partly outside the grid's box
+        mesh = scenes.box_mesh((0.1, 0.2, 0.3), (1.1, 0.9, 0.8), rotate_deg=-20.0)
+        scene = scenes.s_mesh_interface(n=n, width=32, height=24, variant="emissive_chromatic", density=dens,
+                                        mesh=mesh, camera="perspective")
     spp = 6
     integ = VolPathIntegrator(scene, maxdepth=8, spp=spp, seed=0, device=0, kernel=kernel)
     rgb, w = integ.render()

@@ -222,3 +222,41 @@ def test_interface_sphere_box_clips_a_larger_sphere():
                    for s in range(spp // 16)])
     want = np.exp(-(1 - 0.25 / n))
     assert abs(Ls.mean() - want) < 4 * np.sqrt(want * (1 - want) / len(Ls))
+
+
+def test_interface_convex_mesh_absorber_chord_transmittance():
+    """f3 convex triangle-mesh interface (a box mesh rotated by 30 degrees inside the grid's
+    box; interaction.cpp:91-97 SkipIntersection): an absorber transmits exp(-chord) along each
+    orthographic ray, the chord through the polyhedron's half-spaces; rays missing it see no
+    medium."""
+    from acceleratedvolrenderer_amd.scene import convex_mesh_planes
+    n, W, H, spp = 16, 8, 8, 256
+    sc = scenes.s_mesh_interface(n=n, width=W, height=H, variant="absorber")
+    planes = convex_mesh_planes(*scenes.box_mesh((0.2, 0.15, 0.2), (0.8, 0.85, 0.8), rotate_deg=30.0))
+    run = ob.OracleRun(sc, max_depth=5)
+    sub = 32
+    o = (np.arange(sub) + 0.5) / sub
+    want = np.empty((H, W))
+    for py in range(H):
+        for px in range(W):
+            x = ((px + o[None, :]) / W).ravel().repeat(sub)
+            y = np.tile(((py + o) / H), sub)
+            num = planes[:, 3][None, :] - (planes[:, 0][None, :] * x[:, None] + planes[:, 1][None, :] * y[:, None]
+                                           + planes[:, 2][None, :] * -1.0)
+            dz = planes[:, 2]
+            t = num / np.where(dz == 0, np.inf, dz)
+            t_in = np.where(dz < 0, t, -np.inf).max(axis=1)
+            t_out = np.where(dz > 0, t, np.inf).min(axis=1)
+            par_out = (num < 0) & (dz == 0)
+            chord = np.where(par_out.any(axis=1), 0.0, np.maximum(0.0, t_out - np.maximum(t_in, 0.0)))
+            want[py, px] = np.exp(-chord).mean()
+    got = np.zeros((H, W))
+    for py in range(H):
+        for px in range(W):
+            Ls = np.array([run.pixel_sample(px, py, s)[0][0] for s in range(spp)])
+            assert set(np.unique(Ls)).issubset({0.0, 1.0})
+            got[py, px] = Ls.mean()
+    var = np.sum(want * (1 - want)) / spp
+    assert abs(got.sum() - want.sum()) < 4 * np.sqrt(var)
+    assert np.all(np.abs(got - want) <= 5 * np.sqrt(want * (1 - want) / spp) + 1.0 / spp)
+    assert np.all(got[want == 1.0] == 1.0)
