@@ -148,3 +148,51 @@ def test_integrator_create_names_and_maxdepth_override():
                                                                                  "volpathcustom")
     with pytest.raises(ValueError, match="integrator type unknown"):
         cp("bdpt", {})
+
+
+def test_convex_mesh_planes_box_and_errors():
+    """Face planes of a convex interface mesh (f3, avr_medium_boundary_convex): a box gives its
+    6 outward planes, every vertex on or inside each; a non-convex mesh and a flat one raise."""
+    import numpy as np
+    import pytest
+    from acceleratedvolrenderer_amd import scenes
+    from acceleratedvolrenderer_amd.scene import convex_mesh_planes
+    v, t = scenes.box_mesh((0.0, 0.0, 0.0), (1.0, 2.0, 3.0))
+    p = convex_mesh_planes(v, t)
+    assert p.shape == (6, 4)
+    assert np.all(v @ p[:, :3].T <= p[:, 3] + 1e-12)
+    centre = np.array([0.5, 1.0, 1.5])
+    assert np.all(p[:, :3] @ centre < p[:, 3])
+    # a dent: move one vertex into the box
+    vd = v.copy()
+    vd[7] = (0.5, 1.0, 1.5)
+    with pytest.raises(ValueError):
+        convex_mesh_planes(vd, t)
+    with pytest.raises(ValueError):
+        convex_mesh_planes(np.zeros((3, 3)), np.array([[0, 1, 2]]))
+
+
+def test_scene_interface_mesh_planes_in_render_space():
+    import numpy as np
+    from acceleratedvolrenderer_amd import scenes
+    sc = scenes.s_mesh_interface(n=4, width=4, height=4)
+    v, _ = scenes.box_mesh((0.2, 0.15, 0.2), (0.8, 0.85, 0.8), rotate_deg=30.0)
+    off = np.asarray(sc.render_from_world, np.float64)[:3, 3]
+    vr = v + off
+    p = sc.interface_planes_render.astype(np.float64)
+    # every render-space vertex lies on at least three planes and inside all of them
+    d = vr @ p[:, :3].T - p[:, 3]
+    assert np.all(d <= 1e-5)
+    assert np.all((np.abs(d) < 1e-5).sum(axis=1) >= 3)
+
+
+def test_boundary_entry_points_reject_bad_arguments_without_a_gpu():
+    from acceleratedvolrenderer_amd import capi
+    lib = capi.load()
+    pl = (capi.ctypes.c_float * 4)(0.0, 0.0, 1.0, 1.0)
+    assert lib.avr_medium_boundary_convex(None, pl, 1) != 0
+    c = (capi.ctypes.c_float * 3)(0.0, 0.0, 0.0)
+    assert lib.avr_medium_boundary_sphere(None, c, 1.0) != 0
+    assert lib.avr_set_majorant_res(None, (capi.ctypes.c_int * 3)(4, 4, 4)) != 0
+    assert lib.avr_set_render_mode(None, 1) != 0
+    assert lib.avr_set_ray_binning(None, 1) != 0
