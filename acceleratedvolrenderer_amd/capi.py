@@ -92,6 +92,8 @@ SIGNATURES = {
     "avr_set_stream": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "avr_set_kernel_mode": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "avr_set_render_mode": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "avr_record_lookups": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_longlong, ctypes.c_void_p]),
+    "avr_density_fetch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_longlong, c_float_p, c_float_p]),
     "avr_set_ray_binning": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "avr_set_majorant_res": (ctypes.c_int, [ctypes.c_void_p, c_int_p]),
     "avr_medium_boundary_sphere": (ctypes.c_int, [ctypes.c_void_p, c_float_p, ctypes.c_float]),
@@ -264,6 +266,18 @@ class Context:
 
     def set_ray_binning(self, on):
         _check(self.lib.avr_set_ray_binning(self.h, 1 if on else 0))
+
+    def record_lookups(self, d_points, cap, d_count):
+        """Trace the wavefront kernels' density fetches into device buffers (0 / None stops)."""
+        _check(self.lib.avr_record_lookups(self.h, ctypes.c_void_p(d_points or None), int(cap),
+                                           ctypes.c_void_p(d_count or None)))
+
+    def density_fetch(self, d_points, n, d_out):
+        """avr_density_fetch on device buffers; returns the kernel time in ms."""
+        ms = ctypes.c_float(0.0)
+        _check(self.lib.avr_density_fetch(self.h, ctypes.c_void_p(d_points), int(n),
+                                          ctypes.cast(ctypes.c_void_p(d_out), c_float_p), ctypes.byref(ms)))
+        return float(ms.value)
 
     def set_kernel_mode(self, mode):
         """0 = persistent megakernel (default), 1 = wavefront queues."""

@@ -387,6 +387,9 @@ int medium_common(avr_context *c, const float *d_density, int nx, int ny, int nz
     m.temp_offset = 0.f;
     m.type = type;
     m.boundary = 0;   // the bounds box until avr_medium_boundary_sphere
+    m.trace = nullptr;
+    m.trace_count = nullptr;
+    m.trace_cap = 0;
     m.cloud_density = cloud ? cloud[0] : 0.f;
     m.cloud_wispiness = cloud ? cloud[1] : 0.f;
     m.cloud_frequency = cloud ? cloud[2] : 0.f;
@@ -803,6 +806,40 @@ int avr_medium_boundary_convex(avr_context *c, const float *planes, int n_planes
     c->med.planes = c->d_planes;
     c->med.n_planes = n_planes;
     c->med.boundary = 2;
+    return AVR_OK;
+}
+
+int avr_record_lookups(avr_context *c, void *d_points, long long cap, void *d_count) {
+    AVR_QUIESCE(c);
+    if (!c || !c->has_medium) return fail(AVR_ERR_STATE, "no medium");
+    if (d_points && (cap < 0 || !d_count)) return fail(AVR_ERR_ARG, "lookup trace needs a capacity and a counter");
+    c->med.trace = (float4 *)d_points;
+    c->med.trace_count = d_points ? (unsigned long long *)d_count : nullptr;
+    c->med.trace_cap = d_points ? cap : 0;
+    return AVR_OK;
+}
+
+int avr_density_fetch(avr_context *c, const void *d_points, long long n, float *d_out, float *ms) {
+    AVR_QUIESCE(c);
+    if (!c || !c->has_medium || c->med.type != 0) return fail(AVR_ERR_STATE, "density fetch needs a GridMedium");
+    if (n < 0 || (n > 0 && (!d_points || !d_out))) return fail(AVR_ERR_ARG, "bad density fetch batch");
+    HIP_TRY(hipSetDevice(c->device));
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    HIP_TRY(hipEventCreate(&e0));
+    HIP_TRY(hipEventCreate(&e1));
+    const int blocks = (int)std::min<long long>((n + 255) / 256, 256LL * 64);
+    HIP_TRY(hipEventRecord(e0, c->stream));
+    if (n > 0)
+        hipLaunchKernelGGL(avr::k_density_fetch, dim3(blocks), dim3(256), 0, c->stream, c->med,
+                           (const float4 *)d_points, n, d_out);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(e1, c->stream));
+    HIP_TRY(hipEventSynchronize(e1));
+    float t = 0.f;
+    HIP_TRY(hipEventElapsedTime(&t, e0, e1));
+    if (ms) *ms = t;
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
     return AVR_OK;
 }
 

@@ -54,6 +54,11 @@ struct DevMedium {
     float sph[4];
     const float4 *planes;
     int n_planes;
+    // optional lookup trace of the wavefront kernels' GridMedium density fetches (unit-box
+    // point, in fetch order), for the standalone density-fetch measurement (avr_record_lookups)
+    float4 *trace;
+    unsigned long long *trace_count;
+    long long trace_cap;
     int unit_box;          // bounds extent exactly 1 on every axis: Offset's divisions are by 1.0f
     // medium type: 0 GridMedium (media.h:265-352), 1 HomogeneousMedium (media.h:217-262),
     // 2 CloudMedium (media.h:430-528). Types 1 and 2 have one majorant segment (the
@@ -508,6 +513,10 @@ __device__ __forceinline__ MediumSample sample_point(const DevMedium &m, V3 p, c
     }
     // Bounds3::Offset (vecmath.h:1323-1332); x / 1.0f == x exactly, so a unit box skips it
     p = m.unit_box ? V3{p.x - m.bmin[0], p.y - m.bmin[1], p.z - m.bmin[2]} : box_offset(m.bmin, m.bmax, p);
+    if (m.trace) {
+        const unsigned long long k = atomicAdd(m.trace_count, 1ull);
+        if ((long long)k < m.trace_cap) m.trace[k] = make_float4(p.x, p.y, p.z, 0.f);
+    }
     float d = m.fat ? fat_lookup(m.fat, m.density, m.nx, m.ny, m.nz, p) : grid_lookup(m.density, m.nx, m.ny, m.nz, p);
     ms.sigma_a = sig_a * d;
     ms.sigma_s = sig_s * d;
@@ -1963,6 +1972,23 @@ __global__ void __launch_bounds__(256) k_film(Params P) {
         P.film.rgb_sum[3 * (size_t)pix + 1] = s1;
         P.film.rgb_sum[3 * (size_t)pix + 2] = s2;
         P.film.w_sum[pix] = ws;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// The density fetch alone: SampledGrid::Lookup (containers.h:804-835) over a batch of
+// unit-box points (Bounds3::Offset applied), one trilinear lookup per point, through the
+// same fat / linear layout code as the path kernels. Measurement kernel for the north star's
+// density-fetch roofline (bench.py `density_fetch`: the recorded lookups of a pass in their
+// trace order, sorted by voxel, shuffled).
+__global__ void __launch_bounds__(256) k_density_fetch(DevMedium m, const float4 *__restrict__ pts, long long n,
+                                                       float *__restrict__ out) {
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+        const float4 p = pts[i];
+        // clamped to the footprint's valid range: a stray point reads the zero border, never
+        // past the grid (the layouts' own bounds checks assume finite coordinates)
+        const V3 q{fminf_(fmaxf_(p.x, -1.f), 2.f), fminf_(fmaxf_(p.y, -1.f), 2.f), fminf_(fmaxf_(p.z, -1.f), 2.f)};
+        out[i] = m.fat ? fat_lookup(m.fat, m.density, m.nx, m.ny, m.nz, q) : grid_lookup(m.density, m.nx, m.ny, m.nz, q);
     }
 }
 

@@ -65,6 +65,15 @@ int avr_context_destroy(avr_context *ctx);
  * VGPRs, ballot-based lane refill), 1 = wavefront kernels k_camera/k_medium/k_shadow with
  * compacted SoA queues between events (pbrt wavefront decomposition). Same estimator. */
 int avr_set_kernel_mode(avr_context *ctx, int mode);
+/* Lookup trace (measurement): while d_points is non-null, the wavefront kernels append the
+ * unit-box point of every GridMedium density fetch (float4 {x, y, z, 0}, fetch order) to
+ * d_points (device, capacity cap) and count them in *d_count (device u64, zeroed by the
+ * caller; counts past cap are not stored). NULL stops tracing. */
+int avr_record_lookups(avr_context *ctx, void *d_points, long long cap, void *d_count);
+/* The density fetch alone (SampledGrid::Lookup, containers.h:804-835, through the same fat /
+ * linear layout code as the path kernels) over n unit-box points (device float4), results
+ * to d_out (device, n floats); synchronous; *ms = the kernel's HIP-event time. */
+int avr_density_fetch(avr_context *ctx, const void *d_points, long long n, float *d_out, float *ms);
 /* Render mode for later renders (SURVEY.md §7 "replay / fast"): 0 = replay (default) — the
  * device evaluates log/atanh/cosh/sin/cos by the canonical f64 sequences and FastExp by pbrt's
  * CPU polynomial (util/math.h:450-471), so every sample replays the CPU VolPathIntegrator's bit

@@ -242,3 +242,35 @@ def test_nanovdb_medium_from_nvdb_file_renders_identically(tmp_path):
         films.append(integ.render())
         integ.close()
     assert np.array_equal(films[0][0], films[1][0]) and np.array_equal(films[0][1], films[1][1])
+
+
+def test_density_fetch_kernel_and_lookup_trace():
+    """The standalone density fetch (avr_density_fetch) is SampledGrid::Lookup bit for bit (oracle
+    grid_lookup), in both grid layouts; the wavefront lookup trace records one point per
+    density fetch the kernels' work counters report."""
+    from acceleratedvolrenderer_amd import VolPathIntegrator, scenes
+    from oracle import binding
+    dens = binding.cloud_grid(24)
+    for layout in ("fat", "linear"):
+        scene = scenes.s_cloud(dens, width=40, height=24)
+        integ = VolPathIntegrator(scene, maxdepth=scenes.CLOUD_MAXDEPTH, spp=4, seed=0, device=0, kernel="wavefront",
+                                  grid_layout=layout)
+        cap = 1 << 20
+        pts = torch.zeros((cap, 4), dtype=torch.float32, device="cuda:0")
+        cnt = torch.zeros(1, dtype=torch.int64, device="cuda:0")
+        integ.ctx.record_lookups(pts.data_ptr(), cap, cnt.data_ptr())
+        integ.render()
+        st = integ.stats()
+        integ.ctx.record_lookups(0, 0, 0)
+        n = int(cnt.item())
+        assert n == st["medium_lookups"] + st["shadow_lookups"] and 0 < n <= cap
+        out = torch.empty(n, dtype=torch.float32, device="cuda:0")
+        ms = integ.ctx.density_fetch(pts.data_ptr(), n, out.data_ptr())
+        assert ms > 0
+        got = out.cpu().numpy()
+        p = pts[:n].cpu().numpy()
+        L = binding.lib()
+        for i in range(0, n, max(1, n // 2000)):
+            want = L.oracle_grid_lookup(binding.fp(dens), 24, 24, 24, float(p[i, 0]), float(p[i, 1]), float(p[i, 2]))
+            assert np.float32(want).view(np.uint32) == got[i].view(np.uint32), (layout, i)
+        integ.close()
