@@ -91,9 +91,6 @@ def parse():
                    help="cloud: the metric workload (S-cloud); uniform: BASELINE C2's uniform cube (orthographic, "
                         "use --res 256 --width 512 --height 512); explosion: C5's emissive NanoVDB stand-in with a "
                         "SpectralFilm (pixelsamples >= 4096)")
-    p.add_argument("--fetch-leg", type=int, default=0,
-                   help="after the timed steps: trace one wavefront pass's density lookups and time the "
-                        "standalone density-fetch kernel on them (trace order, sorted by voxel, shuffled)")
     p.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     return p.parse_args()
 
@@ -428,55 +425,6 @@ def main():
                      "majorant_res": list(fres), "majorant_probe_ms": {str(k): round(v, 4) for k, v in fms.items()},
                      "parity": "statistical (hardware log/exp/sin/cos, tuned majorant): tests/test_gpu_fast.py"}
         log(f"fast mode: {fast_line['value']} Msamples/s (majorant {fres})")
-    # Third leg: the density fetch on its own (north star: ">= 0.5 HBM roofline on the
-    # density-fetch kernel", "coalesced along sorted ray packets"). One wavefront pass traces
-    # its GridMedium lookups (unit-box points, fetch order); avr_density_fetch then times the
-    # same trilinear gathers as a standalone kernel in that order, sorted by the footprint's
-    # voxel (a perfectly binned packet order) and shuffled.
-    fetch_line = None
-    if args.fetch_leg and world == 1 and vdb is None and args.scene == "cloud":
-        cap = 48 * 1024 * 1024
-        pts = torch.empty((cap, 4), dtype=torch.float32, device=f"cuda:{dev}")
-        cnt = torch.zeros(1, dtype=torch.int64, device=f"cuda:{dev}")
-        integ.ctx.set_kernel_mode(1)
-        integ.ctx.record_lookups(pts.data_ptr(), cap, cnt.data_ptr())
-        integ.ctx.render(0, S, 0, maxdepth)
-        integ.ctx.sync()
-        integ.ctx.record_lookups(0, 0, 0)
-        integ.ctx.set_kernel_mode(0)
-        nl = int(min(int(cnt.item()), cap))
-        p = pts[:nl]
-        out = torch.empty(nl, dtype=torch.float32, device=f"cuda:{dev}")
-        # the kernel assumes finite unit-box points: check on the host side before launching
-        ok = nl > 0 and bool(torch.isfinite(p[:, :3]).all().item())
-        lo, hi = (float(p[:, :3].min().item()), float(p[:, :3].max().item())) if ok else (0.0, 0.0)
-        log(f"density fetch: {nl} traced lookups, points in [{lo:.4f}, {hi:.4f}]")
-        ok = ok and lo > -0.01 and hi < 1.01
-
-        def fetch_ms(arr):
-            integ.ctx.density_fetch(arr.data_ptr(), nl, out.data_ptr())   # warm
-            return sorted(integ.ctx.density_fetch(arr.data_ptr(), nl, out.data_ptr()) for _ in range(3))[1]
-
-        if not ok:
-            raise SystemExit("density fetch: traced points outside the unit box")
-        gx = torch.floor(p[:, 0] * n - 0.5).to(torch.int64) + 1
-        gy = torch.floor(p[:, 1] * n - 0.5).to(torch.int64) + 1
-        gz = torch.floor(p[:, 2] * n - 0.5).to(torch.int64) + 1
-        key = (gz * (n + 1) + gy) * (n + 1) + gx
-        orders = {"trace_order": p, "sorted_by_voxel": p[torch.argsort(key)].contiguous(),
-                  "shuffled": p[torch.randperm(nl, device=p.device)].contiguous()}
-        del gx, gy, gz, key
-        torch.cuda.synchronize()   # torch's stream is not ordered with the context stream
-        fb = 32 + 16 + 4   # trilinear footprint + the point + the result
-        fetch_line = {"lookups": nl, "bytes_per_lookup": fb, "layout": integ.ctx.grid_layout_active() and "fat" or "linear",
-                      "peak_GBps": HBM_PEAK_GBPS}
-        for name, arr in orders.items():
-            ms = fetch_ms(arr)
-            gbps = fb * nl / (ms / 1e3) / 1e9
-            fetch_line[name] = {"ms": round(ms, 4), "GBps": round(gbps, 1), "frac": round(gbps / HBM_PEAK_GBPS, 4)}
-        log(f"density fetch: {fetch_line}")
-        del orders, p, pts, out
-
     # roofline of the dominant kernel: algorithmic bytes / summed device time of its launches
     med_s = agg["ms_medium"] / 1e3
     launches = max(1, agg["medium_launches"])
@@ -592,7 +540,6 @@ def main():
                 "cache": cache,
             },
             "fast_mode": fast_line,
-            "density_fetch": fetch_line,
             "grid_layout": grid_layout,
             "simd_utilisation": (agg["active_lane_iterations"] / (64.0 * agg["loop_iterations"])
                                  if agg.get("loop_iterations") else None),
