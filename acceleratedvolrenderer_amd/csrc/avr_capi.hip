@@ -97,6 +97,8 @@ struct avr_context {
     void (*kpaths[kNumPaths])(avr::Params) = {};
     int render_mode = 0;      // 0 replay (canonical math, per-sample parity), 1 fast (hardware math)
     int ray_binning = 0;      // wavefront organisation: counting-sort queues by (majorant cell, octant)
+    int majorant_occupancy = 0;   // NanoVDB k_paths: coarse occupancy level of the majorant in LDS (opt-in)
+    unsigned *d_occ = nullptr;
     float4 *d_planes = nullptr;   // convex interface half-spaces (avr_medium_boundary_convex)
     int *d_bin_keys = nullptr, *d_bin_out = nullptr, *d_bin_hist = nullptr;
     long long bin_cap = 0;
@@ -334,7 +336,12 @@ int build_majorant(avr_context *c, const int mres[3]) {
     if (c->d_majorant) (void)hipFree(c->d_majorant);
     c->d_majorant = nullptr;
     const int nm = mres[0] * mres[1] * mres[2];
-    HIP_TRY(dalloc(&c->d_majorant, (size_t)nm));
+    if (c->d_occ) (void)hipFree(c->d_occ);
+    c->d_occ = nullptr;
+    m.occ = nullptr;
+    // nm cells + one trailing 0: the read target of empty cells under the occupancy level
+    HIP_TRY(dalloc(&c->d_majorant, (size_t)nm + 1));
+    HIP_TRY(hipMemsetAsync(c->d_majorant + nm, 0, sizeof(float), c->stream));
     for (int i = 0; i < 3; ++i) m.mres[i] = mres[i];
     if (type == 0) {
         hipLaunchKernelGGL(avr::k_majorant, dim3(nm), dim3(256), 0, c->stream, m.density, m.nx, m.ny, m.nz, mres[0],
@@ -351,6 +358,14 @@ int build_majorant(avr_context *c, const int mres[3]) {
                            make_int4(b[0], b[1], b[2], 0), make_int4(b[3], b[4], b[5], 0), mres[0], mres[1], mres[2],
                            c->d_majorant);
         HIP_TRY(hipGetLastError());
+        const int nw = (nm + 63) / 64;
+        if (c->majorant_occupancy && nw <= avr::kOccWords) {
+            HIP_TRY(hipMalloc(&c->d_occ, (size_t)nw * sizeof(unsigned)));
+            hipLaunchKernelGGL(avr::k_majorant_occupancy, dim3((nw + 255) / 256), dim3(256), 0, c->stream,
+                               c->d_majorant, nm, c->d_occ, nw);
+            HIP_TRY(hipGetLastError());
+            m.occ = c->d_occ;
+        }
     } else {   // single segment, sigma_maj = sigma_t * 1 (density <= 1 for the cloud)
         const float one = 1.f;
         HIP_TRY(hipMemcpyAsync(c->d_majorant, &one, sizeof(float), hipMemcpyHostToDevice, c->stream));
@@ -549,6 +564,18 @@ int avr_set_ray_binning(avr_context *c, int on) {
     return AVR_OK;
 }
 
+int avr_set_majorant_occupancy(avr_context *c, int on) {
+    AVR_QUIESCE(c);
+    if (!c || (on != 0 && on != 1)) return fail(AVR_ERR_ARG, "majorant occupancy must be 0 or 1");
+    HIP_TRY(hipSetDevice(c->device));
+    c->majorant_occupancy = on;
+    if (c->has_medium) {   // rebuild the current majorant (same values) with / without the level
+        const int r[3] = {c->med.mres[0], c->med.mres[1], c->med.mres[2]};
+        return build_majorant(c, r);
+    }
+    return AVR_OK;
+}
+
 int avr_set_kernel_mode(avr_context *c, int mode) {
     if (!c || (mode != 0 && mode != 1)) return fail(AVR_ERR_ARG, "kernel mode must be 0 (persistent) or 1 (wavefront)");
     c->kernel_mode = mode;
@@ -572,6 +599,7 @@ int avr_context_destroy(avr_context *c) {
     if (c->d_heads) (void)hipFree(c->d_heads);
     for (int *b : {c->d_bin_keys, c->d_bin_out, c->d_bin_hist}) if (b) (void)hipFree(b);
     if (c->d_planes) (void)hipFree(c->d_planes);
+    if (c->d_occ) (void)hipFree(c->d_occ);
     if (c->d_advance) (void)hipFree(c->d_advance);
     if (c->d_filter) (void)hipFree(c->d_filter);
     if (c->d_temperature) (void)hipFree(c->d_temperature);

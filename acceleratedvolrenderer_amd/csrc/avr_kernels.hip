@@ -27,6 +27,8 @@
 
 namespace avr {
 
+constexpr int kOccWords = 4096;   // majorant occupancy words k_paths stages (64^3 cells in pairs)
+
 struct DevMedium {
     const float *density;
     int nx, ny, nz;
@@ -38,8 +40,12 @@ struct DevMedium {
     const float *Le;                  // 471
     const float *lescale;
     int lnx, lny, lnz;
-    const float *majorant;
+    const float *majorant;            // mres cells + one trailing 0 (the empty-cell read target)
     int mres[3];
+    // coarse occupancy level of the majorant (NanoVDB's 64^3 grid, k_paths): bit b of word w is
+    // set unless linear cells 64w+2b and 64w+2b+1 both have majorant 0; null when the grid has
+    // more than 64 * kOccWords cells. Staged in LDS by k_paths (16 KiB at 64^3).
+    const unsigned *occ;
     // "fat" copy of the density grid (the trilinear footprint of every lookup stored
     // contiguously): entry (ix,iy,iz), ix in [-1, nx-1], holds the 8 taps
     // v(ix..ix+1, iy..iy+1, iz..iz+1) (zero outside the grid) as two float4 = 32 B, so a
@@ -1111,6 +1117,14 @@ __device__ __forceinline__ void ddal_init(DdaL &q, const DevMedium &m, Ray ray, 
 // wait for it lands at the next ddal_next (a load inside ddal_next's predicated block is
 // followed by a phi copy that waits right away).
 __device__ __forceinline__ void ddal_prefetch(DdaL &q, const float *maj) { q.mcur = maj[q.pidx]; }
+// With the coarse occupancy level in LDS: a cell whose pair bit is clear has majorant 0, and
+// its lane reads the trailing zero cell maj[ncells] instead (one cached line shared by every
+// such lane) — the L2 read of the 1 MiB grid is left to the occupied cells. Same value either way.
+__device__ __forceinline__ void ddal_prefetch_occ(DdaL &q, const float *maj, const unsigned *occ, int ncells) {
+    const int p = q.pidx;
+    const unsigned w = occ[p >> 6];
+    q.mcur = maj[((w >> ((p >> 1) & 31)) & 1u) ? p : ncells];
+}
 // Next(): false when exhausted. `maj` is the LDS copy; sy/sz the linear strides of y and z.
 __device__ __forceinline__ bool ddal_next(DdaL &q, const float *maj, int sy, int sz, int ncells, float *s0, float *s1,
                                           float *mval) {
@@ -1371,6 +1385,14 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
     // the host routes GridMedium majorant grids of more than 4096 cells to the wavefront kernels
     if constexpr (!kVdb) stage_majorant(P.med, s_maj);
     const float *__restrict__ majp = kVdb ? P.med.majorant : s_maj;
+    // NanoVDB: the majorant's coarse occupancy level (one bit per cell pair, 16 KiB at 64^3;
+    // 33 + 16 KiB per block keeps three blocks of 256 lanes per CU)
+    __shared__ unsigned s_occ[kVdb ? kOccWords : 1];
+    const bool useOcc = kVdb && P.med.occ != nullptr;
+    if (useOcc) {
+        const int nw = (P.med.mres[0] * P.med.mres[1] * P.med.mres[2] + 63) >> 6;
+        for (int i = threadIdx.x; i < nw; i += blockDim.x) s_occ[i] = P.med.occ[i];
+    }
     const int nlds = P.lights.n < 4 ? P.lights.n : 4;
     for (int i = threadIdx.x; i < kNTable; i += blockDim.x) {
         s_tab[i] = P.med.sigma_a[i];
@@ -1744,7 +1766,8 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
                     }
                 }
                 // unconditional (all busy lanes): in flight during the candidate test below
-                ddal_prefetch(it, majp);
+                if (kVdb && useOcc) ddal_prefetch_occ(it, majp, s_occ, maj_n);
+                else ddal_prefetch(it, majp);
                 if (walk == 0 && !needNext) {
                     // Fast reject: the candidate t = tMin - log(1-u)/sigma_maj is decided against
                     // segMax from the hardware log2 (v_log_f32, ~1 ulp) when it lies outside an
@@ -2121,6 +2144,21 @@ __global__ void __launch_bounds__(256) k_majorant_vdb(vdb::Grid g, float3 bmin, 
         for (int w = 1; w < (int)(blockDim.x / 64); ++w) r = r < red[w] ? red[w] : r;
         out[cell] = r;
     }
+}
+
+// Coarse occupancy level of a majorant grid (DevMedium::occ): one bit per pair of linear cells,
+// set unless both cells' majorants are 0 (NaN counts as occupied).
+__global__ void __launch_bounds__(256) k_majorant_occupancy(const float *__restrict__ maj, int n, unsigned *occ,
+                                                            int nwords) {
+    const int w = blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= nwords) return;
+    unsigned bits = 0;
+    for (int b = 0; b < 32; ++b) {
+        const int i = 64 * w + 2 * b;
+        const bool nz = (i < n && !(maj[i] == 0.f)) || (i + 1 < n && !(maj[i + 1] == 0.f));
+        bits |= (unsigned)nz << b;
+    }
+    occ[w] = bits;
 }
 
 // RGBGridMedium's 16^3 majorant (media.cpp:364-377): per cell, sigmaScale * (max over the

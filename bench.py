@@ -80,6 +80,8 @@ def parse():
     p.add_argument("--majorant-res", type=int, default=None,
                    help="GridMedium majorant resolution per axis: 0 = pbrt's 16^3 (replay default), -1 = tuned "
                         "on the device among 1,2,4,8,16 (fast-mode default, outside the timed region)")
+    p.add_argument("--occupancy", type=int, default=0,
+                   help="NanoVDB: coarse majorant occupancy level in LDS (avr_set_majorant_occupancy; -2 %%, off)")
     p.add_argument("--ray-binning", type=int, default=0,
                    help="wavefront kernels: counting-sort the queues by (majorant cell, octant) before each launch")
     p.add_argument("--nvdb", default=None,
@@ -185,7 +187,7 @@ def pmc_passes(args, kernel_substr="k_paths", timeout_s=240):
     child = [sys.executable, os.path.join(ROOT, "bench.py"), "--pmc-child", "--no-cpu-baseline", "--pmc", "off",
              "--steps", "2", "--warmup", "1"]
     for k in ("res", "width", "height", "spp_per_step", "max_paths", "kernel", "medium", "refill_min", "grid_layout",
-              "dda_budget", "zsobol_table", "sampler", "filter", "mode", "majorant_res", "ray_binning", "nvdb",
+              "dda_budget", "zsobol_table", "sampler", "filter", "mode", "majorant_res", "ray_binning", "occupancy", "nvdb",
               "scene"):
         if getattr(args, k) is not None:
             child += [f"--{k.replace('_', '-')}", str(getattr(args, k))]
@@ -331,6 +333,8 @@ def main():
     integ.ctx.set_sampler_table(args.zsobol_table)
     if args.ray_binning:
         integ.ctx.set_ray_binning(1)
+    if args.occupancy:
+        integ.ctx.set_majorant_occupancy(1)
     maj_res = tuple(scene.medium.majorant_res)
     tune_ms = None
     if args.majorant_res == -1 or (args.majorant_res is None and args.mode == "fast" and vdb is None):
@@ -541,6 +545,7 @@ def main():
             },
             "fast_mode": fast_line,
             "grid_layout": grid_layout,
+            "majorant_occupancy": bool(args.occupancy) if vdb is not None else None,
             "simd_utilisation": (agg["active_lane_iterations"] / (64.0 * agg["loop_iterations"])
                                  if agg.get("loop_iterations") else None),
             "cpu_baseline": cpu,

@@ -87,6 +87,13 @@ int avr_set_render_mode(avr_context *ctx, int mode);
  * octant) before each k_medium / k_shadow launch, so a wave's lanes gather from nearby voxels
  * (north star "density fetches coalesced along sorted ray packets"). Results unchanged. */
 int avr_set_ray_binning(avr_context *ctx, int on);
+/* NanoVDBMedium in the persistent kernel: 1 = stage a coarse occupancy level of the majorant
+ * grid (one bit per cell pair, up to 64^3 cells) in LDS, so majorant-0 cells skip the L2 read
+ * of the majorant; 0 (default) = read every cell's majorant (measured 2 % faster: occupied
+ * cells then wait for the LDS bit before their L2 read). Rebuilds the current majorant.
+ * Results unchanged (no reference counterpart: a DDAMajorantIterator, media.h:141-214, memory
+ * schedule only). */
+int avr_set_majorant_occupancy(avr_context *ctx, int on);
 /* k_paths: refill a wave's idle lanes with new samples once at least `lanes` (1..64)
  * are idle (or none is busy); larger values batch the camera-ray setup across lanes.
  * 0 = default by render mode (32 replay, 40 fast). */

@@ -244,6 +244,34 @@ def test_nanovdb_medium_from_nvdb_file_renders_identically(tmp_path):
     assert np.array_equal(films[0][0], films[1][0]) and np.array_equal(films[0][1], films[1][1])
 
 
+@pytest.mark.parametrize("mres", [None, 21, 70])
+def test_nanovdb_majorant_occupancy_level_changes_nothing(mres):
+    """The coarse occupancy level of NanoVDB's majorant in LDS (avr_set_majorant_occupancy):
+    majorant-0 cells read a trailing zero instead of their own 0 — the films and work counters
+    equal the run without the level and the wavefront kernels' run. Resolutions: pbrt's 64^3,
+    an odd 21^3 (pairs straddle rows, a ragged last word) and 70^3 (more cells than the LDS
+    level holds: no level)."""
+    from acceleratedvolrenderer_amd import VolPathIntegrator, scenes
+    from oracle import binding
+    dens = binding.cloud_grid(32)
+    g = scenes.vdb_grid(dens)
+    runs = []
+    for kernel, occ in (("persistent", 1), ("persistent", 0), ("wavefront", 1)):
+        scene = scenes.s_cloud_vdb(g, width=40, height=24)
+        if mres:
+            scene.medium.majorant_res = (mres,) * 3
+        integ = VolPathIntegrator(scene, maxdepth=scenes.CLOUD_MAXDEPTH, spp=4, seed=0, device=0, kernel=kernel)
+        integ.ctx.set_majorant_occupancy(occ)
+        rgb, w = integ.render()
+        runs.append((rgb, w, integ.stats()))
+        integ.close()
+    (r0, w0, s0), (r1, w1, s1), (r2, w2, _) = runs
+    assert np.array_equal(r0, r1) and np.array_equal(w0, w1)
+    assert np.array_equal(r0, r2) and np.array_equal(w0, w2)
+    for k in ("medium_lookups", "shadow_lookups", "medium_dda_steps"):
+        assert s0[k] == s1[k], k
+
+
 def test_density_fetch_kernel_and_lookup_trace():
     """The standalone density fetch (avr_density_fetch) is SampledGrid::Lookup bit for bit (oracle
     grid_lookup), in both grid layouts; the wavefront lookup trace records one point per

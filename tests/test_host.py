@@ -196,3 +196,4 @@ def test_boundary_entry_points_reject_bad_arguments_without_a_gpu():
     assert lib.avr_set_majorant_res(None, (capi.ctypes.c_int * 3)(4, 4, 4)) != 0
     assert lib.avr_set_render_mode(None, 1) != 0
     assert lib.avr_set_ray_binning(None, 1) != 0
+    assert lib.avr_set_majorant_occupancy(None, 1) != 0
