@@ -48,24 +48,35 @@ def _compile(args):
     return obj
 
 
-def build(force=False, verbose=False, jobs=None):
-    if not force and up_to_date():
+def build(force=False, verbose=False, jobs=None, variant=None, defines=()):
+    """Build the library. `variant` + `defines` (e.g. ["-DAVR_PATHS_WAVES_GRAY=4"]) build an
+    experiment copy into variants/<variant>/libavr_hip.so instead (load it with AVR_LIB)."""
+    out, objdir = OUT, OBJDIR
+    if variant:
+        out = os.path.join(ROOT, "variants", variant, "libavr_hip.so")
+        objdir = os.path.join(ROOT, "variants", variant, "obj")
+    elif not force and up_to_date():
         return OUT
-    os.makedirs(OBJDIR, exist_ok=True)
-    units = [(SRC, os.path.join(OBJDIR, "avr_capi.o"), ["-DAVR_KP_SPLIT"], verbose)]
+    os.makedirs(objdir, exist_ok=True)
+    defines = list(defines)
+    units = [(SRC, os.path.join(objdir, "avr_capi.o"), ["-DAVR_KP_SPLIT"] + defines, verbose)]
     for med, fast in KP_UNITS:
-        units.append((KPATHS, os.path.join(OBJDIR, f"avr_kpaths_m{med}_f{fast}.o"),
-                      [f"-DAVR_KP_MED={med}", f"-DAVR_KP_FAST={fast}"], verbose))
+        units.append((KPATHS, os.path.join(objdir, f"avr_kpaths_m{med}_f{fast}.o"),
+                      [f"-DAVR_KP_MED={med}", f"-DAVR_KP_FAST={fast}"] + defines, verbose))
     jobs = jobs or max(1, min(len(units), int(os.environ.get("MAX_JOBS", os.cpu_count() or 4))))
     with ThreadPoolExecutor(jobs) as ex:
         objs = list(ex.map(_compile, units))
-    cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC"] + objs + ["-o", OUT + ".tmp"] + LIBS
+    cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC"] + objs + ["-o", out + ".tmp"] + LIBS
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.check_call(cmd)
-    os.replace(OUT + ".tmp", OUT)
-    return OUT
+    os.replace(out + ".tmp", out)
+    return out
 
 
 if __name__ == "__main__":
-    print(build(force=True, verbose=True))
+    import sys
+    if len(sys.argv) > 1:   # python -m acceleratedvolrenderer_amd.build <variant> -DNAME=VALUE ...
+        print(build(verbose=True, variant=sys.argv[1], defines=sys.argv[2:]))
+    else:
+        print(build(force=True, verbose=True))
