@@ -43,7 +43,7 @@ for name in ("bench.log", "zs_gauss.log"):
 clk, simds = 2.4e9, 1024
 valu = s2["SQ_INSTS_VALU"]
 out = {
-    "round": int(rnd[1:]), "source": f"{d} (scripts/gpu_round1_{os.path.basename(d)}.sh), MI355X, S-cloud-1024 720p, "
+    "round": int(rnd[1:]), "source": f"{d} (tools/pmc_pass.sh), MI355X, S-cloud-1024 720p, "
                                       f"16 spp per launch, {sampler} sampler, {filt} filter",
     "kernel": kname, "rocprof_kernel_stats": {k: kp[k] for k in ("Calls", "AverageNs", "MinNs", "MaxNs")},
     "rocprof_avg_launch_ns": avg_ns,
@@ -62,6 +62,15 @@ out = {
                          "wait_inst_any (dependency/issue stall)": s1["SQ_WAIT_INST_ANY"] / s1["SQ_WAVE_CYCLES"],
                          "wait_any (s_waitcnt: memory/LDS)": s1["SQ_WAIT_ANY"] / s1["SQ_WAVE_CYCLES"]},
 }
+if os.path.isdir(os.path.join(d, "pmc_tcc")):
+    t, _ = pmc("pmc_tcc")
+    hit, miss = t.get("TCC_HIT_sum", 0.0), t.get("TCC_MISS_sum", 0.0)
+    out["TCC"] = {"TCC_HIT_sum": hit, "TCC_MISS_sum": miss, "hit_rate": hit / max(1.0, hit + miss)}
+if bench:
+    spl = bench["config"]["global_batch"]   # samples per step = per k_paths launch
+    out["samples_per_launch"] = spl
+    out["valu_wave_instructions_per_sample"] = valu / spl
+    out["bench_value"] = bench["value"]
 dst = os.path.join(ROOT, "profiles", f"{rnd}_pmc_k_paths_{sampler}_{filt}.json")
 json.dump(out, open(dst, "w"), indent=1)
 print(dst, round(out["valu_issue_fraction"], 3), out["wave_cycle_split"])
