@@ -697,14 +697,11 @@ template <int K> struct PathSampler {
     }
 };
 
-// GetCameraSample (samplers.h:797-815) after the wavelength draw: pixel 2D through the
-// film's filter (BoxFilter::Sample filters.h:67-70 or GaussianFilter's FilterSampler),
-// time (1D) and lens (2D); returns pFilm and the filter weight.
-template <typename Smp>
-__device__ __forceinline__ void camera_sample(const Params &P, Smp &smp, int px, int py, float *pFilmX, float *pFilmY,
-                                              float *weight, const smp::FilterTables *ft = nullptr) {
-    float fu0, fu1;
-    smp.get2d(P, &fu0, &fu1);
+// The pixel sample of GetCameraSample (samplers.h:797-815) from its 2D draw (fu0, fu1): the
+// film's filter (BoxFilter::Sample filters.h:67-70 or GaussianFilter's FilterSampler);
+// returns pFilm and the filter weight.
+__device__ __forceinline__ void camera_filter(const Params &P, int px, int py, float fu0, float fu1, float *pFilmX,
+                                              float *pFilmY, float *weight, const smp::FilterTables *ft) {
     float fpx, fpy;
     *weight = 1.f;
     if (P.film.filter_type == 0) {
@@ -715,9 +712,69 @@ __device__ __forceinline__ void camera_sample(const Params &P, Smp &smp, int px,
     }
     *pFilmX = ((float)px + fpx) + 0.5f;
     *pFilmY = ((float)py + fpy) + 0.5f;
+}
+// GetCameraSample after the wavelength draw: pixel 2D through the filter, time (1D) and
+// lens (2D).
+template <typename Smp>
+__device__ __forceinline__ void camera_sample(const Params &P, Smp &smp, int px, int py, float *pFilmX, float *pFilmY,
+                                              float *weight, const smp::FilterTables *ft = nullptr) {
+    float fu0, fu1;
+    smp.get2d(P, &fu0, &fu1);
+    camera_filter(P, px, py, fu0, fu1, pFilmX, pFilmY, weight, ft);
     smp.get1d(P);                 // time
     float l0, l1;
     smp.get2d(P, &l0, &l1);       // lens
+}
+
+// Cooperative ZSobol draws in k_paths' service rounds. Each lane with `req` needs N draws at
+// its dimension + off[j] (a 2D draw where two[j]); the wave's N * popc(req) draws are spread
+// over all 64 lanes — busy lanes included, which wait through the handler anyway — so a
+// round evaluates the sampler ceil(N * popc / 64) times instead of N times, and each
+// requester pulls its results back with ds_bpermute. Results are bit-identical to the
+// sequential get1d / get2d calls (ZSobol::draw_at: a pure function of sample and dimension);
+// the requesters' dimension then advances by `adv`. s_st: this wave's 64 LDS entries.
+template <int kW, int N>
+__device__ __forceinline__ void coop_draws(smp::ZSobol &z, const smp::ZSobolParams &zp, bool req, const int (&off)[N],
+                                           const bool (&two)[N], int adv, float (&r0)[N], float (&r1)[N], uint3 *s_st) {
+    const uint64_t mask = __ballot(req);
+    const int lane = lane_id();
+    const int rank = __popcll(mask & ((1ull << lane) - 1ull));
+    if (req) s_st[rank] = make_uint3(z.morton, z.hi, z.dimension);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    _Pragma("unroll") for (int j = 0; j < N; ++j) r0[j] = r1[j] = 0.f;
+    const int total = __popcll(mask) * N;
+    for (int c = 0; c < total; c += 64) {
+        const int t = c + lane;
+        float v0 = 0.f, v1 = 0.f;
+        if (t < total) {
+            const int r = t / N, j = t - r * N;
+            int o = off[0];
+            bool tw = two[0];
+            _Pragma("unroll") for (int jj = 1; jj < N; ++jj) {
+                o = j == jj ? off[jj] : o;
+                tw = j == jj ? two[jj] : tw;
+            }
+            const uint3 st = s_st[r];
+            smp::ZSobol q;
+            q.morton = st.x;
+            q.hi = st.y;
+            q.dimension = 0;
+            q.template draw_at<kW>(zp, st.z + (uint32_t)o, tw, &v0, &v1);
+        }
+        _Pragma("unroll") for (int j = 0; j < N; ++j) {
+            const int src = rank * N + j - c;
+            const bool mine = req && src >= 0 && src < 64;
+            const float a0 = __shfl(v0, src & 63);
+            if (mine) r0[j] = a0;
+            if (two[j]) {
+                const float a1 = __shfl(v1, src & 63);
+                if (mine) r1[j] = a1;
+            }
+        }
+    }
+    if (req) z.dimension += (uint32_t)adv;
 }
 
 __device__ __forceinline__ const float *base_of(const smp::FilterTables &t) { return t.f; }
@@ -1353,6 +1410,8 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
     // per lane: the camera sample's wavelength u and filter weight, parked here until the
     // path ends and its 32-B record is written (off the VGPR budget)
     __shared__ float2 s_rec[256];
+    // ZSobol: the requesters' sampler state for the cooperative draws (coop_draws), 64 per wave
+    __shared__ uint3 s_zst[kSmp != 0 ? 256 : 1];
     // the camera (cameraFromRaster, renderFromCamera: 28 floats used only by the refill), read
     // from LDS there instead of occupying kernel-argument SGPRs for the whole kernel
     __shared__ DevCamera s_cam;
@@ -1550,10 +1609,24 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
             }
         }
         if (__ballot(ev == EV_PHASE)) {
+            // ZSobol: the phase 2D draw and the next segment's three 1D draws of every lane in
+            // EV_PHASE, evaluated cooperatively by the whole wave
+            float q0[4], q1[4];
+            if constexpr (kZSobol) {
+                constexpr int off[4] = {0, 2, 3, 4};
+                constexpr bool two[4] = {true, false, false, false};
+                coop_draws<PathSampler<kSmp>::kW, 4>(smp.z, P.zs, ev == EV_PHASE, off, two, 5, q0, q1,
+                                                     s_zst + (threadIdx.x & ~63u));
+            }
             if (ev == EV_PHASE) {
                 // phase-function sampling (integrators.cpp:1046-1061), then the next segment
                 float up0, up1;
-                smp.get2d(P, &up0, &up1);
+                if constexpr (kZSobol) {
+                    up0 = q0[0];
+                    up1 = q1[0];
+                } else {
+                    smp.get2d(P, &up0, &up1);
+                }
                 float phPdf;
                 const V3 wi = hg_sample<kFast>(-pd, m.g, up0, up1, &phPdf);
                 if (phPdf == 0) {
@@ -1562,11 +1635,11 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
                     beta = beta * (phPdf / phPdf);
                     r_l = r_u / phPdf;
                     pd = wi;
-                    const float h0 = smp.get1d(P);
-                    const float h1 = smp.get1d(P);
+                    const float h0 = kZSobol ? q0[1] : smp.get1d(P);
+                    const float h1 = kZSobol ? q0[2] : smp.get1d(P);
                     seqA = hash_u32(f2u(h0));
                     seqB = hash_u32(f2u(h1));
-                    u = smp.get1d(P);
+                    u = kZSobol ? q0[3] : smp.get1d(P);
                     sd = pd;
                     segPending = true;
                     mode = M_MEDIUM;
@@ -1642,28 +1715,46 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
             base = __shfl(base, leader);
             granted = __shfl(granted, leader);
             exhausted = __shfl(exhausted, leader);
+            const uint64_t lt = lane == 0 ? 0ull : (needMask & ((~0ull) >> (64 - lane)));
+            const int k = __popcll(lt);
+            const bool fresh = mode == M_FETCH && k < granted;
+            int px = 0, py = 0, sIdx = 0;
+            if (fresh) {
+                g = (int)(base + k);
+                const int pix = g % npix;
+                sIdx = g / npix;
+                px = pix % P.film.width;
+                py = pix / P.film.width;
+                if constexpr (kZSobol) smp.start(P, px, py, P.sample_base + sIdx);
+            }
+            // ZSobol: the camera sample's draws (wavelength 1D at dimension 0, pixel 2D at 1;
+            // time and lens at 3..5 are unused) and the first segment's three 1D draws (6..8)
+            // of every new sample, evaluated cooperatively by the whole wave
+            float c0[5], c1[5];
+            if constexpr (kZSobol) {
+                constexpr int off[5] = {0, 1, 6, 7, 8};
+                constexpr bool two[5] = {false, true, false, false, false};
+                coop_draws<PathSampler<kSmp>::kW, 5>(smp.z, P.zs, fresh, off, two, 9, c0, c1,
+                                                     s_zst + (threadIdx.x & ~63u));
+            }
             if (mode == M_FETCH) {
-                const uint64_t lt = lane == 0 ? 0ull : (needMask & ((~0ull) >> (64 - lane)));
-                const int k = __popcll(lt);
-                if (k < granted) {
-                    g = (int)(base + k);
+                if (fresh) {
                     ++nPaths;
                     // ---- camera ray (EvaluatePixelSample, integrators.cpp:235-268) ----
-                    const int pix = g % npix, sIdx = g / npix;
-                    const int px = pix % P.film.width, py = pix / P.film.width;
-                    if constexpr (kZSobol) {
-                        smp.start(P, px, py, P.sample_base + sIdx);
-                    } else {
+                    if constexpr (!kZSobol) {
                         const uint64_t seq = hash_3u32((uint32_t)px, (uint32_t)py, (uint32_t)P.seed);
                         smp.rng.set_sequence(seq, mix_bits(seq));
                         // == rng.Advance((sample_base + sIdx) * 65536) (rng.h:132-146), precomputed
                         smp.rng.state = P.advance[2 * sIdx] * smp.rng.state + smp.rng.inc * P.advance[2 * sIdx + 1];
                     }
-                    const float ulam = smp.get1d(P);
+                    const float ulam = kZSobol ? c0[0] : smp.get1d(P);
                     // wavelengths (pdf: recomputed by k_film from the record's u_lambda)
                     lam = kFast ? film_sample_lambda_fast(P.film, ulam) : film_sample_lambda(P.film, ulam);
                     float pFilmX, pFilmY, fweight;
-                    camera_sample(P, smp, px, py, &pFilmX, &pFilmY, &fweight, &s_ftab);
+                    if constexpr (kZSobol)
+                        camera_filter(P, px, py, c0[1], c1[1], &pFilmX, &pFilmY, &fweight, &s_ftab);
+                    else
+                        camera_sample(P, smp, px, py, &pFilmX, &pFilmY, &fweight, &s_ftab);
                     s_rec[threadIdx.x] = make_float2(ulam, fweight);
                     const DevCamera &cam = s_cam;
                     const float *r = cam.raster;
@@ -1688,11 +1779,11 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
                         if (kEmissive && (kMed == 0 || kMed == 1)) Le_l = sample_table(m.Le, li);
                     }
                     // first medium segment: RNG from two sampler dims, u from a third (984-989)
-                    const float h0 = smp.get1d(P);
-                    const float h1 = smp.get1d(P);
+                    const float h0 = kZSobol ? c0[2] : smp.get1d(P);
+                    const float h1 = kZSobol ? c0[3] : smp.get1d(P);
                     seqA = hash_u32(f2u(h0));
                     seqB = hash_u32(f2u(h1));
-                    u = smp.get1d(P);
+                    u = kZSobol ? c0[4] : smp.get1d(P);
                     sd = pd;
                     segPending = true;
                     mode = M_MEDIUM;
