@@ -321,8 +321,8 @@ def main():
     else:
         scene = scenes.s_cloud(density, width=args.width, height=args.height, sampler=args.sampler, spp=spp_total,
                                filter=args.filter)
-        if args.majorant_res and args.majorant_res > 0:
-            scene.medium.majorant_res = (args.majorant_res,) * 3
+    if args.majorant_res and args.majorant_res > 0:
+        scene.medium.majorant_res = (args.majorant_res,) * 3
     integ = VolPathIntegrator(scene, maxdepth=maxdepth, spp=args.spp_per_step, seed=0, device=dev,
                               max_paths=args.max_paths, kernel=args.kernel, grid_layout=args.grid_layout,
                               mode=args.mode)
@@ -337,8 +337,14 @@ def main():
         integ.ctx.set_majorant_occupancy(1)
     maj_res = tuple(scene.medium.majorant_res)
     tune_ms = None
-    if args.majorant_res == -1 or (args.majorant_res is None and args.mode == "fast" and vdb is None):
-        maj_res, tune_ms = integ.tune_majorant(probe=(0, 4))
+    if args.majorant_res == -1 or (args.majorant_res is None and args.mode == "fast"):
+        cands = (1, 2, 4, 8, 16) + ((32, 64) if vdb is not None else ())
+        maj_res, tune_ms = integ.tune_majorant(candidates=cands, probe=(0, 4))
+        if world > 1:   # every rank renders with rank 0's choice
+            t = torch.tensor(list(maj_res), dtype=torch.int64, device=f"cuda:{dev}")
+            dist.broadcast(t, src=0)
+            maj_res = tuple(int(v) for v in t.tolist())
+            integ.ctx.set_majorant_res(maj_res)
         log(f"tuned majorant {maj_res} (probe ms {tune_ms})")
         args.majorant_res = maj_res[0]   # the counter passes (child processes) render the same majorant
 
