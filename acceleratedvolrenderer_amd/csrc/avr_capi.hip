@@ -1339,7 +1339,7 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
             EV_MARK(e1);
             p.rec_mode = 1;   // k_film reads the records k_paths wrote
             p.fast = c->render_mode;
-            hipLaunchKernelGGL(avr::k_film, dim3(blocks_for(P)), dim3(256), 0, c->stream, p);
+            hipLaunchKernelGGL(avr::k_film, dim3(blocks_for(P)), dim3(256), avr::film_lds_bytes(c->film.nbuckets), c->stream, p);
             HIP_TRY(hipGetLastError());
             EV_MARK(e2);
             c->timed.push_back({e0, e1, &avr_stats::ms_medium, true});
@@ -1429,7 +1429,7 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
             first = false;
         }
         EV_MARK(f0);
-        hipLaunchKernelGGL(avr::k_film, dim3(blocks_for(P)), dim3(256), 0, c->stream, p);
+        hipLaunchKernelGGL(avr::k_film, dim3(blocks_for(P)), dim3(256), avr::film_lds_bytes(c->film.nbuckets), c->stream, p);
         HIP_TRY(hipGetLastError());
         EV_MARK(f1);
         c->timed.push_back({f0, f1, &avr_stats::ms_film, false});

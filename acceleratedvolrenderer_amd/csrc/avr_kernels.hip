@@ -1308,6 +1308,9 @@ __global__ void __launch_bounds__(256) k_bin_scatter(const int *__restrict__ que
 #ifndef AVR_PATHS_WAVES_GRAY
 #define AVR_PATHS_WAVES_GRAY 3   // 168 VGPRs, no scratch (4 waves -> 128 VGPRs spills ~100 B/lane)
 #endif
+#ifndef AVR_COOP_SPEC
+#define AVR_COOP_SPEC 1
+#endif
 #ifndef AVR_PATHS_WAVES_SPEC
 #define AVR_PATHS_WAVES_SPEC 2   // 4-wavelength state: ~220 VGPRs without scratch
 #endif
@@ -1481,6 +1484,9 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
     Spec L{}, lam{}, Le_l{};
     S beta{}, r_u{}, r_l{}, sig_a{}, sig_s{};
     constexpr bool kZSobol = kSmp != 0;   // kSmp: 0 Independent, 2 / 3 ZSobol with 32 / 64-bit index
+    // cooperative ZSobol draws (coop_draws) in the phase handler and the refill; the
+    // 4-wavelength instantiations may opt out (AVR_COOP_SPEC=0: per-lane draws as pbrt does)
+    constexpr bool kCoop = kZSobol && (kGray || AVR_COOP_SPEC);
     PathSampler<kSmp> smp{};
     int depth = 0;
     V3 po{}, pd{};         // segment origin (== the path vertex) and the path's ray direction
@@ -1516,8 +1522,11 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
                 // SampleLd: light pick (BVH infinite-light branch) + shadow-ray spawn (1282-1338)
                 const V3 wo = -pd;
                 const float ul = smp.get1d(P);
-                float uL0, uL1;
-                smp.get2d(P, &uL0, &uL1);   // uLight (unused by distant lights)
+                float uL0 = 0.f, uL1 = 0.f;
+                // uLight: read by the image light only; the other instantiations just step the
+                // ZSobol dimension past it (the independent sampler's PCG32 still draws twice)
+                if constexpr (kImage || !kZSobol) smp.get2d(P, &uL0, &uL1);
+                else smp.z.dimension += 2;
                 ev = EV_PHASE;                       // unless a shadow ray is spawned
                 L = L + Spec::c(0.f);                // L += SampleLd(...) == 0 if nothing spawns
                 const int nl = P.lights.n;
@@ -1612,7 +1621,7 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
             // ZSobol: the phase 2D draw and the next segment's three 1D draws of every lane in
             // EV_PHASE, evaluated cooperatively by the whole wave
             float q0[4], q1[4];
-            if constexpr (kZSobol) {
+            if constexpr (kCoop) {
                 constexpr int off[4] = {0, 2, 3, 4};
                 constexpr bool two[4] = {true, false, false, false};
                 coop_draws<PathSampler<kSmp>::kW, 4>(smp.z, P.zs, ev == EV_PHASE, off, two, 5, q0, q1,
@@ -1621,7 +1630,7 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
             if (ev == EV_PHASE) {
                 // phase-function sampling (integrators.cpp:1046-1061), then the next segment
                 float up0, up1;
-                if constexpr (kZSobol) {
+                if constexpr (kCoop) {
                     up0 = q0[0];
                     up1 = q1[0];
                 } else {
@@ -1635,11 +1644,11 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
                     beta = beta * (phPdf / phPdf);
                     r_l = r_u / phPdf;
                     pd = wi;
-                    const float h0 = kZSobol ? q0[1] : smp.get1d(P);
-                    const float h1 = kZSobol ? q0[2] : smp.get1d(P);
+                    const float h0 = kCoop ? q0[1] : smp.get1d(P);
+                    const float h1 = kCoop ? q0[2] : smp.get1d(P);
                     seqA = hash_u32(f2u(h0));
                     seqB = hash_u32(f2u(h1));
-                    u = kZSobol ? q0[3] : smp.get1d(P);
+                    u = kCoop ? q0[3] : smp.get1d(P);
                     sd = pd;
                     segPending = true;
                     mode = M_MEDIUM;
@@ -1731,7 +1740,7 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
             // time and lens at 3..5 are unused) and the first segment's three 1D draws (6..8)
             // of every new sample, evaluated cooperatively by the whole wave
             float c0[5], c1[5];
-            if constexpr (kZSobol) {
+            if constexpr (kCoop) {
                 constexpr int off[5] = {0, 1, 6, 7, 8};
                 constexpr bool two[5] = {false, true, false, false, false};
                 coop_draws<PathSampler<kSmp>::kW, 5>(smp.z, P.zs, fresh, off, two, 9, c0, c1,
@@ -1747,11 +1756,11 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
                         // == rng.Advance((sample_base + sIdx) * 65536) (rng.h:132-146), precomputed
                         smp.rng.state = P.advance[2 * sIdx] * smp.rng.state + smp.rng.inc * P.advance[2 * sIdx + 1];
                     }
-                    const float ulam = kZSobol ? c0[0] : smp.get1d(P);
+                    const float ulam = kCoop ? c0[0] : smp.get1d(P);
                     // wavelengths (pdf: recomputed by k_film from the record's u_lambda)
                     lam = kFast ? film_sample_lambda_fast(P.film, ulam) : film_sample_lambda(P.film, ulam);
                     float pFilmX, pFilmY, fweight;
-                    if constexpr (kZSobol)
+                    if constexpr (kCoop)
                         camera_filter(P, px, py, c0[1], c1[1], &pFilmX, &pFilmY, &fweight, &s_ftab);
                     else
                         camera_sample(P, smp, px, py, &pFilmX, &pFilmY, &fweight, &s_ftab);
@@ -1779,11 +1788,11 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
                         if (kEmissive && (kMed == 0 || kMed == 1)) Le_l = sample_table(m.Le, li);
                     }
                     // first medium segment: RNG from two sampler dims, u from a third (984-989)
-                    const float h0 = kZSobol ? c0[2] : smp.get1d(P);
-                    const float h1 = kZSobol ? c0[3] : smp.get1d(P);
+                    const float h0 = kCoop ? c0[2] : smp.get1d(P);
+                    const float h1 = kCoop ? c0[3] : smp.get1d(P);
                     seqA = hash_u32(f2u(h0));
                     seqB = hash_u32(f2u(h1));
-                    u = kZSobol ? c0[4] : smp.get1d(P);
+                    u = kCoop ? c0[4] : smp.get1d(P);
                     sd = pd;
                     segPending = true;
                     mode = M_MEDIUM;
@@ -2023,11 +2032,31 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
 // ---------------------------------------------------------------------------
 // Film — NaN/Inf guard (integrators.cpp:272-282), PixelSensor::ToSensorRGB (film.h:95-100),
 // RGBFilm::AddSample (film.h:239-255): per pixel, the pass's samples in sampleIndex order.
+// SpectralFilm: a pixel's bucket sums (up to kFilmLdsBuckets of them) are accumulated in this
+// thread's LDS slice and written back once per pass — the same fp64 additions in the same
+// order as the read-modify-writes on HBM, without their 2 x 4 dependent round trips per sample.
+constexpr int kFilmLdsBuckets = 16;
+inline size_t film_lds_bytes(int nb) { return nb > 0 && nb <= kFilmLdsBuckets ? 2 * (size_t)nb * 256 * sizeof(double) : 0; }
 __global__ void __launch_bounds__(256) k_film(Params P) {
+    extern __shared__ double s_bk[];   // [sum | weight][bucket][thread]: film_lds_bytes(nb)
     const int npix = P.pass_pixels;
+    const int nb = P.film.nbuckets;
+    const bool ldsBuckets = nb > 0 && nb <= kFilmLdsBuckets;
     for (int pix = blockIdx.x * blockDim.x + threadIdx.x; pix < npix; pix += gridDim.x * blockDim.x) {
         double s0 = P.film.rgb_sum[3 * (size_t)pix], s1 = P.film.rgb_sum[3 * (size_t)pix + 1],
                s2 = P.film.rgb_sum[3 * (size_t)pix + 2], ws = P.film.w_sum[pix];
+        double *gbs = P.film.bucket_sum + (size_t)pix * nb, *gbw = P.film.bucket_w + (size_t)pix * nb;
+        double *bs = gbs, *bw = gbw;
+        int bstride = 1;
+        if (ldsBuckets) {
+            bs = s_bk + threadIdx.x;
+            bw = s_bk + nb * 256 + threadIdx.x;
+            bstride = 256;
+            for (int b = 0; b < nb; ++b) {
+                bs[b * 256] = gbs[b];
+                bw[b * 256] = gbw[b];
+            }
+        }
         for (int s = 0; s < P.pass_samples; ++s) {
             const size_t id = (size_t)s * npix + pix;
             Spec L;
@@ -2071,17 +2100,20 @@ __global__ void __launch_bounds__(256) k_film(Params P) {
                 const float lm = fmaxf_(fmaxf_(fmaxf_(L.v0, L.v1), L.v2), L.v3);
                 if (lm > P.film.max_component) L = L * (P.film.max_component / lm);
                 L = L * (w * 106.856895f);
-                const int nb = P.film.nbuckets;
-                double *bs = P.film.bucket_sum + (size_t)pix * nb, *bw = P.film.bucket_w + (size_t)pix * nb;
                 const float lv[4] = {lam.v0, lam.v1, lam.v2, lam.v3}, Lv[4] = {L.v0, L.v1, L.v2, L.v3};
                 _Pragma("unroll") for (int i = 0; i < 4; ++i) {
                     int b = (int)((float)nb * (lv[i] - P.film.lmin) / (P.film.lmax - P.film.lmin));
                     b = b < 0 ? 0 : (b > nb - 1 ? nb - 1 : b);
-                    bs[b] += (double)Lv[i];
-                    bw[b] += (double)w;
+                    bs[b * bstride] += (double)Lv[i];
+                    bw[b * bstride] += (double)w;
                 }
             }
         }
+        if (ldsBuckets)
+            for (int b = 0; b < nb; ++b) {
+                gbs[b] = bs[b * 256];
+                gbw[b] = bw[b * 256];
+            }
         P.film.rgb_sum[3 * (size_t)pix] = s0;
         P.film.rgb_sum[3 * (size_t)pix + 1] = s1;
         P.film.rgb_sum[3 * (size_t)pix + 2] = s2;
