@@ -4,8 +4,8 @@
 // wavefront/integrator.cpp:290-493) for the volumetric path.
 //
 // Scheduling: the requested sample range is cut into passes of S sample indices
-// over all P pixels (P*S <= max_paths, default 16M paths in flight — HBM is 288 GB,
-// pbrt's GPU path caps at 1M). Each pass: k_camera, then depth iterations of
+// over all P pixels (P*S <= max_paths, default 16M paths in flight for the wavefront
+// kernels and 64M 32-B sample records for k_paths — HBM is 288 GB, pbrt's GPU path caps at 1M). Each pass: k_camera, then depth iterations of
 // {k_medium, k_shadow} over compacted queues until no path survives, then k_film.
 // Everything is enqueued on one HIP stream; the host reads back one int (the
 // survivor count) per depth iteration to size the next launch and stop early.
@@ -55,7 +55,12 @@ hipError_t dalloc(T **p, size_t n) { return hipMalloc((void **)p, std::max<size_
 
 struct avr_context {
     int device = 0;
+    // paths per pass: max_paths when the caller set one, else 16M for the wavefront kernels
+    // (full SoA path state, ~250 B per path) and 64M for k_paths (a 32-B record per sample
+    // only: 2 GiB of HBM; longer passes amortise the persistent kernel's drain tail)
     long long max_paths = 16ll << 20;
+    bool max_paths_set = false;
+    long long rec_cap = 0;   // k_paths records allocated (ps.rec, 2 float4 per sample)
     hipStream_t own_stream = nullptr, stream = nullptr;
     // medium
     avr::DevMedium med{};
@@ -162,7 +167,7 @@ void release_comms(avr_context *c) {
 }
 
 void free_paths(avr_context *c) {
-    float4 *f4[] = {c->ps.o, c->ps.d, c->ps.lambda, c->ps.pdf, c->ps.beta, c->ps.r_u, c->ps.r_l, c->ps.L, c->ps.rec,
+    float4 *f4[] = {c->ps.o, c->ps.d, c->ps.lambda, c->ps.pdf, c->ps.beta, c->ps.r_u, c->ps.r_l, c->ps.L,
                     c->sh.o, c->sh.d, c->sh.bf, c->sh.Ls, c->sh.rp};
     for (auto p : f4) if (p) (void)hipFree(p);
     if (c->ps.smp_state) (void)hipFree(c->ps.smp_state);
@@ -172,9 +177,26 @@ void free_paths(avr_context *c) {
     if (c->sh.path) (void)hipFree(c->sh.path);
     if (c->sh.pdfs) (void)hipFree(c->sh.pdfs);
     for (auto &q : c->d_queue) if (q) (void)hipFree(q), q = nullptr;
+    float4 *rec = c->ps.rec;   // the k_paths records are managed by ensure_records
     c->ps = {};
+    c->ps.rec = rec;
     c->sh = {};
     c->cap = 0;
+}
+
+void free_records(avr_context *c) {
+    if (c->ps.rec) (void)hipFree(c->ps.rec);
+    c->ps.rec = nullptr;
+    c->rec_cap = 0;
+}
+
+// k_paths' per-sample records (32 B each), independent of the wavefront SoA
+int ensure_records(avr_context *c, long long n) {
+    if (n <= c->rec_cap) return AVR_OK;
+    free_records(c);
+    HIP_TRY(dalloc(&c->ps.rec, 2 * (size_t)n));
+    c->rec_cap = n;
+    return AVR_OK;
 }
 
 int ensure_paths(avr_context *c, long long n) {
@@ -186,7 +208,6 @@ int ensure_paths(avr_context *c, long long n) {
     HIP_TRY(dalloc(&c->ps.r_l, N)); HIP_TRY(dalloc(&c->ps.L, N));
     HIP_TRY(dalloc(&c->ps.smp_state, N)); HIP_TRY(dalloc(&c->ps.smp_inc, N)); HIP_TRY(dalloc(&c->ps.depth, N));
     HIP_TRY(dalloc(&c->ps.weight, N));
-    HIP_TRY(dalloc(&c->ps.rec, 2 * N));   // k_paths: 32-B record per sample
     HIP_TRY(dalloc(&c->sh.path, N)); HIP_TRY(dalloc(&c->sh.o, N)); HIP_TRY(dalloc(&c->sh.d, N));
     HIP_TRY(dalloc(&c->sh.bf, N)); HIP_TRY(dalloc(&c->sh.Ls, N)); HIP_TRY(dalloc(&c->sh.rp, N));
     HIP_TRY(dalloc(&c->sh.pdfs, N));
@@ -477,7 +498,7 @@ int avr_context_create(int device, long long max_paths, avr_context **out) {
     HIP_TRY(hipSetDevice(device));
     auto *c = new avr_context();
     c->device = device;
-    if (max_paths > 0) c->max_paths = max_paths;
+    if (max_paths > 0) c->max_paths = max_paths, c->max_paths_set = true;
     hipError_t e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
     if (e != hipSuccess) { delete c; return fail(AVR_ERR_HIP, hipGetErrorString(e)); }
     c->stream = c->own_stream;
@@ -588,6 +609,7 @@ int avr_context_destroy(avr_context *c) {
     (void)hipStreamSynchronize(c->stream);
     release_comms(c);
     free_paths(c);
+    free_records(c);
     float *fs[] = {c->d_density_owned, c->d_sigma_a, c->d_sigma_s, c->d_Le, c->d_lescale, c->d_majorant,
                    c->d_lightL, c->d_xyz};
     if (c->d_lights) (void)hipFree(c->d_lights);
@@ -1274,9 +1296,18 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
     }
     const long long P = (long long)c->film.width * c->film.height;
     if (P > (1ll << 30)) return fail(AVR_ERR_ARG, "film too large");
-    const long long Smax = std::max<long long>(1, c->max_paths / P);
+    // k_paths runs every medium type with every light type: GridMedium, RGBGridMedium and
+    // the single-segment Homogeneous/CloudMedium keep the majorant in LDS (at most 4096
+    // cells = pbrt's 16^3; larger grids take the wavefront kernels), NanoVDBMedium reads
+    // its 64^3 majorant through L2
+    const int mcells = c->med.mres[0] * c->med.mres[1] * c->med.mres[2];
+    const bool persistent = c->kernel_mode == 0 &&
+                            (((c->med.type != 3) && mcells <= 4096) || c->med.type == 3) &&
+                            c->med.mres[0] <= 255 && c->med.mres[1] <= 255 && c->med.mres[2] <= 255;
+    const long long maxp = c->max_paths_set ? c->max_paths : (persistent ? (64ll << 20) : c->max_paths);
+    const long long Smax = std::max<long long>(1, maxp / P);
     const long long need = P * std::min<long long>(Smax, std::max(1, spp_end - spp_begin));
-    int rc = ensure_paths(c, need);
+    int rc = persistent ? ensure_records(c, need) : ensure_paths(c, need);
     if (rc) return rc;
     EV_MARK(evStart);
     for (long long base = spp_begin; base < spp_end; base += Smax) {
@@ -1299,14 +1330,6 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
         p.sample_base = (int)base;
         p.stats = c->d_stats;
         const long long n0 = P * S;
-        // k_paths runs every medium type with every light type: GridMedium, RGBGridMedium and
-        // the single-segment Homogeneous/CloudMedium keep the majorant in LDS (at most 4096
-        // cells = pbrt's 16^3; larger grids take the wavefront kernels), NanoVDBMedium reads
-        // its 64^3 majorant through L2
-        const int mcells = c->med.mres[0] * c->med.mres[1] * c->med.mres[2];
-        const bool persistent = c->kernel_mode == 0 &&
-                                (((c->med.type != 3) && mcells <= 4096) || c->med.type == 3) &&
-                                c->med.mres[0] <= 255 && c->med.mres[1] <= 255 && c->med.mres[2] <= 255;
         c->last_persistent = persistent;
         c->last_fast = persistent && c->render_mode == 1;
         if (persistent) {

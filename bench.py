@@ -56,7 +56,8 @@ def parse():
     p.add_argument("--res", type=int, default=1024, help="density grid resolution (n^3)")
     p.add_argument("--width", type=int, default=1280)
     p.add_argument("--height", type=int, default=720)
-    p.add_argument("--spp-per-step", type=int, default=16)
+    p.add_argument("--spp-per-step", type=int, default=64,
+                   help="sample indices per pass (one step); 64 x 720p = 59M k_paths records, 1.9 GB)")
     p.add_argument("--max-paths", type=int, default=0)
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU-baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")

@@ -57,8 +57,9 @@ typedef struct avr_stats {
 const char *avr_last_error(void);
 
 /* Context on HIP device `device` (one process per GPU; no implicit peer access).
- * `max_paths` bounds the paths in flight per pass (0 = default 16M; at most 2^31 - 1:
- * path ids are 32-bit, AVR_ERR_ARG above). */
+ * `max_paths` bounds the paths in flight per pass (0 = default: 64M for the persistent
+ * kernel, whose per-path HBM state is one 32-B sample record, 16M for the wavefront
+ * kernels; at most 2^31 - 1: path ids are 32-bit, AVR_ERR_ARG above). */
 int avr_context_create(int device, long long max_paths, avr_context **out);
 int avr_context_destroy(avr_context *ctx);
 /* Kernel organisation: 0 = persistent-wave megakernel k_paths (default: path state in

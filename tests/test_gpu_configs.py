@@ -110,7 +110,9 @@ def cloud1080():
     gen.sync()
     gen.close()
     scene = scenes.s_cloud(density, width=1920, height=1080, sampler="zsobol", spp=1024, filter="gaussian")
-    integ = VolPathIntegrator(scene, maxdepth=scenes.CLOUD_MAXDEPTH, spp=1024, device=0)
+    # 16M paths per pass (the wavefront default; k_paths' own default is 64M): several passes
+    # per render at 1080p, so the shard tests also cover pass splitting
+    integ = VolPathIntegrator(scene, maxdepth=scenes.CLOUD_MAXDEPTH, spp=1024, device=0, max_paths=16 << 20)
     yield integ, density
     integ.close()
 
