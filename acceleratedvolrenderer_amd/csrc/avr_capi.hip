@@ -1347,7 +1347,7 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
             p.refill_min = c->refill_min > 0 ? c->refill_min : (c->render_mode == 1 ? 40 : 32);
             {
                 const int mres = std::max(c->med.mres[0], std::max(c->med.mres[1], c->med.mres[2]));
-                p.dda_budget = c->dda_budget > 0 ? c->dda_budget : (mres > 16 ? 32 : 12);
+                p.dda_budget = c->dda_budget > 0 ? c->dda_budget : (mres > 16 ? 32 : 10);
             }
             p.heads = c->d_heads;
             HIP_TRY(hipMemsetAsync(c->d_heads, 0, 8 * sizeof(int), c->stream));

@@ -100,7 +100,7 @@ int avr_set_majorant_occupancy(avr_context *ctx, int on);
  * 0 = default by render mode (32 replay, 40 fast). */
 int avr_set_refill_min(avr_context *ctx, int lanes);
 /* k_paths: majorant-grid cells a lane may cross per tracking iteration before yielding to
- * the wave (0 = default: 12 for majorant grids up to 16^3, 32 for finer ones such as
+ * the wave (0 = default: 10 for majorant grids up to 16^3, 32 for finer ones such as
  * NanoVDB's 64^3 — measured optima); bounds the divergence of the DDA walk. No effect on
  * results. */
 int avr_set_dda_budget(avr_context *ctx, int cells);
