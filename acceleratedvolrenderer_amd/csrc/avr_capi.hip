@@ -1344,7 +1344,7 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
                                (long long)base, S);
             HIP_TRY(hipGetLastError());
             p.advance = c->d_advance;
-            p.refill_min = c->refill_min > 0 ? c->refill_min : (c->render_mode == 1 ? 40 : 32);
+            p.refill_min = c->refill_min > 0 ? c->refill_min : 32;   // replay and fast (measured optimum of both)
             {
                 const int mres = std::max(c->med.mres[0], std::max(c->med.mres[1], c->med.mres[2]));
                 p.dda_budget = c->dda_budget > 0 ? c->dda_budget : (mres > 16 ? 32 : 10);

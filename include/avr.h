@@ -97,7 +97,7 @@ int avr_set_ray_binning(avr_context *ctx, int on);
 int avr_set_majorant_occupancy(avr_context *ctx, int on);
 /* k_paths: refill a wave's idle lanes with new samples once at least `lanes` (1..64)
  * are idle (or none is busy); larger values batch the camera-ray setup across lanes.
- * 0 = default by render mode (32 replay, 40 fast). */
+ * 0 = default (32; the measured optimum in both render modes). */
 int avr_set_refill_min(avr_context *ctx, int lanes);
 /* k_paths: majorant-grid cells a lane may cross per tracking iteration before yielding to
  * the wave (0 = default: 10 for majorant grids up to 16^3, 32 for finer ones such as
