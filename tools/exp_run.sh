@@ -1,8 +1,7 @@
 set -o pipefail
 mkdir -p gpurun_out
-B="--pmc off --no-cpu-baseline --steps 4 --warmup 1"
-for sc in "--scene explosion" "--width 1920 --height 1080" "--scene uniform --res 256 --width 512 --height 512" "--medium nanovdb"; do
-  n=$(echo "$sc" | tr -d ' -' | cut -c1-20)
-  timeout -k 10 300 python bench.py $B $sc > gpurun_out/f5_cfg_$n.json 2>gpurun_out/f5_err.log || { tail gpurun_out/f5_err.log; exit 1; }
-  python -c "import json; d=json.load(open('gpurun_out/f5_cfg_$n.json')); print('$sc', d['value'], (d.get('fast_mode') or {}).get('value'), d['ms_per_step'], d['roofline']['avg_launch_ms'])"
+B="--pmc off --no-cpu-baseline --fast-leg 0 --steps 4 --warmup 1 --medium nanovdb"
+for a in "--dda-budget 32" "--dda-budget 24" "--dda-budget 40" "--dda-budget 28" "--dda-budget 32"; do
+  timeout -k 10 200 python bench.py $B $a > gpurun_out/e10_b.json 2>gpurun_out/e10_err.log || { tail gpurun_out/e10_err.log; exit 1; }
+  python -c "import json; d=json.load(open('gpurun_out/e10_b.json')); print('$a', d['value'], d['roofline']['avg_launch_ms'])"
 done
