@@ -5,6 +5,7 @@ The persistent path kernel k_paths has 112 instantiations (medium kind x emissio
 state x sampler x image light x render mode); they are compiled as eight objects
 (csrc/avr_kpaths.hip, one per medium kind and render mode) in parallel with the C-ABI
 unit (csrc/avr_capi.hip, -DAVR_KP_SPLIT), then linked."""
+import hashlib
 import os
 import subprocess
 from concurrent.futures import ThreadPoolExecutor
@@ -32,11 +33,25 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fP
 LIBS = ["-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"]
 
 
+def source_hash(defines=()):
+    """sha256 over every source the library is built from, the compiler flags and the unit
+    list: the library is rebuilt whenever this differs from the hash recorded next to it."""
+    h = hashlib.sha256()
+    for d in DEPS:
+        h.update(os.path.basename(d).encode() + b"\0")
+        with open(d, "rb") as f:
+            h.update(f.read())
+    h.update(repr((FLAGS, LIBS, KP_UNITS, list(defines))).encode())
+    return h.hexdigest()
+
+
 def up_to_date():
-    if not os.path.exists(OUT):
+    """True when libavr_hip.so exists and was built from exactly the current sources (the
+    recorded source hash matches; file times alone can make a stale library look new)."""
+    if not os.path.exists(OUT) or not os.path.exists(OUT + ".srchash"):
         return False
-    t = os.path.getmtime(OUT)
-    return all(os.path.getmtime(d) <= t for d in DEPS if os.path.exists(d))
+    with open(OUT + ".srchash") as f:
+        return f.read().strip() == source_hash()
 
 
 def _compile(args):
@@ -71,6 +86,8 @@ def build(force=False, verbose=False, jobs=None, variant=None, defines=()):
         print(" ".join(cmd), flush=True)
     subprocess.check_call(cmd)
     os.replace(out + ".tmp", out)
+    with open(out + ".srchash", "w") as f:
+        f.write(source_hash(defines) + "\n")
     return out
 
 

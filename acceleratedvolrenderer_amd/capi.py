@@ -114,6 +114,12 @@ SIGNATURES = {
                                               ctypes.c_int, c_int_p]),
     "avr_generate_cloud": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_longlong,
                                           ctypes.c_longlong, ctypes.c_float, ctypes.c_float, ctypes.c_float]),
+    "avr_generate_rgb_explosion": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                                  ctypes.c_int, ctypes.c_longlong, ctypes.c_longlong]),
+    "avr_medium_rgbgrid_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                 c_float_p, c_float_p, c_float_p, ctypes.c_void_p, ctypes.c_void_p,
+                                                 ctypes.c_float, ctypes.c_float, ctypes.c_void_p, c_float_p,
+                                                 ctypes.c_float]),
     "avr_read_majorant": (ctypes.c_int, [ctypes.c_void_p, c_float_p]),
     "avr_lights": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, c_int_p, c_float_p, c_float_p, c_float_p,
                                   ctypes.c_float]),
@@ -319,6 +325,14 @@ class Context:
         if getattr(med, "type_id", 0) == 1:
             _check(self.lib.avr_medium_homogeneous(self.h, _fp(args[0]), _fp(args[1]), _fp(args[2]), _fp(args[3]),
                                                    _fp(args[4]), float(med.g), _fp(Le)))
+        elif getattr(med, "type_id", 0) == 4 and getattr(med, "on_device", False):
+            ill = f32(med.illuminant)
+            self._keep += [ill]
+            ptr = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None
+            _check(self.lib.avr_medium_rgbgrid_device(
+                self.h, med.nx, med.ny, med.nz, _fp(args[0]), _fp(args[1]), _fp(args[2]), ptr(med.rgb_sigma_a),
+                ptr(med.rgb_sigma_s), float(med.sigma_scale), float(med.g), ptr(med.rgb_Le), _fp(ill),
+                float(med.Le_scale)))
         elif getattr(med, "type_id", 0) == 4:
             grids = [f32(g) if g is not None else None for g in (med.rgb_sigma_a, med.rgb_sigma_s, med.rgb_Le)]
             ill = f32(med.illuminant)
@@ -388,6 +402,11 @@ class Context:
     def generate_cloud(self, d_out_ptr, n, first, count, density=1.0, wispiness=1.0, frequency=5.0):
         _check(self.lib.avr_generate_cloud(self.h, ctypes.c_void_p(d_out_ptr), int(n), int(first), int(count),
                                            float(density), float(wispiness), float(frequency)))
+
+    def generate_rgb_explosion(self, d_sa_ptr, d_ss_ptr, d_le_ptr, n, first, count):
+        """k_rgb_explosion into three float4 device arrays (pointers at element `first`)."""
+        _check(self.lib.avr_generate_rgb_explosion(self.h, ctypes.c_void_p(d_sa_ptr), ctypes.c_void_p(d_ss_ptr),
+                                                   ctypes.c_void_p(d_le_ptr), int(n), int(first), int(count)))
 
     def medium_bounds(self):
         out = np.zeros(6, np.float32)

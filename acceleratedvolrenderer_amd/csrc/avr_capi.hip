@@ -118,7 +118,7 @@ struct avr_context {
     float *d_vdb_leaves[2] = {nullptr, nullptr}, *d_vdb_tiles[2] = {nullptr, nullptr};
     int vdb_ibbox[6] = {};    // density grid's active index bbox (majorant clamp)
     // RGBGridMedium grids (sigma_a, sigma_s, Le as float4 {c0, c1, c2, scale}) and illuminant
-    float4 *d_rgb[3] = {nullptr, nullptr, nullptr};
+    float4 *d_rgb[3] = {nullptr, nullptr, nullptr};   // owned copies (avr_medium_rgbgrid only)
     float *d_illum = nullptr;
     // lights: host copy of the device list, ImageInfiniteLight buffers
     avr::DevLight h_lights[avr::kMaxLights] = {};
@@ -135,7 +135,7 @@ struct avr_context {
     uint32_t *d_zs_table = nullptr;
     int zs_dims = 256;
     int zs_key[3] = {-1, -1, -1};
-    int refill_min = 0;       // 0: by render mode (32 replay, 40 fast: measured optima)
+    int refill_min = 0;       // 0: the default, 32 lanes in both render modes (measured optimum)
     int dda_budget = 0;       // 0: by majorant resolution (12 cells up to 16^3, 32 for NanoVDB's 64^3)
     int grid_layout = 1;
     bool gray = false;        // sigma_a and sigma_s constant over 360..830 nm      // 1: build the fat (footprint) copy when memory allows, 0: linear only
@@ -177,24 +177,28 @@ void free_paths(avr_context *c) {
     if (c->sh.path) (void)hipFree(c->sh.path);
     if (c->sh.pdfs) (void)hipFree(c->sh.pdfs);
     for (auto &q : c->d_queue) if (q) (void)hipFree(q), q = nullptr;
-    float4 *rec = c->ps.rec;   // the k_paths records are managed by ensure_records
+    float4 *rec = c->ps.rec, *contrib = c->ps.contrib;   // the k_paths records: ensure_records
     c->ps = {};
     c->ps.rec = rec;
+    c->ps.contrib = contrib;
     c->sh = {};
     c->cap = 0;
 }
 
 void free_records(avr_context *c) {
     if (c->ps.rec) (void)hipFree(c->ps.rec);
-    c->ps.rec = nullptr;
+    if (c->ps.contrib) (void)hipFree(c->ps.contrib);
+    c->ps.rec = c->ps.contrib = nullptr;
     c->rec_cap = 0;
 }
 
-// k_paths' per-sample records (32 B each), independent of the wavefront SoA
+// k_paths' per-sample records (32 B each) and RGBFilm's per-sample contributions (16 B each,
+// k_film_rgb -> k_film_sum), independent of the wavefront SoA
 int ensure_records(avr_context *c, long long n) {
     if (n <= c->rec_cap) return AVR_OK;
     free_records(c);
     HIP_TRY(dalloc(&c->ps.rec, 2 * (size_t)n));
+    HIP_TRY(dalloc(&c->ps.contrib, (size_t)n));
     c->rec_cap = n;
     return AVR_OK;
 }
@@ -256,7 +260,8 @@ void free_vdb(avr_context *c) {
 }
 
 // Map::set (NanoVDB): the float inverse matrix and translation are roundings of the f64 map
-bool vdb_map(const avr_vdb_grid *G, avr::vdb::Grid &g) {
+template <typename GridT>
+bool vdb_map(const avr_vdb_grid *G, GridT &g) {
     for (int k = 0; k < 9; ++k) {
         if (!std::isfinite(G->world_to_index[k])) return false;
         g.inv[k] = (float)G->world_to_index[k];
@@ -281,8 +286,9 @@ void vdb_world_bbox(const avr_vdb_grid *G, double lo[3], double hi[3]) {
     }
 }
 
-// Flatten one tree into the block-slot layout of avr_vdb.h and upload it
-int upload_vdb(avr_context *c, const avr_vdb_grid *G, int k, avr::vdb::Grid &g) {
+// Flatten one tree into the block-slot layout of avr_vdb.h, then into its apron layout on
+// the device (what the kernels sample)
+int upload_vdb(avr_context *c, const avr_vdb_grid *G, int k, avr::vdb::Apron &g) {
     if (G->n_leaves < 0 || G->n_tiles < 0 || (G->n_leaves && (!G->leaf_origin || !G->leaf_values)) ||
         (G->n_tiles && (!G->tile_origin || !G->tile_size || !G->tile_value)))
         return fail(AVR_ERR_ARG, "bad vdb grid arrays");
@@ -328,22 +334,66 @@ int upload_vdb(avr_context *c, const avr_vdb_grid *G, int k, avr::vdb::Grid &g) 
         if (s >= 0) return fail(AVR_ERR_ARG, "duplicate leaf origin");
         s = l;
     }
-    g.ox = nslot ? (int)lo[0] : 0; g.oy = nslot ? (int)lo[1] : 0; g.oz = nslot ? (int)lo[2] : 0;
-    g.lnx = (int)nb[0]; g.lny = (int)nb[1]; g.lnz = (int)nb[2];
-    HIP_TRY(dalloc(&c->d_vdb_slot[k], slot.size()));
-    HIP_TRY(hipMemcpyAsync(c->d_vdb_slot[k], slot.data(), slot.size() * sizeof(int), hipMemcpyHostToDevice, c->stream));
+    avr::vdb::Grid base{};
+    base.background = g.background;
+    for (int q = 0; q < 9; ++q) base.inv[q] = g.inv[q];
+    for (int q = 0; q < 3; ++q) base.vec[q] = g.vec[q];
+    base.ox = nslot ? (int)lo[0] : 0; base.oy = nslot ? (int)lo[1] : 0; base.oz = nslot ? (int)lo[2] : 0;
+    base.lnx = (int)nb[0]; base.lny = (int)nb[1]; base.lnz = (int)nb[2];
+    // the base layout (slots, leaves, tiles) lives on the device only while the apron blocks
+    // are filled from it (avr_vdb.h "Apron layout"): a lookup then reads one slot and one block
+    std::vector<int> aslot;
+    std::vector<long long> list;
+    avr::vdb::build_apron_slots(slot.data(), base.lnx, base.lny, base.lnz, G->tile_value, G->n_tiles, G->background,
+                                aslot, list);
+    std::vector<float> consts((size_t)G->n_tiles + 1);
+    for (int t = 0; t < G->n_tiles; ++t) consts[t] = G->tile_value[t];
+    consts[G->n_tiles] = G->background;
+    struct Tmp {
+        int *slot = nullptr;
+        float *leaves = nullptr, *tiles = nullptr;
+        long long *list = nullptr;
+        ~Tmp() {
+            if (slot) (void)hipFree(slot);
+            if (leaves) (void)hipFree(leaves);
+            if (tiles) (void)hipFree(tiles);
+            if (list) (void)hipFree(list);
+        }
+    } tmp;
+    HIP_TRY(dalloc(&tmp.slot, slot.size()));
+    HIP_TRY(hipMemcpyAsync(tmp.slot, slot.data(), slot.size() * sizeof(int), hipMemcpyHostToDevice, c->stream));
     const size_t nleaf = (size_t)G->n_leaves * 512;
-    HIP_TRY(dalloc(&c->d_vdb_leaves[k], nleaf));
+    HIP_TRY(dalloc(&tmp.leaves, std::max<size_t>(nleaf, 1)));
     if (nleaf)
-        HIP_TRY(hipMemcpyAsync(c->d_vdb_leaves[k], G->leaf_values, nleaf * sizeof(float), hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(dalloc(&c->d_vdb_tiles[k], (size_t)G->n_tiles));
+        HIP_TRY(hipMemcpyAsync(tmp.leaves, G->leaf_values, nleaf * sizeof(float), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(dalloc(&tmp.tiles, std::max<size_t>((size_t)G->n_tiles, 1)));
     if (G->n_tiles)
-        HIP_TRY(hipMemcpyAsync(c->d_vdb_tiles[k], G->tile_value, G->n_tiles * sizeof(float), hipMemcpyHostToDevice, c->stream));
-    // the slot vector dies here: finish the copies first
+        HIP_TRY(hipMemcpyAsync(tmp.tiles, G->tile_value, G->n_tiles * sizeof(float), hipMemcpyHostToDevice, c->stream));
+    base.slot = tmp.slot;
+    base.leaves = tmp.leaves;
+    base.tiles = tmp.tiles;
+    HIP_TRY(dalloc(&c->d_vdb_slot[k], aslot.size()));
+    HIP_TRY(hipMemcpyAsync(c->d_vdb_slot[k], aslot.data(), aslot.size() * sizeof(int), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(dalloc(&c->d_vdb_tiles[k], consts.size()));
+    HIP_TRY(hipMemcpyAsync(c->d_vdb_tiles[k], consts.data(), consts.size() * sizeof(float), hipMemcpyHostToDevice,
+                           c->stream));
+    HIP_TRY(dalloc(&c->d_vdb_leaves[k], std::max<size_t>(list.size(), 1) * avr::vdb::kApronVals));
+    if (!list.empty()) {
+        HIP_TRY(dalloc(&tmp.list, list.size()));
+        HIP_TRY(hipMemcpyAsync(tmp.list, list.data(), list.size() * sizeof(long long), hipMemcpyHostToDevice, c->stream));
+        const long long nl = (long long)list.size();
+        const int nblk = (int)std::min<long long>(nl, 1 << 20);
+        hipLaunchKernelGGL(avr::k_vdb_apron, dim3(nblk), dim3(256), 0, c->stream, base, tmp.list, nl,
+                           c->d_vdb_leaves[k]);
+        HIP_TRY(hipGetLastError());
+    }
+    // the host vectors and the base layout die here: finish the copies and the fill first
     HIP_TRY(hipStreamSynchronize(c->stream));
     g.slot = c->d_vdb_slot[k];
-    g.leaves = c->d_vdb_leaves[k];
-    g.tiles = c->d_vdb_tiles[k];
+    g.blocks = c->d_vdb_leaves[k];
+    g.consts = c->d_vdb_tiles[k];
+    g.ox = base.ox; g.oy = base.oy; g.oz = base.oz;
+    g.lnx = base.lnx; g.lny = base.lny; g.lnz = base.lnz;
     return AVR_OK;
 }
 
@@ -566,7 +616,7 @@ int avr_set_dda_budget(avr_context *c, int cells) {
 }
 
 int avr_set_refill_min(avr_context *c, int lanes) {
-    if (!c || lanes < 0 || lanes > 64) return fail(AVR_ERR_ARG, "refill threshold must be 1..64 lanes (0: default)");
+    if (!c || lanes < 0 || lanes > 64) return fail(AVR_ERR_ARG, "refill threshold must be 0..64 lanes (0 = default)");
     c->refill_min = lanes;
     return AVR_OK;
 }
@@ -728,7 +778,7 @@ int avr_medium_nanovdb(avr_context *c, const avr_vdb_grid *density, const avr_vd
     HIP_TRY(hipStreamSynchronize(c->stream));
     free_vdb(c);
     int rc;
-    avr::vdb::Grid gd{}, gt{};
+    avr::vdb::Apron gd{}, gt{};
     if ((rc = upload_vdb(c, density, 0, gd))) return rc;
     if (temperature && (rc = upload_vdb(c, temperature, 1, gt))) return rc;
     // bounds: density world bbox, union the temperature grid's (media.cpp:531-549)
@@ -757,9 +807,9 @@ int avr_medium_nanovdb(avr_context *c, const avr_vdb_grid *density, const avr_vd
     return AVR_OK;
 }
 
-int avr_medium_rgbgrid(avr_context *c, int nx, int ny, int nz, const float bounds[6], const float rfm[16],
-                       const float mfr[16], const float *sigma_a, const float *sigma_s, float sigma_scale, float g,
-                       const float *Le, const float *illuminant, float Le_scale) {
+static int medium_rgbgrid(avr_context *c, int nx, int ny, int nz, const float bounds[6], const float rfm[16],
+                          const float mfr[16], const float *sigma_a, const float *sigma_s, float sigma_scale, float g,
+                          const float *Le, const float *illuminant, float Le_scale, bool on_device) {
     AVR_QUIESCE(c);
     if (!c || !bounds || !rfm || !mfr) return fail(AVR_ERR_ARG, "null medium argument");
     if (nx < 1 || ny < 1 || nz < 1) return fail(AVR_ERR_ARG, "bad grid");
@@ -773,16 +823,22 @@ int avr_medium_rgbgrid(avr_context *c, int nx, int ny, int nz, const float bound
     HIP_TRY(hipStreamSynchronize(c->stream));
     free_rgb(c);
     const float *src[3] = {sigma_a, sigma_s, Le};
+    const float4 *grid[3] = {nullptr, nullptr, nullptr};
     for (int k = 0; k < 3; ++k) {
         if (!src[k]) continue;
+        if (on_device) {   // the caller's device arrays, adopted (not copied)
+            grid[k] = reinterpret_cast<const float4 *>(src[k]);
+            continue;
+        }
         HIP_TRY(dalloc(&c->d_rgb[k], n));
         HIP_TRY(hipMemcpyAsync(c->d_rgb[k], src[k], n * sizeof(float4), hipMemcpyHostToDevice, c->stream));
+        grid[k] = c->d_rgb[k];
     }
     int rc;
     if (Le && (rc = upload_table(&c->d_illum, illuminant, avr::kNTable, c->stream))) return rc;
-    c->med.rgb_a = c->d_rgb[0];
-    c->med.rgb_s = c->d_rgb[1];
-    c->med.rgb_le = c->d_rgb[2];
+    c->med.rgb_a = grid[0];
+    c->med.rgb_s = grid[1];
+    c->med.rgb_le = grid[2];
     c->med.illuminant = c->d_illum;
     c->med.rgb_sigma_scale = sigma_scale;
     c->med.rgb_le_scale = Le_scale;
@@ -795,6 +851,33 @@ int avr_medium_rgbgrid(avr_context *c, int nx, int ny, int nz, const float bound
                             4, nullptr)))
         return rc;
     c->med.emissive = (Le && Le_scale > 0) ? 1 : 0;   // IsEmissive (media.h:374)
+    return AVR_OK;
+}
+
+int avr_medium_rgbgrid(avr_context *c, int nx, int ny, int nz, const float bounds[6], const float rfm[16],
+                       const float mfr[16], const float *sigma_a, const float *sigma_s, float sigma_scale, float g,
+                       const float *Le, const float *illuminant, float Le_scale) {
+    return medium_rgbgrid(c, nx, ny, nz, bounds, rfm, mfr, sigma_a, sigma_s, sigma_scale, g, Le, illuminant, Le_scale,
+                          false);
+}
+
+int avr_medium_rgbgrid_device(avr_context *c, int nx, int ny, int nz, const float bounds[6], const float rfm[16],
+                              const float mfr[16], const float *d_sigma_a, const float *d_sigma_s, float sigma_scale,
+                              float g, const float *d_Le, const float *illuminant, float Le_scale) {
+    return medium_rgbgrid(c, nx, ny, nz, bounds, rfm, mfr, d_sigma_a, d_sigma_s, sigma_scale, g, d_Le, illuminant,
+                          Le_scale, true);
+}
+
+int avr_generate_rgb_explosion(avr_context *c, float *d_sigma_a, float *d_sigma_s, float *d_Le, int n, long long first,
+                               long long count) {
+    if (!c || !d_sigma_a || !d_sigma_s || !d_Le || n < 1 || count < 0 || first < 0 ||
+        first + count > (long long)n * n * n)
+        return fail(AVR_ERR_ARG, "bad rgb explosion args");
+    HIP_TRY(hipSetDevice(c->device));
+    hipLaunchKernelGGL(avr::k_rgb_explosion, dim3(blocks_for(count, 256, 256 * 32)), dim3(256), 0, c->stream,
+                       reinterpret_cast<float4 *>(d_sigma_a), reinterpret_cast<float4 *>(d_sigma_s),
+                       reinterpret_cast<float4 *>(d_Le), n, first, count);
+    HIP_TRY(hipGetLastError());
     return AVR_OK;
 }
 
@@ -912,16 +995,21 @@ int avr_tune_majorant(avr_context *c, const int *candidates, int n, int spp_begi
     AVR_QUIESCE(c);
     if (!c || !candidates || n < 1 || !chosen) return fail(AVR_ERR_ARG, "null argument");
     if (!c->has_medium || !c->has_film || !c->has_camera) return fail(AVR_ERR_STATE, "scene incomplete");
+    if (c->med.type == 1 || c->med.type == 2)
+        return fail(AVR_ERR_ARG, "homogeneous / cloud media have a single majorant segment");
     if (spp_end <= spp_begin) return fail(AVR_ERR_ARG, "empty probe sample range");
     for (int k = 0; k < 3 * n; ++k)
         if (candidates[k] < 1 || candidates[k] > 255) return fail(AVR_ERR_ARG, "majorant resolution must be 1..255");
     HIP_TRY(hipSetDevice(c->device));
-    // the probes render into the film: keep its sums and put them back afterwards
+    // the probes render into the film: keep its sums and put them back afterwards — also when
+    // a probe fails, together with the majorant resolution the medium had before
+    const int mres0[3] = {c->med.mres[0], c->med.mres[1], c->med.mres[2]};
     const size_t np = (size_t)c->film.width * c->film.height;
     const size_t nd = (4 + 2 * (size_t)std::max(0, c->film.nbuckets)) * np;
     double *saved = nullptr;
     HIP_TRY(dalloc(&saved, nd));
     int rc = avr_film_export_device(c, saved);
+    const bool haveSaved = rc == AVR_OK;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (!rc && (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess)) rc = fail(AVR_ERR_HIP, "event");
     float best = -1.f;
@@ -942,18 +1030,30 @@ int avr_tune_majorant(avr_context *c, const int *candidates, int n, int spp_begi
         if (ms) ms[k] = t;
         if (best < 0 || t < best) { best = t; bestk = k; }
     }
-    if (!rc) rc = build_majorant(c, candidates + 3 * bestk);
-    if (!rc) {
+    // the chosen resolution, or after a failure the original one (the first error is kept)
+    const std::string err = g_err;
+    const int rcProbe = rc;
+    int rcRestore = build_majorant(c, rc ? mres0 : candidates + 3 * bestk);
+    if (haveSaved) {
         // restore the film sums
-        double *d = saved;
-        HIP_TRY(hipMemcpyAsync(c->film.rgb_sum, d, 3 * np * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
-        HIP_TRY(hipMemcpyAsync(c->film.w_sum, d + 3 * np, np * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
-        if (c->film.nbuckets > 0)
-            HIP_TRY(hipMemcpyAsync(c->film.bucket_sum, d + 4 * np, 2 * np * c->film.nbuckets * sizeof(double),
-                                   hipMemcpyDeviceToDevice, c->stream));
-        HIP_TRY(hipStreamSynchronize(c->stream));
-        for (int i = 0; i < 3; ++i) chosen[i] = candidates[3 * bestk + i];
+        const double *d = saved;
+        hipError_t e = hipMemcpyAsync(c->film.rgb_sum, d, 3 * np * sizeof(double), hipMemcpyDeviceToDevice, c->stream);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(c->film.w_sum, d + 3 * np, np * sizeof(double), hipMemcpyDeviceToDevice, c->stream);
+        if (e == hipSuccess && c->film.nbuckets > 0)
+            e = hipMemcpyAsync(c->film.bucket_sum, d + 4 * np, 2 * np * c->film.nbuckets * sizeof(double),
+                               hipMemcpyDeviceToDevice, c->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+        if (e != hipSuccess && !rcRestore) rcRestore = fail(AVR_ERR_HIP, std::string("film restore: ") + hipGetErrorString(e));
     }
+    if (rcProbe) {
+        rc = rcProbe;
+        g_err = err;
+    } else {
+        rc = rcRestore;
+    }
+    if (!rc)
+        for (int i = 0; i < 3; ++i) chosen[i] = candidates[3 * bestk + i];
     if (e0) (void)hipEventDestroy(e0);
     if (e1) (void)hipEventDestroy(e1);
     (void)hipFree(saved);
@@ -1362,7 +1462,16 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
             EV_MARK(e1);
             p.rec_mode = 1;   // k_film reads the records k_paths wrote
             p.fast = c->render_mode;
-            hipLaunchKernelGGL(avr::k_film, dim3(blocks_for(P)), dim3(256), avr::film_lds_bytes(c->film.nbuckets), c->stream, p);
+            if (c->film.nbuckets == 0) {
+                // RGBFilm: the per-sample sensor conversion (f64 canonical wavelengths and pdfs)
+                // with one lane per sample, then the fp64 sums per pixel in sample order
+                hipLaunchKernelGGL(avr::k_film_rgb, dim3(blocks_for(n0, 256, 256 * 64)), dim3(256), 0, c->stream, p);
+                HIP_TRY(hipGetLastError());
+                hipLaunchKernelGGL(avr::k_film_sum, dim3(blocks_for(P)), dim3(256), 0, c->stream, p);
+            } else {
+                hipLaunchKernelGGL(avr::k_film, dim3(blocks_for(P)), dim3(256), avr::film_lds_bytes(c->film.nbuckets),
+                                   c->stream, p);
+            }
             HIP_TRY(hipGetLastError());
             EV_MARK(e2);
             c->timed.push_back({e0, e1, &avr_stats::ms_medium, true});

@@ -79,7 +79,7 @@ struct DevMedium {
     // 3 NanoVDBMedium (media.h:602-685): density and optional temperature as sparse grids
     // sampled in index space (avr_vdb.h); Le = LeScale * Blackbody(T) where T > 100 K,
     // emissive iff a temperature grid is present (the integrator tests mp.Le itself)
-    vdb::Grid vdb, vdb_temp;
+    vdb::Apron vdb, vdb_temp;
     float vdb_lescale;
     // 4 RGBGridMedium (media.h:355-427): per-voxel RGBUnboundedSpectrum sigma_a / sigma_s and
     // RGBIlluminantSpectrum Le as {c0, c1, c2, scale} (nx*ny*nz each, null = absent), the
@@ -177,6 +177,8 @@ struct PathSoA {
     // k_paths' per-sample record, 32 B at 2*id: {L[4]} then {u_lambda, filter weight, 0, 0}
     // (k_film re-derives the wavelengths from u_lambda); one 32-B sector per sample
     float4 *rec;
+    // RGBFilm's per-sample contribution {w * rgb, w} (k_film_rgb), summed by k_film_sum
+    float4 *contrib;
 };
 struct ShadowSoA {
     int *path;
@@ -2035,6 +2037,77 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
 // SpectralFilm: a pixel's bucket sums (up to kFilmLdsBuckets of them) are accumulated in this
 // thread's LDS slice and written back once per pass — the same fp64 additions in the same
 // order as the read-modify-writes on HBM, without their 2 x 4 dependent round trips per sample.
+// One sample of the pass: L, the wavelengths and CameraSample::filterWeight, from k_paths'
+// 32-B record (L, {u_lambda, weight}: the wavelengths re-derived from u_lambda with the
+// function k_paths sampled them with) or the wavefront SoA
+__device__ __forceinline__ void film_load_sample(const Params &P, size_t id, Spec *L, Spec *lam, float *w) {
+    *w = 1.f;
+    if (P.rec_mode) {
+        const float4 r0 = P.ps.rec[2 * id], r1 = P.ps.rec[2 * id + 1];
+        *L = spec4(r0);
+        *lam = P.fast ? film_sample_lambda_fast(P.film, r1.x) : film_sample_lambda(P.film, r1.x);
+        if (P.film.filter_type != 0) *w = r1.y;
+    } else {
+        *L = spec4(P.ps.L[id]);
+        *lam = spec4(P.ps.lambda[id]);
+        if (P.film.filter_type != 0) *w = P.ps.weight[id];
+    }
+}
+// The NaN/Inf guard (integrators.cpp:272-282; a bad sample's L becomes 0, in place) and
+// PixelSensor::ToSensorRGB with RGBFilm's maxComponentValue clamp (film.h:95-100, 239-250)
+__device__ __forceinline__ void film_sensor_rgb(const Params &P, Spec &L, const Spec &lam, float rgb[3]) {
+    const Spec pdf = {film_lambda_pdf(P.film, lam.v0), film_lambda_pdf(P.film, lam.v1),
+                      film_lambda_pdf(P.film, lam.v2), film_lambda_pdf(P.film, lam.v3)};
+    const LambdaIdx li = lambda_index(lam);
+    bool bad = __builtin_isnan(L.v0) || __builtin_isnan(L.v1) || __builtin_isnan(L.v2) || __builtin_isnan(L.v3);
+    if (!bad) {
+        const Spec Ys = sample_table(P.film.xyz + kNTable, li);
+        float y = safe_div(Ys * L, pdf).avg() / 106.856895f;
+        bad = __builtin_isinf(y);
+    }
+    if (bad) L = Spec::c(0.f);
+    const Spec Ld = safe_div(L, pdf);
+    for (int c = 0; c < 3; ++c) rgb[c] = (sample_table(P.film.xyz + kNTable * c, li) * Ld).avg() * P.film.imaging_ratio;
+    float mx = fmaxf_(fmaxf_(rgb[0], rgb[1]), rgb[2]);
+    if (mx > P.film.max_component)
+        for (int c = 0; c < 3; ++c) rgb[c] *= P.film.max_component / mx;
+}
+
+// RGBFilm after k_paths, in two steps. k_film_rgb: one lane per SAMPLE converts k_paths'
+// record to its film contribution {w * rgb, w} (the f64 canonical wavelength and pdf
+// sequences have the whole pass of lanes to hide their latency, instead of one lane walking a
+// pixel's samples); k_film_sum: per pixel, the fp64 sums in sampleIndex order — the same
+// float products added in the same order as k_film, so the film is bit-identical.
+__global__ void __launch_bounds__(256) k_film_rgb(Params P) {
+    const long long n = (long long)P.pass_pixels * P.pass_samples;
+    for (long long id = blockIdx.x * (long long)blockDim.x + threadIdx.x; id < n; id += (long long)gridDim.x * blockDim.x) {
+        Spec L, lam;
+        float w;
+        film_load_sample(P, (size_t)id, &L, &lam, &w);
+        float rgb[3];
+        film_sensor_rgb(P, L, lam, rgb);
+        P.ps.contrib[id] = make_float4(w * rgb[0], w * rgb[1], w * rgb[2], w);
+    }
+}
+__global__ void __launch_bounds__(256) k_film_sum(Params P) {
+    const int npix = P.pass_pixels;
+    for (int pix = blockIdx.x * blockDim.x + threadIdx.x; pix < npix; pix += gridDim.x * blockDim.x) {
+        double s0 = P.film.rgb_sum[3 * (size_t)pix], s1 = P.film.rgb_sum[3 * (size_t)pix + 1],
+               s2 = P.film.rgb_sum[3 * (size_t)pix + 2], ws = P.film.w_sum[pix];
+        for (int s = 0; s < P.pass_samples; ++s) {
+            const float4 c = P.ps.contrib[(size_t)s * npix + pix];
+            s0 += (double)c.x;
+            s1 += (double)c.y;
+            s2 += (double)c.z;
+            ws += (double)c.w;
+        }
+        P.film.rgb_sum[3 * (size_t)pix] = s0;
+        P.film.rgb_sum[3 * (size_t)pix + 1] = s1;
+        P.film.rgb_sum[3 * (size_t)pix + 2] = s2;
+        P.film.w_sum[pix] = ws;
+    }
+}
+
 constexpr int kFilmLdsBuckets = 16;
 inline size_t film_lds_bytes(int nb) { return nb > 0 && nb <= kFilmLdsBuckets ? 2 * (size_t)nb * 256 * sizeof(double) : 0; }
 __global__ void __launch_bounds__(256) k_film(Params P) {
@@ -2059,37 +2132,11 @@ __global__ void __launch_bounds__(256) k_film(Params P) {
         }
         for (int s = 0; s < P.pass_samples; ++s) {
             const size_t id = (size_t)s * npix + pix;
-            Spec L;
-            Spec lam;
-            float w = 1.f;   // CameraSample::filterWeight
-            if (P.rec_mode) {
-                // k_paths' 32-B record: L, {u_lambda, weight}; the wavelengths are re-derived
-                // from u_lambda with the function k_paths sampled them with
-                const float4 r0 = P.ps.rec[2 * id], r1 = P.ps.rec[2 * id + 1];
-                L = spec4(r0);
-                lam = P.fast ? film_sample_lambda_fast(P.film, r1.x) : film_sample_lambda(P.film, r1.x);
-                if (P.film.filter_type != 0) w = r1.y;
-            } else {
-                L = spec4(P.ps.L[id]);
-                lam = spec4(P.ps.lambda[id]);
-                if (P.film.filter_type != 0) w = P.ps.weight[id];
-            }
-            const Spec pdf = {film_lambda_pdf(P.film, lam.v0), film_lambda_pdf(P.film, lam.v1),
-                              film_lambda_pdf(P.film, lam.v2), film_lambda_pdf(P.film, lam.v3)};
-            const LambdaIdx li = lambda_index(lam);
-            bool bad = __builtin_isnan(L.v0) || __builtin_isnan(L.v1) || __builtin_isnan(L.v2) || __builtin_isnan(L.v3);
-            if (!bad) {
-                const Spec Ys = sample_table(P.film.xyz + kNTable, li);
-                float y = safe_div(Ys * L, pdf).avg() / 106.856895f;
-                bad = __builtin_isinf(y);
-            }
-            if (bad) L = Spec::c(0.f);
-            const Spec Ld = safe_div(L, pdf);
+            Spec L, lam;
+            float w;
+            film_load_sample(P, id, &L, &lam, &w);
             float rgb[3];
-            for (int c = 0; c < 3; ++c) rgb[c] = (sample_table(P.film.xyz + kNTable * c, li) * Ld).avg() * P.film.imaging_ratio;
-            float mx = fmaxf_(fmaxf_(rgb[0], rgb[1]), rgb[2]);
-            if (mx > P.film.max_component)
-                for (int c = 0; c < 3; ++c) rgb[c] *= P.film.max_component / mx;
+            film_sensor_rgb(P, L, lam, rgb);
             s0 += (double)(w * rgb[0]);
             s1 += (double)(w * rgb[1]);
             s2 += (double)(w * rgb[2]);
@@ -2229,7 +2276,7 @@ __global__ void __launch_bounds__(256) k_majorant(const float *__restrict__ dens
 // of filter slop (int truncation of the f64 i -/+ 1), clamped to the active index bbox
 // (inclusive); the cell holds the max of getValue over that box (0 when it is empty).
 // One workgroup per cell.
-__global__ void __launch_bounds__(256) k_majorant_vdb(vdb::Grid g, float3 bmin, float3 bmax, int4 ibmin, int4 ibmax,
+__global__ void __launch_bounds__(256) k_majorant_vdb(vdb::Apron g, float3 bmin, float3 bmax, int4 ibmin, int4 ibmax,
                                                       int rx, int ry, int rz, float *out) {
     const int cell = blockIdx.x;
     const int x = cell % rx, y = (cell / rx) % ry, z = cell / (rx * ry);
@@ -2266,6 +2313,19 @@ __global__ void __launch_bounds__(256) k_majorant_vdb(vdb::Grid g, float3 bmin, 
         float r = red[0];
         for (int w = 1; w < (int)(blockDim.x / 64); ++w) r = r < red[w] ? red[w] : r;
         out[cell] = r;
+    }
+}
+
+// Apron blocks of a NanoVDB grid (avr_vdb.h "Apron layout"): block i holds getValue of the
+// base layout over the 9^3 neighbourhood of extended block list[i]; one workgroup per block
+__global__ void __launch_bounds__(256) k_vdb_apron(vdb::Grid base, const long long *__restrict__ list, long long n,
+                                                   float *__restrict__ out) {
+    const int ne_x = base.lnx + 1, ne_y = base.lny + 1;
+    for (long long i = blockIdx.x; i < n; i += gridDim.x) {
+        const long long e = list[i];
+        const int ex = (int)(e % ne_x), ey = (int)((e / ne_x) % ne_y), ez = (int)(e / ((long long)ne_x * ne_y));
+        for (int k = threadIdx.x; k < vdb::kApronVals; k += blockDim.x)
+            out[i * vdb::kApronVals + k] = vdb::apron_value(base, ex, ey, ez, k);
     }
 }
 
@@ -2450,6 +2510,32 @@ __global__ void __launch_bounds__(256) k_cloud(float *out, int n, long long firs
         const long long idx = first + k;
         const int x = (int)(idx % n), y = (int)((idx / n) % n), z = (int)(idx / ((long long)n * n));
         out[k] = cloud_density(V3{(x + 0.5f) / n, (y + 0.5f) / n, (z + 0.5f) / n}, density, wispiness, frequency);
+    }
+}
+
+// Synthetic RGB-coefficient explosion — BASELINE config C5's "emissive RGB-coefficient
+// explosion volume" (asset absent) as an RGBGridMedium (media.h:355-427): per voxel
+// {c0, c1, c2, scale} of RGBSigmoidPolynomial spectra (color.h:332-365) for sigma_a, sigma_s
+// (RGBUnboundedSpectrum) and Le (RGBIlluminantSpectrum), voxel centres (i + 0.5) / n, in
+// [first, first + count) of the x-fastest grid. A Perlin-perturbed ball: density
+// d = clamp(1.2 (1 - r / 0.42) + 0.18 w1, 0, 1), heat t = clamp(1 - r / 0.3 + 0.25 w2, 0, 1);
+// smoke sigma_a {0, 0, 0.3} x 2d (flat), sigma_s {0, 0.002, -1.1} x 6d (redder scattering),
+// fire Le: a rising sigmoid with its edge at 650 - 180 t nm (hotter = whiter), scale 8 t^2.
+__global__ void __launch_bounds__(256) k_rgb_explosion(float4 *sa, float4 *ss, float4 *le, int n, long long first,
+                                                       long long count) {
+    for (long long k = blockIdx.x * (long long)blockDim.x + threadIdx.x; k < count; k += (long long)gridDim.x * blockDim.x) {
+        const long long idx = first + k;
+        const int x = (int)(idx % n), y = (int)((idx / n) % n), z = (int)(idx / ((long long)n * n));
+        const float px = (x + 0.5f) / n, py = (y + 0.5f) / n, pz = (z + 0.5f) / n;
+        const float dx = px - 0.5f, dy = py - 0.5f, dz = pz - 0.5f;
+        const float r = __builtin_sqrtf(dx * dx + dy * dy + dz * dz);
+        const float w1 = perlin(8 * px, 8 * py, 8 * pz), w2 = perlin(6 * px + 3.1f, 6 * py + 1.7f, 6 * pz + 0.3f);
+        const float d = clampf(1.2f * (1 - r / 0.42f) + 0.18f * w1, 0.f, 1.f);
+        const float t = clampf(1 - r / 0.3f + 0.25f * w2, 0.f, 1.f);
+        sa[k] = make_float4(0.f, 0.f, 0.3f, 2.f * d);
+        ss[k] = make_float4(0.f, 0.002f, -1.1f, 6.f * d);
+        const float edge = 650.f - 180.f * t;
+        le[k] = make_float4(0.f, 0.03f, -0.03f * edge, 8.f * t * t);
     }
 }
 

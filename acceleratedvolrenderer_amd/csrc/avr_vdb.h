@@ -8,12 +8,15 @@
 //   * SampleFromVoxels<Tree, 1, false>(xyz): ijk = floor(xyz), uvw = xyz - ijk, the 2x2x2
 //     stencil of getValue, lerp(a, b, w) = a + w * (b - a) along z, then y, then x
 //     (TrilinearSampler::sample).
-// Storage: one int per 8^3 block of the grid's leaf-aligned extent (a leaf index, a tile,
-// or background) and 512 floats per leaf, x-major ((x&7) << 6 | (y&7) << 3 | z&7) as
-// NanoVDB's LeafNode. Standalone (no HIP headers) for the host-compiled tests.
+// Storage: the base layout (Grid) is one int per 8^3 block of the grid's leaf-aligned extent
+// (a leaf index, a tile, or background) and 512 floats per leaf, x-major
+// ((x&7) << 6 | (y&7) << 3 | z&7) as NanoVDB's LeafNode; the kernels sample the apron layout
+// (Apron, below) built from it. Standalone (no HIP headers) for the host-compiled tests.
 #pragma once
 
 #include <cstdint>
+#include <cstddef>
+#include <vector>
 
 #ifndef AVR_HD
 #define AVR_HD __host__ __device__ __forceinline__
@@ -46,7 +49,8 @@ AVR_HD float get_value(const Grid &g, int x, int y, int z) {
     return g.tiles[-s - 1];
 }
 
-AVR_HD void world_to_index(const Grid &g, float x, float y, float z, float *ix, float *iy, float *iz) {
+template <typename G>
+AVR_HD void world_to_index(const G &g, float x, float y, float z, float *ix, float *iy, float *iz) {
     const float dx = x - g.vec[0], dy = y - g.vec[1], dz = z - g.vec[2];
     *ix = __builtin_fmaf(dx, g.inv[0], __builtin_fmaf(dy, g.inv[1], dz * g.inv[2]));
     *iy = __builtin_fmaf(dx, g.inv[3], __builtin_fmaf(dy, g.inv[4], dz * g.inv[5]));
@@ -105,6 +109,132 @@ AVR_HD float sample_world(const Grid &g, float x, float y, float z) {
     float ix, iy, iz;
     world_to_index(g, x, y, z, &ix, &iy, &iz);
     return sample_trilinear(g, ix, iy, iz);
+}
+
+// ---------------------------------------------------------------------------
+// Apron layout — what the kernels sample. The trilinear stencil of base voxel r spans r and
+// r + 1 per axis, so it leaves r's 8^3 block only through that block's +1 faces. Each block
+// b of the extended range [-1, ln - 1] per axis whose 9^3 neighbourhood [8b, 8b + 8]^3 is not
+// one constant stores that neighbourhood (getValue of every voxel: its own leaf values, the
+// first voxels of the +x/+y/+z neighbours, tiles, background) as an apron block of 729
+// floats; a constant neighbourhood stores only its value. A lookup then reads ONE slot and
+// eight values of ONE apron block (one dependent round trip instead of the base layout's 8
+// slot reads followed by 8 leaf reads), and every tap is the value getValue returns, so the
+// sampler's result is bit-identical.
+constexpr int kApron = 9;                       // voxels per axis of an apron block
+constexpr int kApronVals = kApron * kApron * kApron;
+
+struct Apron {
+    const int *slot;          // (lnx+1)*(lny+1)*(lnz+1), extended block e = b + 1: >= 0 apron
+                              //   block, < 0: constant consts[-s-1]
+    const float *blocks;      // 729 per apron block, x-major: x * 81 + y * 9 + z
+    const float *consts;      // constant neighbourhood values (tiles, the background)
+    int ox, oy, oz;           // index of base block 0's first voxel
+    int lnx, lny, lnz;        // base blocks per axis
+    float background;
+    float inv[9];
+    float vec[3];
+};
+
+// getValue(x, y, z) from the apron layout (every voxel of the base extent lies in its own
+// block's apron; outside the extended range: background)
+AVR_HD float get_value(const Apron &g, int x, int y, int z) {
+    const int rx = x - g.ox, ry = y - g.oy, rz = z - g.oz;
+    const int ex = (rx >> 3) + 1, ey = (ry >> 3) + 1, ez = (rz >> 3) + 1;
+    if (ex < 0 || ey < 0 || ez < 0 || ex > g.lnx || ey > g.lny || ez > g.lnz) return g.background;
+    const int s = g.slot[((long long)ez * (g.lny + 1) + ey) * (g.lnx + 1) + ex];
+    if (s < 0) return g.consts[-s - 1];
+    return g.blocks[(long long)s * kApronVals + (rx & 7) * (kApron * kApron) + (ry & 7) * kApron + (rz & 7)];
+}
+
+// SampleFromVoxels<Tree, 1, false> at index-space xyz from the apron layout: the same eight
+// getValue taps and the same lerps as sample_trilinear
+AVR_HD float sample_trilinear(const Apron &g, float x, float y, float z) {
+    const float fx = __builtin_floorf(x), fy = __builtin_floorf(y), fz = __builtin_floorf(z);
+    const int i = (int)fx, j = (int)fy, k = (int)fz;
+    const float u = x - fx, v = y - fy, w = z - fz;
+    const int rx = i - g.ox, ry = j - g.oy, rz = k - g.oz;
+    const int ex = (rx >> 3) + 1, ey = (ry >> 3) + 1, ez = (rz >> 3) + 1;
+    float v000, v001, v010, v011, v100, v101, v110, v111;
+    if (ex < 0 || ey < 0 || ez < 0 || ex > g.lnx || ey > g.lny || ez > g.lnz) {
+        v000 = v001 = v010 = v011 = v100 = v101 = v110 = v111 = g.background;
+    } else {
+        const int s = g.slot[((long long)ez * (g.lny + 1) + ey) * (g.lnx + 1) + ex];
+        if (s < 0) {
+            v000 = v001 = v010 = v011 = v100 = v101 = v110 = v111 = g.consts[-s - 1];
+        } else {
+            const float *b = g.blocks + (long long)s * kApronVals + (rx & 7) * (kApron * kApron) + (ry & 7) * kApron +
+                             (rz & 7);
+            v000 = b[0];
+            v001 = b[1];
+            v010 = b[kApron];
+            v011 = b[kApron + 1];
+            v100 = b[kApron * kApron];
+            v101 = b[kApron * kApron + 1];
+            v110 = b[kApron * kApron + kApron];
+            v111 = b[kApron * kApron + kApron + 1];
+        }
+    }
+    return lerp_vdb(lerp_vdb(lerp_vdb(v000, v001, w), lerp_vdb(v010, v011, w), v),
+                    lerp_vdb(lerp_vdb(v100, v101, w), lerp_vdb(v110, v111, w), v), u);
+}
+AVR_HD float sample_world(const Apron &g, float x, float y, float z) {
+    float ix, iy, iz;
+    world_to_index(g, x, y, z, &ix, &iy, &iz);
+    return sample_trilinear(g, ix, iy, iz);
+}
+
+// Apron slot of extended block (ex, ey, ez) from the base layout's slots (host side of the
+// build): -1 when the 9^3 neighbourhood touches a leaf (an apron block is needed), else the
+// base slot whose constant fills all of it (a tile -(t+1) or kBackgroundSlot), or -2 when the
+// constant blocks around it disagree (an apron block is needed as well).
+inline int apron_classify(const int *slot, int lnx, int lny, int lnz, const float *tiles, float background, int ex,
+                          int ey, int ez) {
+    int first = 0;
+    float c0 = 0.f;
+    for (int d = 0; d < 8; ++d) {
+        const int bx = ex - 1 + (d & 1), by = ey - 1 + ((d >> 1) & 1), bz = ez - 1 + (d >> 2);
+        int s = kBackgroundSlot;
+        if (bx >= 0 && by >= 0 && bz >= 0 && bx < lnx && by < lny && bz < lnz)
+            s = slot[((long long)bz * lny + by) * lnx + bx];
+        if (s >= 0) return -1;
+        const float c = s == kBackgroundSlot ? background : tiles[-s - 1];
+        if (d == 0) {
+            first = s;
+            c0 = c;
+        } else if (__builtin_memcmp(&c, &c0, sizeof(float)) != 0) {
+            return -2;
+        }
+    }
+    return first;
+}
+
+// The apron slots of a base layout (host): aslot[(ez * (lny+1) + ey) * (lnx+1) + ex] is the
+// apron block index (blocks listed in `list` by extended linear index) or -(c+1) with c the
+// constant's index in consts = {tile values..., background} (c = ntiles: the background).
+inline void build_apron_slots(const int *slot, int lnx, int lny, int lnz, const float *tiles, int ntiles, float background,
+                              std::vector<int> &aslot, std::vector<long long> &list) {
+    const long long ne = (long long)(lnx + 1) * (lny + 1) * (lnz + 1);
+    aslot.assign((std::size_t)ne, 0);
+    list.clear();
+    for (int ez = 0; ez <= lnz; ++ez)
+        for (int ey = 0; ey <= lny; ++ey)
+            for (int ex = 0; ex <= lnx; ++ex) {
+                const long long e = ((long long)ez * (lny + 1) + ey) * (lnx + 1) + ex;
+                const int k = apron_classify(slot, lnx, lny, lnz, tiles, background, ex, ey, ez);
+                if (k == -1 || k == -2) {
+                    aslot[(std::size_t)e] = (int)list.size();
+                    list.push_back(e);
+                } else {
+                    aslot[(std::size_t)e] = k == kBackgroundSlot ? -(ntiles + 1) : k;   // tile t: -(t+1)
+                }
+            }
+}
+
+// Values of apron block (ex, ey, ez): getValue over [8b, 8b + 8]^3, b = e - 1, x-major
+AVR_HD float apron_value(const Grid &base, int ex, int ey, int ez, int k) {
+    const int a = k / (kApron * kApron), bb = (k / kApron) % kApron, c = k % kApron;
+    return get_value(base, base.ox + 8 * (ex - 1) + a, base.oy + 8 * (ey - 1) + bb, base.oz + 8 * (ez - 1) + c);
 }
 
 }  // namespace vdb

@@ -50,3 +50,29 @@ def ensure_world(requested, script, argv, env=None):
     e.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     rc = subprocess.call(launch_command(requested, script, argv), env=e)
     sys.exit(rc)
+
+
+def sample_plan(world, steps, warmup, spp_per_step, base_spp=256, pixelsamples=0):
+    """Sample indices of `bench.py --gpus N` (weak scaling: every rank renders spp_per_step
+    sample indices of every pixel per step; the sampler is indexed by (pixel, sampleIndex),
+    samplers.h:252-254, so disjoint index ranges are disjoint paths).
+
+    Returns (pixelsamples, warm, timed): warm[r] / timed[r] are rank r's first sample index of
+    each warmup / timed step. The timed steps of all ranks cover [0, steps * world * S) once
+    — no (pixel, index) pair is rendered twice, so the reduced film is one render at
+    pixelsamples spp — and pixelsamples is the smallest power of two >= that range and
+    >= base_spp (BASELINE config C3: 256), unless given. Warmup steps re-render indices of
+    the same range (their film is cleared before the timed region)."""
+    S = int(spp_per_step)
+    if S < 1:
+        raise ValueError(f"spp per step must be >= 1 (got {S})")
+    need = int(steps) * int(world) * S
+    P = int(pixelsamples) if pixelsamples else max(int(base_spp), 1)
+    if not pixelsamples:
+        while P < need:
+            P *= 2
+    if P < need or P % S:
+        raise ValueError(f"pixelsamples {P} cannot hold {steps} steps x {world} ranks x {S} distinct sample indices")
+    timed = [[(k * world + r) * S for k in range(steps)] for r in range(world)]
+    warm = [[((k * world + r) * S) % P for k in range(warmup)] for r in range(world)]
+    return P, warm, timed

@@ -10,7 +10,9 @@ below (tests/test_nvdb.py) and by rendering a round-tripped grid, not against Na
 
 File   := Header(16) { MetaData(176) name[nameSize] GridBuffer[fileSize] } x gridCount
 Header := magic u64 "NanoVDB0" | version u32 (major<<21|minor<<10|patch) | gridCount u16 | codec u16
-          (0 = NONE; ZIP / BLOSC streams are refused)
+          (0 = NONE, 1 = ZIP: the GridBuffer is stored as u64 compressedBytes + one zlib stream
+          of it, io::Internal::write/read in nanovdb/util/IO.h; 2 = BLOSC is refused — no blosc
+          library here)
 GridBuffer := GridData(672) TreeData(64) Root Upper* Lower* Leaf*
   GridData: magic, checksum, version, flags, gridIndex, gridCount, gridSize, name[256],
             Map {matF[9] invMatF[9] vecF[3] taperF, matD[9] invMatD[9] vecD[3] taperD},
@@ -27,6 +29,7 @@ GridBuffer := GridData(672) TreeData(64) Root Upper* Lower* Leaf*
 Every node starts on a 32-byte boundary (NANOVDB_DATA_ALIGNMENT).
 """
 import struct
+import zlib
 
 import numpy as np
 
@@ -37,6 +40,9 @@ VERSION = (32 << 21) | (3 << 10) | 3
 GRID_TYPE_FLOAT = 1
 GRID_CLASS_FOG_VOLUME = 2
 CODEC_NONE = 0
+CODEC_ZIP = 1
+CODEC_BLOSC = 2
+CODECS = {"none": CODEC_NONE, "zip": CODEC_ZIP}
 
 GRID_DATA = 672
 TREE_DATA = 64
@@ -229,22 +235,32 @@ def grid_buffer(grid, name="density"):
     return bytes(buf)
 
 
-def write_nvdb(path, grids):
-    """Write {name: NanoVDBGrid} (or [(name, grid)]) as an uncompressed .nvdb file."""
+def write_nvdb(path, grids, codec="none"):
+    """Write {name: NanoVDBGrid} (or [(name, grid)]) as an .nvdb file, uncompressed (codec
+    "none") or ZIP-coded ("zip": each grid buffer as u64 compressed size + zlib stream, as
+    NanoVDB's io::Internal::write does with NANOVDB_USE_ZIP)."""
+    if codec not in CODECS:
+        raise ValueError(f"codec {codec!r}: one of {sorted(CODECS)} (BLOSC is not available)")
+    cid = CODECS[codec]
     items = list(grids.items()) if isinstance(grids, dict) else list(grids)
     with open(path, "wb") as f:
-        f.write(struct.pack("<QIHH", MAGIC, VERSION, len(items), CODEC_NONE))
+        f.write(struct.pack("<QIHH", MAGIC, VERSION, len(items), cid))
         for name, g in items:
             gb = grid_buffer(g, name)
+            if cid == CODEC_ZIP:
+                z = zlib.compress(gb)
+                stored = struct.pack("<Q", len(z)) + z
+            else:
+                stored = gb
             nm = name.encode() + b"\0"
             lo, hi = g.world_bbox()
             vc = int(np.count_nonzero(np.asarray(g.leaf_values) != g.background))
-            f.write(struct.pack("<QQQQII6d6i3dI4I3IHHI", len(gb), len(gb), 0, vc, GRID_TYPE_FLOAT,
+            f.write(struct.pack("<QQQQII6d6i3dI4I3IHHI", len(gb), len(stored), 0, vc, GRID_TYPE_FLOAT,
                                 GRID_CLASS_FOG_VOLUME, *[float(v) for v in lo], *[float(v) for v in hi],
                                 *[int(c) for c in g.index_bbox], 1.0, 1.0, 1.0, len(nm),
-                                *_node_counts(gb), 0, 0, 0, CODEC_NONE, 0, VERSION))
+                                *_node_counts(gb), 0, 0, 0, cid, 0, VERSION))
             f.write(nm)
-            f.write(gb)
+            f.write(stored)
 
 
 def _node_counts(gb):
@@ -278,27 +294,44 @@ def _segments(path):
             name = f.read(name_size).rstrip(b"\0").decode(errors="replace")
             pos = f.tell()
             f.seek(file_size, 1)
-            out.append((name, gtype, gcodec if gcodec else codec, file_size, (pos, grid_size)))
+            out.append((name, gtype, gcodec if gcodec else codec, file_size, (pos, grid_size, file_size)))
         return out
 
 
 def read_nvdb(path, name=None):
-    """NanoVDB io::readGrid(path[, name]) for an uncompressed FloatGrid -> NanoVDBGrid
-    (the first grid when name is None, as NanoVDBMedium::Create's readGrid does)."""
+    """NanoVDB io::readGrid(path[, name]) for an uncompressed or ZIP-coded FloatGrid ->
+    NanoVDBGrid (the first grid when name is None, as NanoVDBMedium::Create's readGrid does)."""
     segs = _segments(path)
     if not segs:
         raise ValueError(f"{path}: no grids")
     pick = segs[0] if name is None else next((s for s in segs if s[0] == name), None)
     if pick is None:
         raise ValueError(f"{path}: no grid named {name!r} (grids: {[s[0] for s in segs]})")
-    gname, gtype, codec, fsize, (pos, gsize) = pick
-    if codec != CODEC_NONE:
-        raise ValueError(f"{path}: grid {gname!r} is compressed (codec {codec}); only uncompressed grids are read")
+    gname, gtype, codec, fsize, (pos, gsize, stored) = pick
+    if codec not in (CODEC_NONE, CODEC_ZIP):
+        raise ValueError(f"{path}: grid {gname!r} uses codec {codec} (BLOSC); only uncompressed and ZIP grids are read")
     if gtype != GRID_TYPE_FLOAT:
         raise ValueError(f"{path}: grid {gname!r} has type {gtype}, NanoVDBMedium needs a FloatGrid")
     with open(path, "rb") as f:
         f.seek(pos)
-        buf = f.read(gsize)
+        raw = f.read(stored if codec == CODEC_ZIP else gsize)
+    if codec == CODEC_ZIP:
+        # io::Internal::read: u64 residual, then uncompress(residual bytes) into gridSize bytes
+        if len(raw) < 8:
+            raise ValueError(f"{path}: grid {gname!r}: truncated ZIP stream")
+        n = struct.unpack_from("<Q", raw, 0)[0]
+        if 8 + n > len(raw):
+            raise ValueError(f"{path}: grid {gname!r}: ZIP stream of {n} bytes exceeds the stored {len(raw) - 8}")
+        try:
+            buf = zlib.decompress(raw[8:8 + n])
+        except zlib.error as e:
+            raise ValueError(f"{path}: grid {gname!r}: bad ZIP stream ({e})") from None
+        if len(buf) != gsize:
+            raise ValueError(f"{path}: grid {gname!r}: ZIP stream holds {len(buf)} bytes, gridSize is {gsize}")
+    else:
+        buf = raw
+    if len(buf) < gsize:
+        raise ValueError(f"{path}: grid {gname!r}: truncated grid buffer")
     return parse_grid_buffer(buf)
 
 

@@ -183,8 +183,11 @@ class RGBGridMedium:
     the colour space, sRGB by default); or the converted {c0, c1, c2, scale} arrays
     (nz, ny, nx, 4) directly as sigma_a_coeffs / sigma_s_coeffs / Le_coeffs. "p0"/"p1"
     bounds, "scale" (sigmaScale), "g", "Lescale" (default 1). `illuminant`: the colour
-    space's illuminant table (default D65 = sRGB's)."""
+    space's illuminant table (default D65 = sRGB's). Coefficient arrays may be device tensors
+    (torch, float32 (nz, ny, nx, 4) on the context's GPU): they are then used in place
+    (avr_medium_rgbgrid_device) and `on_device` is True."""
     type_id = 4
+    on_device = False
     device_density = None
     majorant_res = (16, 16, 16)
     temperature = None
@@ -194,6 +197,11 @@ class RGBGridMedium:
                  world_from_medium=None, scale=1.0, g=0.0, Lescale=1.0, rgb_table=None, illuminant=None,
                  sigma_a_coeffs=None, sigma_s_coeffs=None, Le_coeffs=None):
         def conv(rgb, coeffs, name):
+            if coeffs is not None and hasattr(coeffs, "data_ptr"):
+                if tuple(coeffs.shape[3:]) != (4,) or coeffs.dim() != 4 or not coeffs.is_contiguous():
+                    raise ValueError(f"{name}_coeffs must be a contiguous (nz, ny, nx, 4) tensor")
+                self.on_device = True
+                return coeffs
             if coeffs is not None:
                 c = np.ascontiguousarray(np.asarray(coeffs, np.float32))
                 if c.ndim != 4 or c.shape[3] != 4:

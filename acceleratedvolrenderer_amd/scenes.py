@@ -214,3 +214,37 @@ def s_explosion(density, temperature, width=1280, height=720, sampler="zsobol", 
     film = SpectralFilm(width, height, nbuckets=nbuckets, filter=GaussianFilter())
     smp = ZSobolSampler(spp) if sampler == "zsobol" else IndependentSampler(spp)
     return Scene(cam, film, med, [UniformInfiniteLight(scale=0.05)], sampler=smp)
+
+
+def rgb_explosion_grids(n=1024, device=0):
+    """The synthetic RGB-coefficient explosion (BASELINE config C5's "emissive RGB-coefficient
+    explosion volume", asset absent) generated on the device by k_rgb_explosion: three
+    float32 (n, n, n, 4) tensors of {c0, c1, c2, scale} — sigma_a, sigma_s (RGBUnboundedSpectrum)
+    and Le (RGBIlluminantSpectrum) — 16 B per voxel per field (48 GiB at n = 1024)."""
+    import torch
+    from . import capi
+    grids = [torch.empty((n, n, n, 4), dtype=torch.float32, device=f"cuda:{device}") for _ in range(3)]
+    ctx = capi.Context(device)
+    try:
+        slab = n * n * 32
+        for first in range(0, n ** 3, slab):
+            cnt = min(slab, n ** 3 - first)
+            ctx.generate_rgb_explosion(*(t.data_ptr() + 16 * first for t in grids), n, first, cnt)
+        ctx.sync()
+    finally:
+        ctx.close()
+    return grids
+
+
+def s_rgb_explosion(sigma_a, sigma_s, Le, width=1280, height=720, sampler="zsobol", spp=4096, nbuckets=16,
+                    filter="gaussian"):
+    """C5 as an RGBGridMedium: the coefficient grids of rgb_explosion_grids (device tensors, or
+    their host copies for the oracle) on the unit cube, g 0.2, seen like s_explosion on a
+    SpectralFilm (C5 is spectral; nbuckets 0 = RGBFilm) with a dim sky."""
+    from .scene import SpectralFilm, RGBGridMedium
+    med = RGBGridMedium(sigma_a_coeffs=sigma_a, sigma_s_coeffs=sigma_s, Le_coeffs=Le, scale=1.0, g=0.2, Lescale=1.0)
+    cam = PerspectiveCamera(fov=45.0, pos=(0.5, 0.5, -0.9), look=(0.5, 0.5, 0.5), up=(0.0, 1.0, 0.0))
+    filt = GaussianFilter() if filter == "gaussian" else BoxFilter()
+    film = SpectralFilm(width, height, nbuckets=nbuckets, filter=filt) if nbuckets else RGBFilm(width, height, filter=filt)
+    smp = ZSobolSampler(spp) if sampler == "zsobol" else IndependentSampler(spp)
+    return Scene(cam, film, med, [UniformInfiniteLight(scale=0.05)], sampler=smp)

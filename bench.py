@@ -59,6 +59,9 @@ def parse():
     p.add_argument("--spp-per-step", type=int, default=64,
                    help="sample indices per pass (one step); 64 x 720p = 59M k_paths records, 1.9 GB)")
     p.add_argument("--max-paths", type=int, default=0)
+    p.add_argument("--pixelsamples", type=int, default=0,
+                   help="sampler pixelsamples (0: the smallest power of two >= 256 holding every timed sample index "
+                        "of every rank, launch.sample_plan)")
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU-baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--pmc", default="auto", choices=["auto", "on", "off"],
@@ -90,10 +93,11 @@ def parse():
                         "writes the synthetic cloud's tree to a temporary .nvdb and reads it back")
     p.add_argument("--fast-leg", type=int, default=1,
                    help="after the replay measurement, time the same steps in fast mode (reported as fast_mode)")
-    p.add_argument("--scene", default="cloud", choices=["cloud", "uniform", "explosion"],
+    p.add_argument("--scene", default="cloud", choices=["cloud", "uniform", "explosion", "rgb-explosion"],
                    help="cloud: the metric workload (S-cloud); uniform: BASELINE C2's uniform cube (orthographic, "
                         "use --res 256 --width 512 --height 512); explosion: C5's emissive NanoVDB stand-in with a "
-                        "SpectralFilm (pixelsamples >= 4096)")
+                        "SpectralFilm (pixelsamples >= 4096); rgb-explosion: C5 as an emissive RGB-coefficient RGBGridMedium "
+                        "(k_rgb_explosion, 3 x 16 GiB at 1024^3) with a SpectralFilm")
     p.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     return p.parse_args()
 
@@ -187,7 +191,7 @@ def pmc_passes(args, kernel_substr="k_paths", timeout_s=240):
         return None, "rocprofv3 not found"
     child = [sys.executable, os.path.join(ROOT, "bench.py"), "--pmc-child", "--no-cpu-baseline", "--pmc", "off",
              "--steps", "2", "--warmup", "1"]
-    for k in ("res", "width", "height", "spp_per_step", "max_paths", "kernel", "medium", "refill_min", "grid_layout",
+    for k in ("res", "width", "height", "spp_per_step", "max_paths", "pixelsamples", "kernel", "medium", "refill_min", "grid_layout",
               "dda_budget", "zsobol_table", "sampler", "filter", "mode", "majorant_res", "ray_binning", "occupancy", "nvdb",
               "scene"):
         if getattr(args, k) is not None:
@@ -254,42 +258,38 @@ def main():
     gen.close()
     tgen = time.perf_counter() - tgen
     log(f"density grid {n}^3 generated in {tgen:.2f} s")
-    # the sampler's pixelsamples covers every sample index the run renders (ZSobol lays out
-    # Morton(pixel) << log2(spp) | index): 256 (config C3) unless more are rendered
+    # sample indices (launch.sample_plan): the timed steps of all ranks render disjoint index
+    # ranges [(k * world + rank) * S, + S) of one frame at `pixelsamples` spp, the smallest power
+    # of two >= steps * world * S and >= 256 (BASELINE config C3's pixelsamples at N = 1 with
+    # 4 steps of 64); ZSobol switches to 64-bit indices by itself where Morton(pixel) << log2 spp
+    # needs more than 32 bits
     S = args.spp_per_step
-    needed = (args.warmup + args.steps) * world * S
-    spp_total = 256
-    while spp_total < needed:
-        spp_total *= 2
-    # ZSobol's 32-bit index needs Morton(pixel) << log2(spp) < 2^32: at most 2^(32 - 2 log2 res)
-    # sample indices (1024 at 720p/1080p). Longer runs wrap the index range: every step still
-    # traces S fresh paths per pixel (nothing is reused), later steps repeat earlier indices.
-    res_pow2 = 1
-    while res_pow2 < max(args.width, args.height):
-        res_pow2 *= 2
-    spp_cap = 1 << (32 - 2 * (res_pow2.bit_length() - 1))
-    wrap = spp_total > spp_cap and args.sampler == "zsobol"
-    if wrap:
-        spp_total = spp_cap
-    if args.scene == "cloud" and args.sampler == "zsobol" and needed > 256:
-        # the metric's configuration (BASELINE C3): pixelsamples 256 — steps past the first 256
-        # sample indices trace the range again (all work recomputed; the sampler's digit count,
-        # hence its per-draw cost, stays C3's)
-        spp_total, wrap = 256, True
-    if wrap and spp_total % S:
-        raise SystemExit(f"--spp-per-step {S} must divide the ZSobol index range {spp_total} for this run length")
+    spp_total, warm_bases, timed_bases = launch.sample_plan(
+        world, args.steps, args.warmup, S, base_spp=4096 if "explosion" in args.scene else 256,
+        pixelsamples=args.pixelsamples)
+    wrap = False
     vdb = None
+    rgb_grids = None
     maxdepth = scenes.CLOUD_MAXDEPTH
     workload_name = {"cloud": f"S-cloud-{n}", "uniform": f"S-uniform-{n} (C2)",
-                     "explosion": f"S-explosion-{n} emissive spectral (C5 stand-in)"}[args.scene]
-    if args.scene == "explosion":
-        spp_total = max(spp_total, 4096)   # C5: 4096 spp (64-bit ZSobol indices at 720p)
+                     "explosion": f"S-explosion-{n} emissive spectral (C5 stand-in)",
+                     "rgb-explosion": f"S-rgb-explosion-{n} emissive RGB-coefficient spectral (C5 stand-in)"}[args.scene]
     if args.scene == "uniform":
         # C2: GridMedium n^3 of 1.0, orthographic; S-uniform's "scatter" variant (distant light + sky)
         density.fill_(1.0)
         scene = scenes.s_uniform(n=n, width=args.width, height=args.height, variant="scatter", density=density)
         from acceleratedvolrenderer_amd.scene import ZSobolSampler, IndependentSampler
         scene.sampler = ZSobolSampler(spp_total) if args.sampler == "zsobol" else IndependentSampler(spp_total)
+        maxdepth = 100
+    elif args.scene == "rgb-explosion":
+        trgb = time.perf_counter()
+        del density
+        density = None
+        torch.cuda.empty_cache()
+        rgb_grids = scenes.rgb_explosion_grids(n=n, device=dev)
+        scene = scenes.s_rgb_explosion(*rgb_grids, width=args.width, height=args.height, sampler=args.sampler,
+                                       spp=spp_total, filter=args.filter)
+        tgen += time.perf_counter() - trgb
         maxdepth = 100
     elif args.scene == "explosion":
         tvdb = time.perf_counter()
@@ -356,10 +356,10 @@ def main():
 
     def step(k):
         # asynchronous on the context stream: steps queue back to back
-        base = ((k * world + rank) * S) % spp_total if wrap else (k * world + rank) * S
+        base = warm_bases[rank][k] if k < args.warmup else timed_bases[rank][k - args.warmup]
         integ.ctx.render(base, base + S, 0, maxdepth)
 
-    log("scene uploaded; warmup")
+    log(f"scene uploaded; pixelsamples {spp_total}; warmup")
     for k in range(args.warmup):
         step(k)
     integ.ctx.film_clear()
@@ -458,11 +458,15 @@ def main():
     achieved = med_bytes / med_s / 1e9 if med_s > 0 else 0.0
     avg_launch_ms = agg["ms_medium"] / launches
     grid_layout = "fat" if integ.ctx.grid_layout_active() else "linear"
-    host_density = None
+    host_density = host_rgb = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and vdb is None:
-        host_density = density.cpu().numpy()
+        if args.scene == "rgb-explosion":
+            host_rgb = [t.cpu().numpy() for t in rgb_grids]
+        else:
+            host_density = density.cpu().numpy()
     integ.close()
     del density
+    rgb_grids = None
     torch.cuda.empty_cache()
 
     out = None
@@ -471,6 +475,9 @@ def main():
         if not args.no_cpu_baseline and world == 1:
             if vdb is not None:
                 host_scene = scene
+            elif args.scene == "rgb-explosion":
+                host_scene = scenes.s_rgb_explosion(*host_rgb, width=args.width, height=args.height,
+                                                    sampler=args.sampler, spp=spp_total, filter=args.filter)
             elif args.scene == "uniform":
                 host_scene = scenes.s_uniform(n=n, width=args.width, height=args.height, variant="scatter",
                                               density=host_density)
@@ -479,7 +486,7 @@ def main():
                 host_scene = scenes.s_cloud(host_density, width=args.width, height=args.height,
                                             sampler=args.sampler, spp=spp_total, filter=args.filter)
             cpu = cpu_baseline(host_scene, S, args.cpu_seconds, f"{workload_name} {args.medium}")
-            host_scene = host_density = None
+            host_scene = host_density = host_rgb = None
         # HBM traffic and the VALU limiter from rocprofv3 counter passes of this same
         # configuration (child processes; the guide's gfx950 rule: FETCH_SIZE x2 + WRITE_SIZE)
         traffic, limiter, pmc_note, cache = None, None, "pmc off", None
@@ -531,13 +538,14 @@ def main():
             "dtype": "f32",
             "data": {"cloud": f"synthetic (CloudMedium::Density {n}^3 generated on device; disney-cloud assets absent)",
                      "uniform": f"synthetic (uniform density {n}^3)",
-                     "explosion": f"synthetic (radial density + temperature NanoVDB grids over {n}^3; explosion asset absent)"}[args.scene],
-            "config": {"workload": f"{workload_name} {'NanoVDBMedium' if vdb is not None else 'GridMedium'}, {'orthographic' if args.scene == 'uniform' else 'perspective'} {args.width}x{args.height}, "
+                     "explosion": f"synthetic (radial density + temperature NanoVDB grids over {n}^3; explosion asset absent)",
+                     "rgb-explosion": f"synthetic (k_rgb_explosion RGB-coefficient sigma_a / sigma_s / Le grids {n}^3 generated on device; explosion asset absent)"}[args.scene],
+            "config": {"workload": f"{workload_name} {'NanoVDBMedium' if vdb is not None else ('RGBGridMedium' if args.scene == 'rgb-explosion' else 'GridMedium')}, {'orthographic' if args.scene == 'uniform' else 'perspective'} {args.width}x{args.height}, "
                                    f"{S} spp/step/GPU, maxdepth {maxdepth}, {args.sampler} sampler "
                                    f"(pixelsamples {spp_total}), {args.filter} filter, {args.mode} mode",
                        "majorant_res": list(maj_res), "majorant_tuning_ms": tune_ms,
                        "global_batch": samples // args.steps, "parallelism": f"sample-shard x{world}",
-                       "sample_index_wrap": wrap},
+                       "pixelsamples": spp_total, "sample_indices_distinct": True},
             "roofline": {
                 "kernel": kname,
                 # the roof this kernel is priced against (no MFMA work on the path); the

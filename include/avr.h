@@ -198,6 +198,13 @@ int avr_medium_rgbgrid(avr_context *ctx, int nx, int ny, int nz, const float bou
                        const float render_from_medium[16], const float medium_from_render[16],
                        const float *sigma_a, const float *sigma_s, float sigma_scale, float g, const float *Le,
                        const float *illuminant, float Le_scale);
+/* Same, but sigma_a / sigma_s / Le are float4 arrays already in device memory of this context's
+ * GPU (e.g. a 1024^3 grid generated on device, 16 GiB per field); the caller keeps ownership
+ * and keeps them alive while the context renders. */
+int avr_medium_rgbgrid_device(avr_context *ctx, int nx, int ny, int nz, const float bounds[6],
+                              const float render_from_medium[16], const float medium_from_render[16],
+                              const float *d_sigma_a, const float *d_sigma_s, float sigma_scale, float g,
+                              const float *d_Le, const float *illuminant, float Le_scale);
 /* Medium interface of the current medium (pbrt: a shape with no material
  * whose MediumInterface has this medium inside and none outside, interaction.cpp:91-97
  * SkipIntersection, shapes.h:152-200 Sphere). radius > 0: a sphere of that radius at `center`
@@ -219,6 +226,12 @@ int avr_medium_bounds(avr_context *ctx, float bounds[6]);
  * (media.h:496-520) at voxel centres (i+0.5)/n — the synthetic S-cloud input. */
 int avr_generate_cloud(avr_context *ctx, float *d_out, int n, long long first, long long count, float density,
                        float wispiness, float frequency);
+/* Fill voxels [first, first + count) of three n^3 float4 device arrays with the synthetic
+ * RGB-coefficient explosion (BASELINE config C5's stand-in as an RGBGridMedium): {c0, c1, c2,
+ * scale} of sigma_a, sigma_s and Le at voxel centres (i + 0.5) / n; each pointer is the
+ * array's element `first`. */
+int avr_generate_rgb_explosion(avr_context *ctx, float *d_sigma_a, float *d_sigma_s, float *d_Le, int n,
+                               long long first, long long count);
 /* Copy the device majorant grid to host (mres product floats). */
 int avr_read_majorant(avr_context *ctx, float *out);
 /* Rebuild the current medium's majorant grid at res[3] cells (1..255 per axis) from the

@@ -1748,15 +1748,23 @@ float oracle_rsp_max(float c0, float c1, float c2) { return Rsp{c0, c1, c2}.MaxV
 // ctor's 16^3 majorant (media.cpp:364-377) over MajorantGrid::VoxelBounds
 void oracle_rgb_majorant(const float *sa, const float *ss, int nx, int ny, int nz, float sigmaScale, int rx, int ry,
                          int rz, float *out) {
-    for (int z = 0; z < rz; ++z)
-        for (int y = 0; y < ry; ++y)
-            for (int x = 0; x < rx; ++x) {
-                Bounds b{{float(x) / rx, float(y) / ry, float(z) / rz},
-                         {float(x + 1) / rx, float(y + 1) / ry, float(z + 1) / rz}};
-                float maxSigma_t = (sa ? RgbGrid{sa, nx, ny, nz, nullptr}.MaxValue(b) : 1) +
-                                   (ss ? RgbGrid{ss, nx, ny, nz, nullptr}.MaxValue(b) : 1);
-                out[x + rx * (y + ry * z)] = sigmaScale * maxSigma_t;
-            }
+    // cells are independent (media.cpp:364-377 builds them in a ParallelFor too): threads over
+    // cells, each cell's max in pbrt's voxel order
+    const int ncell = rx * ry * rz;
+    auto cell = [&](int c) {
+        const int x = c % rx, y = (c / rx) % ry, z = c / (rx * ry);
+        Bounds b{{float(x) / rx, float(y) / ry, float(z) / rz}, {float(x + 1) / rx, float(y + 1) / ry, float(z + 1) / rz}};
+        float maxSigma_t = (sa ? RgbGrid{sa, nx, ny, nz, nullptr}.MaxValue(b) : 1) +
+                           (ss ? RgbGrid{ss, nx, ny, nz, nullptr}.MaxValue(b) : 1);
+        out[c] = sigmaScale * maxSigma_t;
+    };
+    const int nt = std::max(1, std::min(16, std::min(ncell, (int)std::thread::hardware_concurrency())));
+    std::vector<std::thread> th;
+    for (int t = 0; t < nt; ++t)
+        th.emplace_back([&, t] {
+            for (int c = t; c < ncell; c += nt) cell(c);
+        });
+    for (auto &x : th) x.join();
 }
 
 // NanoVDB grids (test infrastructure handles; see VdbTree)

@@ -10,12 +10,16 @@ tests/test_gpu_parity.py) and through size-independent properties:
       shards [k spp/8, (k+1) spp/8) rendered one after another and summed in fp64 equal one
       unsharded render to summation order (rtol 1e-10), their last pass bit-identical, and
       a strided replay subset.
-  C5  emissive NanoVDB explosion over a 1024^3 index extent (scenes.explosion_vdb), 1280x720
-      SpectralFilm: replay subset; and the emission-only absorber's line integral
+  C5  the emissive RGB-coefficient explosion as BASELINE names it — an RGBGridMedium of
+      1024^3 {c0, c1, c2, scale} voxels for sigma_a / sigma_s / Le generated on the device
+      (k_rgb_explosion), 1280x720 SpectralFilm, 4096 pixelsamples: majorant bit-exact and a
+      replay subset; the emissive NanoVDB explosion over a 1024^3 index extent
+      (scenes.explosion_vdb), same film: replay subset; and the emission-only absorber's line integral
       E[L(lambda)] = Le(lambda) (1 - exp(-sigma_a D)) through a uniform density block inside
       a uniform-temperature region (Le constant wherever sigma_a > 0).
 Memory: C4 holds the 4 GiB grid, its 34.5 GB fat copy and a 4 GiB host copy for the oracle;
-C5 ~2 GB of leaves per copy."""
+C5's RGB grids 48 GiB on the device and their 48 GiB host copy; C5's NanoVDB grids ~2 GB of
+leaves per copy."""
 import numpy as np
 import pytest
 
@@ -186,6 +190,32 @@ def test_c5_explosion_1024_spectral_replay_subset(explosion):
     canon = binding.OracleRun(scene, max_depth=10, seed=0, libm="canonical")
     exact, total = _replay_subset(integ, canon, 0, 8, stride=7919)
     print(f"C5 explosion 1024^3 NanoVDB spectral 720p: {exact}/{total} samples bit-identical")
+    assert exact / total >= 0.999
+    integ.close()
+
+
+def test_c5_rgb_explosion_1024_spectral_majorant_and_replay_subset():
+    from acceleratedvolrenderer_amd import VolPathIntegrator, scenes
+    from oracle import binding
+    n = 1024
+    grids = scenes.rgb_explosion_grids(n, device=0)
+    scene = scenes.s_rgb_explosion(*grids, spp=4096)
+    md = scenes.CLOUD_MAXDEPTH
+    integ = VolPathIntegrator(scene, maxdepth=md, spp=4096, device=0)
+    integ.ctx.film_clear()
+    integ.ctx.render(64, 72, 0, md)
+    bs, bw = integ.spectral_sums()
+    rgb, w = integ.film_sums()
+    assert np.all(np.isfinite(bs)) and float(bs.sum()) > 0 and np.all(np.isfinite(rgb))
+    maj = integ.ctx.majorant(16 ** 3)
+    host = [g.cpu().numpy() for g in grids]
+    del grids
+    hscene = scenes.s_rgb_explosion(*host, spp=4096)
+    canon = binding.OracleRun(hscene, max_depth=md, seed=0, libm="canonical")
+    assert maj.view(np.uint32).tolist() == canon.majorant.view(np.uint32).tolist()
+    exact, total = _replay_subset(integ, canon, 64, 8, stride=7919)
+    print(f"C5 RGB-coefficient explosion 1024^3 spectral 720p: majorant bit-exact, {exact}/{total} samples "
+          f"bit-identical, film sum {float(bs.sum()):.4e}")
     assert exact / total >= 0.999
     integ.close()
 

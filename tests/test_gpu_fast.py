@@ -44,13 +44,22 @@ def _scene(kind):
     raise ValueError(kind)
 
 
+@pytest.mark.parametrize("maj", ["pbrt", "tuned1"])
 @pytest.mark.parametrize("kind", ["uniform", "cloud"])
-def test_fast_mode_statistical_parity(kind):
+def test_fast_mode_statistical_parity(kind, maj):
+    """maj "pbrt": pbrt's own 16^3 majorant; "tuned1": the 1^3 majorant avr_tune_majorant picks
+    for the bench's S-cloud (bench.py fast_mode leg) — correlated parity against the platform
+    oracle built with the same majorant, unbiasedness against the oracle at pbrt's 16^3."""
     from acceleratedvolrenderer_amd import VolPathIntegrator
     from oracle import binding
     scene, maxdepth = _scene(kind)
+    pbrt_scene, _ = _scene(kind)
+    if maj == "tuned1":
+        scene.medium.majorant_res = (1, 1, 1)
     spp = 16
     fast = VolPathIntegrator(scene, maxdepth=maxdepth, spp=spp, seed=0, device=0, mode="fast")
+    if maj == "tuned1":
+        assert fast.ctx.majorant(1).tolist() == binding.build_majorant(scene.medium.density, (1, 1, 1)).tolist()
     rgb_f, w_f = fast.render()
     ref = binding.OracleRun(scene, max_depth=maxdepth, seed=0)
     rgb_o, w_o = ref.render(0, spp, nthreads=8)
@@ -59,14 +68,19 @@ def test_fast_mode_statistical_parity(kind):
     img_f, img_o, img_1 = fast.image(rgb_f, w_f), fast.image(rgb_o, w_o), fast.image(rgb_1, w_1)
     err, noise = _rel_rms(img_f, img_o), _rel_rms(img_1, img_o)
 
-    # unbiasedness: 64x the samples on the device vs the oracle's frame mean
+    # unbiasedness: 64x the samples on the device vs the frame mean of the oracle at pbrt's
+    # own majorant (any conservative majorant is the same estimator in expectation)
+    if maj == "tuned1":
+        rgb_o, w_o = binding.OracleRun(pbrt_scene, max_depth=maxdepth, seed=0).render(0, spp, nthreads=8)
+        rgb_1, w_1 = binding.OracleRun(pbrt_scene, max_depth=maxdepth, seed=1).render(0, spp, nthreads=8)
+        img_o, img_1 = fast.image(rgb_o, w_o), fast.image(rgb_1, w_1)
     rgb_big, w_big = fast.render(0, 64 * spp if kind == "uniform" else 1024)
     img_big = fast.image(rgb_big, w_big)
     o_mean = 0.5 * (img_o.mean() + img_1.mean())
     # standard error of the oracle's two-seed frame mean from the per-pixel seed difference
     # (var of (o + o1) / 2 over N pixels = var(o - o1) / (4 N)); the device mean adds ~1/32 of it
     se = 1.02 * float(np.std(img_o - img_1)) / (2 * np.sqrt(img_o.size))
-    print(f"fast/{kind}: film rel RMS vs platform oracle {err:.3e} (MC noise {noise:.3e}); frame mean "
+    print(f"fast/{kind}/{maj}: film rel RMS vs platform oracle {err:.3e} (MC noise {noise:.3e}); frame mean "
           f"{img_big.mean():.6f} vs oracle {o_mean:.6f} (se {se:.2e})")
     assert err <= 0.5 * noise
     assert abs(img_big.mean() - o_mean) <= 4 * se + 1e-6 * abs(o_mean)
@@ -150,4 +164,41 @@ def test_tune_majorant_keeps_the_film_and_picks_a_candidate():
     got = integ.ctx.majorant(chosen[0] ** 3)
     assert got.view(np.uint32).tolist() == binding.build_majorant(dens, chosen).view(np.uint32).tolist()
     print(f"tuned majorant {chosen}, probe ms {ms}")
+    integ.close()
+
+
+def test_tune_majorant_failure_restores_film_and_majorant():
+    """A probe that fails (here: an invalid max_depth reaches avr_render) leaves the context as
+    it was: the film sums and the majorant grid at its previous resolution."""
+    from acceleratedvolrenderer_amd import scenes, VolPathIntegrator
+    from oracle import binding
+    dens = binding.cloud_grid(24)
+    scene = scenes.s_cloud(dens, width=32, height=18)
+    integ = VolPathIntegrator(scene, maxdepth=scenes.CLOUD_MAXDEPTH, spp=2, seed=0, device=0)
+    rgb, w = integ.render()
+    maj = integ.ctx.majorant(16 ** 3)
+    with pytest.raises(RuntimeError, match="sample range"):
+        integ.ctx.tune_majorant([(1, 1, 1), (4, 4, 4)], 0, 2, 0, -1)
+    rgb2, w2 = integ.film_sums()
+    assert np.array_equal(rgb, rgb2) and np.array_equal(w, w2)
+    assert integ.ctx.majorant(16 ** 3).view(np.uint32).tolist() == maj.view(np.uint32).tolist()
+    # and the context still renders the same samples
+    rgb3, w3 = integ.render()
+    assert np.array_equal(rgb3, rgb) and np.array_equal(w3, w)
+    integ.close()
+
+
+def test_tune_majorant_refuses_single_segment_media():
+    """HomogeneousMedium / CloudMedium have one majorant segment (no grid to tune), as
+    avr_set_majorant_res refuses them."""
+    from acceleratedvolrenderer_amd import scenes, VolPathIntegrator
+    from acceleratedvolrenderer_amd import HomogeneousMedium
+    from acceleratedvolrenderer_amd.scene import Scene
+    base = scenes.s_uniform(n=4, width=8, height=8, variant="scatter")
+    scene = Scene(base.camera, base.film, HomogeneousMedium(sigma_a=0.5, sigma_s=2.0, g=0.3), base.lights)
+    integ = VolPathIntegrator(scene, maxdepth=5, spp=1, seed=0, device=0)
+    with pytest.raises(RuntimeError, match="single majorant segment"):
+        integ.ctx.tune_majorant([(1, 1, 1), (2, 2, 2)], 0, 1, 0, 5)
+    with pytest.raises(RuntimeError, match="single majorant segment"):
+        integ.ctx.set_majorant_res((2, 2, 2))
     integ.close()

@@ -72,3 +72,52 @@ def test_fullsize_multipass_and_determinism(cloud):
     for a, b, c in zip(two, one, again):
         assert np.array_equal(a, b) and np.array_equal(b, c)
     assert float(one[1].sum()) > 0.9 * 1280 * 720 * 32 * 0.5   # Gaussian filter weights, every pixel sampled
+
+
+def test_fullsize_fast_mode_at_the_tuned_majorant(cloud):
+    """The bench's fast_mode leg at its configuration: hardware math and the 1^3 majorant
+    avr_tune_majorant picks for the S-cloud-1024 (bench.py). On a strided pixel subset:
+    per-pixel means of the hero-wavelength radiance track the platform oracle built with the
+    same majorant (relative RMS <= 0.5 x the two-seed oracle noise), and the subset mean over
+    more samples agrees with the oracle at pbrt's own 16^3 majorant within 4 standard errors."""
+    import copy
+    from acceleratedvolrenderer_amd import scenes
+    from oracle import binding
+    integ, host = cloud
+    md = scenes.CLOUD_MAXDEPTH
+    f = host.film
+    npix = f.width * f.height
+    pixels = np.arange(0, npix, 4099)
+    host1 = copy.copy(host)
+    host1.medium = copy.copy(host.medium)
+    host1.medium.majorant_res = (1, 1, 1)
+    plat = binding.OracleRun(host1, max_depth=md, seed=0)
+    plat_b = binding.OracleRun(host1, max_depth=md, seed=1)
+    integ.ctx.set_render_mode("fast")
+    integ.ctx.set_majorant_res((1, 1, 1))
+    try:
+        gpu = []
+        for p0 in (64, 80, 96, 112):
+            integ.ctx.film_clear()
+            integ.ctx.render(p0, p0 + 16, 0, md)
+            _, _, L, _, _ = integ.ctx.last_pass_samples(npix, 16)
+            gpu.append(np.stack([L[s * npix + pixels, 0] for s in range(16)], 1))
+        gpu = np.concatenate(gpu, 1)                                      # (pixels, 64)
+    finally:
+        integ.ctx.set_render_mode("replay")
+        integ.ctx.set_majorant_res((16, 16, 16))
+    px, py = pixels % f.width, pixels // f.width
+    per = lambda run, s0, n: np.array([[run.pixel_sample(int(x), int(y), s0 + s)[0][0] for s in range(n)]
+                                       for x, y in zip(px, py)])
+    o0, o1 = per(plat, 64, 16), per(plat_b, 64, 16)
+    g, a, b = gpu[:, :16].mean(1), o0.mean(1), o1.mean(1)
+    err = float(np.sqrt(np.mean((g - a) ** 2)) / np.sqrt(np.mean(a ** 2)))
+    noise = float(np.sqrt(np.mean((b - a) ** 2)) / np.sqrt(np.mean(a ** 2)))
+    # unbiasedness against pbrt's 16^3 majorant (replay streams of the canonical/platform oracle)
+    ref = binding.OracleRun(host, max_depth=md, seed=0)
+    r = per(ref, 64, 64)
+    se = float(np.sqrt(gpu.var() / gpu.size + r.var() / r.size))
+    print(f"full-size fast@1^3: subset rel RMS {err:.3e} (noise {noise:.3e}); mean {gpu.mean():.5f} vs "
+          f"oracle@16^3 {r.mean():.5f} (se {se:.2e})")
+    assert err <= 0.5 * noise
+    assert abs(gpu.mean() - r.mean()) <= 4 * se

@@ -46,3 +46,24 @@ def test_launcher_refuses_a_mismatched_world():
     r = _run(["--gpus", "2"], e)
     assert r.returncode != 0
     assert "WORLD_SIZE=3" in r.stderr
+
+
+def test_bench_sample_plan_renders_distinct_indices_at_every_world_size():
+    """bench.py's step arithmetic (launch.sample_plan): over the timed steps of all ranks every
+    (pixel, sample index) pair is rendered exactly once, inside [0, pixelsamples), for the
+    driver's 1/2/4/8-GPU runs; N = 1 with 4 steps of 64 keeps config C3's 256 spp."""
+    from acceleratedvolrenderer_amd.launch import sample_plan
+    for world in (1, 2, 4, 8):
+        for steps, warmup, S in ((4, 1, 64), (10, 2, 64), (3, 0, 16)):
+            P, warm, timed = sample_plan(world, steps, warmup, S)
+            idx = [b + i for r in range(world) for b in timed[r] for i in range(S)]
+            assert len(idx) == len(set(idx)) == steps * world * S
+            assert min(idx) == 0 and max(idx) < P and P >= 256 and P & (P - 1) == 0
+            assert all(0 <= b and b + S <= P for r in range(world) for b in warm[r])
+            assert len(warm[0]) == warmup and all(len(t) == steps for t in timed)
+    assert sample_plan(1, 4, 1, 64)[0] == 256
+    assert sample_plan(8, 4, 1, 64)[0] == 2048
+    assert sample_plan(1, 4, 1, 64, base_spp=4096)[0] == 4096
+    import pytest
+    with pytest.raises(ValueError):
+        sample_plan(8, 4, 1, 64, pixelsamples=256)

@@ -41,6 +41,33 @@ def test_round_trip_dense_grid_with_tiles_and_negative_origins(tmp_path):
     assert np.array_equal(gw[0], rw[0]) and np.array_equal(gw[1], rw[1])
 
 
+@pytest.mark.parametrize("codec", ["none", "zip"])
+def test_zip_codec_round_trip(tmp_path, codec):
+    """ZIP-coded grids (NanoVDB io::Internal::write with NANOVDB_USE_ZIP: u64 compressed size +
+    one zlib stream per grid buffer) read back to the same tree as the uncompressed file; a
+    file mixing both is read grid by grid."""
+    rng = np.random.default_rng(9)
+    d = np.zeros((24, 24, 24), np.float32)
+    d[4:20, 2:22, 6:18] = rng.random((16, 20, 12), dtype=np.float32)
+    d[16:24, 16:24, 16:24] = 0.5
+    g = NanoVDBGrid.from_dense(d, index_min=(-8, 16, 0), voxel_size=0.1)
+    t = NanoVDBGrid.from_dense(np.full((8, 8, 8), 1200.0, np.float32), background=0.0)
+    p = tmp_path / f"{codec}.nvdb"
+    nvdb.write_nvdb(p, [("density", g), ("temperature", t)], codec=codec)
+    segs = nvdb.list_grids(p)
+    assert [s[2] for s in segs] == [nvdb.CODECS[codec]] * 2
+    if codec == "zip":   # the stored segment is smaller than the grid buffer it holds
+        plain = tmp_path / "plain.nvdb"
+        nvdb.write_nvdb(plain, [("density", g), ("temperature", t)])
+        assert segs[0][3] < nvdb.list_grids(plain)[0][3]
+    r = nvdb.read_nvdb(p)
+    lo, hi = g.index_bbox[:3] - 9, g.index_bbox[3:] + 9
+    probes = np.stack(np.meshgrid(*(np.arange(lo[k], hi[k] + 1, 2) for k in range(3)), indexing="ij"), -1).reshape(-1, 3)
+    _same_tree(g, r, probes)
+    rt = nvdb.read_nvdb(p, "temperature")
+    assert np.array_equal(rt.values([[3, 4, 5], [9, 0, 0]]), np.array([1200.0, 0.0], np.float32))
+
+
 def test_upper_and_root_tiles_and_several_grids(tmp_path):
     leaf = np.arange(512, dtype=np.float32).reshape(8, 8, 8) / 512
     g = NanoVDBGrid(leaf_origins=[(0, 0, 0), (-8, 128, 4096)], leaf_values=[leaf, 1 - leaf], background=0.0,
@@ -70,10 +97,28 @@ def test_reader_errors(tmp_path):
     with pytest.raises(ValueError, match="magic"):
         nvdb.read_nvdb(bad)
     zipped = bytearray(raw)
-    struct.pack_into("<H", zipped, 14, 1)          # file codec ZIP
+    struct.pack_into("<H", zipped, 14, 1)          # file codec ZIP over an uncompressed buffer
     (tmp_path / "zip.nvdb").write_bytes(bytes(zipped))
-    with pytest.raises(ValueError, match="compressed"):
+    with pytest.raises(ValueError, match="ZIP"):
         nvdb.read_nvdb(tmp_path / "zip.nvdb")
+    blosc = bytearray(raw)
+    struct.pack_into("<H", blosc, 14, 2)           # file codec BLOSC: refused
+    (tmp_path / "blosc.nvdb").write_bytes(bytes(blosc))
+    with pytest.raises(ValueError, match="BLOSC"):
+        nvdb.read_nvdb(tmp_path / "blosc.nvdb")
+    with pytest.raises(ValueError, match="codec"):
+        nvdb.write_nvdb(tmp_path / "x.nvdb", {"density": g}, codec="blosc")
+    z = tmp_path / "z.nvdb"
+    nvdb.write_nvdb(z, {"density": g}, codec="zip")
+    zr = bytearray(z.read_bytes())
+    (tmp_path / "ztrunc.nvdb").write_bytes(bytes(zr[:-10]))   # stream cut short
+    with pytest.raises(ValueError):
+        nvdb.read_nvdb(tmp_path / "ztrunc.nvdb")
+    zc = bytearray(zr)
+    zc[16 + 176 + len(b"density") + 1 + 8 + 4] ^= 0xFF        # corrupt the deflate stream
+    (tmp_path / "zbad.nvdb").write_bytes(bytes(zc))
+    with pytest.raises(ValueError, match="ZIP"):
+        nvdb.read_nvdb(tmp_path / "zbad.nvdb")
     typed = bytearray(raw)
     struct.pack_into("<I", typed, 16 + 32, 2)      # MetaData gridType Double
     (tmp_path / "dbl.nvdb").write_bytes(bytes(typed))

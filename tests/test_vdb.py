@@ -158,6 +158,32 @@ def hdr(tmp_path_factory):
         "  for (int k = 0; k < 9; ++k) g.inv[k] = inv[k];\n"
         "  for (int k = 0; k < 3; ++k) g.vec[k] = vec[k];\n"
         "  for (int i = 0; i < n; ++i) out[i] = sample_world(g, p[3 * i], p[3 * i + 1], p[3 * i + 2]);\n"
+        "}\n"
+        # the apron layout the kernels sample, built on the host exactly as upload_vdb +
+        # k_vdb_apron build it on the device
+        'extern "C" long long sample_apron(const int *slot, const float *leaves, const float *tiles, int ntiles,\n'
+        "                       const int *o, const int *nb, float bg, const float *inv, const float *vec, int n,\n"
+        "                       const float *p, float *out, float *vals) {\n"
+        "  Grid g{slot, leaves, tiles, o[0], o[1], o[2], nb[0], nb[1], nb[2], bg};\n"
+        "  std::vector<int> aslot; std::vector<long long> list;\n"
+        "  build_apron_slots(slot, nb[0], nb[1], nb[2], tiles, ntiles, bg, aslot, list);\n"
+        "  std::vector<float> consts(tiles, tiles + ntiles); consts.push_back(bg);\n"
+        "  std::vector<float> blocks(list.size() * kApronVals);\n"
+        "  for (std::size_t i = 0; i < list.size(); ++i) {\n"
+        "    const long long e = list[i];\n"
+        "    const int ex = e % (nb[0] + 1), ey = (e / (nb[0] + 1)) % (nb[1] + 1), ez = e / ((nb[0] + 1) * (nb[1] + 1));\n"
+        "    for (int k = 0; k < kApronVals; ++k) blocks[i * kApronVals + k] = apron_value(g, ex, ey, ez, k);\n"
+        "  }\n"
+        "  Apron a{aslot.data(), blocks.data(), consts.data(), o[0], o[1], o[2], nb[0], nb[1], nb[2], bg};\n"
+        "  for (int k = 0; k < 9; ++k) a.inv[k] = inv[k];\n"
+        "  for (int k = 0; k < 3; ++k) a.vec[k] = vec[k];\n"
+        "  for (int i = 0; i < n; ++i) out[i] = sample_world(a, p[3 * i], p[3 * i + 1], p[3 * i + 2]);\n"
+        "  // getValue over the extent +-10 voxels from the apron layout\n"
+        "  long long q = 0;\n"
+        "  for (int z = o[2] - 10; z < o[2] + 8 * nb[2] + 10; ++z)\n"
+        "    for (int y = o[1] - 10; y < o[1] + 8 * nb[1] + 10; ++y)\n"
+        "      for (int x = o[0] - 10; x < o[0] + 8 * nb[0] + 10; ++x) vals[q++] = get_value(a, x, y, z) - get_value(g, x, y, z);\n"
+        "  return (long long)list.size();\n"
         "}\n")
     so = d / "shim.so"
     subprocess.check_call(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-shared", "-fPIC", str(src), "-o", str(so)])
@@ -186,6 +212,50 @@ def test_device_header_equals_oracle(hdr):
                ctypes.c_float(float(g.background)), arr(inv, F), arr(vec, F), len(p), arr(p, F), arr(out, F))
     want = tree.sample_world(p)
     assert out.view(np.uint32).tolist() == want.view(np.uint32).tolist()
+
+
+@pytest.mark.parametrize("case", ["tiles", "two_tiles", "single_leaf"])
+def test_apron_layout_equals_oracle(hdr, case):
+    """The apron layout (one slot + one 9^3 block per lookup) samples the same bits as the
+    oracle's tree, and its getValue equals the base layout's everywhere around the extent."""
+    if case == "tiles":
+        e = _dense(9, (21, 19, 26))
+        e[0:8, 0:8, 0:8] = 0.6
+        g = NanoVDBGrid.from_dense(e, index_min=(-8, 0, -16), index_to_world=_rotated_map(20), background=0.0)
+    elif case == "two_tiles":   # neighbouring tiles of different values, a background hole, bg != 0
+        e = np.full((24, 16, 16), 0.25, np.float32)
+        e[0:8, 0:8, 0:8] = 0.6
+        e[8:16, 0:8, 8:16] = 0.9
+        e[16:24, 8:16, 0:8] = 0.0
+        e[3, 12, 5] = 1.5
+        g = NanoVDBGrid.from_dense(e, index_min=(8, -8, 0), background=0.25)
+    else:
+        e = np.zeros((3, 3, 3), np.float32)
+        e[1, 1, 1] = 2.0
+        g = NanoVDBGrid.from_dense(e, index_min=(7, 7, 7), voxel_size=0.5, background=0.0)
+    slot, lo, nb = _slots(g)
+    tree = binding.VdbTree(g)
+    b = binding.vdb_bounds(tree)
+    rng = np.random.default_rng(12)
+    p = (b[:3] - 0.3 + rng.random((20000, 3)) * (b[3:] - b[:3] + 0.6)).astype(np.float32)
+    out = np.zeros(len(p), np.float32)
+    I = ctypes.POINTER(ctypes.c_int)
+    F = ctypes.POINTER(ctypes.c_float)
+    arr = lambda a, t: np.ascontiguousarray(a).ctypes.data_as(t)
+    inv = g.world_to_index.astype(np.float32).reshape(-1)
+    vec = g.index_to_world[:, 3].astype(np.float32)
+    lo32, nb32 = lo.astype(np.int32), nb.astype(np.int32)
+    tiles = g.tile_values if len(g.tile_values) else np.zeros(1, np.float32)
+    nvals = int(np.prod(8 * nb + 20))
+    vals = np.full(nvals, np.nan, np.float32)
+    hdr.sample_apron.restype = ctypes.c_longlong
+    nblk = hdr.sample_apron(arr(slot, I), arr(g.leaf_values, F), arr(tiles, F), len(g.tile_values), arr(lo32, I),
+                            arr(nb32, I), ctypes.c_float(float(g.background)), arr(inv, F), arr(vec, F), len(p),
+                            arr(p, F), arr(out, F), arr(vals, F))
+    assert nblk >= len(g.leaf_origins)
+    want = tree.sample_world(p)
+    assert out.view(np.uint32).tolist() == want.view(np.uint32).tolist()
+    assert np.all(vals == 0)
 
 
 def test_oracle_vdb_absorber_known_answer():
