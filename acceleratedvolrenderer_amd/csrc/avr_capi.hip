@@ -60,7 +60,7 @@ struct avr_context {
     // only: 2 GiB of HBM; longer passes amortise the persistent kernel's drain tail)
     long long max_paths = 16ll << 20;
     bool max_paths_set = false;
-    long long rec_cap = 0;   // k_paths records allocated (ps.rec, 2 float4 per sample)
+    long long rec_cap = 0;   // k_paths records and camera stage allocated (samples)
     hipStream_t own_stream = nullptr, stream = nullptr;
     // medium
     avr::DevMedium med{};
@@ -117,6 +117,7 @@ struct avr_context {
     int *d_vdb_slot[2] = {nullptr, nullptr};
     float *d_vdb_leaves[2] = {nullptr, nullptr}, *d_vdb_tiles[2] = {nullptr, nullptr};
     int vdb_ibbox[6] = {};    // density grid's active index bbox (majorant clamp)
+    long long vdb_napron[2] = {0, 0};   // apron blocks of the density / temperature grid
     // RGBGridMedium grids (sigma_a, sigma_s, Le as float4 {c0, c1, c2, scale}) and illuminant
     float4 *d_rgb[3] = {nullptr, nullptr, nullptr};   // owned copies (avr_medium_rgbgrid only)
     float *d_illum = nullptr;
@@ -177,28 +178,37 @@ void free_paths(avr_context *c) {
     if (c->sh.path) (void)hipFree(c->sh.path);
     if (c->sh.pdfs) (void)hipFree(c->sh.pdfs);
     for (auto &q : c->d_queue) if (q) (void)hipFree(q), q = nullptr;
-    float4 *rec = c->ps.rec, *contrib = c->ps.contrib;   // the k_paths records: ensure_records
+    // the k_paths records and camera stage are managed by ensure_records
+    float4 *rec = c->ps.rec, *cam0 = c->ps.cam0, *cam1 = c->ps.cam1, *cam2 = c->ps.cam2, *cam4 = c->ps.cam4;
+    uint4 *cam3 = c->ps.cam3, *cam5 = c->ps.cam5;
     c->ps = {};
     c->ps.rec = rec;
-    c->ps.contrib = contrib;
+    c->ps.cam0 = cam0; c->ps.cam1 = cam1; c->ps.cam2 = cam2; c->ps.cam3 = cam3; c->ps.cam4 = cam4; c->ps.cam5 = cam5;
     c->sh = {};
     c->cap = 0;
 }
 
 void free_records(avr_context *c) {
-    if (c->ps.rec) (void)hipFree(c->ps.rec);
-    if (c->ps.contrib) (void)hipFree(c->ps.contrib);
-    c->ps.rec = c->ps.contrib = nullptr;
+    for (void *p : {(void *)c->ps.rec, (void *)c->ps.cam0, (void *)c->ps.cam1, (void *)c->ps.cam2, (void *)c->ps.cam3,
+                    (void *)c->ps.cam4, (void *)c->ps.cam5})
+        if (p) (void)hipFree(p);
+    c->ps.rec = c->ps.cam0 = c->ps.cam1 = c->ps.cam2 = c->ps.cam4 = nullptr;
+    c->ps.cam3 = c->ps.cam5 = nullptr;
     c->rec_cap = 0;
 }
 
-// k_paths' per-sample records (32 B each) and RGBFilm's per-sample contributions (16 B each,
-// k_film_rgb -> k_film_sum), independent of the wavefront SoA
+// k_paths' per-sample records (L, 16 B) and its camera stage (k_paths_camera: 5 x 16 B, plus
+// 16 B of PCG32 state for the IndependentSampler), independent of the wavefront SoA
 int ensure_records(avr_context *c, long long n) {
     if (n <= c->rec_cap) return AVR_OK;
     free_records(c);
-    HIP_TRY(dalloc(&c->ps.rec, 2 * (size_t)n));
-    HIP_TRY(dalloc(&c->ps.contrib, (size_t)n));
+    HIP_TRY(dalloc(&c->ps.rec, (size_t)n));
+    HIP_TRY(dalloc(&c->ps.cam0, (size_t)n));
+    HIP_TRY(dalloc(&c->ps.cam1, (size_t)n));
+    HIP_TRY(dalloc(&c->ps.cam2, (size_t)n));
+    HIP_TRY(dalloc(&c->ps.cam3, (size_t)n));
+    HIP_TRY(dalloc(&c->ps.cam4, (size_t)n));
+    HIP_TRY(dalloc(&c->ps.cam5, (size_t)n));
     c->rec_cap = n;
     return AVR_OK;
 }
@@ -389,6 +399,7 @@ int upload_vdb(avr_context *c, const avr_vdb_grid *G, int k, avr::vdb::Apron &g)
     }
     // the host vectors and the base layout die here: finish the copies and the fill first
     HIP_TRY(hipStreamSynchronize(c->stream));
+    c->vdb_napron[k] = (long long)list.size();
     g.slot = c->d_vdb_slot[k];
     g.blocks = c->d_vdb_leaves[k];
     g.consts = c->d_vdb_tiles[k];
@@ -552,13 +563,13 @@ int avr_context_create(int device, long long max_paths, avr_context **out) {
     hipError_t e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
     if (e != hipSuccess) { delete c; return fail(AVR_ERR_HIP, hipGetErrorString(e)); }
     c->stream = c->own_stream;
-    if (dalloc(&c->d_counts, 4) != hipSuccess || dalloc(&c->d_stats, avr::kNumStats) != hipSuccess ||
+    if (dalloc(&c->d_counts, 4) != hipSuccess || dalloc(&c->d_stats, avr::kNumStats + 8) != hipSuccess ||
         hipHostMalloc((void **)&c->h_count, sizeof(int) * 4) != hipSuccess) {
         delete c;
         return fail(AVR_ERR_HIP, "context allocation failed");
     }
     if (dalloc(&c->d_heads, 8) != hipSuccess ||
-        hipMemset(c->d_stats, 0, sizeof(unsigned long long) * avr::kNumStats) != hipSuccess) {
+        hipMemset(c->d_stats, 0, sizeof(unsigned long long) * (avr::kNumStats + 8)) != hipSuccess) {
         delete c;
         return fail(AVR_ERR_HIP, "context allocation failed");
     }
@@ -800,6 +811,23 @@ int avr_medium_nanovdb(avr_context *c, const avr_vdb_grid *density, const avr_vd
     if ((rc = medium_common(c, nullptr, 1, 1, 1, bounds, rfm, mfr, sigma_a, sigma_s, g, nullptr, nullptr, 1, 1, 1, mres,
                             3, nullptr)))
         return rc;
+    // the density grid's fat copy (avr_set_grid_layout 1, as for GridMedium): 32 B per base voxel
+    // of every apron block, when it fits in free HBM with 8 GiB to spare
+    if (c->grid_layout == 1 && c->vdb_napron[0] > 0) {
+        const size_t nfat = (size_t)c->vdb_napron[0] * 512;
+        size_t freeB = 0, totalB = 0;
+        HIP_TRY(hipMemGetInfo(&freeB, &totalB));
+        if (nfat * 32 + (8ull << 30) < freeB && hipMalloc((void **)&c->d_fat, nfat * 32) == hipSuccess) {
+            hipLaunchKernelGGL(avr::k_vdb_fat, dim3(blocks_for((long long)nfat, 256, 256 * 64)), dim3(256), 0, c->stream,
+                               c->med.vdb.blocks, c->vdb_napron[0], c->d_fat);
+            HIP_TRY(hipGetLastError());
+            HIP_TRY(hipStreamSynchronize(c->stream));
+            c->med.vdb.fat = reinterpret_cast<const float *>(c->d_fat);
+        } else {
+            (void)hipGetLastError();
+            c->d_fat = nullptr;
+        }
+    }
     c->med.vdb_lescale = Lescale;
     c->med.temp_offset = temperature_offset;
     c->med.temp_scale = temperature_scale;
@@ -1362,6 +1390,10 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
         // SobolSample takes indices below 2^SobolMatrixSize = 2^52 (lowdiscrepancy.h:170)
         if (2 * zs.nBase4Digits - (zs.log2spp & 1) > 52)
             return fail(AVR_ERR_ARG, "zsobol: resolution x spp beyond the 2^52 Sobol' index range");
+        // Morton(pixel) and the pixel-only digits (zsobol_upper, the pixel table) are 32-bit
+        const int res = (int)avr::smp::round_up_pow2((uint32_t)std::max(c->film.width, c->film.height));
+        if (2 * avr::smp::ilog2((uint32_t)res) > 32)
+            return fail(AVR_ERR_ARG, "zsobol: film resolution beyond 65536 (Morton(pixel) exceeds 32 bits)");
     }
     HIP_TRY(hipSetDevice(c->device));
     if (c->sampler_kind == 1) {
@@ -1451,6 +1483,22 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
             }
             p.heads = c->d_heads;
             HIP_TRY(hipMemsetAsync(c->d_heads, 0, 8 * sizeof(int), c->stream));
+            // the camera stage: one lane per sample (k_paths_camera)
+            {
+                const int sv = c->sampler_kind == 0 ? 0 : (avr::smp::zsobol_wide(p.zs) ? 2 : 1);
+                // ZSobol quads: 4-aligned sample ranges, at most 8 lower base-4 digits
+                p.cam_quad = (base % 4 == 0 && S % 4 == 0 && p.zs.log2spp <= 16) ? 1 : 0;
+                using KC = void (*)(avr::Params);
+                static const KC kcam[2][3] = {
+                    {avr::k_paths_camera<0, false>, avr::k_paths_camera<2, false>, avr::k_paths_camera<3, false>},
+                    {avr::k_paths_camera<0, true>, avr::k_paths_camera<2, true>, avr::k_paths_camera<3, true>}};
+                EV_MARK(ec);
+                hipLaunchKernelGGL(kcam[c->render_mode ? 1 : 0][sv], dim3(blocks_for(n0, 256, 256 * 8)), dim3(256), 0,
+                                   c->stream, p);
+                HIP_TRY(hipGetLastError());
+                EV_MARK(ec1);
+                c->timed.push_back({ec, ec1, &avr_stats::ms_camera, false});
+            }
             EV_MARK(e0);
             // gray medium: sigma_a and sigma_s tables constant over all 471 wavelengths
             const int mk = c->med.type == 3 ? 1 : (c->med.type == 4 ? 2 : (c->med.type == 1 || c->med.type == 2 ? 3 : 0));
@@ -1462,16 +1510,8 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
             EV_MARK(e1);
             p.rec_mode = 1;   // k_film reads the records k_paths wrote
             p.fast = c->render_mode;
-            if (c->film.nbuckets == 0) {
-                // RGBFilm: the per-sample sensor conversion (f64 canonical wavelengths and pdfs)
-                // with one lane per sample, then the fp64 sums per pixel in sample order
-                hipLaunchKernelGGL(avr::k_film_rgb, dim3(blocks_for(n0, 256, 256 * 64)), dim3(256), 0, c->stream, p);
-                HIP_TRY(hipGetLastError());
-                hipLaunchKernelGGL(avr::k_film_sum, dim3(blocks_for(P)), dim3(256), 0, c->stream, p);
-            } else {
-                hipLaunchKernelGGL(avr::k_film, dim3(blocks_for(P)), dim3(256), avr::film_lds_bytes(c->film.nbuckets),
-                                   c->stream, p);
-            }
+            hipLaunchKernelGGL(avr::k_film, dim3(blocks_for(P)), dim3(256), avr::film_lds_bytes(c->film.nbuckets),
+                               c->stream, p);
             HIP_TRY(hipGetLastError());
             EV_MARK(e2);
             c->timed.push_back({e0, e1, &avr_stats::ms_medium, true});
@@ -1785,24 +1825,10 @@ int avr_last_pass_samples(avr_context *c, float *L, float *lambda, float *pdf, l
     const long long n = (long long)c->film.width * c->film.height * c->last_S;
     if (n_max < n) return fail(AVR_ERR_ARG, "buffer too small for the last pass");
     if (n > 0 && c->last_persistent) {
-        // k_paths records {L}, {u_lambda, weight}: wavelengths and pdfs re-derived on the host
-        // with the device's functions (canonical math: bit-identical to k_film's; a fast-mode
-        // pass's hardware log is approximated by the host libm)
-        std::vector<float4> rec(2 * (size_t)n);
-        HIP_TRY(hipMemcpy(rec.data(), c->ps.rec, 2 * n * sizeof(float4), hipMemcpyDeviceToHost));
-        const avr::DevFilm &f = c->film;
-        for (long long i = 0; i < n; ++i) {
-            const float4 r0 = rec[2 * i], u = rec[2 * i + 1];
-            const avr::Spec l = f.nbuckets > 0 ? avr::sample_uniform_lambda(u.x, f.lmin, f.lmax)
-                                               : (c->last_fast ? avr::sample_visible_lambda_fast(u.x)
-                                                               : avr::sample_visible_lambda(u.x));
-            const float lv[4] = {l.v0, l.v1, l.v2, l.v3};
-            L[4 * i] = r0.x; L[4 * i + 1] = r0.y; L[4 * i + 2] = r0.z; L[4 * i + 3] = r0.w;
-            for (int k = 0; k < 4; ++k) {
-                lambda[4 * i + k] = lv[k];
-                pdf[4 * i + k] = f.nbuckets > 0 ? 1 / (f.lmax - f.lmin) : avr::visible_wavelength_pdf(lv[k]);
-            }
-        }
+        // k_paths' records (L) and its camera stage's wavelengths and pdfs, as k_film read them
+        HIP_TRY(hipMemcpy(L, c->ps.rec, n * sizeof(float4), hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(lambda, c->ps.cam2, n * sizeof(float4), hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(pdf, c->ps.cam4, n * sizeof(float4), hipMemcpyDeviceToHost));
     } else if (n > 0) {
         HIP_TRY(hipMemcpy(L, c->ps.L, n * sizeof(float4), hipMemcpyDeviceToHost));
         HIP_TRY(hipMemcpy(lambda, c->ps.lambda, n * sizeof(float4), hipMemcpyDeviceToHost));
@@ -1821,9 +1847,9 @@ int avr_last_pass_weights(avr_context *c, float *w, long long n_max) {
     if (c->filter_type == 0) {
         for (long long i = 0; i < n; ++i) w[i] = 1.f;   // BoxFilter::Sample weight
     } else if (n > 0 && c->last_persistent) {
-        std::vector<float4> rec(2 * (size_t)n);
-        HIP_TRY(hipMemcpy(rec.data(), c->ps.rec, 2 * n * sizeof(float4), hipMemcpyDeviceToHost));
-        for (long long i = 0; i < n; ++i) w[i] = rec[2 * i + 1].y;
+        std::vector<float4> cam1((size_t)n);
+        HIP_TRY(hipMemcpy(cam1.data(), c->ps.cam1, n * sizeof(float4), hipMemcpyDeviceToHost));
+        for (long long i = 0; i < n; ++i) w[i] = cam1[i].w;
     } else if (n > 0) {
         HIP_TRY(hipMemcpy(w, c->ps.weight, n * sizeof(float), hipMemcpyDeviceToHost));
     }
@@ -1907,12 +1933,14 @@ int avr_film_reduce_rccl(avr_context **ctxs, int n, int root) {
 #include "avr_graph_capi.hip"
 
 #ifdef AVR_PROFILE_SECTIONS
-// Variant builds only (not part of include/avr.h): read and clear the k_paths section cycles.
-extern "C" int avr_debug_sections(unsigned long long *out) {
-    HIP_TRY(hipDeviceSynchronize());
-    HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(avr::g_sections), 8 * sizeof(unsigned long long)));
-    unsigned long long z[8] = {};
-    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(avr::g_sections), z, sizeof(z)));
+// Variant builds only (not part of include/avr.h): read and clear the k_paths section cycles
+// of this context (stats[kNumStats .. kNumStats + 4], written by every k_paths unit).
+extern "C" int avr_debug_sections(avr_context *c, unsigned long long *out) {
+    if (!c || !out) return fail(AVR_ERR_ARG, "null argument");
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(hipMemcpy(out, c->d_stats + avr::kNumStats, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemset(c->d_stats + avr::kNumStats, 0, 8 * sizeof(unsigned long long)));
     return AVR_OK;
 }
 #endif

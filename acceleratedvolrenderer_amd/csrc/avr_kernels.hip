@@ -174,11 +174,14 @@ struct PathSoA {
     uint64_t *smp_state, *smp_inc;
     int *depth;
     float *weight;                    // per-sample filter weight (GaussianFilter only)
-    // k_paths' per-sample record, 32 B at 2*id: {L[4]} then {u_lambda, filter weight, 0, 0}
-    // (k_film re-derives the wavelengths from u_lambda); one 32-B sector per sample
+    // k_paths' per-sample record: L (16 B at id), written once at path end
     float4 *rec;
-    // RGBFilm's per-sample contribution {w * rgb, w} (k_film_rgb), summed by k_film_sum
-    float4 *contrib;
+    // k_paths' camera stage (k_paths_camera, one lane per sample of the pass), read by the
+    // refill and by k_film: cam0 {o, u}, cam1 {d, filter weight}, cam2 lambda, cam3 the first
+    // segment's RNG SetSequence arguments {seqA, seqB} (u64 each), cam4 the wavelength pdfs,
+    // cam5 the IndependentSampler's PCG32 {state, inc} after the camera draws
+    float4 *cam0, *cam1, *cam2, *cam4;
+    uint4 *cam3, *cam5;
 };
 struct ShadowSoA {
     int *path;
@@ -221,6 +224,7 @@ struct Params {
     int rec_mode;                     // k_film: 1 = read k_paths' records (ps.rec), 0 = wavefront SoA
     const int *sh_perm;               // k_shadow: processing order of the shadow queue (ray binning), or null
     int fast;                         // render mode: 0 replay (canonical math), 1 fast (hardware math)
+    int cam_quad;                     // k_paths_camera: ZSobol quads (pass aligned to 4 sample indices)
 };
 
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
@@ -793,6 +797,235 @@ __device__ __forceinline__ const float *stage_majorant(const DevMedium &m, float
     return lds;
 }
 
+// GaussianFilter's FilterSampler tables (pbrt's default radius 1.5: 48 x 48 function + CDFs,
+// ~19 KB) staged in LDS when they fit, so the camera sample's two binary searches run on LDS;
+// the descriptor pointing at them is published in *s_ftab. Returns after a block barrier.
+constexpr int kFiltLds = 4864;
+__device__ __forceinline__ void stage_filter(const Params &P, float *s_filt, smp::FilterTables *s_ftab) {
+    if (P.film.filter_type != 0) {
+        const smp::FilterTables &g = P.film.gauss;
+        const int nf = smp::filter_table_floats(g.nx, g.ny);
+        if (nf <= kFiltLds) {
+            const float *base = g.f;
+            for (int i = threadIdx.x; i < nf; i += blockDim.x) s_filt[i] = base[i];
+        }
+        if (threadIdx.x == 0) {
+            smp::FilterTables t = g;
+            if (nf <= kFiltLds) {
+                t.f = s_filt;
+                t.ccdf = s_filt + (g.ccdf - g.f);
+                t.cint = s_filt + (g.cint - g.f);
+                t.mcdf = s_filt + (g.mcdf - g.f);
+            }
+            *s_ftab = t;
+        }
+    }
+    __syncthreads();
+}
+
+// ZSobol draws shared by a QUAD of lanes holding samples 4m .. 4m+3 of one pixel (the camera
+// stage's layout): their Morton indices differ only in bits 0-1, so every base-4 digit's
+// permutation — MixBits of the index bits above the digit and the dimension, one 64-bit
+// multiply chain each — is the same for the four lanes. Lane q of the quad computes the
+// permutations of lower digits q and q + 4 only and the quad exchanges them by DPP quad_perm
+// broadcasts (no LDS); each lane applies them to its own digits. Same index, bit for bit, as
+// zsobol_lower (an odd log2(spp)'s base-2 digit depends on bit 1 and stays per lane).
+template <int J>
+__device__ __forceinline__ uint32_t quad_bcast(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, J * 0x55, 0xf, 0xf, false);
+}
+template <int J, typename M>
+__device__ __forceinline__ void quad_digit(M morton, const uint32_t (&mine)[2], int iLo, int iHi, int pw, uint32_t &idx) {
+    const int i = iLo + J;
+    const uint32_t p = quad_bcast<J & 3>(mine[J >> 2]);   // every lane of the quad executes it
+    if (i <= iHi) {
+        const int shift = 2 * i - pw;
+        idx |= smp::zperm(p, (uint32_t)(morton >> shift) & 3u) << shift;
+    }
+}
+template <typename M>
+__device__ __forceinline__ uint32_t zsobol_lower_quad(M morton, uint32_t dimension, const smp::ZSobolParams &zp) {
+    constexpr int kBits = 8 * (int)sizeof(M);
+    const int pw = zp.log2spp & 1;
+    const int iLo = pw, iHi = smp::zsobol_split(zp) - 1;   // at most 8 digits (log2 spp <= 16)
+    const int q = lane_id() & 3;
+    const uint32_t dmix = 0x55555555u * dimension;
+    uint32_t mine[2] = {0, 0};
+    _Pragma("unroll") for (int r = 0; r < 2; ++r) {
+        const int i = iLo + q + 4 * r;
+        if (i <= iHi) {
+            const int shift = 2 * i - pw;
+            const M higher = shift + 2 >= kBits ? M(0) : M(morton >> (shift + 2));
+            mine[r] = smp::mix_perm24<M>((M)(higher ^ (M)dmix));
+        }
+    }
+    uint32_t idx = 0;
+    quad_digit<0>(morton, mine, iLo, iHi, pw, idx);
+    quad_digit<1>(morton, mine, iLo, iHi, pw, idx);
+    quad_digit<2>(morton, mine, iLo, iHi, pw, idx);
+    quad_digit<3>(morton, mine, iLo, iHi, pw, idx);
+    if (iHi - iLo >= 4) {
+        quad_digit<4>(morton, mine, iLo, iHi, pw, idx);
+        quad_digit<5>(morton, mine, iLo, iHi, pw, idx);
+        quad_digit<6>(morton, mine, iLo, iHi, pw, idx);
+        quad_digit<7>(morton, mine, iLo, iHi, pw, idx);
+    }
+    if (pw) {   // the final base-2 digit (as zsobol_lower)
+        const uint32_t digit = (uint32_t)morton & 1u;
+        const M x = (M)(morton >> 1) ^ (M)dmix;
+        uint64_t v = (uint64_t)x;
+        v ^= v >> 31;
+        v *= 0x7fb5d329728ea185ull;
+        v ^= v >> 27;
+        v *= 0x81dadef4bc2dd44dull;
+        v ^= v >> 33;
+        idx |= digit ^ (uint32_t)(v & 1);
+    }
+    return idx;
+}
+// ZSobol::get1d / get2d with the quad-shared lower digits (kW: 1 32-bit, 2 64-bit index)
+template <int kW>
+__device__ __forceinline__ void zsobol_draw_quad(smp::ZSobol &z, const smp::ZSobolParams &zp, bool two, float *u0,
+                                                 float *u1) {
+    uint32_t a, ah = 0;
+    const uint32_t pm = kW == 2 ? (uint32_t)((((uint64_t)z.hi << 32) | z.morton) >> zp.log2spp) : z.morton >> zp.log2spp;
+    const uint32_t up = (zp.upper && (int)z.dimension < zp.dmax) ? zp.upper[(size_t)pm * (size_t)zp.dmax + z.dimension]
+                                                                   : smp::zsobol_upper(pm, z.dimension, zp);
+    if constexpr (kW == 2) {
+        const uint64_t m = ((uint64_t)z.hi << 32) | z.morton;
+        const uint64_t idx = ((uint64_t)up << zp.log2spp) | zsobol_lower_quad<uint64_t>(m, z.dimension, zp);
+        a = (uint32_t)idx;
+        ah = (uint32_t)(idx >> 32);
+    } else {
+        a = (up << zp.log2spp) | zsobol_lower_quad<uint32_t>(z.morton, z.dimension, zp);
+    }
+    z.dimension += two ? 2 : 1;
+    const uint64_t h = smp::hash_2u32(z.dimension, (uint32_t)zp.seed);
+    *u0 = smp::u32_to_unit(smp::fast_owen(smp::sobol_bits(a, 0), (uint32_t)h));
+    if (two) *u1 = smp::u32_to_unit(smp::fast_owen(smp::sobol_bits64(a, ah, 1), (uint32_t)(h >> 32)));
+}
+
+#ifndef AVR_KPATHS_TU
+// k_paths' camera stage — everything a path needs before its first medium segment, with one
+// lane per (pixel, sample) of the pass: the sampler's camera draws (wavelength 1D at dimension
+// 0, pixel 2D at 1, time and lens at 3..5 unused, the first segment's three 1D draws at 6..8:
+// RNG(Hash(u0), Hash(u1)) and the first free-flight u, integrators.cpp:984-989), the
+// wavelengths and their pdfs (canonical f64 sequences, or the hardware log in fast mode), the
+// filter sample (BoxFilter / GaussianFilter's FilterSampler), the camera ray
+// (cameras.cpp:284-306, 404-427) and its medium-interface entry. k_paths' refill then loads
+// 64 B per new path instead of running this per service round with most lanes idle, and
+// k_film reads the wavelengths, pdfs and filter weight instead of re-deriving them.
+// kSmp: 0 IndependentSampler, 2 / 3 ZSobolSampler with 32- / 64-bit indices.
+#ifndef AVR_CAM_EXPERIMENT
+#define AVR_CAM_EXPERIMENT 0
+#endif
+__device__ __forceinline__ float u32_to_unit_exp(uint32_t v) { return (float)(v >> 8) * 0x1p-24f; }
+#ifndef AVR_CAM_WAVES
+#define AVR_CAM_WAVES 1   // minimum waves per SIMD asked of k_paths_camera (1: the compiler's choice)
+#endif
+template <int kSmp, bool kFast>
+__global__ void __launch_bounds__(256, AVR_CAM_WAVES) k_paths_camera(Params P) {
+    __shared__ float s_filt[kFiltLds];
+    __shared__ smp::FilterTables s_ftab;
+    stage_filter(P, s_filt, &s_ftab);
+    const int npix = P.pass_pixels;
+    const long long n = (long long)npix * P.pass_samples;
+    // ZSobol quads (zsobol_draw_quad): lanes 4a .. 4a+3 take samples 4m .. 4m+3 of one pixel
+    // when the pass is quad-aligned (sample_base and pass_samples multiples of 4, log2 spp <=
+    // 16; the host sets P.cam_quad), so each store still writes 16 consecutive pixels per wave
+    const bool quad = kSmp != 0 && P.cam_quad;
+    for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < n; t += (long long)gridDim.x * blockDim.x) {
+        int pix, s;
+        if (quad) {
+            const long long qd = t >> 2;
+            pix = (int)(qd % npix);
+            s = (int)(qd / npix) * 4 + (int)(t & 3);
+        } else {
+            pix = (int)(t % npix);
+            s = (int)(t / npix);
+        }
+        const long long id = (long long)s * npix + pix;
+        const int px = pix % P.film.width, py = pix / P.film.width;
+        PathSampler<kSmp> smp;
+        if constexpr (kSmp == 0) {
+            const uint64_t seq = hash_3u32((uint32_t)px, (uint32_t)py, (uint32_t)P.seed);
+            smp.rng.set_sequence(seq, mix_bits(seq));
+            // == rng.Advance((sample_base + s) * 65536) (rng.h:132-146), precomputed (k_advance)
+            smp.rng.state = P.advance[2 * s] * smp.rng.state + smp.rng.inc * P.advance[2 * s + 1];
+        } else {
+            smp.start(P, px, py, P.sample_base + s);
+        }
+        // the sampler's draws: a ZSobol quad shares its digit permutations
+        auto get1 = [&]() -> float {
+#if AVR_CAM_EXPERIMENT == 2   // measurement only: no sampler work (breaks replay)
+            static_assert(kSmp >= 0, "");
+            if constexpr (kSmp != 0) return u32_to_unit_exp((uint32_t)(id * 2654435761u + smp.z.dimension++ * 40503u));
+#endif
+            if constexpr (kSmp != 0) {
+                if (quad) {
+                    float a, b;
+                    zsobol_draw_quad<PathSampler<kSmp>::kW>(smp.z, P.zs, false, &a, &b);
+                    return a;
+                }
+            }
+            return smp.get1d(P);
+        };
+        const float ulam = get1();
+#if AVR_CAM_EXPERIMENT == 1   // measurement only: wavelengths without transcendentals (breaks replay)
+        const Spec lam = {360 + 470 * ulam, 360 + 470 * (1 - ulam), 400 + 400 * ulam, 600 - 200 * ulam};
+        const Spec pdf = Spec::c(1.f / 470);
+#else
+        const Spec lam = kFast ? film_sample_lambda_fast(P.film, ulam) : film_sample_lambda(P.film, ulam);
+        const Spec pdf = {film_lambda_pdf(P.film, lam.v0), film_lambda_pdf(P.film, lam.v1),
+                          film_lambda_pdf(P.film, lam.v2), film_lambda_pdf(P.film, lam.v3)};
+#endif
+        float pFilmX, pFilmY, fweight;
+        if constexpr (kSmp != 0) {
+            float fu0, fu1;
+#if AVR_CAM_EXPERIMENT == 2
+            fu0 = get1();
+            fu1 = get1();
+#else
+            if (quad) zsobol_draw_quad<PathSampler<kSmp>::kW>(smp.z, P.zs, true, &fu0, &fu1);
+            else smp.get2d(P, &fu0, &fu1);
+#endif
+            camera_filter(P, px, py, fu0, fu1, &pFilmX, &pFilmY, &fweight, &s_ftab);
+            smp.z.dimension += 3;   // time (1D) and lens (2D): drawn by pbrt, unused by pinholes
+        } else {
+            camera_sample(P, smp, px, py, &pFilmX, &pFilmY, &fweight, &s_ftab);
+        }
+        const float *r = P.cam.raster;
+        V3 pCam = {r[0] * pFilmX + r[1] * pFilmY + r[2] * 0.f + r[3], r[4] * pFilmX + r[5] * pFilmY + r[6] * 0.f + r[7],
+                   r[8] * pFilmX + r[9] * pFilmY + r[10] * 0.f + r[11]};
+        const float wp = r[12] * pFilmX + r[13] * pFilmY + r[14] * 0.f + r[15];
+        if (wp != 1) pCam = pCam / wp;
+        Ray ray;
+        if (P.cam.type == 0) ray = {pCam, {0.f, 0.f, 1.f}};
+        else ray = {{0.f, 0.f, 0.f}, normalize(pCam)};
+        ray = xf_ray(P.cam.render_from_camera, ray, nullptr, /*forward=*/true);
+        const V3 o = P.med.boundary ? interface_entry(P.med, ray.o, ray.d) : ray.o;
+        // first medium segment: RNG from two sampler dims, u from a third (984-989)
+        const float h0 = get1();
+        const float h1 = get1();
+        const float u = get1();
+        const uint64_t seqA = hash_u32(f2u(h0)), seqB = hash_u32(f2u(h1));
+        // ZSobol: the first scatter's light-pick draw (dimension 9) ahead of time (k_paths' NEE
+        // handler reads it instead of evaluating the sampler for its lanes)
+        const float ulight = kSmp != 0 ? get1() : 0.f;
+        P.ps.cam0[id] = make_float4(o.x, o.y, o.z, u);
+        P.ps.cam1[id] = make_float4(ray.d.x, ray.d.y, ray.d.z, fweight);
+        P.ps.cam2[id] = to4(lam);
+        P.ps.cam3[id] = make_uint4((uint32_t)seqA, (uint32_t)(seqA >> 32), (uint32_t)seqB, (uint32_t)(seqB >> 32));
+        P.ps.cam4[id] = to4(pdf);
+        if constexpr (kSmp == 0)
+            P.ps.cam5[id] = make_uint4((uint32_t)smp.rng.state, (uint32_t)(smp.rng.state >> 32), (uint32_t)smp.rng.inc,
+                                       (uint32_t)(smp.rng.inc >> 32));
+        else
+            P.ps.cam5[id] = make_uint4(f2u(ulight), 0u, 0u, 0u);
+    }
+}
+#endif
+
 // ---------------------------------------------------------------------------
 // Camera rays — RayIntegrator::EvaluatePixelSample (cpu/integrators.cpp:235-268),
 // GetCameraSample (samplers.h:797-815), BoxFilter::Sample (filters.h:67-70),
@@ -1313,6 +1546,9 @@ __global__ void __launch_bounds__(256) k_bin_scatter(const int *__restrict__ que
 #ifndef AVR_COOP_SPEC
 #define AVR_COOP_SPEC 1
 #endif
+#ifndef AVR_NEE_AHEAD
+#define AVR_NEE_AHEAD 1
+#endif
 #ifndef AVR_PATHS_WAVES_SPEC
 #define AVR_PATHS_WAVES_SPEC 2   // 4-wavelength state: ~220 VGPRs without scratch
 #endif
@@ -1359,9 +1595,11 @@ __device__ __forceinline__ Spec smul(const Spec &a, const Spec &b) { return a * 
 
 // Section profiling (variant builds with -DAVR_PROFILE_SECTIONS only; tools/section_profile.py):
 // per wave, s_memtime cycles spent in {event handlers, refill, segment starts, DDA walk,
-// collision (exact candidate, fetch, callback)} summed into g_sections.
+// collision (exact candidate, fetch, callback)} summed into the context's section counters.
 #ifdef AVR_PROFILE_SECTIONS
-__device__ unsigned long long g_sections[8];
+// the cycles land in stats[kNumStats .. kNumStats + 4] (the context allocates kNumStats + 8
+// counters): one buffer shared by every k_paths translation unit, unlike a __device__ global
+// (each separately compiled unit would hold its own copy)
 struct SecProf {
     unsigned long long acc[5] = {0, 0, 0, 0, 0};
     unsigned long long last = 0;
@@ -1374,15 +1612,15 @@ struct SecProf {
         last = t;
         cur = next;
     }
-    __device__ __forceinline__ void flush() {
+    __device__ __forceinline__ void flush(unsigned long long *stats) {
         mark(0);
         if (lane_id() == 0)
-            for (int i = 0; i < 5; ++i) atomicAdd(&g_sections[i], acc[i]);
+            for (int i = 0; i < 5; ++i) atomicAdd(&stats[kNumStats + i], acc[i]);
     }
 };
 #define AVR_SEC_INIT SecProf secp; secp.last = clock64();
 #define AVR_SEC(i) secp.mark(i);
-#define AVR_SEC_FLUSH secp.flush();
+#define AVR_SEC_FLUSH secp.flush(P.stats);
 #else
 #define AVR_SEC_INIT
 #define AVR_SEC(i)
@@ -1412,40 +1650,11 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
     // ImageInfiniteLight shadow rays (non-delta NEE): the sampled (u, v), p_l and the phase
     // value per lane, parked here while the lane traces its shadow ray (off the VGPR budget)
     __shared__ float4 s_img[kImage ? 256 : 1];
-    // per lane: the camera sample's wavelength u and filter weight, parked here until the
-    // path ends and its 32-B record is written (off the VGPR budget)
-    __shared__ float2 s_rec[256];
     // ZSobol: the requesters' sampler state for the cooperative draws (coop_draws), 64 per wave
     __shared__ uint3 s_zst[kSmp != 0 ? 256 : 1];
-    // the camera (cameraFromRaster, renderFromCamera: 28 floats used only by the refill), read
-    // from LDS there instead of occupying kernel-argument SGPRs for the whole kernel
-    __shared__ DevCamera s_cam;
-    if (threadIdx.x == 0) s_cam = P.cam;
-    // GaussianFilter's FilterSampler tables (pbrt's default radius 1.5: 48 x 48 function +
-    // CDFs, ~19 KB) staged here when they fit: the camera-ray refill's two binary searches
-    // then run on LDS instead of dependent L2 loads
-    constexpr int kFiltLds = 4864;
-    __shared__ float s_filt[kFiltLds];
-    // the table descriptor itself also lives in LDS (read by the refill only)
-    __shared__ smp::FilterTables s_ftab;
-    if (P.film.filter_type != 0) {
-        const smp::FilterTables &g = P.film.gauss;
-        const int nf = smp::filter_table_floats(g.nx, g.ny);
-        if (nf <= kFiltLds) {
-            const float *base = g.f;
-            for (int i = threadIdx.x; i < nf; i += blockDim.x) s_filt[i] = base[i];
-        }
-        if (threadIdx.x == 0) {
-            smp::FilterTables t = g;
-            if (nf <= kFiltLds) {
-                t.f = s_filt;
-                t.ccdf = s_filt + (g.ccdf - base_of(g));
-                t.cint = s_filt + (g.cint - base_of(g));
-                t.mcdf = s_filt + (g.mcdf - base_of(g));
-            }
-            s_ftab = t;
-        }
-    }
+    // ZSobol: each lane's next light-pick draw (SampleLd's 1D, integrators.cpp:1302), evaluated
+    // ahead with the previous bounce's cooperative phase draws (or by the camera stage)
+    __shared__ float s_ul[kSmp != 0 ? 256 : 1];
     // the host routes GridMedium majorant grids of more than 4096 cells to the wavefront kernels
     if constexpr (!kVdb) stage_majorant(P.med, s_maj);
     const float *__restrict__ majp = kVdb ? P.med.majorant : s_maj;
@@ -1489,6 +1698,8 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
     // cooperative ZSobol draws (coop_draws) in the phase handler and the refill; the
     // 4-wavelength instantiations may opt out (AVR_COOP_SPEC=0: per-lane draws as pbrt does)
     constexpr bool kCoop = kZSobol && (kGray || AVR_COOP_SPEC);
+    // the next light-pick draw evaluated ahead with the phase draws (s_ul)
+    constexpr bool kUlAhead = kCoop && AVR_NEE_AHEAD;
     PathSampler<kSmp> smp{};
     int depth = 0;
     V3 po{}, pd{};         // segment origin (== the path vertex) and the path's ray direction
@@ -1523,7 +1734,13 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
             if (ev == EV_SCATTER) {
                 // SampleLd: light pick (BVH infinite-light branch) + shadow-ray spawn (1282-1338)
                 const V3 wo = -pd;
-                const float ul = smp.get1d(P);
+                float ul;
+                if constexpr (kUlAhead) {
+                    ul = s_ul[threadIdx.x];   // drawn ahead (same sampler dimension)
+                    smp.z.dimension += 1;
+                } else {
+                    ul = smp.get1d(P);
+                }
                 float uL0 = 0.f, uL1 = 0.f;
                 // uLight: read by the image light only; the other instantiations just step the
                 // ZSobol dimension past it (the independent sampler's PCG32 still draws twice)
@@ -1622,12 +1839,24 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
         if (__ballot(ev == EV_PHASE)) {
             // ZSobol: the phase 2D draw and the next segment's three 1D draws of every lane in
             // EV_PHASE, evaluated cooperatively by the whole wave
-            float q0[4], q1[4];
-            if constexpr (kCoop) {
+            // (and, at offset 5, the next bounce's light-pick draw, parked in s_ul)
+            float q0[5], q1[5];
+            if constexpr (kUlAhead) {
+                constexpr int off[5] = {0, 2, 3, 4, 5};
+                constexpr bool two[5] = {true, false, false, false, false};
+                coop_draws<PathSampler<kSmp>::kW, 5>(smp.z, P.zs, ev == EV_PHASE, off, two, 5, q0, q1,
+                                                     s_zst + (threadIdx.x & ~63u));
+                if (ev == EV_PHASE) s_ul[threadIdx.x] = q0[4];
+            } else if constexpr (kCoop) {
                 constexpr int off[4] = {0, 2, 3, 4};
                 constexpr bool two[4] = {true, false, false, false};
-                coop_draws<PathSampler<kSmp>::kW, 4>(smp.z, P.zs, ev == EV_PHASE, off, two, 5, q0, q1,
+                float r0[4], r1[4];
+                coop_draws<PathSampler<kSmp>::kW, 4>(smp.z, P.zs, ev == EV_PHASE, off, two, 5, r0, r1,
                                                      s_zst + (threadIdx.x & ~63u));
+                _Pragma("unroll") for (int j = 0; j < 4; ++j) {
+                    q0[j] = r0[j];
+                    q1[j] = r1[j];
+                }
             }
             if (ev == EV_PHASE) {
                 // phase-function sampling (integrators.cpp:1046-1061), then the next segment
@@ -1689,11 +1918,8 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
         }
         if (__ballot(ev == EV_END)) {
             if (ev == EV_END) {
-                // the 32-B per-sample record: L, then {u_lambda, filter weight}
-                float4 *rp = P.ps.rec + 2 * (size_t)g;
-                const float2 q = s_rec[threadIdx.x];
-                rp[0] = to4(L);
-                rp[1] = make_float4(q.x, q.y, 0.f, 0.f);
+                // the per-sample record: L (k_film takes the rest from the camera stage)
+                P.ps.rec[g] = to4(L);
                 mode = M_FETCH;
                 ev = EV_NONE;
             }
@@ -1729,57 +1955,29 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
             const uint64_t lt = lane == 0 ? 0ull : (needMask & ((~0ull) >> (64 - lane)));
             const int k = __popcll(lt);
             const bool fresh = mode == M_FETCH && k < granted;
-            int px = 0, py = 0, sIdx = 0;
-            if (fresh) {
-                g = (int)(base + k);
-                const int pix = g % npix;
-                sIdx = g / npix;
-                px = pix % P.film.width;
-                py = pix / P.film.width;
-                if constexpr (kZSobol) smp.start(P, px, py, P.sample_base + sIdx);
-            }
-            // ZSobol: the camera sample's draws (wavelength 1D at dimension 0, pixel 2D at 1;
-            // time and lens at 3..5 are unused) and the first segment's three 1D draws (6..8)
-            // of every new sample, evaluated cooperatively by the whole wave
-            float c0[5], c1[5];
-            if constexpr (kCoop) {
-                constexpr int off[5] = {0, 1, 6, 7, 8};
-                constexpr bool two[5] = {false, true, false, false, false};
-                coop_draws<PathSampler<kSmp>::kW, 5>(smp.z, P.zs, fresh, off, two, 9, c0, c1,
-                                                     s_zst + (threadIdx.x & ~63u));
-            }
             if (mode == M_FETCH) {
                 if (fresh) {
                     ++nPaths;
-                    // ---- camera ray (EvaluatePixelSample, integrators.cpp:235-268) ----
-                    if constexpr (!kZSobol) {
-                        const uint64_t seq = hash_3u32((uint32_t)px, (uint32_t)py, (uint32_t)P.seed);
-                        smp.rng.set_sequence(seq, mix_bits(seq));
-                        // == rng.Advance((sample_base + sIdx) * 65536) (rng.h:132-146), precomputed
-                        smp.rng.state = P.advance[2 * sIdx] * smp.rng.state + smp.rng.inc * P.advance[2 * sIdx + 1];
+                    // ---- a new path from the camera stage (k_paths_camera) ----
+                    g = (int)(base + k);
+                    const float4 c0 = P.ps.cam0[g], c1 = P.ps.cam1[g], c2 = P.ps.cam2[g];
+                    const uint4 c3 = P.ps.cam3[g];
+                    if constexpr (kZSobol) {
+                        const int pix = g % npix, sIdx = g / npix;
+                        smp.start(P, pix % P.film.width, pix / P.film.width, P.sample_base + sIdx);
+                        smp.z.dimension = 9;   // past the camera draws and the first segment's three
+                        if constexpr (kUlAhead) s_ul[threadIdx.x] = __uint_as_float(P.ps.cam5[g].x);
+                    } else {
+                        const uint4 c5 = P.ps.cam5[g];
+                        smp.rng.state = ((uint64_t)c5.y << 32) | c5.x;
+                        smp.rng.inc = ((uint64_t)c5.w << 32) | c5.z;
                     }
-                    const float ulam = kCoop ? c0[0] : smp.get1d(P);
-                    // wavelengths (pdf: recomputed by k_film from the record's u_lambda)
-                    lam = kFast ? film_sample_lambda_fast(P.film, ulam) : film_sample_lambda(P.film, ulam);
-                    float pFilmX, pFilmY, fweight;
-                    if constexpr (kCoop)
-                        camera_filter(P, px, py, c0[1], c1[1], &pFilmX, &pFilmY, &fweight, &s_ftab);
-                    else
-                        camera_sample(P, smp, px, py, &pFilmX, &pFilmY, &fweight, &s_ftab);
-                    s_rec[threadIdx.x] = make_float2(ulam, fweight);
-                    const DevCamera &cam = s_cam;
-                    const float *r = cam.raster;
-                    V3 pCam = {r[0] * pFilmX + r[1] * pFilmY + r[2] * 0.f + r[3],
-                               r[4] * pFilmX + r[5] * pFilmY + r[6] * 0.f + r[7],
-                               r[8] * pFilmX + r[9] * pFilmY + r[10] * 0.f + r[11]};
-                    const float wp = r[12] * pFilmX + r[13] * pFilmY + r[14] * 0.f + r[15];
-                    if (wp != 1) pCam = pCam / wp;
-                    Ray ray;
-                    if (cam.type == 0) ray = {pCam, {0.f, 0.f, 1.f}};
-                    else ray = {{0.f, 0.f, 0.f}, normalize(pCam)};
-                    ray = xf_ray(cam.render_from_camera, ray, nullptr, /*forward=*/true);
-                    po = m.boundary ? interface_entry(m, ray.o, ray.d) : ray.o;
-                    pd = ray.d;
+                    po = {c0.x, c0.y, c0.z};
+                    u = c0.w;
+                    pd = {c1.x, c1.y, c1.z};
+                    lam = spec4(c2);
+                    seqA = ((uint64_t)c3.y << 32) | c3.x;
+                    seqB = ((uint64_t)c3.w << 32) | c3.z;
                     L = Spec::c(0.f);
                     beta = r_u = r_l = sconst<S>(1.f);
                     depth = 0;
@@ -1789,12 +1987,6 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
                         sig_s = sfrom<S>(sample_table(tab_ss, li));
                         if (kEmissive && (kMed == 0 || kMed == 1)) Le_l = sample_table(m.Le, li);
                     }
-                    // first medium segment: RNG from two sampler dims, u from a third (984-989)
-                    const float h0 = kCoop ? c0[2] : smp.get1d(P);
-                    const float h1 = kCoop ? c0[3] : smp.get1d(P);
-                    seqA = hash_u32(f2u(h0));
-                    seqB = hash_u32(f2u(h1));
-                    u = kCoop ? c0[4] : smp.get1d(P);
                     sd = pd;
                     segPending = true;
                     mode = M_MEDIUM;
@@ -2037,27 +2229,27 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
 // SpectralFilm: a pixel's bucket sums (up to kFilmLdsBuckets of them) are accumulated in this
 // thread's LDS slice and written back once per pass — the same fp64 additions in the same
 // order as the read-modify-writes on HBM, without their 2 x 4 dependent round trips per sample.
-// One sample of the pass: L, the wavelengths and CameraSample::filterWeight, from k_paths'
-// 32-B record (L, {u_lambda, weight}: the wavelengths re-derived from u_lambda with the
-// function k_paths sampled them with) or the wavefront SoA
-__device__ __forceinline__ void film_load_sample(const Params &P, size_t id, Spec *L, Spec *lam, float *w) {
+// One sample of the pass: L, the wavelengths, their pdfs and CameraSample::filterWeight —
+// after k_paths: L from its record, the rest from its camera stage (k_paths_camera); after the
+// wavefront kernels: their SoA (pdfs recomputed with the sampling function's pdf)
+__device__ __forceinline__ void film_load_sample(const Params &P, size_t id, Spec *L, Spec *lam, Spec *pdf, float *w) {
     *w = 1.f;
     if (P.rec_mode) {
-        const float4 r0 = P.ps.rec[2 * id], r1 = P.ps.rec[2 * id + 1];
-        *L = spec4(r0);
-        *lam = P.fast ? film_sample_lambda_fast(P.film, r1.x) : film_sample_lambda(P.film, r1.x);
-        if (P.film.filter_type != 0) *w = r1.y;
+        *L = spec4(P.ps.rec[id]);
+        *lam = spec4(P.ps.cam2[id]);
+        *pdf = spec4(P.ps.cam4[id]);
+        if (P.film.filter_type != 0) *w = P.ps.cam1[id].w;
     } else {
         *L = spec4(P.ps.L[id]);
         *lam = spec4(P.ps.lambda[id]);
+        *pdf = {film_lambda_pdf(P.film, lam->v0), film_lambda_pdf(P.film, lam->v1), film_lambda_pdf(P.film, lam->v2),
+                film_lambda_pdf(P.film, lam->v3)};
         if (P.film.filter_type != 0) *w = P.ps.weight[id];
     }
 }
 // The NaN/Inf guard (integrators.cpp:272-282; a bad sample's L becomes 0, in place) and
 // PixelSensor::ToSensorRGB with RGBFilm's maxComponentValue clamp (film.h:95-100, 239-250)
-__device__ __forceinline__ void film_sensor_rgb(const Params &P, Spec &L, const Spec &lam, float rgb[3]) {
-    const Spec pdf = {film_lambda_pdf(P.film, lam.v0), film_lambda_pdf(P.film, lam.v1),
-                      film_lambda_pdf(P.film, lam.v2), film_lambda_pdf(P.film, lam.v3)};
+__device__ __forceinline__ void film_sensor_rgb(const Params &P, Spec &L, const Spec &lam, const Spec &pdf, float rgb[3]) {
     const LambdaIdx li = lambda_index(lam);
     bool bad = __builtin_isnan(L.v0) || __builtin_isnan(L.v1) || __builtin_isnan(L.v2) || __builtin_isnan(L.v3);
     if (!bad) {
@@ -2071,41 +2263,6 @@ __device__ __forceinline__ void film_sensor_rgb(const Params &P, Spec &L, const 
     float mx = fmaxf_(fmaxf_(rgb[0], rgb[1]), rgb[2]);
     if (mx > P.film.max_component)
         for (int c = 0; c < 3; ++c) rgb[c] *= P.film.max_component / mx;
-}
-
-// RGBFilm after k_paths, in two steps. k_film_rgb: one lane per SAMPLE converts k_paths'
-// record to its film contribution {w * rgb, w} (the f64 canonical wavelength and pdf
-// sequences have the whole pass of lanes to hide their latency, instead of one lane walking a
-// pixel's samples); k_film_sum: per pixel, the fp64 sums in sampleIndex order — the same
-// float products added in the same order as k_film, so the film is bit-identical.
-__global__ void __launch_bounds__(256) k_film_rgb(Params P) {
-    const long long n = (long long)P.pass_pixels * P.pass_samples;
-    for (long long id = blockIdx.x * (long long)blockDim.x + threadIdx.x; id < n; id += (long long)gridDim.x * blockDim.x) {
-        Spec L, lam;
-        float w;
-        film_load_sample(P, (size_t)id, &L, &lam, &w);
-        float rgb[3];
-        film_sensor_rgb(P, L, lam, rgb);
-        P.ps.contrib[id] = make_float4(w * rgb[0], w * rgb[1], w * rgb[2], w);
-    }
-}
-__global__ void __launch_bounds__(256) k_film_sum(Params P) {
-    const int npix = P.pass_pixels;
-    for (int pix = blockIdx.x * blockDim.x + threadIdx.x; pix < npix; pix += gridDim.x * blockDim.x) {
-        double s0 = P.film.rgb_sum[3 * (size_t)pix], s1 = P.film.rgb_sum[3 * (size_t)pix + 1],
-               s2 = P.film.rgb_sum[3 * (size_t)pix + 2], ws = P.film.w_sum[pix];
-        for (int s = 0; s < P.pass_samples; ++s) {
-            const float4 c = P.ps.contrib[(size_t)s * npix + pix];
-            s0 += (double)c.x;
-            s1 += (double)c.y;
-            s2 += (double)c.z;
-            ws += (double)c.w;
-        }
-        P.film.rgb_sum[3 * (size_t)pix] = s0;
-        P.film.rgb_sum[3 * (size_t)pix + 1] = s1;
-        P.film.rgb_sum[3 * (size_t)pix + 2] = s2;
-        P.film.w_sum[pix] = ws;
-    }
 }
 
 constexpr int kFilmLdsBuckets = 16;
@@ -2132,11 +2289,11 @@ __global__ void __launch_bounds__(256) k_film(Params P) {
         }
         for (int s = 0; s < P.pass_samples; ++s) {
             const size_t id = (size_t)s * npix + pix;
-            Spec L, lam;
+            Spec L, lam, pdf;
             float w;
-            film_load_sample(P, id, &L, &lam, &w);
+            film_load_sample(P, id, &L, &lam, &pdf, &w);
             float rgb[3];
-            film_sensor_rgb(P, L, lam, rgb);
+            film_sensor_rgb(P, L, lam, pdf, rgb);
             s0 += (double)(w * rgb[0]);
             s1 += (double)(w * rgb[1]);
             s2 += (double)(w * rgb[2]);
@@ -2326,6 +2483,18 @@ __global__ void __launch_bounds__(256) k_vdb_apron(vdb::Grid base, const long lo
         const int ex = (int)(e % ne_x), ey = (int)((e / ne_x) % ne_y), ez = (int)(e / ((long long)ne_x * ne_y));
         for (int k = threadIdx.x; k < vdb::kApronVals; k += blockDim.x)
             out[i * vdb::kApronVals + k] = vdb::apron_value(base, ex, ey, ez, k);
+    }
+}
+
+// The fat copy of a NanoVDB density grid's apron blocks (vdb::Apron::fat): entry (block i,
+// base voxel k) = the eight stencil taps of apron_fat_entry as two float4
+__global__ void __launch_bounds__(256) k_vdb_fat(const float *__restrict__ blocks, long long n, float4 *__restrict__ fat) {
+    const long long total = n * 512;
+    for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total; e += (long long)gridDim.x * blockDim.x) {
+        float t[8];
+        vdb::apron_fat_entry(blocks, e >> 9, (int)(e & 511), t);
+        fat[2 * e] = make_float4(t[0], t[1], t[2], t[3]);
+        fat[2 * e + 1] = make_float4(t[4], t[5], t[6], t[7]);
     }
 }
 

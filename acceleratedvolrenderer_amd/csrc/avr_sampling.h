@@ -115,6 +115,9 @@ AVR_HD bool zsobol_wide(const ZSobolParams &zp) { return zp.nBase4Digits > 16; }
 // pieces: 2^32 = 16 (mod 24). M = 32-bit: x zero-extended, so v ^= v >> 31 is done in 32 bits.
 template <typename M>
 AVR_HD uint32_t mix_perm24(M x) {
+    // a 64-bit prefix below 2^32 mixes exactly as its 32-bit value (x >> 31 < 2 either way): the
+    // sample digits of indices up to 34 bits (e.g. 4096 spp at 720p) keep the 32-bit multiplies
+    if (sizeof(M) == 8 && ((uint64_t)x >> 32) == 0) return mix_perm24<uint32_t>((uint32_t)x);
     uint64_t v = sizeof(M) == 4 ? (uint64_t)(uint32_t)(x ^ (x >> 31)) : ((uint64_t)x ^ ((uint64_t)x >> 31));
     v *= 0x7fb5d329728ea185ull;
     v ^= v >> 27;

@@ -134,7 +134,26 @@ struct Apron {
     float background;
     float inv[9];
     float vec[3];
+    // optional "fat" copy (the density grid's, like GridMedium's): per apron block, for each of
+    // its 8^3 base voxels the eight stencil taps as 32 contiguous bytes (8 floats in
+    // apron_fat_entry's order), so a lookup after the slot read is ONE 32-B access
+    const float *fat;
 };
+
+// The fat entry of base voxel k = (x*8 + y)*8 + z of apron block i: the stencil taps
+// v000 v001 v010 v011 | v100 v101 v110 v111 (digits = x, y, z offsets), as sample_trilinear
+// reads them from the 9^3 block
+AVR_HD void apron_fat_entry(const float *blocks, long long i, int k, float out[8]) {
+    const float *b = blocks + i * kApronVals + (k >> 6) * (kApron * kApron) + ((k >> 3) & 7) * kApron + (k & 7);
+    out[0] = b[0];
+    out[1] = b[1];
+    out[2] = b[kApron];
+    out[3] = b[kApron + 1];
+    out[4] = b[kApron * kApron];
+    out[5] = b[kApron * kApron + 1];
+    out[6] = b[kApron * kApron + kApron];
+    out[7] = b[kApron * kApron + kApron + 1];
+}
 
 // getValue(x, y, z) from the apron layout (every voxel of the base extent lies in its own
 // block's apron; outside the extended range: background)
@@ -162,6 +181,16 @@ AVR_HD float sample_trilinear(const Apron &g, float x, float y, float z) {
         const int s = g.slot[((long long)ez * (g.lny + 1) + ey) * (g.lnx + 1) + ex];
         if (s < 0) {
             v000 = v001 = v010 = v011 = v100 = v101 = v110 = v111 = g.consts[-s - 1];
+        } else if (g.fat) {
+            const float *f = g.fat + ((long long)s * 512 + ((rx & 7) << 6) + ((ry & 7) << 3) + (rz & 7)) * 8;
+#if defined(__HIP_DEVICE_COMPILE__)
+            const float4 lo = *reinterpret_cast<const float4 *>(f), hi = *reinterpret_cast<const float4 *>(f + 4);
+            v000 = lo.x; v001 = lo.y; v010 = lo.z; v011 = lo.w;
+            v100 = hi.x; v101 = hi.y; v110 = hi.z; v111 = hi.w;
+#else
+            v000 = f[0]; v001 = f[1]; v010 = f[2]; v011 = f[3];
+            v100 = f[4]; v101 = f[5]; v110 = f[6]; v111 = f[7];
+#endif
         } else {
             const float *b = g.blocks + (long long)s * kApronVals + (rx & 7) * (kApron * kApron) + (ry & 7) * kApron +
                              (rz & 7);

@@ -61,6 +61,8 @@ const char *avr_last_error(void);
  * kernel, whose per-path HBM state is one 32-B sample record, 16M for the wavefront
  * kernels; at most 2^31 - 1: path ids are 32-bit, AVR_ERR_ARG above). */
 int avr_context_create(int device, long long max_paths, avr_context **out);
+/* Also releases the RCCL communicators the context shares with the other contexts of its
+ * last avr_film_reduce_rccl list (see there: not concurrently with work on those contexts). */
 int avr_context_destroy(avr_context *ctx);
 /* Kernel organisation: 0 = persistent-wave megakernel k_paths (default: path state in
  * VGPRs, ballot-based lane refill), 1 = wavefront kernels k_camera/k_medium/k_shadow with
@@ -104,11 +106,13 @@ int avr_set_refill_min(avr_context *ctx, int lanes);
  * NanoVDB's 64^3 — measured optima); bounds the divergence of the DDA walk. No effect on
  * results. */
 int avr_set_dda_budget(avr_context *ctx, int cells);
-/* Density layout for the NEXT avr_medium_grid* call: 1 (default) also builds a "fat"
- * footprint copy — entry (ix,iy,iz) holds the 8 trilinear taps as 32 contiguous bytes,
- * (n+1)^3 x 32 B, built on device if it fits in free HBM with 8 GiB to spare — so a
- * density fetch is one 32-B access in one cache line; 0 keeps only pbrt's linear layout
- * (containers.h:834). Results are bit-identical either way. */
+/* Density layout for the NEXT avr_medium_grid* / avr_medium_nanovdb call: 1 (default) also
+ * builds a "fat" footprint copy — GridMedium: entry (ix,iy,iz) holds the 8 trilinear taps as
+ * 32 contiguous bytes, (n+1)^3 x 32 B; NanoVDBMedium: the same 32 B per base voxel of every
+ * 9^3 apron block of the density grid (512 x 32 B per block) — built on device if it fits in
+ * free HBM with 8 GiB to spare, so a density fetch is one 32-B access in one cache line; 0
+ * keeps only pbrt's linear layout (containers.h:834) / the apron blocks. Results are
+ * bit-identical either way. */
 int avr_set_grid_layout(avr_context *ctx, int layout);
 /* 1 if the current medium uses the fat layout, else 0. */
 int avr_grid_layout_active(avr_context *ctx);
@@ -326,7 +330,11 @@ int avr_film_spectral_device_ptrs(avr_context *ctx, void **d_bucket_sums, void *
  * buckets) into ctxs[root]'s film over RCCL (xGMI); the other films are left as they are.
  * Films must match in resolution and buckets; one context per device. The communicators
  * are created on the first reduce of a context list (ncclCommInitAll) and cached on the
- * contexts for later reduces of the same list; avr_context_destroy releases them. */
+ * contexts for later reduces of the same list; avr_context_destroy releases them.
+ * Threading: the cached communicators tie the listed contexts together. Destroying one of
+ * them, or reducing over a different list that contains one of them, destroys the whole
+ * group's communicators; neither may run while another thread renders, reduces or reads on
+ * any context of that group (calls on one context are serialized by the caller anyway). */
 int avr_film_reduce_rccl(avr_context **ctxs, int n, int root);
 /* Device pointers of the film sums (for an RCCL reduce across GPUs). */
 int avr_film_device_ptrs(avr_context *ctx, void **d_rgb_sum, void **d_w_sum);

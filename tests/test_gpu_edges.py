@@ -138,6 +138,13 @@ def test_zsobol_64bit_indices_replay_and_range_is_checked(kernel):
     with pytest.raises(RuntimeError, match="2\\^52"):
         integ.ctx.render(0, 1, 0, 1)
     integ.close()
+    # a film whose rounded-up resolution exceeds 65536: Morton(pixel) needs more than the 32
+    # bits of the pixel-digit table and of zsobol_upper, so the render is refused
+    wide = Scene(base.camera, _scene(70000, 1, dens).film, base.medium, base.lights, sampler=ZSobolSampler(1))
+    integ = VolPathIntegrator(wide, device=0, maxdepth=1, spp=1, kernel=kernel)
+    with pytest.raises(RuntimeError, match="65536"):
+        integ.ctx.render(0, 1, 0, 1)
+    integ.close()
 
 
 @pytest.mark.parametrize("kernel", ["persistent", "wavefront"])

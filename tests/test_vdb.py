@@ -163,7 +163,7 @@ def hdr(tmp_path_factory):
         # k_vdb_apron build it on the device
         'extern "C" long long sample_apron(const int *slot, const float *leaves, const float *tiles, int ntiles,\n'
         "                       const int *o, const int *nb, float bg, const float *inv, const float *vec, int n,\n"
-        "                       const float *p, float *out, float *vals) {\n"
+        "                       const float *p, float *out, float *vals, int fat) {\n"
         "  Grid g{slot, leaves, tiles, o[0], o[1], o[2], nb[0], nb[1], nb[2], bg};\n"
         "  std::vector<int> aslot; std::vector<long long> list;\n"
         "  build_apron_slots(slot, nb[0], nb[1], nb[2], tiles, ntiles, bg, aslot, list);\n"
@@ -177,6 +177,9 @@ def hdr(tmp_path_factory):
         "  Apron a{aslot.data(), blocks.data(), consts.data(), o[0], o[1], o[2], nb[0], nb[1], nb[2], bg};\n"
         "  for (int k = 0; k < 9; ++k) a.inv[k] = inv[k];\n"
         "  for (int k = 0; k < 3; ++k) a.vec[k] = vec[k];\n"
+        "  std::vector<float> fatv(fat ? list.size() * 512 * 8 : 0);\n"
+        "  for (long long e = 0; e < (long long)fatv.size() / 8; ++e) apron_fat_entry(blocks.data(), e >> 9, (int)(e & 511), &fatv[8 * e]);\n"
+        "  a.fat = fat ? fatv.data() : nullptr;\n"
         "  for (int i = 0; i < n; ++i) out[i] = sample_world(a, p[3 * i], p[3 * i + 1], p[3 * i + 2]);\n"
         "  // getValue over the extent +-10 voxels from the apron layout\n"
         "  long long q = 0;\n"
@@ -214,10 +217,12 @@ def test_device_header_equals_oracle(hdr):
     assert out.view(np.uint32).tolist() == want.view(np.uint32).tolist()
 
 
+@pytest.mark.parametrize("fat", [0, 1])
 @pytest.mark.parametrize("case", ["tiles", "two_tiles", "single_leaf"])
-def test_apron_layout_equals_oracle(hdr, case):
-    """The apron layout (one slot + one 9^3 block per lookup) samples the same bits as the
-    oracle's tree, and its getValue equals the base layout's everywhere around the extent."""
+def test_apron_layout_equals_oracle(hdr, case, fat):
+    """The apron layout (one slot + one 9^3 block per lookup; fat: + one 32-B tap entry per
+    base voxel) samples the same bits as the oracle's tree, and its getValue equals the base
+    layout's everywhere around the extent."""
     if case == "tiles":
         e = _dense(9, (21, 19, 26))
         e[0:8, 0:8, 0:8] = 0.6
@@ -251,7 +256,7 @@ def test_apron_layout_equals_oracle(hdr, case):
     hdr.sample_apron.restype = ctypes.c_longlong
     nblk = hdr.sample_apron(arr(slot, I), arr(g.leaf_values, F), arr(tiles, F), len(g.tile_values), arr(lo32, I),
                             arr(nb32, I), ctypes.c_float(float(g.background)), arr(inv, F), arr(vec, F), len(p),
-                            arr(p, F), arr(out, F), arr(vals, F))
+                            arr(p, F), arr(out, F), arr(vals, F), fat)
     assert nblk >= len(g.leaf_origins)
     want = tree.sample_world(p)
     assert out.view(np.uint32).tolist() == want.view(np.uint32).tolist()

@@ -1,6 +1,7 @@
 """k_paths time split by section on the bench workload (profiling variant build).
 
-Builds variants/libavr_prof.so with -DAVR_PROFILE_SECTIONS (here, on the CPU: `--build`), then
+Builds variants/prof/libavr_hip.so with -DAVR_PROFILE_SECTIONS (build.build(variant="prof"),
+here on the CPU: `--build`), then
 on the GPU runs S-cloud passes through it and prints, per section, the share of wave cycles
 (s_memtime, summed over waves): event handlers, refill + camera rays, segment starts, DDA
 walk, collision (exact candidate + density fetch + callbacks).
@@ -12,21 +13,18 @@ import argparse
 import ctypes
 import json
 import os
-import subprocess
 import sys
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-VARIANT = os.path.join(ROOT, "variants", "libavr_prof.so")
+VARIANT = os.path.join(ROOT, "variants", "prof", "libavr_hip.so")
 NAMES = ["events", "refill+camera", "segment starts", "dda walk", "collision"]
 
 
 def build():
     sys.path.insert(0, ROOT)
     from acceleratedvolrenderer_amd import build as b
-    cmd = [b.HIPCC] + b.FLAGS + ["-DAVR_PROFILE_SECTIONS", b.SRC, "-o", VARIANT] + b.LIBS
-    subprocess.check_call(cmd)
-    print(VARIANT)
+    print(b.build(variant="prof", defines=["-DAVR_PROFILE_SECTIONS"]))
 
 
 def main():
@@ -59,17 +57,17 @@ def main():
         scene = scenes.s_cloud(density, sampler=a.sampler, spp=256, filter=a.filter)
     integ = VolPathIntegrator(scene, maxdepth=scenes.CLOUD_MAXDEPTH, spp=16, device=0)
     lib = capi.load()
-    lib.avr_debug_sections.argtypes = [ctypes.POINTER(ctypes.c_ulonglong)]
+    lib.avr_debug_sections.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_ulonglong)]
     out = (ctypes.c_ulonglong * 8)()
     integ.ctx.render(0, 16, 0, scenes.CLOUD_MAXDEPTH)   # warmup (pixel tables)
     integ.ctx.sync()
-    lib.avr_debug_sections(out)
+    lib.avr_debug_sections(integ.ctx.h, out)
     t0 = time.perf_counter()
     for k in range(1, 1 + a.steps):
         integ.ctx.render(16 * k, 16 * (k + 1), 0, scenes.CLOUD_MAXDEPTH)
     integ.ctx.sync()
     dt = time.perf_counter() - t0
-    lib.avr_debug_sections(out)
+    lib.avr_debug_sections(integ.ctx.h, out)
     tot = sum(out[i] for i in range(5))
     res = {NAMES[i]: round(out[i] / tot, 4) for i in range(5)}
     st = integ.stats()
