@@ -151,6 +151,7 @@ SIGNATURES = {
     "avr_set_filter": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, c_float_p, ctypes.c_float]),
     "avr_set_sampler": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]),
     "avr_set_sampler_table": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "avr_set_pixel_order": (ctypes.c_int, [ctypes.c_void_p, c_int_p, ctypes.c_longlong]),
     "avr_film": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, c_float_p, c_float_p, ctypes.c_float,
                                 ctypes.c_float]),
     "avr_film_clear": (ctypes.c_int, [ctypes.c_void_p]),
@@ -309,6 +310,15 @@ class Context:
     def set_sampler_table(self, dims):
         """ZSobol pixel-table dimensions (0 = compute every digit per call)."""
         _check(self.lib.avr_set_sampler_table(self.h, int(dims)))
+
+    def set_pixel_order(self, order):
+        """avr_set_pixel_order: the persistent kernel's pixel order (a permutation of the film's
+        row-major pixel ids), or None for scanline order."""
+        if order is None:
+            _check(self.lib.avr_set_pixel_order(self.h, None, 0))
+            return
+        o = np.ascontiguousarray(np.asarray(order, np.int32).reshape(-1))
+        _check(self.lib.avr_set_pixel_order(self.h, o.ctypes.data_as(c_int_p), len(o)))
 
     def set_stream(self, stream_ptr):
         _check(self.lib.avr_set_stream(self.h, ctypes.c_void_p(stream_ptr)))

@@ -94,6 +94,10 @@ struct avr_context {
     bool last_persistent = false;   // which organisation the last avr_render ran
     bool last_fast = false;         // ... and whether k_paths ran in fast mode
     int *d_heads = nullptr;   // 8 per-XCD work counters of k_paths
+    // k_paths' pixel order (avr_set_pixel_order): slot -> pixel and pixel -> slot, and the
+    // host copy of the latter (to return the last pass in pixel order); empty = scanline
+    int *d_pix_order = nullptr, *d_pix_slot = nullptr;
+    std::vector<int> h_pix_slot;
     // k_paths<emissive, gray, sampler, medium, image, fast> at slot
     // ((((fast*2 + image)*4 + medium(0 grid, 1 vdb, 2 rgb, 3 homogeneous/cloud))*3 + sampler(0
     // independent, 1 zsobol 32-bit, 2 zsobol 64-bit))*2 + emissive)*2 + gray
@@ -186,6 +190,13 @@ void free_paths(avr_context *c) {
     c->ps.cam0 = cam0; c->ps.cam1 = cam1; c->ps.cam2 = cam2; c->ps.cam3 = cam3; c->ps.cam4 = cam4; c->ps.cam5 = cam5;
     c->sh = {};
     c->cap = 0;
+}
+
+void free_pixel_order(avr_context *c) {
+    if (c->d_pix_order) (void)hipFree(c->d_pix_order);
+    if (c->d_pix_slot) (void)hipFree(c->d_pix_slot);
+    c->d_pix_order = c->d_pix_slot = nullptr;
+    c->h_pix_slot.clear();
 }
 
 void free_records(avr_context *c) {
@@ -694,6 +705,7 @@ int avr_context_destroy(avr_context *c) {
     if (c->d_reference) (void)hipFree(c->d_reference);
     if (c->d_metric) (void)hipFree(c->d_metric);
     if (c->d_fat) (void)hipFree(c->d_fat);
+    free_pixel_order(c);
     if (c->d_stats) (void)hipFree(c->d_stats);
     if (c->h_count) (void)hipHostFree(c->h_count);
     for (auto e : c->evpool) (void)hipEventDestroy(e);
@@ -1204,6 +1216,7 @@ int avr_film(avr_context *c, int width, int height, const float fr[2], const flo
     if (c->film.rgb_sum) (void)hipFree(c->film.rgb_sum);
     if (c->film.w_sum) (void)hipFree(c->film.w_sum);
     if (c->film.bucket_sum) (void)hipFree(c->film.bucket_sum);
+    free_pixel_order(c);   // an order is for one film resolution
     c->film = {};
     c->film.width = width;
     c->film.height = height;
@@ -1275,6 +1288,28 @@ int avr_set_filter(avr_context *c, int type, const float radius[2], float sigma)
     c->ftab.mcdf = c->ftab.cint + ny;
     c->ftab.mint = *mint;
     c->filter_type = 1;
+    return AVR_OK;
+}
+
+int avr_set_pixel_order(avr_context *c, const int *order, long long n) {
+    AVR_QUIESCE(c);
+    if (!c || !c->has_film) return fail(AVR_ERR_STATE, "pixel order needs a film");
+    HIP_TRY(hipSetDevice(c->device));
+    free_pixel_order(c);
+    if (!order) return AVR_OK;   // scanline
+    const long long np = (long long)c->film.width * c->film.height;
+    if (n != np) return fail(AVR_ERR_ARG, "pixel order must list every pixel of the film once");
+    std::vector<int> slot((size_t)np, -1);
+    for (long long j = 0; j < np; ++j) {
+        const int p = order[j];
+        if (p < 0 || p >= np || slot[(size_t)p] >= 0) return fail(AVR_ERR_ARG, "pixel order is not a permutation");
+        slot[(size_t)p] = (int)j;
+    }
+    HIP_TRY(dalloc(&c->d_pix_order, (size_t)np));
+    HIP_TRY(dalloc(&c->d_pix_slot, (size_t)np));
+    HIP_TRY(hipMemcpy(c->d_pix_order, order, np * sizeof(int), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(c->d_pix_slot, slot.data(), np * sizeof(int), hipMemcpyHostToDevice));
+    c->h_pix_slot.swap(slot);
     return AVR_OK;
 }
 
@@ -1486,6 +1521,7 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
             // the camera stage: one lane per sample (k_paths_camera)
             {
                 const int sv = c->sampler_kind == 0 ? 0 : (avr::smp::zsobol_wide(p.zs) ? 2 : 1);
+                p.pix_order = c->d_pix_order;
                 // ZSobol quads: 4-aligned sample ranges, at most 8 lower base-4 digits
                 p.cam_quad = (base % 4 == 0 && S % 4 == 0 && p.zs.log2spp <= 16) ? 1 : 0;
                 using KC = void (*)(avr::Params);
@@ -1508,7 +1544,8 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
             hipLaunchKernelGGL(c->kpaths[kv], dim3(c->paths_grid[kv]), dim3(256), 0, c->stream, p);
             HIP_TRY(hipGetLastError());
             EV_MARK(e1);
-            p.rec_mode = 1;   // k_film reads the records k_paths wrote
+            p.rec_mode = 1;   // k_film reads the records k_paths wrote (in slot order)
+            p.pix_slot = c->d_pix_slot;
             p.fast = c->render_mode;
             hipLaunchKernelGGL(avr::k_film, dim3(blocks_for(P)), dim3(256), avr::film_lds_bytes(c->film.nbuckets),
                                c->stream, p);
@@ -1829,6 +1866,16 @@ int avr_last_pass_samples(avr_context *c, float *L, float *lambda, float *pdf, l
         HIP_TRY(hipMemcpy(L, c->ps.rec, n * sizeof(float4), hipMemcpyDeviceToHost));
         HIP_TRY(hipMemcpy(lambda, c->ps.cam2, n * sizeof(float4), hipMemcpyDeviceToHost));
         HIP_TRY(hipMemcpy(pdf, c->ps.cam4, n * sizeof(float4), hipMemcpyDeviceToHost));
+        if (!c->h_pix_slot.empty()) {   // slot order -> pixel order
+            const long long np = (long long)c->film.width * c->film.height;
+            std::vector<float> tmp(4 * (size_t)np);
+            for (float *a : {L, lambda, pdf})
+                for (long long sb = 0; sb < n; sb += np) {
+                    std::memcpy(tmp.data(), a + 4 * sb, 4 * np * sizeof(float));
+                    for (long long p = 0; p < np; ++p)
+                        std::memcpy(a + 4 * (sb + p), tmp.data() + 4 * (size_t)c->h_pix_slot[(size_t)p], 4 * sizeof(float));
+                }
+        }
     } else if (n > 0) {
         HIP_TRY(hipMemcpy(L, c->ps.L, n * sizeof(float4), hipMemcpyDeviceToHost));
         HIP_TRY(hipMemcpy(lambda, c->ps.lambda, n * sizeof(float4), hipMemcpyDeviceToHost));
@@ -1849,7 +1896,9 @@ int avr_last_pass_weights(avr_context *c, float *w, long long n_max) {
     } else if (n > 0 && c->last_persistent) {
         std::vector<float4> cam1((size_t)n);
         HIP_TRY(hipMemcpy(cam1.data(), c->ps.cam1, n * sizeof(float4), hipMemcpyDeviceToHost));
-        for (long long i = 0; i < n; ++i) w[i] = cam1[i].w;
+        const long long np = (long long)c->film.width * c->film.height;
+        for (long long i = 0; i < n; ++i)
+            w[i] = cam1[c->h_pix_slot.empty() ? i : (i / np) * np + c->h_pix_slot[(size_t)(i % np)]].w;
     } else if (n > 0) {
         HIP_TRY(hipMemcpy(w, c->ps.weight, n * sizeof(float), hipMemcpyDeviceToHost));
     }

@@ -225,6 +225,10 @@ struct Params {
     const int *sh_perm;               // k_shadow: processing order of the shadow queue (ray binning), or null
     int fast;                         // render mode: 0 replay (canonical math), 1 fast (hardware math)
     int cam_quad;                     // k_paths_camera: ZSobol quads (pass aligned to 4 sample indices)
+    // k_paths' pixel order (avr_set_pixel_order; null = scanline): pass-local slot j of a sample
+    // index holds pixel pix_order[j]; pix_slot is the inverse (pixel -> slot, read by k_film)
+    const int *pix_order;
+    const int *pix_slot;
 };
 
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
@@ -275,7 +279,14 @@ __device__ __forceinline__ float fat_lookup(const float4 *__restrict__ fat, cons
     if (ix < -1 || ix >= nx || iy < -1 || iy >= ny || iz < -1 || iz >= nz) return grid_lookup(v, nx, ny, nz, p);
     float dx = psx - (float)ix, dy = psy - (float)iy, dz = psz - (float)iz;
     const size_t e = (((size_t)(iz + 1) * (ny + 1) + (iy + 1)) * (nx + 1) + (ix + 1)) * 2;
+#if AVR_NT_FETCH
+    typedef float v4f __attribute__((ext_vector_type(4)));
+    const v4f va = __builtin_nontemporal_load(reinterpret_cast<const v4f *>(fat + e)),
+              vb = __builtin_nontemporal_load(reinterpret_cast<const v4f *>(fat + e + 1));
+    const float4 a = make_float4(va.x, va.y, va.z, va.w), b = make_float4(vb.x, vb.y, vb.z, vb.w);
+#else
     const float4 a = fat[e], b = fat[e + 1];
+#endif
     float d00 = lerp(dx, a.x, a.y);
     float d10 = lerp(dx, a.z, a.w);
     float d01 = lerp(dx, b.x, b.y);
@@ -569,9 +580,16 @@ __device__ __forceinline__ bool dda_init(Dda &it, const DevMedium &m, Ray ray, f
         return false;
     }
     it.tMin = tMin; it.tMax = tMax;
-    const float diag0 = m.bmax[0] - m.bmin[0], diag1 = m.bmax[1] - m.bmin[1], diag2 = m.bmax[2] - m.bmin[2];
-    V3 go = box_offset(m.bmin, m.bmax, ray.o);
-    V3 gd = {ray.d.x / diag0, ray.d.y / diag1, ray.d.z / diag2};
+    // Bounds3::Offset and d / Diagonal(): divisions by exactly 1.0f for a unit box (x / 1 == x)
+    V3 go, gd;
+    if (m.unit_box) {
+        go = {ray.o.x - m.bmin[0], ray.o.y - m.bmin[1], ray.o.z - m.bmin[2]};
+        gd = ray.d;
+    } else {
+        const float diag0 = m.bmax[0] - m.bmin[0], diag1 = m.bmax[1] - m.bmin[1], diag2 = m.bmax[2] - m.bmin[2];
+        go = box_offset(m.bmin, m.bmax, ray.o);
+        gd = {ray.d.x / diag0, ray.d.y / diag1, ray.d.z / diag2};
+    }
     V3 gi = go + gd * tMin;
     dda_axis(gi.x, gd.x, m.mres[0], tMin, it.vx, it.nx, it.dx, it.sx);
     dda_axis(gi.y, gd.y, m.mres[1], tMin, it.vy, it.ny, it.dy, it.sy);
@@ -739,9 +757,11 @@ __device__ __forceinline__ void camera_sample(const Params &P, Smp &smp, int px,
 // requester pulls its results back with ds_bpermute. Results are bit-identical to the
 // sequential get1d / get2d calls (ZSobol::draw_at: a pure function of sample and dimension);
 // the requesters' dimension then advances by `adv`. s_st: this wave's 64 LDS entries.
+constexpr int kDimHash = 264;   // Hash(d, seed) of the first dimensions, staged in LDS by k_paths
 template <int kW, int N>
 __device__ __forceinline__ void coop_draws(smp::ZSobol &z, const smp::ZSobolParams &zp, bool req, const int (&off)[N],
-                                           const bool (&two)[N], int adv, float (&r0)[N], float (&r1)[N], uint3 *s_st) {
+                                           const bool (&two)[N], int adv, float (&r0)[N], float (&r1)[N], uint3 *s_st,
+                                           const uint64_t *dhash = nullptr) {
     const uint64_t mask = __ballot(req);
     const int lane = lane_id();
     const int rank = __popcll(mask & ((1ull << lane) - 1ull));
@@ -767,7 +787,7 @@ __device__ __forceinline__ void coop_draws(smp::ZSobol &z, const smp::ZSobolPara
             q.morton = st.x;
             q.hi = st.y;
             q.dimension = 0;
-            q.template draw_at<kW>(zp, st.z + (uint32_t)o, tw, &v0, &v1);
+            q.template draw_at<kW>(zp, st.z + (uint32_t)o, tw, &v0, &v1, dhash, dhash ? kDimHash : 0);
         }
         _Pragma("unroll") for (int j = 0; j < N; ++j) {
             const int src = rank * N + j - c;
@@ -935,16 +955,18 @@ __global__ void __launch_bounds__(256, AVR_CAM_WAVES) k_paths_camera(Params P) {
     // 16; the host sets P.cam_quad), so each store still writes 16 consecutive pixels per wave
     const bool quad = kSmp != 0 && P.cam_quad;
     for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < n; t += (long long)gridDim.x * blockDim.x) {
-        int pix, s;
+        int slot, s;
         if (quad) {
             const long long qd = t >> 2;
-            pix = (int)(qd % npix);
+            slot = (int)(qd % npix);
             s = (int)(qd / npix) * 4 + (int)(t & 3);
         } else {
-            pix = (int)(t % npix);
+            slot = (int)(t % npix);
             s = (int)(t / npix);
         }
-        const long long id = (long long)s * npix + pix;
+        // the camera stage and k_paths walk the pass in slot order; slot -> pixel by pix_order
+        const long long id = (long long)s * npix + slot;
+        const int pix = P.pix_order ? P.pix_order[slot] : slot;
         const int px = pix % P.film.width, py = pix / P.film.width;
         PathSampler<kSmp> smp;
         if constexpr (kSmp == 0) {
@@ -1546,6 +1568,9 @@ __global__ void __launch_bounds__(256) k_bin_scatter(const int *__restrict__ que
 #ifndef AVR_COOP_SPEC
 #define AVR_COOP_SPEC 1
 #endif
+#ifndef AVR_DIM_HASH
+#define AVR_DIM_HASH 1   // the cooperative draws read Hash(d, seed) from the LDS table
+#endif
 #ifndef AVR_NEE_AHEAD
 #define AVR_NEE_AHEAD 1
 #endif
@@ -1601,21 +1626,24 @@ __device__ __forceinline__ Spec smul(const Spec &a, const Spec &b) { return a * 
 // counters): one buffer shared by every k_paths translation unit, unlike a __device__ global
 // (each separately compiled unit would hold its own copy)
 struct SecProf {
-    unsigned long long acc[5] = {0, 0, 0, 0, 0};
+    // 0 NEE spawn, 1 refill, 2 segment starts, 3 DDA walk, 4 collision, 5 shadow done,
+    // 6 phase sampling, 7 escape + path end
+    unsigned long long acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     unsigned long long last = 0;
     int cur = 0;
     __device__ __forceinline__ void mark(int next) {
         const unsigned long long t = clock64();
         const unsigned long long d = t - last;
         if (cur == 0) acc[0] += d; else if (cur == 1) acc[1] += d; else if (cur == 2) acc[2] += d;
-        else if (cur == 3) acc[3] += d; else acc[4] += d;
+        else if (cur == 3) acc[3] += d; else if (cur == 4) acc[4] += d; else if (cur == 5) acc[5] += d;
+        else if (cur == 6) acc[6] += d; else acc[7] += d;
         last = t;
         cur = next;
     }
     __device__ __forceinline__ void flush(unsigned long long *stats) {
         mark(0);
         if (lane_id() == 0)
-            for (int i = 0; i < 5; ++i) atomicAdd(&stats[kNumStats + i], acc[i]);
+            for (int i = 0; i < 8; ++i) atomicAdd(&stats[kNumStats + i], acc[i]);
     }
 };
 #define AVR_SEC_INIT SecProf secp; secp.last = clock64();
@@ -1652,6 +1680,16 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
     __shared__ float4 s_img[kImage ? 256 : 1];
     // ZSobol: the requesters' sampler state for the cooperative draws (coop_draws), 64 per wave
     __shared__ uint3 s_zst[kSmp != 0 ? 256 : 1];
+    // NEE toward a delta light: the light's spectrum at the path's wavelengths and the phase
+    // value f_hat, computed when the shadow ray is spawned and read back when it finishes
+    // (SampleLd evaluates them once, integrators.cpp:1311-1331)
+    __shared__ float4 s_ls[256];
+    __shared__ float s_fhat[256];
+    // ZSobol: Hash(d, seed) of the first kDimHash dimensions — each draw's FastOwen seeds,
+    // read by the cooperative draws instead of a MurmurHash64A per draw
+    __shared__ uint64_t s_dh[kSmp != 0 ? kDimHash : 1];
+    if constexpr (kSmp != 0)
+        for (int i = threadIdx.x; i < kDimHash; i += blockDim.x) s_dh[i] = smp::hash_2u32((uint32_t)i, (uint32_t)P.zs.seed);
     // ZSobol: each lane's next light-pick draw (SampleLd's 1D, integrators.cpp:1302), evaluated
     // ahead with the previous bounce's cooperative phase draws (or by the camera stage)
     __shared__ float s_ul[kSmp != 0 ? 256 : 1];
@@ -1785,7 +1823,10 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
                         } else if (lt.type == 0) {
                             const V3 wi = {lt.w[0], lt.w[1], lt.w[2]};
                             const Spec Ls = sample_table(light_table(idx), lambda_index(lam)) * lt.scale;
-                            if (Ls.nonzero() && hg_eval(dot(wo, wi), m.g) != 0) {
+                            const float fval = hg_eval(dot(wo, wi), m.g);
+                            if (Ls.nonzero() && fval != 0) {
+                                s_ls[threadIdx.x] = to4(Ls);
+                                s_fhat[threadIdx.x] = fval;
                                 const V3 pOut = po + wi * (2 * P.lights.scene_radius);
                                 const V3 d = pOut - po;
                                 light = idx;
@@ -1804,6 +1845,7 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
                 }
             }
         }
+        AVR_SEC(5)
         if (__ballot(ev == EV_SHADOW_DONE)) {
             if (ev == EV_SHADOW_DONE) {
                 // finish SampleLd (1379-1398); SampleT_maj returned 1 if the callback stopped
@@ -1823,11 +1865,11 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
                         sr_u = sr_u * (r_u * im.w);
                         contrib = smul(Ls, beta * f_hat * T_ray) / savg(sr_l + sr_u);
                     } else {
-                        const V3 wi = {lt.w[0], lt.w[1], lt.w[2]};
+                        // the delta light's spectrum and f_hat of the spawn (same wo, wi)
                         const float pInf = float(P.lights.n) / float(P.lights.n + 0);
                         const float p_l = pInf / P.lights.n * 1.f;
-                        const S f_hat = sconst<S>(hg_eval(dot(-pd, wi), m.g));
-                        const Spec Ls = sample_table(light_table(light), lambda_index(lam)) * lt.scale;
+                        const S f_hat = sconst<S>(s_fhat[threadIdx.x]);
+                        const Spec Ls = spec4(s_ls[threadIdx.x]);
                         sr_l = sr_l * (r_u * p_l);
                         contrib = smul(Ls, beta * f_hat * T_ray) / savg(sr_l);
                     }
@@ -1836,6 +1878,7 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
                 ev = EV_PHASE;
             }
         }
+        AVR_SEC(6)
         if (__ballot(ev == EV_PHASE)) {
             // ZSobol: the phase 2D draw and the next segment's three 1D draws of every lane in
             // EV_PHASE, evaluated cooperatively by the whole wave
@@ -1845,14 +1888,14 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
                 constexpr int off[5] = {0, 2, 3, 4, 5};
                 constexpr bool two[5] = {true, false, false, false, false};
                 coop_draws<PathSampler<kSmp>::kW, 5>(smp.z, P.zs, ev == EV_PHASE, off, two, 5, q0, q1,
-                                                     s_zst + (threadIdx.x & ~63u));
+                                                     s_zst + (threadIdx.x & ~63u), AVR_DIM_HASH ? s_dh : nullptr);
                 if (ev == EV_PHASE) s_ul[threadIdx.x] = q0[4];
             } else if constexpr (kCoop) {
                 constexpr int off[4] = {0, 2, 3, 4};
                 constexpr bool two[4] = {true, false, false, false};
                 float r0[4], r1[4];
                 coop_draws<PathSampler<kSmp>::kW, 4>(smp.z, P.zs, ev == EV_PHASE, off, two, 5, r0, r1,
-                                                     s_zst + (threadIdx.x & ~63u));
+                                                     s_zst + (threadIdx.x & ~63u), AVR_DIM_HASH ? s_dh : nullptr);
                 _Pragma("unroll") for (int j = 0; j < 4; ++j) {
                     q0[j] = r0[j];
                     q1[j] = r1[j];
@@ -1887,6 +1930,7 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
                 }
             }
         }
+        AVR_SEC(7)
         if (__ballot(ev == EV_ESCAPE)) {
             if (ev == EV_ESCAPE) {
                 // escaped (integrators.cpp:1078-1107)
@@ -1963,7 +2007,8 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
                     const float4 c0 = P.ps.cam0[g], c1 = P.ps.cam1[g], c2 = P.ps.cam2[g];
                     const uint4 c3 = P.ps.cam3[g];
                     if constexpr (kZSobol) {
-                        const int pix = g % npix, sIdx = g / npix;
+                        const int slot = g % npix, sIdx = g / npix;
+                        const int pix = P.pix_order ? P.pix_order[slot] : slot;
                         smp.start(P, pix % P.film.width, pix / P.film.width, P.sample_base + sIdx);
                         smp.z.dimension = 9;   // past the camera draws and the first segment's three
                         if constexpr (kUlAhead) s_ul[threadIdx.x] = __uint_as_float(P.ps.cam5[g].x);
@@ -2287,8 +2332,9 @@ __global__ void __launch_bounds__(256) k_film(Params P) {
                 bw[b * 256] = gbw[b];
             }
         }
+        const int slot = P.pix_slot ? P.pix_slot[pix] : pix;   // where k_paths traced this pixel
         for (int s = 0; s < P.pass_samples; ++s) {
-            const size_t id = (size_t)s * npix + pix;
+            const size_t id = (size_t)s * npix + slot;
             Spec L, lam, pdf;
             float w;
             film_load_sample(P, id, &L, &lam, &pdf, &w);

@@ -252,13 +252,16 @@ struct ZSobol {
     // The draw get1d (two = false: *u0) or get2d (two = true: *u0, *u1) would return with
     // the state's dimension at `dim`, without touching the state: a pure function of
     // (morton, hi, dim), so any lane can evaluate it for another.
+    // `dhash`: optional table of Hash(d, seed) for d < dhash_n (the draw's scramble seeds)
     template <int kW = 0>
-    AVR_HD void draw_at(const ZSobolParams &zp, uint32_t dim, bool two, float *u0, float *u1) const {
+    AVR_HD void draw_at(const ZSobolParams &zp, uint32_t dim, bool two, float *u0, float *u1,
+                        const uint64_t *dhash = nullptr, uint32_t dhash_n = 0) const {
         ZSobol s = *this;
         s.dimension = dim;
         uint32_t a, ah;
         s.index<kW>(zp, &a, &ah);
-        const uint64_t h = hash_2u32(dim + (two ? 2u : 1u), (uint32_t)zp.seed);
+        const uint32_t hd = dim + (two ? 2u : 1u);
+        const uint64_t h = hd < dhash_n ? dhash[hd] : hash_2u32(hd, (uint32_t)zp.seed);
         *u0 = u32_to_unit(fast_owen(sobol_bits(a, 0), (uint32_t)h));
         *u1 = u32_to_unit(fast_owen(sobol_bits64(a, ah, 1), (uint32_t)(h >> 32)));
     }

@@ -115,6 +115,39 @@ class VolPathIntegrator:
         chosen, ms = self.ctx.tune_majorant(cands, probe[0], probe[1], self.seed, self.maxdepth)
         return chosen, {c[0]: float(t) for c, t in zip(cands, ms)}
 
+    def entry_cell_order(self):
+        """A pixel order for avr_set_pixel_order (the north star's "sorted ray
+        packets"): pixels sorted by the majorant cell where the ray through the pixel centre
+        enters the medium's bounds (pixels whose ray misses them last), scanline order within a
+        cell. Host arithmetic in f64 (an ordering heuristic, not a sample)."""
+        sc = self.scene
+        f = sc.film
+        y, x = np.mgrid[0:f.height, 0:f.width]
+        pr = np.stack([x.ravel() + 0.5, y.ravel() + 0.5, np.zeros(x.size), np.ones(x.size)], 1)
+        pc = pr @ np.asarray(sc.camera_from_raster, np.float64).T
+        pc = pc[:, :3] / pc[:, 3:4]
+        if int(sc.camera.type_id) == 0:    # orthographic: origin on the film plane, along +z
+            o_c, d_c = pc, np.tile([0.0, 0.0, 1.0], (len(pc), 1))
+        else:
+            o_c, d_c = np.zeros_like(pc), pc / np.linalg.norm(pc, axis=1, keepdims=True)
+        rfc = np.asarray(sc.render_from_camera, np.float64)
+        mfr = np.asarray(sc.medium_from_render, np.float64)
+        m = mfr @ rfc
+        o = o_c @ m[:3, :3].T + m[:3, 3]
+        d = d_c @ m[:3, :3].T
+        b = np.asarray(sc.medium.bounds, np.float64)
+        with np.errstate(divide="ignore", invalid="ignore"):
+            t0 = (b[:3] - o) / d
+            t1 = (b[3:] - o) / d
+        tn = np.nanmax(np.minimum(t0, t1), axis=1)
+        tf = np.nanmin(np.maximum(t0, t1), axis=1)
+        hit = (tf >= np.maximum(tn, 0)) & np.isfinite(tn)
+        p = o + d * np.maximum(tn, 0)[:, None]
+        res = np.asarray(sc.medium.majorant_res, np.int64)
+        c = np.clip(((p - b[:3]) / (b[3:] - b[:3]) * res).astype(np.int64), 0, res - 1)
+        key = np.where(hit, (c[:, 2] * res[1] + c[:, 1]) * res[0] + c[:, 0], res.prod())
+        return np.argsort(key, kind="stable").astype(np.int32)
+
     def render(self, spp_begin=0, spp_end=None, clear=True):
         """Render sample indices [spp_begin, spp_end); returns (rgb_sum, w_sum) fp64."""
         if spp_end is None:

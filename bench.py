@@ -86,6 +86,9 @@ def parse():
                         "on the device among 1,2,4,8,16 (fast-mode default, outside the timed region)")
     p.add_argument("--occupancy", type=int, default=0,
                    help="NanoVDB: coarse majorant occupancy level in LDS (avr_set_majorant_occupancy; -2 %%, off)")
+    p.add_argument("--pixel-order", default="scanline", choices=["scanline", "entry-cell"],
+                   help="k_paths pixel order: scanline, or sorted by the majorant cell where the pixel's camera ray "
+                        "enters the medium (N1: coherent ray packets, avr_set_pixel_order)")
     p.add_argument("--ray-binning", type=int, default=0,
                    help="wavefront kernels: counting-sort the queues by (majorant cell, octant) before each launch")
     p.add_argument("--nvdb", default=None,
@@ -191,7 +194,8 @@ def pmc_passes(args, kernel_substr="k_paths", timeout_s=240):
         return None, "rocprofv3 not found"
     child = [sys.executable, os.path.join(ROOT, "bench.py"), "--pmc-child", "--no-cpu-baseline", "--pmc", "off",
              "--steps", "2", "--warmup", "1"]
-    for k in ("res", "width", "height", "spp_per_step", "max_paths", "pixelsamples", "kernel", "medium", "refill_min", "grid_layout",
+    for k in ("res", "width", "height", "spp_per_step", "max_paths", "pixelsamples", "pixel_order", "kernel", "medium",
+              "refill_min", "grid_layout",
               "dda_budget", "zsobol_table", "sampler", "filter", "mode", "majorant_res", "ray_binning", "occupancy", "nvdb",
               "scene"):
         if getattr(args, k) is not None:
@@ -339,6 +343,8 @@ def main():
     integ.ctx.set_sampler_table(args.zsobol_table)
     if args.ray_binning:
         integ.ctx.set_ray_binning(1)
+    if args.pixel_order == "entry-cell":
+        integ.ctx.set_pixel_order(integ.entry_cell_order())
     if args.occupancy:
         integ.ctx.set_majorant_occupancy(1)
     maj_res = tuple(scene.medium.majorant_res)
@@ -548,9 +554,10 @@ def main():
                        "pixelsamples": spp_total, "sample_indices_distinct": True},
             "roofline": {
                 "kernel": kname,
-                # the roof this kernel is priced against (no MFMA work on the path); the
-                # counters' verdict on what actually limits it is `limiter`
-                "bound": "hbm",
+                # what limits the kernel, from the counter passes (`limiter`); `achieved` /
+                # `peak` / `frac` stay priced against the HBM roof (no MFMA work on the path)
+                "bound": ("valu" if limiter and limiter["kind"].startswith("valu") else "hbm"),
+                "priced_against": "hbm",
                 "achieved": round(achieved, 2),
                 "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s",

@@ -116,6 +116,14 @@ int avr_set_dda_budget(avr_context *ctx, int cells);
 int avr_set_grid_layout(avr_context *ctx, int layout);
 /* 1 if the current medium uses the fat layout, else 0. */
 int avr_grid_layout_active(avr_context *ctx);
+/* The persistent kernel's pixel order (SURVEY §7 step 6 / north star "density-grid fetches
+ * coalesced along sorted ray packets"): `order` lists every pixel of the current film once
+ * (row-major ids); within each sample index of a pass the camera stage and k_paths hand
+ * pixels to lanes in that order, so consecutive lanes start coherent camera rays (e.g.
+ * sorted by the majorant cell where the ray enters the medium). NULL restores scanline
+ * order; a new film resets it. Results are identical in any order (per-pixel sums still
+ * add the pixel's samples in sampleIndex order). */
+int avr_set_pixel_order(avr_context *ctx, const int *order, long long n);
 /* Run all work of this context on `hip_stream` (a hipStream_t; NULL = the context's own stream). */
 int avr_set_stream(avr_context *ctx, void *hip_stream);
 

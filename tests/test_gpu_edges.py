@@ -309,3 +309,32 @@ def test_density_fetch_kernel_and_lookup_trace():
             want = L.oracle_grid_lookup(binding.fp(dens), 24, 24, 24, float(p[i, 0]), float(p[i, 1]), float(p[i, 2]))
             assert np.float32(want).view(np.uint32) == got[i].view(np.uint32), (layout, i)
         integ.close()
+
+
+@pytest.mark.parametrize("sampler", ["zsobol", "independent"])
+def test_pixel_order_changes_order_not_results(sampler):
+    """avr_set_pixel_order (N1: k_paths hands pixels to lanes sorted by the majorant cell of
+    the camera ray's entry): the film and every sample are bit-identical to scanline order."""
+    from acceleratedvolrenderer_amd import VolPathIntegrator, scenes
+    from oracle import binding
+    dens = binding.cloud_grid(24)
+    scene = scenes.s_cloud(dens, width=40, height=24, sampler=sampler, spp=64, filter="gaussian")
+    integ = VolPathIntegrator(scene, maxdepth=scenes.CLOUD_MAXDEPTH, spp=8, seed=0, device=0)
+    rgb, w = integ.render()
+    _, _, L, lam, pdf = integ.ctx.last_pass_samples(40 * 24, 8)
+    wts = integ.ctx.last_pass_weights(40 * 24, 8)
+    order = integ.entry_cell_order()
+    assert sorted(order.tolist()) == list(range(40 * 24)) and order.tolist() != list(range(40 * 24))
+    integ.ctx.set_pixel_order(order)
+    rgb2, w2 = integ.render()
+    _, _, L2, lam2, pdf2 = integ.ctx.last_pass_samples(40 * 24, 8)
+    assert np.array_equal(rgb, rgb2) and np.array_equal(w, w2)
+    for a, b in ((L, L2), (lam, lam2), (pdf, pdf2)):
+        assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    assert np.array_equal(wts, integ.ctx.last_pass_weights(40 * 24, 8))
+    with pytest.raises(RuntimeError):
+        integ.ctx.set_pixel_order(np.zeros(40 * 24, np.int32))   # not a permutation
+    integ.ctx.set_pixel_order(None)
+    rgb3, _ = integ.render()
+    assert np.array_equal(rgb, rgb3)
+    integ.close()

@@ -3,8 +3,9 @@
 Builds variants/prof/libavr_hip.so with -DAVR_PROFILE_SECTIONS (build.build(variant="prof"),
 here on the CPU: `--build`), then
 on the GPU runs S-cloud passes through it and prints, per section, the share of wave cycles
-(s_memtime, summed over waves): event handlers, refill + camera rays, segment starts, DDA
-walk, collision (exact candidate + density fetch + callbacks).
+(s_memtime, summed over waves): the event handlers (NEE spawn, shadow done, phase sampling,
+escape + end), refill, segment starts, DDA walk, collision (exact candidate + density fetch +
+callbacks).
 
 usage: python tools/section_profile.py --build            (CPU, before gpurun)
        python tools/section_profile.py [--res 1024] [--medium grid|nanovdb] [--steps 3]
@@ -18,7 +19,8 @@ import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 VARIANT = os.path.join(ROOT, "variants", "prof", "libavr_hip.so")
-NAMES = ["events", "refill+camera", "segment starts", "dda walk", "collision"]
+NAMES = ["nee spawn", "refill", "segment starts", "dda walk", "collision", "shadow done", "phase sampling",
+         "escape+end"]
 
 
 def build():
@@ -68,8 +70,8 @@ def main():
     integ.ctx.sync()
     dt = time.perf_counter() - t0
     lib.avr_debug_sections(integ.ctx.h, out)
-    tot = sum(out[i] for i in range(5))
-    res = {NAMES[i]: round(out[i] / tot, 4) for i in range(5)}
+    tot = sum(out[i] for i in range(8))
+    res = {NAMES[i]: round(out[i] / tot, 4) for i in range(8)}
     st = integ.stats()
     print(json.dumps({"medium": a.medium, "res": n, "Msamples_per_s": 1280 * 720 * 16 * a.steps / dt / 1e6,
                       "section_share": res, "wave_cycles": tot, "loop_iterations": st.get("loop_iterations"),
