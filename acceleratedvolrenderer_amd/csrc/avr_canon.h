@@ -45,23 +45,42 @@ __device__ __forceinline__ double kd() {
     return dfrom(((uint64_t)hi << 32) | lo);
 }
 #define AVR_KD(bits, value) (::avr::canon::kd<bits>())
+// a * b + K with K read straight from its SGPR pair (VOP3 v_fma_f64): the compiler's own choice
+// for fma(a, b, K) is v_fmac_f64 after two v_mov_b32 copying K into the accumulator — two extra
+// VALU issues per polynomial step of the canonical f64 sequences
+template <uint64_t B>
+__device__ __forceinline__ double fmak(double a, double b) {
+    const double c = kd<B>();
+    double r;
+    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(c));
+    return r;
+}
+#ifndef AVR_FMAK_ASM
+#define AVR_FMAK_ASM 1
+#endif
+#if AVR_FMAK_ASM
+#define AVR_FMAK(a, b, bits, value) (::avr::canon::fmak<bits>((a), (b)))
+#else
+#define AVR_FMAK(a, b, bits, value) (fma((a), (b), ::avr::canon::kd<bits>()))
+#endif
 #else
 #define AVR_KD(bits, value) (value)
+#define AVR_FMAK(a, b, bits, value) (fma((a), (b), (value)))
 #endif
 
 // 2*atanh(s)/(2s) = 1 + z/3 + z^2/5 + ... + z^11/23 with z = s^2 (|s| <= 0.1716, z^12/25 < 2e-20)
 AVR_HD double atanh_series(double z) {
     double p = AVR_KD(0x3fa642c8590b2164ull, 0x1.642c8590b2164p-5);
-    p = fma(p, z, AVR_KD(0x3fa8618618618618ull, 0x1.8618618618618p-5));
-    p = fma(p, z, AVR_KD(0x3faaf286bca1af28ull, 0x1.af286bca1af28p-5));
-    p = fma(p, z, AVR_KD(0x3fae1e1e1e1e1e1eull, 0x1.e1e1e1e1e1e1ep-5));
-    p = fma(p, z, AVR_KD(0x3fb1111111111111ull, 0x1.1111111111111p-4));
-    p = fma(p, z, AVR_KD(0x3fb3b13b13b13b14ull, 0x1.3b13b13b13b14p-4));
-    p = fma(p, z, AVR_KD(0x3fb745d1745d1746ull, 0x1.745d1745d1746p-4));
-    p = fma(p, z, AVR_KD(0x3fbc71c71c71c71cull, 0x1.c71c71c71c71cp-4));
-    p = fma(p, z, AVR_KD(0x3fc2492492492492ull, 0x1.2492492492492p-3));
-    p = fma(p, z, AVR_KD(0x3fc999999999999aull, 0x1.999999999999ap-3));
-    p = fma(p, z, AVR_KD(0x3fd5555555555555ull, 0x1.5555555555555p-2));
+    p = AVR_FMAK(p, z, 0x3fa8618618618618ull, 0x1.8618618618618p-5);
+    p = AVR_FMAK(p, z, 0x3faaf286bca1af28ull, 0x1.af286bca1af28p-5);
+    p = AVR_FMAK(p, z, 0x3fae1e1e1e1e1e1eull, 0x1.e1e1e1e1e1e1ep-5);
+    p = AVR_FMAK(p, z, 0x3fb1111111111111ull, 0x1.1111111111111p-4);
+    p = AVR_FMAK(p, z, 0x3fb3b13b13b13b14ull, 0x1.3b13b13b13b14p-4);
+    p = AVR_FMAK(p, z, 0x3fb745d1745d1746ull, 0x1.745d1745d1746p-4);
+    p = AVR_FMAK(p, z, 0x3fbc71c71c71c71cull, 0x1.c71c71c71c71cp-4);
+    p = AVR_FMAK(p, z, 0x3fc2492492492492ull, 0x1.2492492492492p-3);
+    p = AVR_FMAK(p, z, 0x3fc999999999999aull, 0x1.999999999999ap-3);
+    p = AVR_FMAK(p, z, 0x3fd5555555555555ull, 0x1.5555555555555p-2);
     p = fma(p, z, 1.0);
     return p;
 }
@@ -102,20 +121,20 @@ AVR_HD void sincos_d(double x, double *sn, double *cs) {
     // sin r = r (1 - z/3! + ... - z^7/15!), cos r = 1 - z (1/2! - z/4! + ... - z^7/16!):
     // truncation below 5e-17 (relative) for |r| <= pi/4
     double ps = AVR_KD(0xbd6ae7f3e733b81full, -0x1.ae7f3e733b81fp-41);   // -1/15!
-    ps = fma(ps, z, AVR_KD(0x3de6124613a86d09ull, 0x1.6124613a86d09p-33));   // 1/13!
-    ps = fma(ps, z, AVR_KD(0xbe5ae64567f544e4ull, -0x1.ae64567f544e4p-26));   // -1/11!
-    ps = fma(ps, z, AVR_KD(0x3ec71de3a556c734ull, 0x1.71de3a556c734p-19));   // 1/9!
-    ps = fma(ps, z, AVR_KD(0xbf2a01a01a01a01aull, -0x1.a01a01a01a01ap-13));   // -1/7!
-    ps = fma(ps, z, AVR_KD(0x3f81111111111111ull, 0x1.1111111111111p-7));   // 1/5!
-    ps = fma(ps, z, AVR_KD(0xbfc5555555555555ull, -0x1.5555555555555p-3));   // -1/3!
+    ps = AVR_FMAK(ps, z, 0x3de6124613a86d09ull, 0x1.6124613a86d09p-33);   // 1/13!
+    ps = AVR_FMAK(ps, z, 0xbe5ae64567f544e4ull, -0x1.ae64567f544e4p-26);   // -1/11!
+    ps = AVR_FMAK(ps, z, 0x3ec71de3a556c734ull, 0x1.71de3a556c734p-19);   // 1/9!
+    ps = AVR_FMAK(ps, z, 0xbf2a01a01a01a01aull, -0x1.a01a01a01a01ap-13);   // -1/7!
+    ps = AVR_FMAK(ps, z, 0x3f81111111111111ull, 0x1.1111111111111p-7);   // 1/5!
+    ps = AVR_FMAK(ps, z, 0xbfc5555555555555ull, -0x1.5555555555555p-3);   // -1/3!
     ps = fma(ps, z, 1.0);
     double pc = AVR_KD(0xbd2ae7f3e733b81full, -0x1.ae7f3e733b81fp-45);   // -1/16!
-    pc = fma(pc, z, AVR_KD(0x3da93974a8c07c9dull, 0x1.93974a8c07c9dp-37));   // 1/14!
-    pc = fma(pc, z, AVR_KD(0xbe21eed8eff8d898ull, -0x1.1eed8eff8d898p-29));   // -1/12!
-    pc = fma(pc, z, AVR_KD(0x3e927e4fb7789f5cull, 0x1.27e4fb7789f5cp-22));   // 1/10!
-    pc = fma(pc, z, AVR_KD(0xbefa01a01a01a01aull, -0x1.a01a01a01a01ap-16));   // -1/8!
-    pc = fma(pc, z, AVR_KD(0x3f56c16c16c16c17ull, 0x1.6c16c16c16c17p-10));   // 1/6!
-    pc = fma(pc, z, AVR_KD(0xbfa5555555555555ull, -0x1.5555555555555p-5));   // -1/4!
+    pc = AVR_FMAK(pc, z, 0x3da93974a8c07c9dull, 0x1.93974a8c07c9dp-37);   // 1/14!
+    pc = AVR_FMAK(pc, z, 0xbe21eed8eff8d898ull, -0x1.1eed8eff8d898p-29);   // -1/12!
+    pc = AVR_FMAK(pc, z, 0x3e927e4fb7789f5cull, 0x1.27e4fb7789f5cp-22);   // 1/10!
+    pc = AVR_FMAK(pc, z, 0xbefa01a01a01a01aull, -0x1.a01a01a01a01ap-16);   // -1/8!
+    pc = AVR_FMAK(pc, z, 0x3f56c16c16c16c17ull, 0x1.6c16c16c16c17p-10);   // 1/6!
+    pc = AVR_FMAK(pc, z, 0xbfa5555555555555ull, -0x1.5555555555555p-5);   // -1/4!
     pc = fma(pc, z, 0.5);
     const double sr = r * ps;
     const double cr = fma(-z, pc, 1.0);
@@ -251,7 +270,7 @@ constexpr double k64OverLn2 = 0x1.71547652b82fep+6;
 // log(x) for a positive normal f64; 0 -> -inf, <0/NaN -> NaN. x = 2^e m, m in [1, 2); k = the
 // fraction of m rounded to 7 bits (k = 128: m / 2 and e + 1, so k = 0 and c = 1 around x = 1);
 // r = (m - c_k) / c_k (m - c_k exact) with |r| <= 2^-8; log1p(r) = r + r^2 q(r) to degree 8.
-AVR_HD double log_t(double x) {
+AVR_HD double log_t(double x, const double *invc = kLogInvC, const double *logc = kLogC) {
     if (!(x > 0)) return x == 0 ? -__builtin_inf() : __builtin_nan("");
     if (x == __builtin_inf()) return x;
     const uint64_t b = dbits(x);
@@ -265,51 +284,51 @@ AVR_HD double log_t(double x) {
         k = 0;
     }
     const double c = 1.0 + (double)k * 0x1p-7;
-    const double r = (m - c) * kLogInvC[k];
+    const double r = (m - c) * invc[k];
     double q = AVR_KD(0xbfc0000000000000ull, -0x1.0000000000000p-3);            // -1/8
-    q = fma(q, r, AVR_KD(0x3fc2492492492492ull, 0x1.2492492492492p-3));         // 1/7
-    q = fma(q, r, AVR_KD(0xbfc5555555555555ull, -0x1.5555555555555p-3));        // -1/6
-    q = fma(q, r, AVR_KD(0x3fc999999999999aull, 0x1.999999999999ap-3));         // 1/5
-    q = fma(q, r, -0.25);
-    q = fma(q, r, AVR_KD(0x3fd5555555555555ull, 0x1.5555555555555p-2));         // 1/3
+    q = AVR_FMAK(q, r, 0x3fc2492492492492ull, 0x1.2492492492492p-3);         // 1/7
+    q = AVR_FMAK(q, r, 0xbfc5555555555555ull, -0x1.5555555555555p-3);        // -1/6
+    q = AVR_FMAK(q, r, 0x3fc999999999999aull, 0x1.999999999999ap-3);         // 1/5
+    q = AVR_FMAK(q, r, 0xbfd0000000000000ull, -0.25);
+    q = AVR_FMAK(q, r, 0x3fd5555555555555ull, 0x1.5555555555555p-2);         // 1/3
     q = fma(q, r, -0.5);
     const double l1 = fma(r * r, q, r);
     const double de = (double)e;
     return fma(de, AVR_KD(0x3fe62e42fee00000ull, 0x1.62e42fee00000p-1),
-               fma(de, AVR_KD(0x3dea39ef35793c76ull, 0x1.a39ef35793c76p-33), kLogC[k] + l1));
+               fma(de, AVR_KD(0x3dea39ef35793c76ull, 0x1.a39ef35793c76p-33), logc[k] + l1));
 }
 
 // atanh(x), |x| < 1: (log(1 + x) - log(1 - x)) / 2 (1 +- x exact for |x| >= 2^-29); x itself
 // below 2^-26 (atanh(x) = x (1 + x^2/3 + ...) rounds to x there)
-AVR_HD double atanh_t(double x) {
+AVR_HD double atanh_t(double x, const double *invc = kLogInvC, const double *logc = kLogC) {
     const double ax = x < 0 ? -x : x;
     if (ax < 0x1p-26) return x;
-    return 0.5 * (log_t(1.0 + x) - log_t(1.0 - x));
+    return 0.5 * (log_t(1.0 + x, invc, logc) - log_t(1.0 - x, invc, logc));
 }
 
 // e^(s r) 2^(n/64) pieces: n = rint(x 64 / ln2), r = x - n ln2/64 (two-part), |r| <= ln2/128;
 // e^r to degree 6
 AVR_HD double exp_poly6(double r) {
     double p = AVR_KD(0x3f56c16c16c16c17ull, 0x1.6c16c16c16c17p-10);            // 1/720
-    p = fma(p, r, AVR_KD(0x3f81111111111111ull, 0x1.1111111111111p-7));         // 1/120
-    p = fma(p, r, AVR_KD(0x3fa5555555555555ull, 0x1.5555555555555p-5));         // 1/24
-    p = fma(p, r, AVR_KD(0x3fc5555555555555ull, 0x1.5555555555555p-3));         // 1/6
+    p = AVR_FMAK(p, r, 0x3f81111111111111ull, 0x1.1111111111111p-7);         // 1/120
+    p = AVR_FMAK(p, r, 0x3fa5555555555555ull, 0x1.5555555555555p-5);         // 1/24
+    p = AVR_FMAK(p, r, 0x3fc5555555555555ull, 0x1.5555555555555p-3);         // 1/6
     p = fma(p, r, 0.5);
     p = fma(p, r, 1.0);
     p = fma(p, r, 1.0);
     return p;
 }
-AVR_HD double exp_scale(int n) {   // 2^(n / 64) = 2^(n >> 6) * kExp2J64[n & 63]
-    return kExp2J64[n & 63] * dfrom((uint64_t)((n >> 6) + 1023) << 52);
+AVR_HD double exp_scale(int n, const double *e2j = kExp2J64) {   // 2^(n / 64) = 2^(n >> 6) * kExp2J64[n & 63]
+    return e2j[n & 63] * dfrom((uint64_t)((n >> 6) + 1023) << 52);
 }
 // cosh(x) = (e^|x| + e^-|x|) / 2 for |x| < 700, both exponentials from one reduction
-AVR_HD double cosh_t(double x) {
+AVR_HD double cosh_t(double x, const double *e2j = kExp2J64) {
     const double ax = x < 0 ? -x : x;
     const double nf = __builtin_rint(ax * k64OverLn2);
     const double r = (ax - nf * kLn2_64Hi) - nf * kLn2_64Lo;
     const int n = (int)nf;
-    const double ep = exp_poly6(r) * exp_scale(n);
-    const double em = exp_poly6(-r) * exp_scale(-n);
+    const double ep = exp_poly6(r) * exp_scale(n, e2j);
+    const double em = exp_poly6(-r) * exp_scale(-n, e2j);
     return 0.5 * (ep + em);
 }
 
@@ -317,6 +336,10 @@ AVR_HD double cosh_t(double x) {
 AVR_HD float log_f(float x) { return (float)log_t((double)x); }
 AVR_HD float atanh_f(float x) { return (float)atanh_t((double)x); }
 AVR_HD float cosh_f(float x) { return (float)cosh_t((double)x); }
+// the same functions reading their tables from a staged copy (LDS): kLogInvC | kLogC | kExp2J64
+constexpr int kCanonTabDoubles = 128 + 128 + 64;
+AVR_HD float atanh_f(float x, const double *tabs) { return (float)atanh_t((double)x, tabs, tabs + 128); }
+AVR_HD float cosh_f(float x, const double *tabs) { return (float)cosh_t((double)x, tabs + 256); }
 AVR_HD void sincos_f(float x, float *s, float *c) {
     double sd, cd;
     sincos_d((double)x, &sd, &cd);

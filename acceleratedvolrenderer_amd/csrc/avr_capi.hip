@@ -185,9 +185,11 @@ void free_paths(avr_context *c) {
     // the k_paths records and camera stage are managed by ensure_records
     float4 *rec = c->ps.rec, *cam0 = c->ps.cam0, *cam1 = c->ps.cam1, *cam2 = c->ps.cam2, *cam4 = c->ps.cam4;
     uint4 *cam3 = c->ps.cam3, *cam5 = c->ps.cam5;
+    float *camw = c->ps.camw;
     c->ps = {};
     c->ps.rec = rec;
     c->ps.cam0 = cam0; c->ps.cam1 = cam1; c->ps.cam2 = cam2; c->ps.cam3 = cam3; c->ps.cam4 = cam4; c->ps.cam5 = cam5;
+    c->ps.camw = camw;
     c->sh = {};
     c->cap = 0;
 }
@@ -201,15 +203,16 @@ void free_pixel_order(avr_context *c) {
 
 void free_records(avr_context *c) {
     for (void *p : {(void *)c->ps.rec, (void *)c->ps.cam0, (void *)c->ps.cam1, (void *)c->ps.cam2, (void *)c->ps.cam3,
-                    (void *)c->ps.cam4, (void *)c->ps.cam5})
+                    (void *)c->ps.cam4, (void *)c->ps.cam5, (void *)c->ps.camw})
         if (p) (void)hipFree(p);
     c->ps.rec = c->ps.cam0 = c->ps.cam1 = c->ps.cam2 = c->ps.cam4 = nullptr;
     c->ps.cam3 = c->ps.cam5 = nullptr;
+    c->ps.camw = nullptr;
     c->rec_cap = 0;
 }
 
-// k_paths' per-sample records (L, 16 B) and its camera stage (k_paths_camera: 5 x 16 B, plus
-// 16 B of PCG32 state for the IndependentSampler), independent of the wavefront SoA
+// k_paths' per-sample records (L, 16 B) and its camera stage (k_paths_camera: 6 x 16 B + the
+// 4-B filter weight), independent of the wavefront SoA
 int ensure_records(avr_context *c, long long n) {
     if (n <= c->rec_cap) return AVR_OK;
     free_records(c);
@@ -220,6 +223,7 @@ int ensure_records(avr_context *c, long long n) {
     HIP_TRY(dalloc(&c->ps.cam3, (size_t)n));
     HIP_TRY(dalloc(&c->ps.cam4, (size_t)n));
     HIP_TRY(dalloc(&c->ps.cam5, (size_t)n));
+    HIP_TRY(dalloc(&c->ps.camw, (size_t)n));
     c->rec_cap = n;
     return AVR_OK;
 }
@@ -1547,7 +1551,7 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
             p.rec_mode = 1;   // k_film reads the records k_paths wrote (in slot order)
             p.pix_slot = c->d_pix_slot;
             p.fast = c->render_mode;
-            hipLaunchKernelGGL(avr::k_film, dim3(blocks_for(P)), dim3(256), avr::film_lds_bytes(c->film.nbuckets),
+            hipLaunchKernelGGL((c->film.nbuckets > 0 ? avr::k_film<true> : avr::k_film<false>), dim3(blocks_for(P)), dim3(256), avr::film_lds_bytes(c->film.nbuckets),
                                c->stream, p);
             HIP_TRY(hipGetLastError());
             EV_MARK(e2);
@@ -1638,7 +1642,7 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
             first = false;
         }
         EV_MARK(f0);
-        hipLaunchKernelGGL(avr::k_film, dim3(blocks_for(P)), dim3(256), avr::film_lds_bytes(c->film.nbuckets), c->stream, p);
+        hipLaunchKernelGGL((c->film.nbuckets > 0 ? avr::k_film<true> : avr::k_film<false>), dim3(blocks_for(P)), dim3(256), avr::film_lds_bytes(c->film.nbuckets), c->stream, p);
         HIP_TRY(hipGetLastError());
         EV_MARK(f1);
         c->timed.push_back({f0, f1, &avr_stats::ms_film, false});

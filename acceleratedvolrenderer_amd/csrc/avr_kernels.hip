@@ -147,6 +147,13 @@ __device__ __forceinline__ Spec film_sample_lambda_fast(const DevFilm &f, float 
 __device__ __forceinline__ float film_lambda_pdf(const DevFilm &f, float l) {
     return f.nbuckets > 0 ? 1 / (f.lmax - f.lmin) : visible_wavelength_pdf(l);
 }
+// the camera stage's: canonical tables staged in LDS (canon::kCanonTabDoubles at `tabs`)
+__device__ __forceinline__ Spec film_sample_lambda(const DevFilm &f, float u, const double *tabs) {
+    return f.nbuckets > 0 ? sample_uniform_lambda(u, f.lmin, f.lmax) : sample_visible_lambda(u, tabs);
+}
+__device__ __forceinline__ float film_lambda_pdf(const DevFilm &f, float l, const double *tabs) {
+    return f.nbuckets > 0 ? 1 / (f.lmax - f.lmin) : visible_wavelength_pdf(l, tabs);
+}
 
 // Interface sphere (DevMedium::boundary 1). Model, shared with the oracle: the medium lives
 // inside the sphere; a camera ray that crosses it starts its first medium segment at the
@@ -179,9 +186,12 @@ struct PathSoA {
     // k_paths' camera stage (k_paths_camera, one lane per sample of the pass), read by the
     // refill and by k_film: cam0 {o, u}, cam1 {d, filter weight}, cam2 lambda, cam3 the first
     // segment's RNG SetSequence arguments {seqA, seqB} (u64 each), cam4 the wavelength pdfs,
-    // cam5 the IndependentSampler's PCG32 {state, inc} after the camera draws
+    // cam5 the IndependentSampler's PCG32 {state, inc} after the camera draws (ZSobol: the
+    // first light-pick draw and the sample's 64-bit Morton index {ul, lo, hi, 0}), camw the
+    // filter weight alone (k_film's 4-B read)
     float4 *cam0, *cam1, *cam2, *cam4;
     uint4 *cam3, *cam5;
+    float *camw;
 };
 struct ShadowSoA {
     int *path;
@@ -904,9 +914,10 @@ __device__ __forceinline__ uint32_t zsobol_lower_quad(M morton, uint32_t dimensi
     return idx;
 }
 // ZSobol::get1d / get2d with the quad-shared lower digits (kW: 1 32-bit, 2 64-bit index)
+constexpr uint32_t kCamDimHash = 16;   // the camera stage's draws end at dimension 10
 template <int kW>
 __device__ __forceinline__ void zsobol_draw_quad(smp::ZSobol &z, const smp::ZSobolParams &zp, bool two, float *u0,
-                                                 float *u1) {
+                                                 float *u1, const uint64_t *dh = nullptr) {
     uint32_t a, ah = 0;
     const uint32_t pm = kW == 2 ? (uint32_t)((((uint64_t)z.hi << 32) | z.morton) >> zp.log2spp) : z.morton >> zp.log2spp;
     const uint32_t up = (zp.upper && (int)z.dimension < zp.dmax) ? zp.upper[(size_t)pm * (size_t)zp.dmax + z.dimension]
@@ -920,7 +931,8 @@ __device__ __forceinline__ void zsobol_draw_quad(smp::ZSobol &z, const smp::ZSob
         a = (up << zp.log2spp) | zsobol_lower_quad<uint32_t>(z.morton, z.dimension, zp);
     }
     z.dimension += two ? 2 : 1;
-    const uint64_t h = smp::hash_2u32(z.dimension, (uint32_t)zp.seed);
+    // Hash(dimension, seed): from the caller's staged table when it covers the dimension
+    const uint64_t h = (dh && z.dimension < kCamDimHash) ? dh[z.dimension] : smp::hash_2u32(z.dimension, (uint32_t)zp.seed);
     *u0 = smp::u32_to_unit(smp::fast_owen(smp::sobol_bits(a, 0), (uint32_t)h));
     if (two) *u1 = smp::u32_to_unit(smp::fast_owen(smp::sobol_bits64(a, ah, 1), (uint32_t)(h >> 32)));
 }
@@ -940,6 +952,12 @@ __device__ __forceinline__ void zsobol_draw_quad(smp::ZSobol &z, const smp::ZSob
 #define AVR_CAM_EXPERIMENT 0
 #endif
 __device__ __forceinline__ float u32_to_unit_exp(uint32_t v) { return (float)(v >> 8) * 0x1p-24f; }
+#ifndef AVR_CAM_DIM_HASH
+#define AVR_CAM_DIM_HASH 1    // the camera stage's ZSobol draws read Hash(dimension, seed) from LDS
+#endif
+#ifndef AVR_CAM_CANON_LDS
+#define AVR_CAM_CANON_LDS 1   // the camera stage's wavelength math reads the canonical tables from LDS
+#endif
 #ifndef AVR_CAM_WAVES
 #define AVR_CAM_WAVES 1   // minimum waves per SIMD asked of k_paths_camera (1: the compiler's choice)
 #endif
@@ -947,7 +965,14 @@ template <int kSmp, bool kFast>
 __global__ void __launch_bounds__(256, AVR_CAM_WAVES) k_paths_camera(Params P) {
     __shared__ float s_filt[kFiltLds];
     __shared__ smp::FilterTables s_ftab;
-    stage_filter(P, s_filt, &s_ftab);
+    __shared__ double s_canon[canon::kCanonTabDoubles];
+    if constexpr (AVR_CAM_CANON_LDS)   // (fast mode too: the pdfs stay canonical)
+        for (int i = threadIdx.x; i < canon::kCanonTabDoubles; i += blockDim.x)
+            s_canon[i] = i < 128 ? canon::kLogInvC[i] : (i < 256 ? canon::kLogC[i - 128] : canon::kExp2J64[i - 256]);
+    __shared__ uint64_t s_cdh[kCamDimHash];
+    if constexpr (kSmp != 0)
+        if (threadIdx.x < kCamDimHash) s_cdh[threadIdx.x] = smp::hash_2u32(threadIdx.x, (uint32_t)P.zs.seed);
+    stage_filter(P, s_filt, &s_ftab);   // (its barrier covers s_canon and s_cdh)
     const int npix = P.pass_pixels;
     const long long n = (long long)npix * P.pass_samples;
     // ZSobol quads (zsobol_draw_quad): lanes 4a .. 4a+3 take samples 4m .. 4m+3 of one pixel
@@ -986,7 +1011,7 @@ __global__ void __launch_bounds__(256, AVR_CAM_WAVES) k_paths_camera(Params P) {
             if constexpr (kSmp != 0) {
                 if (quad) {
                     float a, b;
-                    zsobol_draw_quad<PathSampler<kSmp>::kW>(smp.z, P.zs, false, &a, &b);
+                    zsobol_draw_quad<PathSampler<kSmp>::kW>(smp.z, P.zs, false, &a, &b, AVR_CAM_DIM_HASH ? s_cdh : nullptr);
                     return a;
                 }
             }
@@ -997,9 +1022,15 @@ __global__ void __launch_bounds__(256, AVR_CAM_WAVES) k_paths_camera(Params P) {
         const Spec lam = {360 + 470 * ulam, 360 + 470 * (1 - ulam), 400 + 400 * ulam, 600 - 200 * ulam};
         const Spec pdf = Spec::c(1.f / 470);
 #else
+#if AVR_CAM_CANON_LDS
+        const Spec lam = kFast ? film_sample_lambda_fast(P.film, ulam) : film_sample_lambda(P.film, ulam, s_canon);
+        const Spec pdf = {film_lambda_pdf(P.film, lam.v0, s_canon), film_lambda_pdf(P.film, lam.v1, s_canon),
+                          film_lambda_pdf(P.film, lam.v2, s_canon), film_lambda_pdf(P.film, lam.v3, s_canon)};
+#else
         const Spec lam = kFast ? film_sample_lambda_fast(P.film, ulam) : film_sample_lambda(P.film, ulam);
         const Spec pdf = {film_lambda_pdf(P.film, lam.v0), film_lambda_pdf(P.film, lam.v1),
                           film_lambda_pdf(P.film, lam.v2), film_lambda_pdf(P.film, lam.v3)};
+#endif
 #endif
         float pFilmX, pFilmY, fweight;
         if constexpr (kSmp != 0) {
@@ -1008,7 +1039,7 @@ __global__ void __launch_bounds__(256, AVR_CAM_WAVES) k_paths_camera(Params P) {
             fu0 = get1();
             fu1 = get1();
 #else
-            if (quad) zsobol_draw_quad<PathSampler<kSmp>::kW>(smp.z, P.zs, true, &fu0, &fu1);
+            if (quad) zsobol_draw_quad<PathSampler<kSmp>::kW>(smp.z, P.zs, true, &fu0, &fu1, AVR_CAM_DIM_HASH ? s_cdh : nullptr);
             else smp.get2d(P, &fu0, &fu1);
 #endif
             camera_filter(P, px, py, fu0, fu1, &pFilmX, &pFilmY, &fweight, &s_ftab);
@@ -1039,11 +1070,12 @@ __global__ void __launch_bounds__(256, AVR_CAM_WAVES) k_paths_camera(Params P) {
         P.ps.cam2[id] = to4(lam);
         P.ps.cam3[id] = make_uint4((uint32_t)seqA, (uint32_t)(seqA >> 32), (uint32_t)seqB, (uint32_t)(seqB >> 32));
         P.ps.cam4[id] = to4(pdf);
+        P.ps.camw[id] = fweight;
         if constexpr (kSmp == 0)
             P.ps.cam5[id] = make_uint4((uint32_t)smp.rng.state, (uint32_t)(smp.rng.state >> 32), (uint32_t)smp.rng.inc,
                                        (uint32_t)(smp.rng.inc >> 32));
-        else
-            P.ps.cam5[id] = make_uint4(f2u(ulight), 0u, 0u, 0u);
+        else   // ZSobol: the first light pick and the sample's Morton index (k_paths' refill)
+            P.ps.cam5[id] = make_uint4(f2u(ulight), smp.z.morton, smp.z.hi, 0u);
     }
 }
 #endif
@@ -1568,6 +1600,9 @@ __global__ void __launch_bounds__(256) k_bin_scatter(const int *__restrict__ que
 #ifndef AVR_COOP_SPEC
 #define AVR_COOP_SPEC 1
 #endif
+#ifndef AVR_REFILL_MORTON
+#define AVR_REFILL_MORTON 1   // the refill takes the sample's Morton index from the camera stage
+#endif
 #ifndef AVR_DIM_HASH
 #define AVR_DIM_HASH 1   // the cooperative draws read Hash(d, seed) from the LDS table
 #endif
@@ -2007,11 +2042,20 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
                     const float4 c0 = P.ps.cam0[g], c1 = P.ps.cam1[g], c2 = P.ps.cam2[g];
                     const uint4 c3 = P.ps.cam3[g];
                     if constexpr (kZSobol) {
+                        // the sample's Morton index from the camera stage (== smp.start of its
+                        // pixel and sample index), past the camera draws and the first segment's three
+#if AVR_REFILL_MORTON
+                        const uint4 c5 = P.ps.cam5[g];
+                        smp.z.morton = c5.y;
+                        smp.z.hi = c5.z;
+                        if constexpr (kUlAhead) s_ul[threadIdx.x] = __uint_as_float(c5.x);
+#else
                         const int slot = g % npix, sIdx = g / npix;
                         const int pix = P.pix_order ? P.pix_order[slot] : slot;
                         smp.start(P, pix % P.film.width, pix / P.film.width, P.sample_base + sIdx);
-                        smp.z.dimension = 9;   // past the camera draws and the first segment's three
                         if constexpr (kUlAhead) s_ul[threadIdx.x] = __uint_as_float(P.ps.cam5[g].x);
+#endif
+                        smp.z.dimension = 9;
                     } else {
                         const uint4 c5 = P.ps.cam5[g];
                         smp.rng.state = ((uint64_t)c5.y << 32) | c5.x;
@@ -2283,7 +2327,7 @@ __device__ __forceinline__ void film_load_sample(const Params &P, size_t id, Spe
         *L = spec4(P.ps.rec[id]);
         *lam = spec4(P.ps.cam2[id]);
         *pdf = spec4(P.ps.cam4[id]);
-        if (P.film.filter_type != 0) *w = P.ps.cam1[id].w;
+        if (P.film.filter_type != 0) *w = P.ps.camw[id];
     } else {
         *L = spec4(P.ps.L[id]);
         *lam = spec4(P.ps.lambda[id]);
@@ -2292,30 +2336,57 @@ __device__ __forceinline__ void film_load_sample(const Params &P, size_t id, Spe
         if (P.film.filter_type != 0) *w = P.ps.weight[id];
     }
 }
+// The X, Y, Z matching tables interleaved per wavelength ({X, Y, Z, 0}, staged in LDS by
+// k_film): one 16-B read per wavelength instead of four table gathers; same values, same sums
+__device__ __forceinline__ float4 xyz_at(const float4 *t, int off) {
+    return (off < 0 || off >= kNTable) ? make_float4(0.f, 0.f, 0.f, 0.f) : t[off];
+}
 // The NaN/Inf guard (integrators.cpp:272-282; a bad sample's L becomes 0, in place) and
 // PixelSensor::ToSensorRGB with RGBFilm's maxComponentValue clamp (film.h:95-100, 239-250)
-__device__ __forceinline__ void film_sensor_rgb(const Params &P, Spec &L, const Spec &lam, const Spec &pdf, float rgb[3]) {
+__device__ __forceinline__ void film_sensor_rgb(const Params &P, Spec &L, const Spec &lam, const Spec &pdf, float rgb[3],
+                                                const float4 *xyz4) {
     const LambdaIdx li = lambda_index(lam);
+    const float4 t0 = xyz_at(xyz4, li.o0), t1 = xyz_at(xyz4, li.o1), t2 = xyz_at(xyz4, li.o2), t3 = xyz_at(xyz4, li.o3);
     bool bad = __builtin_isnan(L.v0) || __builtin_isnan(L.v1) || __builtin_isnan(L.v2) || __builtin_isnan(L.v3);
-    if (!bad) {
-        const Spec Ys = sample_table(P.film.xyz + kNTable, li);
+    // y = avg(Y L / pdf) / CIE_Y_integral is finite whenever max|L| max|Y| < 1e37 min(pdf) (each
+    // term below 1e37, the sum below 4e37 < FLT_MAX); only samples outside that bound (or with
+    // an overflowing bound) evaluate it
+    const float aL = fmaxf_(fmaxf_(__builtin_fabsf(L.v0), __builtin_fabsf(L.v1)),
+                            fmaxf_(__builtin_fabsf(L.v2), __builtin_fabsf(L.v3)));
+    const float aY = fmaxf_(fmaxf_(__builtin_fabsf(t0.y), __builtin_fabsf(t1.y)),
+                            fmaxf_(__builtin_fabsf(t2.y), __builtin_fabsf(t3.y)));
+    const float mp = fminf_(fminf_(pdf.v0, pdf.v1), fminf_(pdf.v2, pdf.v3));
+    if (!bad && !(aL * aY < 1e37f * mp)) {
+        const Spec Ys = {t0.y, t1.y, t2.y, t3.y};
         float y = safe_div(Ys * L, pdf).avg() / 106.856895f;
         bad = __builtin_isinf(y);
     }
     if (bad) L = Spec::c(0.f);
     const Spec Ld = safe_div(L, pdf);
-    for (int c = 0; c < 3; ++c) rgb[c] = (sample_table(P.film.xyz + kNTable * c, li) * Ld).avg() * P.film.imaging_ratio;
+    rgb[0] = (Spec{t0.x, t1.x, t2.x, t3.x} * Ld).avg() * P.film.imaging_ratio;
+    rgb[1] = (Spec{t0.y, t1.y, t2.y, t3.y} * Ld).avg() * P.film.imaging_ratio;
+    rgb[2] = (Spec{t0.z, t1.z, t2.z, t3.z} * Ld).avg() * P.film.imaging_ratio;
     float mx = fmaxf_(fmaxf_(rgb[0], rgb[1]), rgb[2]);
     if (mx > P.film.max_component)
         for (int c = 0; c < 3; ++c) rgb[c] *= P.film.max_component / mx;
 }
 
 constexpr int kFilmLdsBuckets = 16;
+#ifndef AVR_FILM_BATCH
+#define AVR_FILM_BATCH 4
+#endif
+constexpr int kFilmBatch = AVR_FILM_BATCH;
 inline size_t film_lds_bytes(int nb) { return nb > 0 && nb <= kFilmLdsBuckets ? 2 * (size_t)nb * 256 * sizeof(double) : 0; }
+// kBuckets: a SpectralFilm (P.film.nbuckets > 0); RGBFilm's instantiation has no bucket code
+template <bool kBuckets>
 __global__ void __launch_bounds__(256) k_film(Params P) {
     extern __shared__ double s_bk[];   // [sum | weight][bucket][thread]: film_lds_bytes(nb)
+    __shared__ float4 s_xyz[kNTable];
+    for (int i = threadIdx.x; i < kNTable; i += blockDim.x)
+        s_xyz[i] = make_float4(P.film.xyz[i], P.film.xyz[kNTable + i], P.film.xyz[2 * kNTable + i], 0.f);
+    __syncthreads();
     const int npix = P.pass_pixels;
-    const int nb = P.film.nbuckets;
+    const int nb = kBuckets ? P.film.nbuckets : 0;
     const bool ldsBuckets = nb > 0 && nb <= kFilmLdsBuckets;
     for (int pix = blockIdx.x * blockDim.x + threadIdx.x; pix < npix; pix += gridDim.x * blockDim.x) {
         double s0 = P.film.rgb_sum[3 * (size_t)pix], s1 = P.film.rgb_sum[3 * (size_t)pix + 1],
@@ -2333,18 +2404,15 @@ __global__ void __launch_bounds__(256) k_film(Params P) {
             }
         }
         const int slot = P.pix_slot ? P.pix_slot[pix] : pix;   // where k_paths traced this pixel
-        for (int s = 0; s < P.pass_samples; ++s) {
-            const size_t id = (size_t)s * npix + slot;
-            Spec L, lam, pdf;
-            float w;
-            film_load_sample(P, id, &L, &lam, &pdf, &w);
+        // one sample into the sums, in sampleIndex order (the fp64 additions' order is the film's)
+        auto add = [&](Spec L, const Spec &lam, const Spec &pdf, float w) {
             float rgb[3];
-            film_sensor_rgb(P, L, lam, pdf, rgb);
+            film_sensor_rgb(P, L, lam, pdf, rgb, s_xyz);
             s0 += (double)(w * rgb[0]);
             s1 += (double)(w * rgb[1]);
             s2 += (double)(w * rgb[2]);
             ws += (double)w;
-            if (P.film.nbuckets > 0) {
+            if (kBuckets) {
                 // SpectralFilm::AddSample (film.h:436-454): clamp by the max component, scale by
                 // weight * CIE_Y_integral, one bucket per wavelength (LambdaToBucket, 500-504)
                 const float lm = fmaxf_(fmaxf_(fmaxf_(L.v0, L.v1), L.v2), L.v3);
@@ -2358,6 +2426,22 @@ __global__ void __launch_bounds__(256) k_film(Params P) {
                     bw[b * bstride] += (double)w;
                 }
             }
+        };
+        // the pass's samples in groups of kFilmBatch: all of a group's loads are issued before
+        // its (possibly storing) accumulation, so a wave keeps kFilmBatch x 52 B per lane in flight
+        int s = 0;
+        for (; s + kFilmBatch <= P.pass_samples; s += kFilmBatch) {
+            Spec L[kFilmBatch], lam[kFilmBatch], pdf[kFilmBatch];
+            float w[kFilmBatch];
+            _Pragma("unroll") for (int k = 0; k < kFilmBatch; ++k)
+                film_load_sample(P, (size_t)(s + k) * npix + slot, &L[k], &lam[k], &pdf[k], &w[k]);
+            _Pragma("unroll") for (int k = 0; k < kFilmBatch; ++k) add(L[k], lam[k], pdf[k], w[k]);
+        }
+        for (; s < P.pass_samples; ++s) {
+            Spec L, lam, pdf;
+            float w;
+            film_load_sample(P, (size_t)s * npix + slot, &L, &lam, &pdf, &w);
+            add(L, lam, pdf, w);
         }
         if (ldsBuckets)
             for (int b = 0; b < nb; ++b) {

@@ -232,6 +232,15 @@ AVR_HD float visible_wavelength_pdf(float l) {
     if (l < 360 || l > 830) return 0;
     return 0.0039398042f / sqr(cr_cosh(0.0072f * (l - 538)));
 }
+// The camera stage's versions: the canonical tables read from a staged (LDS) copy and the
+// four evaluations left unfenced, so their table reads overlap — same arithmetic, same bits
+AVR_HD float sample_visible_wavelength(float u, const double *tabs) {
+    return 538 - 138.888889f * canon::atanh_f(0.85691062f - 1.82750197f * u, tabs);
+}
+AVR_HD float visible_wavelength_pdf(float l, const double *tabs) {
+    if (l < 360 || l > 830) return 0;
+    return 0.0039398042f / sqr(canon::cosh_f(0.0072f * (l - 538), tabs));
+}
 struct Lambda { Spec l, pdf; };
 // Device: the four f64 evaluations are kept apart (scheduling barriers) so their
 // temporaries are not all live at once in the register-bound path kernel.
@@ -262,6 +271,10 @@ AVR_HD Spec sample_visible_lambda(float u) {
 }
 // SampledWavelengths::SampleUniform (spectrum.h:287-306): Lerp(u, min, max), then steps of
 // (max - min) / 4 wrapped into the range; pdf 1 / (max - min)
+AVR_HD Spec sample_visible_lambda(float u, const double *tabs) {
+    return {sample_visible_wavelength(visible_up(u, 0), tabs), sample_visible_wavelength(visible_up(u, 1), tabs),
+            sample_visible_wavelength(visible_up(u, 2), tabs), sample_visible_wavelength(visible_up(u, 3), tabs)};
+}
 AVR_HD Spec sample_uniform_lambda(float u, float lmin, float lmax) {
     Spec l;
     l.v0 = (1 - u) * lmin + u * lmax;
