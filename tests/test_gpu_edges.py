@@ -338,3 +338,34 @@ def test_pixel_order_changes_order_not_results(sampler):
     rgb3, _ = integ.render()
     assert np.array_equal(rgb, rgb3)
     integ.close()
+
+
+@pytest.mark.parametrize("kernel", ["persistent", "wavefront"])
+def test_film_nan_inf_guard_with_overflowing_radiance(kernel):
+    """The NaN / Inf guard before RGBFilm::AddSample (integrators.cpp:272-282): a sample whose
+    L.y(lambda) overflows is dropped (L = 0). An emissive medium whose Lescale spans 1e26..1e38
+    along x puts samples below k_film's finite-y bound (no divisions) and between the bound and
+    FLT_MAX (the exact guard evaluates y and keeps or drops them; sensor RGB components may
+    overflow to inf in kept samples, as in pbrt): the GPU film must equal the canonical
+    oracle's, sample for sample and sum for sum (inf included)."""
+    from acceleratedvolrenderer_amd import scenes
+    from acceleratedvolrenderer_amd.scene import GridMedium
+    n, W, H, spp = 8, 24, 16, 4
+    dens = (0.5 + np.random.default_rng(11).random((n, n, n), dtype=np.float32)).astype(np.float32)
+    scene = _scene(W, H, dens, variant="emissive")
+    x = np.linspace(0.0, 1.0, n)
+    les = np.broadcast_to((10.0 ** (26.0 + 12.0 * x)).astype(np.float32), (n, n, n)).copy()
+    m = scene.medium
+    scene.medium = GridMedium(dens, sigma_a=0.6, sigma_s=1.5, g=-0.2, Le=(0.5 + np.linspace(0, 1, 471) ** 2)
+                              .astype(np.float32), Lescale=les)
+    del m
+    integ, frac, rgb, w, rgb_o, w_o = _replay(scene, 4, spp, kernel)
+    _, _, L, _, _ = integ.ctx.last_pass_samples(W * H, spp)
+    big = np.max(np.abs(L), axis=1)
+    print(f"{kernel}: {int(np.sum(big < 1e30))} samples < 1e30, {int(np.sum((big >= 1e30) & np.isfinite(big)))} "
+          f"in [1e30, FLT_MAX], {int(np.sum(~np.isfinite(big)))} non-finite; replay {frac:.4f}")
+    assert np.sum(big < 1e30) > 0 and np.sum((big >= 1e33) & np.isfinite(big)) > 0
+    assert not np.isfinite(rgb_o).all(), "some kept samples overflow a sensor RGB component"
+    assert frac == 1.0
+    assert np.array_equal(w, w_o) and np.array_equal(rgb, rgb_o, equal_nan=True)
+    integ.close()
