@@ -187,8 +187,7 @@ struct PathSoA {
     // refill and by k_film: cam0 {o, u}, cam1 {d, filter weight}, cam2 lambda, cam3 the first
     // segment's RNG SetSequence arguments {seqA, seqB} (u64 each), cam4 the wavelength pdfs,
     // cam5 the IndependentSampler's PCG32 {state, inc} after the camera draws (ZSobol: the
-    // first light-pick draw and the sample's 64-bit Morton index {ul, lo, hi, 0}), camw the
-    // filter weight alone (k_film's 4-B read)
+    // first light-pick draw in .x), camw the filter weight alone (k_film's 4-B read)
     float4 *cam0, *cam1, *cam2, *cam4;
     uint4 *cam3, *cam5;
     float *camw;
@@ -1074,8 +1073,8 @@ __global__ void __launch_bounds__(256, AVR_CAM_WAVES) k_paths_camera(Params P) {
         if constexpr (kSmp == 0)
             P.ps.cam5[id] = make_uint4((uint32_t)smp.rng.state, (uint32_t)(smp.rng.state >> 32), (uint32_t)smp.rng.inc,
                                        (uint32_t)(smp.rng.inc >> 32));
-        else   // ZSobol: the first light pick and the sample's Morton index (k_paths' refill)
-            P.ps.cam5[id] = make_uint4(f2u(ulight), smp.z.morton, smp.z.hi, 0u);
+        else   // ZSobol: the first light pick (k_paths' refill)
+            P.ps.cam5[id] = make_uint4(f2u(ulight), 0u, 0u, 0u);
     }
 }
 #endif
@@ -1438,13 +1437,12 @@ struct DdaL {
     int pidx;              // cell whose majorant mcur holds (vidx, clamped into the grid)
     float mcur;            // majorant of cell pidx, loaded one step ahead (software pipelining):
                            // the caller reloads it (ddal_prefetch) unconditionally every iteration
-    bool zn;               // AVR_VDB_ZSKIP: cell pidx is known zero from the LDS occupancy level
 };
 __device__ __forceinline__ void ddal_init(DdaL &q, const DevMedium &m, Ray ray, float raytMax, const float *maj) {
     Dda it;
     if (!dda_init(it, m, ray, raytMax)) {
         q.tMin = kInf; q.tMax = -kInf;
-        q.nx = q.ny = q.nz = q.dx = q.dy = q.dz = 0; q.vidx = 0; q.rem = 0; q.pidx = 0; q.mcur = 0; q.zn = false;
+        q.nx = q.ny = q.nz = q.dx = q.dy = q.dz = 0; q.vidx = 0; q.rem = 0; q.pidx = 0; q.mcur = 0;
         return;
     }
     q.tMin = it.tMin; q.tMax = it.tMax;
@@ -1459,7 +1457,6 @@ __device__ __forceinline__ void ddal_init(DdaL &q, const DevMedium &m, Ray ray, 
     q.rem = cx | (cy << 8) | (cz << 16);
     q.pidx = q.vidx;
     q.mcur = maj[q.vidx];
-    q.zn = false;
 }
 // Reload mcur from pidx: one load per loop iteration into the loop-carried register, so the
 // wait for it lands at the next ddal_next (a load inside ddal_next's predicated block is
@@ -1473,17 +1470,9 @@ __device__ __forceinline__ void ddal_prefetch_occ(DdaL &q, const float *maj, con
     const unsigned w = occ[p >> 6];
     q.mcur = maj[((w >> ((p >> 1) & 31)) & 1u) ? p : ncells];
 }
-// AVR_VDB_ZSKIP: the L2 read is issued for every cell as ddal_prefetch does, and the cell's
-// occupancy pair bit comes from LDS next to it; a wave whose stepping lanes all sit in
-// known-zero cells then yields 0 without waiting for the read (same value either way)
-__device__ __forceinline__ void ddal_prefetch_zn(DdaL &q, const float *maj, const unsigned *occ) {
-    const int p = q.pidx;
-    q.mcur = maj[p];
-    q.zn = ((occ[p >> 6] >> ((p >> 1) & 31)) & 1u) == 0;
-}
 // Next(): false when exhausted. `maj` is the LDS copy; sy/sz the linear strides of y and z.
 __device__ __forceinline__ bool ddal_next(DdaL &q, const float *maj, int sy, int sz, int ncells, float *s0, float *s1,
-                                          float *mval, float mcur) {
+                                          float *mval) {
     // fields are copied to values first: a select between struct members invites the
     // compiler to turn the struct into a scratch array indexed by the axis
     const float tMin = q.tMin, tMax = q.tMax, nx = q.nx, ny = q.ny, nz = q.nz;
@@ -1497,7 +1486,7 @@ __device__ __forceinline__ bool ddal_next(DdaL &q, const float *maj, int sy, int
     const float dA = ax0 ? dx : (ax1 ? dy : dz);
     const int shift = ax0 ? 0 : (ax1 ? 8 : 16);
     const int stride = ax0 ? 1 : (ax1 ? sy : sz);
-    *mval = mcur;
+    *mval = q.mcur;
     *s0 = tMin;
     const float tExit = fminf_(tMax, nextA);
     *s1 = tExit;
@@ -1609,12 +1598,6 @@ __global__ void __launch_bounds__(256) k_bin_scatter(const int *__restrict__ que
 #endif
 #ifndef AVR_COOP_SPEC
 #define AVR_COOP_SPEC 1
-#endif
-#ifndef AVR_VDB_ZSKIP
-#define AVR_VDB_ZSKIP 0   // NanoVDB with the occupancy level: skip the majorant wait in all-zero steps
-#endif
-#ifndef AVR_REFILL_MORTON
-#define AVR_REFILL_MORTON 1   // the refill takes the sample's Morton index from the camera stage
 #endif
 #ifndef AVR_DIM_HASH
 #define AVR_DIM_HASH 1   // the cooperative draws read Hash(d, seed) from the LDS table
@@ -2055,19 +2038,11 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
                     const float4 c0 = P.ps.cam0[g], c1 = P.ps.cam1[g], c2 = P.ps.cam2[g];
                     const uint4 c3 = P.ps.cam3[g];
                     if constexpr (kZSobol) {
-                        // the sample's Morton index from the camera stage (== smp.start of its
-                        // pixel and sample index), past the camera draws and the first segment's three
-#if AVR_REFILL_MORTON
-                        const uint4 c5 = P.ps.cam5[g];
-                        smp.z.morton = c5.y;
-                        smp.z.hi = c5.z;
-                        if constexpr (kUlAhead) s_ul[threadIdx.x] = __uint_as_float(c5.x);
-#else
+                        // the sample's ZSobol state past the camera draws and the first segment's three
                         const int slot = g % npix, sIdx = g / npix;
                         const int pix = P.pix_order ? P.pix_order[slot] : slot;
                         smp.start(P, pix % P.film.width, pix / P.film.width, P.sample_base + sIdx);
                         if constexpr (kUlAhead) s_ul[threadIdx.x] = __uint_as_float(P.ps.cam5[g].x);
-#endif
                         smp.z.dimension = 9;
                     } else {
                         const uint4 c5 = P.ps.cam5[g];
@@ -2139,19 +2114,9 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
             // loop has one wave-uniform exit so the body stays predicated (no per-exit masks).
             int walk = 0;
             for (int b = 0; b < P.dda_budget; ++b) {
-                float mc = it.mcur;
-                if constexpr (kVdb && AVR_VDB_ZSKIP) {
-                    if (useOcc) {
-                        mc = 0.f;
-                        if (__ballot(walk == 0 && needNext && !it.zn)) {   // the only wait for the read
-                            mc = it.mcur;
-                            asm volatile("" : "+v"(mc));
-                        }
-                    }
-                }
                 if (walk == 0 && needNext) {
                     float s0, s1;
-                    if (!ddal_next(it, majp, maj_sy, maj_sz, maj_n, &s0, &s1, &mv, mc)) {
+                    if (!ddal_next(it, majp, maj_sy, maj_sz, maj_n, &s0, &s1, &mv)) {
                         walk = 2;
                     } else {
                         ++nSteps;
@@ -2172,12 +2137,8 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
                     }
                 }
                 // unconditional (all busy lanes): in flight during the candidate test below
-                if (kVdb && useOcc) {
-                    if constexpr (AVR_VDB_ZSKIP) ddal_prefetch_zn(it, majp, s_occ);
-                    else ddal_prefetch_occ(it, majp, s_occ, maj_n);
-                } else {
-                    ddal_prefetch(it, majp);
-                }
+                if (kVdb && useOcc) ddal_prefetch_occ(it, majp, s_occ, maj_n);
+                else ddal_prefetch(it, majp);
                 if (walk == 0 && !needNext) {
                     // Fast reject: the candidate t = tMin - log(1-u)/sigma_maj is decided against
                     // segMax from the hardware log2 (v_log_f32, ~1 ulp) when it lies outside an
