@@ -24,6 +24,7 @@ import csv
 import glob
 import json
 import os
+import re
 import shutil
 import subprocess
 import sys
@@ -185,10 +186,11 @@ def cpu_baseline(scene_host, spp_per_step, budget_s, label="S-cloud"):
                       f"scene, {t_used:.1f} s on {cores} threads"}
 
 
-def pmc_passes(args, kernel_substr="k_paths", timeout_s=240):
+def pmc_passes(args, kernel_re=r"\bk_paths<|\dk_pathsI", timeout_s=240):
     """rocprofv3 counter passes of this same bench configuration, one child process per
     pass (--pmc only: no tracing in the same run), each killed after timeout_s. Returns
-    per-launch averages of the dominant kernel's counters, or None."""
+    per-launch averages of the dominant kernel's counters, or None. kernel_re matches the
+    kernel name, demangled or mangled (k_paths itself, not the camera stage k_paths_camera)."""
     exe = shutil.which("rocprofv3")
     if exe is None:
         return None, "rocprofv3 not found"
@@ -219,7 +221,7 @@ def pmc_passes(args, kernel_substr="k_paths", timeout_s=240):
             per = {}
             for fn in files:
                 for row in csv.DictReader(open(fn)):
-                    if kernel_substr in row["Kernel_Name"]:
+                    if re.search(kernel_re, row["Kernel_Name"]):
                         per.setdefault(row["Counter_Name"], {}).setdefault(row.get("Dispatch_Id", ""), 0.0)
                         per[row["Counter_Name"]][row.get("Dispatch_Id", "")] += float(row["Counter_Value"])
             for cn, disp in per.items():
@@ -498,7 +500,7 @@ def main():
         traffic, limiter, pmc_note, cache = None, None, "pmc off", None
         want_pmc = args.pmc == "on" or (args.pmc == "auto" and world == 1)
         if want_pmc:
-            ctr, err = pmc_passes(args, kernel_substr="k_paths" if persistent else "k_medium")
+            ctr, err = pmc_passes(args, kernel_re=r"\bk_paths<|\dk_pathsI" if persistent else r"\bk_medium\b|\dk_mediumE")
             if ctr is None:
                 pmc_note = err
                 log(f"pmc: {err}")
