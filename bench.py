@@ -111,6 +111,30 @@ def log(msg):
     print(f"[bench] {msg}", file=sys.stderr, flush=True)
 
 
+class heartbeat:
+    """`with heartbeat("what"):` logs every `every` s while a long host step runs (NanoVDB
+    tree builds, the oracle's scene), so a supervisor watching the output sees progress."""
+
+    def __init__(self, what, every=30.0):
+        import threading
+        self.what, self.every, self.stop = what, every, threading.Event()
+        self.thread = threading.Thread(target=self._run, daemon=True)
+
+    def _run(self):
+        t0 = time.perf_counter()
+        while not self.stop.wait(self.every):
+            log(f"{self.what}: {time.perf_counter() - t0:.0f} s")
+
+    def __enter__(self):
+        self.thread.start()
+        return self
+
+    def __exit__(self, *exc):
+        self.stop.set()
+        self.thread.join()
+        return False
+
+
 def host_cpu_info():
     """Host cores this process may use: the affinity mask, capped by a cgroup CPU quota."""
     info = {"nproc": os.cpu_count() or 1}
@@ -209,12 +233,25 @@ def pmc_passes(args, kernel_re=r"\bk_paths<|\dk_pathsI", timeout_s=240):
             d = os.path.join(tmp, name)
             cmd = [exe, "--pmc", *counters, "-d", d, "-o", "run", "--output-format", "csv", "--"] + child
             log(f"pmc pass {name}: {' '.join(counters)}")
-            try:
-                r = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, timeout=timeout_s)
-            except subprocess.TimeoutExpired:
-                return None, f"pmc pass {name} timed out"
-            if r.returncode != 0:
-                return None, f"pmc pass {name} exited {r.returncode}: {r.stderr.decode(errors='replace')[-300:]}"
+            # the child rebuilds the scene (minutes for a host-built NanoVDB tree): log a heartbeat
+            # every 30 s so a supervisor that watches the output does not take the pass for a hang
+            errf = tempfile.TemporaryFile(dir=tmp)
+            proc = subprocess.Popen(cmd, stdout=subprocess.DEVNULL, stderr=errf)
+            t0 = time.perf_counter()
+            while True:
+                try:
+                    rc = proc.wait(timeout=30)
+                    break
+                except subprocess.TimeoutExpired:
+                    el = time.perf_counter() - t0
+                    if el > timeout_s:
+                        proc.kill()
+                        proc.wait()
+                        return None, f"pmc pass {name} timed out"
+                    log(f"pmc pass {name}: running {el:.0f} s")
+            if rc != 0:
+                errf.seek(0)
+                return None, f"pmc pass {name} exited {rc}: {errf.read().decode(errors='replace')[-300:]}"
             files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
             if not files:
                 return None, f"pmc pass {name}: no counter file"
@@ -315,7 +352,8 @@ def main():
             from acceleratedvolrenderer_amd.vdb import NanoVDBGrid
             vdb = NanoVDBGrid.read_nvdb(args.nvdb)
         else:
-            vdb = scenes.vdb_grid(density.cpu().numpy())
+            with heartbeat("NanoVDB tree from the dense grid"):
+                vdb = scenes.vdb_grid(density.cpu().numpy())
             if args.nvdb == "roundtrip":
                 from acceleratedvolrenderer_amd.vdb import NanoVDBGrid
                 tmpf = os.path.join(tempfile.mkdtemp(prefix="avr_nvdb_", dir=os.environ.get("TMPDIR", "/tmp")),
@@ -493,7 +531,8 @@ def main():
             else:
                 host_scene = scenes.s_cloud(host_density, width=args.width, height=args.height,
                                             sampler=args.sampler, spp=spp_total, filter=args.filter)
-            cpu = cpu_baseline(host_scene, S, args.cpu_seconds, f"{workload_name} {args.medium}")
+            with heartbeat("cpu baseline"):
+                cpu = cpu_baseline(host_scene, S, args.cpu_seconds, f"{workload_name} {args.medium}")
             host_scene = host_density = host_rgb = None
         # HBM traffic and the VALU limiter from rocprofv3 counter passes of this same
         # configuration (child processes; the guide's gfx950 rule: FETCH_SIZE x2 + WRITE_SIZE)
