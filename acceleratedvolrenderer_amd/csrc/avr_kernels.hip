@@ -616,7 +616,7 @@ __device__ __forceinline__ bool dda_next(Dda &it, const float *maj, const int *r
     // cmpToAxis = {2, 1, 2, 1, 2, 2, 0, 0}
     const int ax = (bits >= 6) ? 0 : ((bits == 1 || bits == 3) ? 1 : 2);
     const float nextA = ax == 0 ? it.nx : (ax == 1 ? it.ny : it.nz);
-    const float tExit = fminf_(it.tMax, nextA);
+    const float tExit = nextA < it.tMax ? nextA : it.tMax;   // std::min(tMax, next), NaN -> tMax
     *mval = maj[it.vx + res[0] * (it.vy + res[1] * it.vz)];
     *s0 = it.tMin;
     *s1 = tExit;
@@ -1488,12 +1488,15 @@ __device__ __forceinline__ bool ddal_next(DdaL &q, const float *maj, int sy, int
     const int stride = ax0 ? 1 : (ax1 ? sy : sz);
     *mval = q.mcur;
     *s0 = tMin;
-    const float tExit = fminf_(tMax, nextA);
+    // tVoxelExit = std::min(tMax, next) — (next < tMax) ? next : tMax, so a NaN crossing gives
+    // tMax as in pbrt; and with it pbrt's "next > tMax -> tMin = tMax" is already tExit
+    const float tExit = nextA < tMax ? nextA : tMax;
     *s1 = tExit;
     const bool last = ((rem >> shift) & 0xff) == 0;   // voxel + step == voxelLimit
-    q.tMin = (nextA > tMax || last) ? tMax : tExit;
+    q.tMin = last ? tMax : tExit;
     q.rem = rem - (1 << shift);
-    const int nv = vidx + (__builtin_signbit(dA) ? -stride : stride);
+    // step +-1 along the axis: the sign of deltaT as +-1 times the axis' linear stride
+    const int nv = vidx + __mul24(stride, (__float_as_int(dA) >> 31) | 1);
     q.vidx = nv;
     // the next cell's majorant is loaded by ddal_prefetch so its latency (L2 for NanoVDB's
     // 64^3 grid) hides behind this step's work; past the last cell the index is clamped
@@ -1501,7 +1504,7 @@ __device__ __forceinline__ bool ddal_next(DdaL &q, const float *maj, int sy, int
     const float nn = nextA + __builtin_fabsf(dA);
     q.nx = ax0 ? nn : nx;
     q.ny = ax1 ? nn : ny;
-    q.nz = (!ax0 && !ax1) ? nn : nz;
+    q.nz = (ax0 || ax1) ? nz : nn;
     return true;
 }
 
