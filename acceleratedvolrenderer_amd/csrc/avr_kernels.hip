@@ -187,7 +187,8 @@ struct PathSoA {
     // refill and by k_film: cam0 {o, u}, cam1 {d, filter weight}, cam2 lambda, cam3 the first
     // segment's RNG SetSequence arguments {seqA, seqB} (u64 each), cam4 the wavelength pdfs,
     // cam5 the IndependentSampler's PCG32 {state, inc} after the camera draws (ZSobol: the
-    // first light-pick draw in .x), camw the filter weight alone (k_film's 4-B read)
+    // first light-pick draw, 4 B per sample packed at the array's start), camw the filter
+    // weight alone (k_film's 4-B read)
     float4 *cam0, *cam1, *cam2, *cam4;
     uint4 *cam3, *cam5;
     float *camw;
@@ -1073,8 +1074,8 @@ __global__ void __launch_bounds__(256, AVR_CAM_WAVES) k_paths_camera(Params P) {
         if constexpr (kSmp == 0)
             P.ps.cam5[id] = make_uint4((uint32_t)smp.rng.state, (uint32_t)(smp.rng.state >> 32), (uint32_t)smp.rng.inc,
                                        (uint32_t)(smp.rng.inc >> 32));
-        else   // ZSobol: the first light pick (k_paths' refill)
-            P.ps.cam5[id] = make_uint4(f2u(ulight), 0u, 0u, 0u);
+        else   // ZSobol: the first light pick (k_paths' refill), packed 4 B per sample
+            reinterpret_cast<float *>(P.ps.cam5)[id] = ulight;
     }
 }
 #endif
@@ -1405,6 +1406,9 @@ __global__ void __launch_bounds__(256) k_shadow(Params P) {
 // Float operation order per path is identical to the wavefront kernels and to the CPU
 // oracle (cpu/integrators.cpp:962-1399, media.h:741-806).
 enum : int { M_FETCH = 0, M_MEDIUM = 1, M_SHADOW = 2, M_DONE = 3 };
+#ifndef AVR_EXP_NOSTORE
+#define AVR_EXP_NOSTORE 0   // measurement only (k_paths without its record store)
+#endif
 
 __device__ __forceinline__ int xcc_id() {
     unsigned v;
@@ -1997,7 +2001,11 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
         if (__ballot(ev == EV_END)) {
             if (ev == EV_END) {
                 // the per-sample record: L (k_film takes the rest from the camera stage)
+#if AVR_EXP_NOSTORE   // measurement only: the record store dropped (breaks the film)
+                if (L.v0 == -1.2345f) P.ps.rec[g] = to4(L);
+#else
                 P.ps.rec[g] = to4(L);
+#endif
                 mode = M_FETCH;
                 ev = EV_NONE;
             }
@@ -2045,7 +2053,7 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
                         const int slot = g % npix, sIdx = g / npix;
                         const int pix = P.pix_order ? P.pix_order[slot] : slot;
                         smp.start(P, pix % P.film.width, pix / P.film.width, P.sample_base + sIdx);
-                        if constexpr (kUlAhead) s_ul[threadIdx.x] = __uint_as_float(P.ps.cam5[g].x);
+                        if constexpr (kUlAhead) s_ul[threadIdx.x] = reinterpret_cast<const float *>(P.ps.cam5)[g];
                         smp.z.dimension = 9;
                     } else {
                         const uint4 c5 = P.ps.cam5[g];
