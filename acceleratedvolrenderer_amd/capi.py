@@ -102,6 +102,7 @@ SIGNATURES = {
     "avr_tune_majorant": (ctypes.c_int, [ctypes.c_void_p, c_int_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                          ctypes.c_int, ctypes.c_int, c_int_p, c_float_p]),
     "avr_set_refill_min": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "avr_light_sampler": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "avr_set_dda_budget": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "avr_set_grid_layout": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "avr_grid_layout_active": (ctypes.c_int, [ctypes.c_void_p]),
@@ -303,6 +304,10 @@ class Context:
 
     def set_dda_budget(self, cells):
         _check(self.lib.avr_set_dda_budget(self.h, int(cells)))
+
+    def set_light_sampler(self, kind):
+        """0: "bvh" / "uniform" (identical for infinite lights); 1: "power" (avr_light_sampler)."""
+        _check(self.lib.avr_light_sampler(self.h, int(kind)))
 
     def set_refill_min(self, lanes):
         _check(self.lib.avr_set_refill_min(self.h, int(lanes)))

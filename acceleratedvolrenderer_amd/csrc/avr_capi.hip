@@ -127,6 +127,11 @@ struct avr_context {
     float *d_illum = nullptr;
     // lights: host copy of the device list, ImageInfiniteLight buffers
     avr::DevLight h_lights[avr::kMaxLights] = {};
+    // PowerLightSampler: each light's Phi-based weight (phi_ok once known: an image light's
+    // needs its avr_light_image), and the sampler the render uses (0 BVH / uniform, 1 power)
+    float h_phi[avr::kMaxLights] = {};
+    bool phi_ok[avr::kMaxLights] = {};
+    int light_sampler = 0;
     void *d_light_img[avr::kMaxLights] = {};
     int n_image_lights = 0, image_lights_ready = 0;
     // film image / --mse-reference-image state
@@ -1107,6 +1112,117 @@ int avr_tune_majorant(avr_context *c, const int *candidates, int n, int spp_begi
 
 static void pc1d_build(const float *f, int n, float mn, float mx, float *cdf, float *funcInt);
 
+// ---------------------------------------------------------------------------
+// PowerLightSampler (lightsamplers.cpp:76-96): weight = Average(SafeDiv(Phi(lambda),
+// lambda.PDF())) at lambda = SampledWavelengths::SampleVisible(0.5) (canonical wavelength
+// math, as the device's), then an AliasTable over the weights (util/sampling.cpp:563-618).
+static avr::Spec visible_half_lambda(avr::Spec *pdf) {
+    const avr::Spec l = avr::sample_visible_lambda(0.5f);
+    *pdf = {avr::visible_wavelength_pdf(l.v0), avr::visible_wavelength_pdf(l.v1), avr::visible_wavelength_pdf(l.v2),
+            avr::visible_wavelength_pdf(l.v3)};
+    return l;
+}
+static float phi_weight(const avr::Spec &phi, const avr::Spec &pdf) {
+    // SafeDiv then SampledSpectrum::Average (spectrum.h:175-181): sum in order, / 4
+    const float a = pdf.v0 != 0 ? phi.v0 / pdf.v0 : 0.f, b = pdf.v1 != 0 ? phi.v1 / pdf.v1 : 0.f;
+    const float c2 = pdf.v2 != 0 ? phi.v2 / pdf.v2 : 0.f, d = pdf.v3 != 0 ? phi.v3 / pdf.v3 : 0.f;
+    return (((a + b) + c2) + d) / 4;
+}
+// DistantLight::Phi (lights.cpp:216-218): scale * Lemit(lambda) * Pi * Sqr(sceneRadius);
+// UniformInfiniteLight::Phi (lights.cpp:974-976): 4 * Pi * Pi * Sqr(sceneRadius) * scale * Lemit(lambda)
+static float phi_table_light(int type, const float *L, float scale, float r) {
+    avr::Spec pdf;
+    const avr::Spec l = visible_half_lambda(&pdf);
+    const avr::Spec Le = avr::sample_table(L, avr::lambda_index(l));
+    avr::Spec phi;
+    if (type == 0) {
+        phi = Le * scale * avr::kPi * (r * r);
+    } else {
+        const float k = 4 * avr::kPi * avr::kPi * (r * r) * scale;
+        phi = avr::Spec{k * Le.v0, k * Le.v1, k * Le.v2, k * Le.v3};
+    }
+    return phi_weight(phi, pdf);
+}
+// RGBSigmoidPolynomial (util/color.h:332-365), the host twin of the device's rsp_eval
+static float rsp_host(float c0, float c1, float c2, float lambda) {
+    const float x = std::fma(lambda, std::fma(lambda, c0, c1), c2);
+    if (std::isinf(x)) return x > 0 ? 1.f : 0.f;
+    return .5f + x / (2 * std::sqrt(1 + x * x));
+}
+// ImageInfiniteLight::Phi (lights.cpp:1042-1060): the image's RGBIlluminantSpectrum summed over
+// the pixels (rows y, then x) at lambda, times 4 Pi^2 R^2 scale / (width * height)
+static float phi_image_light(const float *coeffs, int res, const float *illum, float scale, float r) {
+    avr::Spec pdf;
+    const avr::Spec l = visible_half_lambda(&pdf);
+    const avr::Spec il = avr::sample_table(illum, avr::lambda_index(l));
+    avr::Spec sum = avr::Spec::c(0.f);
+    for (size_t p = 0; p < (size_t)res * res; ++p) {
+        const float *c = coeffs + 4 * p;
+        const avr::Spec s{c[3] * rsp_host(c[0], c[1], c[2], l.v0), c[3] * rsp_host(c[0], c[1], c[2], l.v1),
+                          c[3] * rsp_host(c[0], c[1], c[2], l.v2), c[3] * rsp_host(c[0], c[1], c[2], l.v3)};
+        sum = sum + s * il;
+    }
+    const float k = 4 * avr::kPi * avr::kPi * (r * r) * scale;
+    const float wh = (float)(res * res);
+    const avr::Spec phi{k * sum.v0 / wh, k * sum.v1 / wh, k * sum.v2 / wh, k * sum.v3 / wh};
+    return phi_weight(phi, pdf);
+}
+// AliasTable construction (util/sampling.cpp:563-618): p = w / sum (double accumulation),
+// then the under / over work lists popped from the back
+static void build_alias(const float *w, int n, float *q, float *p, int *alias) {
+    double acc = 0.;
+    for (int i = 0; i < n; ++i) acc += w[i];
+    const float sum = (float)acc;
+    for (int i = 0; i < n; ++i) p[i] = w[i] / sum;
+    struct Outcome { float pHat; int index; };
+    std::vector<Outcome> under, over;
+    for (int i = 0; i < n; ++i) {
+        const float pHat = p[i] * (float)n;
+        (pHat < 1 ? under : over).push_back({pHat, i});
+    }
+    while (!under.empty() && !over.empty()) {
+        const Outcome un = under.back(), ov = over.back();
+        under.pop_back();
+        over.pop_back();
+        q[un.index] = un.pHat;
+        alias[un.index] = ov.index;
+        const float pExcess = un.pHat + ov.pHat - 1;
+        (pExcess < 1 ? under : over).push_back({pExcess, ov.index});
+    }
+    for (const Outcome &o : over) q[o.index] = 1, alias[o.index] = -1;
+    for (const Outcome &u : under) q[u.index] = 1, alias[u.index] = -1;
+}
+// (Re)build the device light list's sampler fields after any light or sampler change
+static int update_light_sampler(avr_context *c) {
+    const int n = c->lights.n;
+    bool ready = c->light_sampler == 1 && n > 0;
+    for (int i = 0; i < n && ready; ++i) ready = c->phi_ok[i];
+    c->lights.power = ready ? 1 : 0;
+    if (n == 0) return AVR_OK;
+    float q[avr::kMaxLights], pm[avr::kMaxLights];
+    int al[avr::kMaxLights];
+    if (ready) {
+        float w[avr::kMaxLights];
+        float tot = 0.f;
+        for (int i = 0; i < n; ++i) tot += (w[i] = c->h_phi[i]);   // std::accumulate(..., 0.f)
+        if (tot == 0.f) std::fill(w, w + n, 1.f);
+        build_alias(w, n, q, pm, al);
+    } else {
+        // BVH / uniform (the kernels' pick ignores the bins then): q = 1, p = pInf / n
+        for (int i = 0; i < n; ++i) q[i] = 1.f, pm[i] = float(n) / float(n + 0) / n, al[i] = -1;
+    }
+    for (int i = 0; i < n; ++i) {
+        c->h_lights[i].aq = q[i];
+        c->h_lights[i].ap = pm[i];
+        c->h_lights[i].alias = al[i];
+    }
+    if (c->d_lights) {
+        HIP_TRY(hipMemcpyAsync(c->d_lights, c->h_lights, sizeof(c->h_lights), hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+    }
+    return AVR_OK;
+}
+
 int avr_lights(avr_context *c, int n, const int *types, const float *w3, const float *L, const float *scale,
                float scene_radius) {
     AVR_QUIESCE(c);
@@ -1136,7 +1252,19 @@ int avr_lights(avr_context *c, int n, const int *types, const float *w3, const f
     c->n_image_lights = 0;
     for (int i = 0; i < n; ++i) c->n_image_lights += types[i] == 2 ? 1 : 0;
     c->image_lights_ready = 0;
-    return AVR_OK;
+    for (int i = 0; i < avr::kMaxLights; ++i) {
+        c->phi_ok[i] = i < n && types[i] != 2;
+        c->h_phi[i] = c->phi_ok[i] ? phi_table_light(types[i], L + (size_t)i * avr::kNTable, scale[i], scene_radius) : 0.f;
+    }
+    return update_light_sampler(c);
+}
+
+int avr_light_sampler(avr_context *c, int kind) {
+    AVR_QUIESCE(c);
+    if (!c || (kind != 0 && kind != 1)) return fail(AVR_ERR_ARG, "light sampler must be 0 (bvh / uniform) or 1 (power)");
+    HIP_TRY(hipSetDevice(c->device));
+    c->light_sampler = kind;
+    return update_light_sampler(c);
 }
 
 // ImageInfiniteLight: pixel spectra, the compensated PiecewiseConstant2D (lights.cpp:1026-1038)
@@ -1197,7 +1325,9 @@ int avr_light_image(avr_context *c, int index, int res, const float *pixel_coeff
     HIP_TRY(hipMemcpyAsync(c->d_lights, c->h_lights, sizeof(c->h_lights), hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     ++c->image_lights_ready;
-    return AVR_OK;
+    c->h_phi[index] = phi_image_light(pixel_coeffs, res, illuminant, L.scale, c->lights.scene_radius);
+    c->phi_ok[index] = true;
+    return update_light_sampler(c);
 }
 
 int avr_camera(avr_context *c, int type, const float cfr[16], const float rfc[16]) {
@@ -1420,6 +1550,8 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
     if (!c->has_medium || !c->has_camera || !c->has_film) return fail(AVR_ERR_STATE, "medium, camera and film required");
     if (spp_begin < 0 || spp_end < spp_begin || max_depth < 0) return fail(AVR_ERR_ARG, "bad sample range");
     if (c->image_lights_ready < c->n_image_lights) return fail(AVR_ERR_STATE, "image light without avr_light_image");
+    if (c->light_sampler == 1 && c->lights.n > 0 && !c->lights.power)
+        return fail(AVR_ERR_STATE, "power light sampler: light weights incomplete");
     avr::smp::ZSobolParams zs{};
     if (c->sampler_kind == 1) {
         // ZSobolSampler indexes (Morton(pixel) << log2(spp)) | sampleIndex: indices must stay
@@ -1548,7 +1680,9 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
             // gray medium: sigma_a and sigma_s tables constant over all 471 wavelengths
             const int mk = c->med.type == 3 ? 1 : (c->med.type == 4 ? 2 : (c->med.type == 1 || c->med.type == 2 ? 3 : 0));
             const int sv = c->sampler_kind == 0 ? 0 : (avr::smp::zsobol_wide(p.zs) ? 2 : 1);
-            const int kv = ((((c->render_mode * 2 + (c->n_image_lights > 0 ? 1 : 0)) * 4 + mk) * 3 + sv) * 2 +
+            // the kImage instantiation also carries the power light sampler's pick (light_pick)
+            const bool general_lights = c->n_image_lights > 0 || c->lights.power;
+            const int kv = ((((c->render_mode * 2 + (general_lights ? 1 : 0)) * 4 + mk) * 3 + sv) * 2 +
                             (c->med.emissive ? 1 : 0)) * 2 + (c->gray && c->med.type != 4 ? 1 : 0);
             hipLaunchKernelGGL(c->kpaths[kv], dim3(c->paths_grid[kv]), dim3(256), 0, c->stream, p);
             HIP_TRY(hipGetLastError());

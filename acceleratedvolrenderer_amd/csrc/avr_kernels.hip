@@ -105,12 +105,50 @@ struct DevLight {
     const float *illum;
     env::Distrib2D dist;
     float rfl[9], lfr[9];
+    // PowerLightSampler (lightsamplers.h:63-99): this light's AliasTable bin {q, p, alias}
+    // (util/sampling.h:822-826) over the lights' Phi; p is the light's PMF
+    float aq, ap;
+    int alias;
 };
 struct DevLights {
     int n;
     const DevLight *list;             // device array (indexed by the sampled light)
     float scene_radius;
+    int power;                        // 1: PowerLightSampler; 0: BVH / uniform (infinite lights)
 };
+
+// VolPath's light pick among infinite lights: BVHLightSampler's infinite branch and
+// UniformLightSampler (lightsamplers.h:266-277, 35-50): index min(u / pInf * n, n - 1), PMF
+// pInf / n; PowerLightSampler (lightsamplers.h:69-75): AliasTable::Sample
+// (util/sampling.cpp:620-645) over the light list's bins. Returns -1 when no light is picked.
+// kGeneral: the power branch is compiled in (the wavefront kernels and k_paths' kImage
+// instantiation, which the host selects for power renders); k_paths' other instantiations
+// keep the BVH pick alone — the branch cost 1.2 % on the headline.
+template <bool kGeneral>
+__device__ __forceinline__ int light_pick(const DevLights &ls, float u, float *pmf) {
+    const int nl = ls.n;
+    if (kGeneral && ls.power) {
+        int offset = (int)(u * nl);
+        offset = offset < nl - 1 ? offset : nl - 1;
+        const float up = fminf_(u * nl - offset, kOneMinusEpsilon);
+        const DevLight &b = ls.list[offset];
+        const int idx = up < b.aq ? offset : b.alias;
+        *pmf = ls.list[idx].ap;
+        return idx;
+    }
+    const float pInf = float(nl) / float(nl + 0);
+    if (!(u < pInf)) return -1;
+    int idx = (int)(u / pInf * nl);
+    idx = idx < nl - 1 ? idx : nl - 1;
+    *pmf = pInf / nl;
+    return idx;
+}
+// the sampler's PMF of light k (PowerLightSampler::PMF, lightsamplers.h:78-82; BVH: pInf / n)
+template <bool kGeneral>
+__device__ __forceinline__ float light_pmf(const DevLights &ls, int k) {
+    if (kGeneral && ls.power) return ls.list[k].ap;
+    return float(ls.n) / float(ls.n + 0) / ls.n;
+}
 
 struct DevCamera {
     int type;                         // 0 orthographic, 1 perspective
@@ -1215,12 +1253,9 @@ __global__ void __launch_bounds__(256) k_medium(Params P) {
                 bool shadowSpawned = false;
                 const int nl = P.lights.n;
                 if (nl > 0) {
-                    float pInf = float(nl) / float(nl + 0);
-                    if (ul < pInf) {
-                        float uu = ul / pInf;
-                        int idx = (int)(uu * nl);
-                        idx = idx < nl - 1 ? idx : nl - 1;
-                        float pmf = pInf / nl;
+                    float pmf = 0.f;
+                    const int idx = light_pick<true>(P.lights, ul, &pmf);
+                    if (idx >= 0) {
                         const DevLight &lt = P.lights.list[idx];
                         if (lt.type == 0 || lt.type == 2) {
                             V3 wi = {lt.w[0], lt.w[1], lt.w[2]};
@@ -1289,7 +1324,7 @@ __global__ void __launch_bounds__(256) k_medium(Params P) {
                     if (depth == 0) L = L + beta * Le / r_u.avg();
                     else {
                         // lightSampler.PMF * PDF_Li(prevIntrContext, ray.d, true): 0 for the uniform light
-                        float p_l = (1.f / (P.lights.n + 0)) * (lt.type == 1 ? 0.f : image_pdf_li(lt, d));
+                        float p_l = light_pmf<true>(P.lights, k) * (lt.type == 1 ? 0.f : image_pdf_li(lt, d));
                         r_l = r_l * p_l;
                         L = L + beta * Le / (r_u + r_l).avg();
                     }
@@ -1406,9 +1441,6 @@ __global__ void __launch_bounds__(256) k_shadow(Params P) {
 // Float operation order per path is identical to the wavefront kernels and to the CPU
 // oracle (cpu/integrators.cpp:962-1399, media.h:741-806).
 enum : int { M_FETCH = 0, M_MEDIUM = 1, M_SHADOW = 2, M_DONE = 3 };
-#ifndef AVR_EXP_NOSTORE
-#define AVR_EXP_NOSTORE 0   // measurement only (k_paths without its record store)
-#endif
 
 __device__ __forceinline__ int xcc_id() {
     unsigned v;
@@ -1826,10 +1858,9 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
                 L = L + Spec::c(0.f);                // L += SampleLd(...) == 0 if nothing spawns
                 const int nl = P.lights.n;
                 if (nl > 0) {
-                    const float pInf = float(nl) / float(nl + 0);
-                    if (ul < pInf) {
-                        int idx = (int)(ul / pInf * nl);
-                        idx = idx < nl - 1 ? idx : nl - 1;
+                    float pmf = 0.f;
+                    const int idx = light_pick<kImage>(P.lights, ul, &pmf);
+                    if (idx >= 0) {
                         const DevLight &lt = P.lights.list[idx];
                         if (kImage && lt.type == 2) {
                             // ImageInfiniteLight::SampleLi with the compensated distribution
@@ -1848,7 +1879,7 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
                                     const V3 d = pOut - po;
                                     light = idx;
                                     T_ray = sr_l = sr_u = sconst<S>(1.f);
-                                    s_img[threadIdx.x] = make_float4(su, sv, (pInf / nl) * lsPdf, fval);
+                                    s_img[threadIdx.x] = make_float4(su, sv, pmf * lsPdf, fval);
                                     seqA = hash_3u32(f2u(po.x), f2u(po.y), f2u(po.z));
                                     seqB = hash_3u32(f2u(d.x), f2u(d.y), f2u(d.z));
                                     sd = d;
@@ -1904,8 +1935,7 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
                         contrib = smul(Ls, beta * f_hat * T_ray) / savg(sr_l + sr_u);
                     } else {
                         // the delta light's spectrum and f_hat of the spawn (same wo, wi)
-                        const float pInf = float(P.lights.n) / float(P.lights.n + 0);
-                        const float p_l = pInf / P.lights.n * 1.f;
+                        const float p_l = light_pmf<kImage>(P.lights, light) * 1.f;
                         const S f_hat = sconst<S>(s_fhat[threadIdx.x]);
                         const Spec Ls = spec4(s_ls[threadIdx.x]);
                         sr_l = sr_l * (r_u * p_l);
@@ -1991,7 +2021,7 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
                     if (depth == 0) L = L + smul(Le, beta) / savg(r_u);
                     else {
                         // lightSampler.PMF * PDF_Li(prevIntrContext, ray.d, true): 0 for the uniform light
-                        r_l = r_l * ((1.f / (P.lights.n + 0)) * pdfLi);
+                        r_l = r_l * (light_pmf<kImage>(P.lights, k) * pdfLi);
                         L = L + smul(Le, beta) / savg(r_u + r_l);
                     }
                 }
@@ -2001,11 +2031,7 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
         if (__ballot(ev == EV_END)) {
             if (ev == EV_END) {
                 // the per-sample record: L (k_film takes the rest from the camera stage)
-#if AVR_EXP_NOSTORE   // measurement only: the record store dropped (breaks the film)
-                if (L.v0 == -1.2345f) P.ps.rec[g] = to4(L);
-#else
                 P.ps.rec[g] = to4(L);
-#endif
                 mode = M_FETCH;
                 ev = EV_NONE;
             }
@@ -2045,18 +2071,23 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
                 if (fresh) {
                     ++nPaths;
                     // ---- a new path from the camera stage (k_paths_camera) ----
-                    g = (int)(base + k);
-                    const float4 c0 = P.ps.cam0[g], c1 = P.ps.cam1[g], c2 = P.ps.cam2[g];
-                    const uint4 c3 = P.ps.cam3[g];
+                    const int gn = (int)(base + k);
+                    const float4 c0 = P.ps.cam0[gn], c1 = P.ps.cam1[gn], c2 = P.ps.cam2[gn];
+                    const uint4 c3 = P.ps.cam3[gn];
+                    // ZSobol: the first light pick drawn ahead; independent: the PCG32 state
+                    [[maybe_unused]] float ul5 = 0.f;
+                    [[maybe_unused]] uint4 c5{};
+                    if constexpr (!kZSobol) c5 = P.ps.cam5[gn];
+                    else if constexpr (kUlAhead) ul5 = reinterpret_cast<const float *>(P.ps.cam5)[gn];
+                    g = gn;
                     if constexpr (kZSobol) {
                         // the sample's ZSobol state past the camera draws and the first segment's three
                         const int slot = g % npix, sIdx = g / npix;
                         const int pix = P.pix_order ? P.pix_order[slot] : slot;
                         smp.start(P, pix % P.film.width, pix / P.film.width, P.sample_base + sIdx);
-                        if constexpr (kUlAhead) s_ul[threadIdx.x] = reinterpret_cast<const float *>(P.ps.cam5)[g];
+                        if constexpr (kUlAhead) s_ul[threadIdx.x] = ul5;
                         smp.z.dimension = 9;
                     } else {
-                        const uint4 c5 = P.ps.cam5[g];
                         smp.rng.state = ((uint64_t)c5.y << 32) | c5.x;
                         smp.rng.inc = ((uint64_t)c5.w << 32) | c5.z;
                     }

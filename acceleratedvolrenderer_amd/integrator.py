@@ -59,10 +59,10 @@ class VolPathIntegrator:
             raise ValueError(f"unknown integrator {name!r}")
         if lightsampler not in ("bvh", "uniform", "power"):
             raise ValueError(f"{lightsampler}: unknown light sampling strategy")
-        # With only infinite/distant lights every pbrt light sampler returns pmf 1/N
-        # (lightsamplers.h:266-277); "power" weights by Phi, not supported yet.
-        if lightsampler == "power" and len(scene.lights) > 1:
-            raise NotImplementedError("power light sampler with several lights")
+        # With only infinite lights "bvh" and "uniform" pick uniformly with pmf 1/N
+        # (lightsamplers.h:266-277, 35-50); "power" draws from an alias table over the lights'
+        # Phi (PowerLightSampler, lightsamplers.cpp:76-96; avr_light_sampler)
+        self.lightsampler = lightsampler
         self.scene = scene
         self.maxdepth = int(maxdepth)
         self.spp = int(spp)
@@ -79,6 +79,7 @@ class VolPathIntegrator:
             raise ValueError("mode must be 'replay' (per-sample parity) or 'fast' (statistical parity)")
         self.mode = mode
         self.ctx.set_render_mode(mode)
+        self.ctx.set_light_sampler(1 if lightsampler == "power" else 0)
         self.ctx.set_scene(scene)
 
     @staticmethod

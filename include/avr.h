@@ -282,6 +282,15 @@ int avr_lights(avr_context *ctx, int n, const int *types, const float *w3, const
 int avr_light_image(avr_context *ctx, int index, int res, const float *pixel_coeffs, const float *distribution,
                     const float *illuminant, const float render_from_light[16], const float light_from_render[16]);
 
+/* VolPath's light sampler (VolPathIntegrator::Create "lightsampler", integrators.cpp:1402-1420;
+ * LightSampler::Create, lightsamplers.cpp:22-37): 0 = "bvh" (default) or "uniform" — identical
+ * for infinite lights (lightsamplers.h:266-277, 35-50); 1 = "power": PowerLightSampler
+ * (lightsamplers.h:63-99, lightsamplers.cpp:76-96), lights picked by an AliasTable over
+ * Average(Phi(lambda) / pdf) at SampleVisible(0.5) (DistantLight / UniformInfiniteLight /
+ * ImageInfiniteLight::Phi, lights.cpp:216, 974, 1042). Kept across avr_lights calls; a power
+ * render needs every image light's avr_light_image first. */
+int avr_light_sampler(avr_context *ctx, int kind);
+
 /* Camera: type 0 orthographic, 1 perspective (cameras.cpp:284-306, 404-427).
  * camera_from_raster: full 4x4 (projective for perspective); render_from_camera: affine 4x4. */
 int avr_camera(avr_context *ctx, int type, const float camera_from_raster[16], const float render_from_camera[16]);

@@ -78,6 +78,7 @@ class OracleScene(ctypes.Structure):
         ("light_illuminant", c_float_p),
         ("film_nbuckets", ctypes.c_int), ("film_lambda_min", ctypes.c_float), ("film_lambda_max", ctypes.c_float),
         ("boundary", ctypes.c_int), ("sphere", ctypes.c_float * 4), ("n_planes", ctypes.c_int), ("planes", c_float_p),
+        ("light_sampler", ctypes.c_int),
     ]
 
 
@@ -317,9 +318,11 @@ def vdb_majorant(dtree, bounds, res=(64, 64, 64)):
 class OracleRun:
     """Holds an OracleScene and the numpy buffers it points into."""
 
-    def __init__(self, scene, max_depth=5, seed=0, libm="platform"):
+    def __init__(self, scene, max_depth=5, seed=0, libm="platform", lightsampler="bvh"):
         if libm not in LIBM_MODES:
             raise ValueError(f"libm must be one of {sorted(LIBM_MODES)}")
+        if lightsampler not in ("bvh", "uniform", "power"):
+            raise ValueError(f"{lightsampler}: unknown light sampling strategy")
         self.libm = libm
         med = scene.medium
         is_vdb = int(getattr(med, "type_id", 0)) == 3
@@ -394,6 +397,7 @@ class OracleRun:
                 s.light_lfr[i][:] = [float(v) for v in scene.light_lfr[i][:3, :3].reshape(-1)]
                 s.light_illuminant = arr(lt.illuminant)
         s.scene_radius = float(scene.scene_radius)
+        s.light_sampler = 1 if lightsampler == "power" else 0
         s.camera_type = int(scene.camera.type_id)
         s.camera_from_raster[:] = [float(v) for v in scene.camera_from_raster.reshape(-1)]
         s.render_from_camera[:] = [float(v) for v in scene.render_from_camera.reshape(-1)]

@@ -929,6 +929,8 @@ typedef struct OracleScene {
     float sphere[4];
     int n_planes;
     const float *planes;
+    // VolPath's "lightsampler": 0 bvh / uniform (identical for infinite lights), 1 power
+    int light_sampler;
 } OracleScene;
 
 }  // extern "C"
@@ -1315,6 +1317,74 @@ struct ImageLight {
     }
 };
 
+// PowerLightSampler (lightsamplers.h:63-99, lightsamplers.cpp:76-96) over the infinite lights:
+// each light's weight Average(SafeDiv(Phi(lambda), lambda.PDF())) at SampleVisible(0.5), then
+// AliasTable (util/sampling.cpp:563-645).
+struct PowerSampler {
+    float q[8] = {}, p[8] = {};
+    int alias[8] = {};
+    static float Weight(const OracleScene &s, const ImageLight *img, int i) {
+        const Lambda l = SampleVisible(0.5f);
+        const float R2 = Sqr(s.scene_radius);
+        Spec phi;
+        if (s.light_type[i] == 0) {          // DistantLight::Phi, lights.cpp:216-218
+            phi = s.light_scale[i] * SampleDense(s.light_L[i], l) * Pi * R2;
+        } else if (s.light_type[i] == 1) {   // UniformInfiniteLight::Phi, lights.cpp:974-976
+            phi = 4 * Pi * Pi * R2 * s.light_scale[i] * SampleDense(s.light_L[i], l);
+        } else {                             // ImageInfiniteLight::Phi, lights.cpp:1042-1060
+            const int res = img[i].res;
+            Spec sumL = Spec::Const(0.f);
+            for (int v = 0; v < res; ++v)
+                for (int u = 0; u < res; ++u) {
+                    const float *c = img[i].img + 4 * ((size_t)v * res + u);
+                    Rsp rsp{c[0], c[1], c[2]};
+                    Spec e;
+                    for (int k = 0; k < NS; ++k) e.v[k] = c[3] * rsp(l.lambda[k]);
+                    sumL = sumL + e * SampleDense(s.light_illuminant, l);
+                }
+            phi = 4 * Pi * Pi * R2 * s.light_scale[i] * sumL;
+            for (int k = 0; k < NS; ++k) phi.v[k] /= (float)(res * res);
+        }
+        Spec w;
+        for (int k = 0; k < NS; ++k) w.v[k] = l.pdf[k] != 0 ? phi.v[k] / l.pdf[k] : 0;   // SafeDiv
+        return w.Average();
+    }
+    void Build(const OracleScene &s, const ImageLight *img) {
+        const int n = s.nlights;
+        std::vector<float> w(n);
+        for (int i = 0; i < n; ++i) w[i] = Weight(s, img, i);
+        if (std::accumulate(w.begin(), w.end(), 0.f) == 0.f) std::fill(w.begin(), w.end(), 1.f);
+        const float sum = std::accumulate(w.begin(), w.end(), 0.);
+        for (int i = 0; i < n; ++i) p[i] = w[i] / sum;
+        struct Outcome { float pHat; size_t index; };
+        std::vector<Outcome> under, over;
+        for (int i = 0; i < n; ++i) {
+            const float pHat = p[i] * (size_t)n;
+            if (pHat < 1) under.push_back({pHat, (size_t)i});
+            else over.push_back({pHat, (size_t)i});
+        }
+        while (!under.empty() && !over.empty()) {
+            Outcome un = under.back(), ov = over.back();
+            under.pop_back();
+            over.pop_back();
+            q[un.index] = un.pHat;
+            alias[un.index] = (int)ov.index;
+            const float pExcess = un.pHat + ov.pHat - 1;
+            if (pExcess < 1) under.push_back({pExcess, ov.index});
+            else over.push_back({pExcess, ov.index});
+        }
+        while (!over.empty()) { q[over.back().index] = 1; alias[over.back().index] = -1; over.pop_back(); }
+        while (!under.empty()) { q[under.back().index] = 1; alias[under.back().index] = -1; under.pop_back(); }
+    }
+    int Sample(int n, float u, float *pmf) const {   // AliasTable::Sample
+        int offset = std::min<int>(u * (size_t)n, n - 1);
+        float up = std::min<float>(u * (size_t)n - offset, OneMinusEpsilon);
+        if (up < q[offset]) { *pmf = p[offset]; return offset; }
+        *pmf = p[alias[offset]];
+        return alias[offset];
+    }
+};
+
 struct SceneView {
     const OracleScene &s;
     Xform mediumX, cameraX, rasterX;
@@ -1322,11 +1392,13 @@ struct SceneView {
     Grid density, lescale, majorant, temperature;
     GaussianSampler gauss;
     ImageLight img[8];
+    PowerSampler power;
     explicit SceneView(const OracleScene &sc) : s(sc) {
         if (sc.filter_type == 1) gauss.Build(sc.filter_radius[0], sc.filter_radius[1], sc.filter_sigma);
         for (int i = 0; i < sc.nlights; ++i)
             if (sc.light_type[i] == 2)
                 img[i].Build(sc.light_img[i], sc.light_res[i], sc.light_dist[i], sc.light_rfl[i], sc.light_lfr[i]);
+        if (sc.light_sampler == 1 && sc.nlights > 0) power.Build(sc, img);
         for (int i = 0; i < 16; ++i) {
             mediumX.m[i / 4][i % 4] = sc.render_from_medium[i];
             mediumX.mInv[i / 4][i % 4] = sc.medium_from_render[i];
@@ -1553,11 +1625,17 @@ static Spec SampleLd(const SceneView &sv, V3 p, V3 wo, const Lambda &l, Sampler 
     float uL0, uL1;
     sampler.Get2D(&uL0, &uL1);   // uLight (unused by distant lights)
     if (s.nlights == 0) return Spec::Const(0.f);
-    float pInfinite = float(s.nlights) / float(s.nlights + 0);
-    if (!(u < pInfinite)) return Spec::Const(0.f);
-    u /= pInfinite;
-    int index = std::min<int>(u * s.nlights, s.nlights - 1);
-    float pmf = pInfinite / s.nlights;
+    int index;
+    float pmf;
+    if (s.light_sampler == 1) {   // PowerLightSampler::Sample (lightsamplers.h:69-75)
+        index = sv.power.Sample(s.nlights, u, &pmf);
+    } else {
+        float pInfinite = float(s.nlights) / float(s.nlights + 0);
+        if (!(u < pInfinite)) return Spec::Const(0.f);
+        u /= pInfinite;
+        index = std::min<int>(u * s.nlights, s.nlights - 1);
+        pmf = pInfinite / s.nlights;
+    }
     if (s.light_type[index] == 1) return Spec::Const(0.f);  // UniformInfiniteLight::SampleLi with allowIncompletePDF
     V3 wi;
     Spec Ls;
@@ -1714,7 +1792,7 @@ static Spec Li(const SceneView &sv, Ray ray, Lambda &l, Sampler &sampler, int *n
                     EqualAreaSphereToSquare(ImageLight::Mul(il.lfr, ray.d), &eu, &ev);
                     pdfLi = il.compensated.PDF(eu, ev) / (4 * Pi);
                 }
-                float p_l = (1.f / (s.nlights + 0)) * pdfLi;
+                float p_l = (s.light_sampler == 1 ? sv.power.p[i] : 1.f / (s.nlights + 0)) * pdfLi;
                 r_l = r_l * p_l;
                 L = L + beta * Le / (r_u + r_l).Average();
             }
