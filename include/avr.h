@@ -100,12 +100,13 @@ int avr_set_majorant_occupancy(avr_context *ctx, int on);
 /* k_paths: refill a wave's idle lanes with new samples once at least `lanes` (1..64)
  * are idle (or none is busy); larger values batch the per-event handlers across lanes.
  * 0 = default (the measured optima in both render modes: 32; 12 for a non-emissive
- * NanoVDB medium at pbrt's 64^3 majorant, whose longer DDA walks favour smaller batches). */
+ * NanoVDB medium at pbrt's 64^3 majorant, whose longer DDA walks favour smaller batches;
+ * 24 for an RGBGridMedium). */
 int avr_set_refill_min(avr_context *ctx, int lanes);
 /* k_paths: majorant-grid cells a lane may cross per tracking iteration before yielding to
- * the wave (0 = default: 10 for majorant grids up to 16^3, 32 for finer ones, 28 for a
- * non-emissive NanoVDB medium at 64^3 — measured optima); bounds the divergence of the DDA
- * walk. No effect on results. */
+ * the wave (0 = default: 10 for majorant grids up to 16^3, 32 for finer ones and for
+ * RGBGridMedium, 28 for a non-emissive NanoVDB medium at 64^3 — measured optima); bounds the
+ * divergence of the DDA walk. No effect on results. */
 int avr_set_dda_budget(avr_context *ctx, int cells);
 /* Density layout for the NEXT avr_medium_grid* / avr_medium_nanovdb call: 1 (default) also
  * builds a "fat" footprint copy — GridMedium: entry (ix,iy,iz) holds the 8 trilinear taps as
