@@ -145,7 +145,7 @@ struct avr_context {
     uint32_t *d_zs_table = nullptr;
     int zs_dims = 256;
     int zs_key[3] = {-1, -1, -1};
-    int refill_min = 0;       // 0: the default (32 lanes; 12 for a non-emissive NanoVDB walk, 24 for RGB grids)
+    int refill_min = 0;       // 0: the default (32 lanes; 12 for a non-emissive NanoVDB walk, 16 for RGB grids)
     int dda_budget = 0;       // 0: by majorant resolution (12 cells up to 16^3, 32 for NanoVDB's 64^3)
     int grid_layout = 1;
     bool gray = false;        // sigma_a and sigma_s constant over 360..830 nm      // 1: build the fat (footprint) copy when memory allows, 0: linear only
@@ -1653,11 +1653,11 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
                 // a non-emissive NanoVDB medium (pbrt's 64^3 majorant: ~4x the DDA steps of the
                 // grid) refills at 12 lanes with 28 cells (S-cloud-1024: 1239 -> 1352 Msamples/s);
                 // an RGBGridMedium (8 sigmoid taps x 4 wavelengths per lookup, 2 waves / SIMD) at
-                // 24 lanes with 32 cells (C5's RGB explosion: 1770 -> 2064 Msamples/s)
+                // 16 lanes with 32 cells (C5's RGB explosion: 1770 -> 2094 Msamples/s)
                 const int mres = std::max(c->med.mres[0], std::max(c->med.mres[1], c->med.mres[2]));
                 const bool vdbWalk = c->med.type == 3 && !c->med.emissive && mres > 16;
                 const bool rgbWalk = c->med.type == 4;
-                p.refill_min = c->refill_min > 0 ? c->refill_min : (vdbWalk ? 12 : (rgbWalk ? 24 : 32));
+                p.refill_min = c->refill_min > 0 ? c->refill_min : (vdbWalk ? 12 : (rgbWalk ? 16 : 32));
                 p.dda_budget = c->dda_budget > 0 ? c->dda_budget : (vdbWalk ? 28 : (rgbWalk || mres > 16 ? 32 : 10));
             }
             p.heads = c->d_heads;
