@@ -133,6 +133,7 @@ SIGNATURES = {
     "avr_film_set_reference": (ctypes.c_int, [ctypes.c_void_p, c_float_p, c_float_p, ctypes.c_int]),
     "avr_film_metric": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, c_float_p]),
     "avr_last_pass_weights": (ctypes.c_int, [ctypes.c_void_p, c_float_p, ctypes.c_longlong]),
+    "avr_last_kernel": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int]),
     "avr_transmittance": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_longlong, c_float_p, c_float_p, c_float_p,
                                          c_float_p]),
     "avr_transmittance_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_longlong, ctypes.c_void_p,
@@ -240,6 +241,7 @@ class Context:
         h = ctypes.c_void_p()
         _check(self.lib.avr_context_create(int(device), int(max_paths), ctypes.byref(h)))
         self.h = h
+        self.device = int(device)
         self._keep = []
 
     def close(self):
@@ -328,8 +330,16 @@ class Context:
     def set_stream(self, stream_ptr):
         _check(self.lib.avr_set_stream(self.h, ctypes.c_void_p(stream_ptr)))
 
+    def _check_device(self, tensors):
+        """Device grids must live on this context's GPU (the kernels dereference them there)."""
+        for t in tensors:
+            if t is not None and hasattr(t, "data_ptr") and t.device.index != self.device:
+                raise ValueError(f"grid tensor on {t.device}, but the context runs on cuda:{self.device}")
+
     def set_scene(self, scene):
         med = scene.medium
+        self._check_device([getattr(med, "device_density", None)] +
+                           ([med.rgb_sigma_a, med.rgb_sigma_s, med.rgb_Le] if getattr(med, "type_id", 0) == 4 else []))
         mres = np.asarray(med.majorant_res, np.int32)
         f32 = lambda a: np.ascontiguousarray(np.asarray(a, np.float32))
         args = [f32(med.bounds), f32(scene.render_from_medium), f32(scene.medium_from_render), f32(med.sigma_a),
@@ -474,6 +484,12 @@ class Context:
                                               ctypes.byref(ns)))
         m = npix * ns.value
         return first.value, ns.value, L[:m], lam[:m], pdf[:m]
+
+    def last_kernel(self):
+        """Template arguments of the last k_paths instantiation rendered ("k_paths<...>")."""
+        buf = ctypes.create_string_buffer(64)
+        _check(self.lib.avr_last_kernel(self.h, buf, 64))
+        return buf.value.decode()
 
     def last_pass_weights(self, npix, max_samples):
         w = np.zeros(npix * max_samples, np.float32)

@@ -98,6 +98,12 @@ struct avr_context {
     // host copy of the latter (to return the last pass in pixel order); empty = scanline
     int *d_pix_order = nullptr, *d_pix_slot = nullptr;
     std::vector<int> h_pix_slot;
+    // bumped whenever the pixel order changes (avr_set_pixel_order, avr_film); the last
+    // render's records are in the order of generation last_order_gen
+    int order_gen = 0, last_order_gen = 0;
+    // template arguments of the last k_paths instantiation launched ("k_paths<em, gray, smp,
+    // med, image, fast>", avr_last_kernel), so a profiler pass can be matched to the timed run
+    char last_kpaths[64] = "";
     // k_paths<emissive, gray, sampler, medium, image, fast> at slot
     // ((((fast*2 + image)*4 + medium(0 grid, 1 vdb, 2 rgb, 3 homogeneous/cloud))*3 + sampler(0
     // independent, 1 zsobol 32-bit, 2 zsobol 64-bit))*2 + emissive)*2 + gray
@@ -200,6 +206,7 @@ void free_paths(avr_context *c) {
 }
 
 void free_pixel_order(avr_context *c) {
+    if (c->d_pix_order) ++c->order_gen;   // back to scanline order
     if (c->d_pix_order) (void)hipFree(c->d_pix_order);
     if (c->d_pix_slot) (void)hipFree(c->d_pix_slot);
     c->d_pix_order = c->d_pix_slot = nullptr;
@@ -1444,6 +1451,7 @@ int avr_set_pixel_order(avr_context *c, const int *order, long long n) {
     HIP_TRY(hipMemcpy(c->d_pix_order, order, np * sizeof(int), hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(c->d_pix_slot, slot.data(), np * sizeof(int), hipMemcpyHostToDevice));
     c->h_pix_slot.swap(slot);
+    ++c->order_gen;
     return AVR_OK;
 }
 
@@ -1689,6 +1697,13 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
                             (c->med.emissive ? 1 : 0)) * 2 + (c->gray && c->med.type != 4 ? 1 : 0);
             hipLaunchKernelGGL(c->kpaths[kv], dim3(c->paths_grid[kv]), dim3(256), 0, c->stream, p);
             HIP_TRY(hipGetLastError());
+            {
+                const int kmed = c->med.type == 3 ? 3 : (c->med.type == 4 ? 4 : (c->med.type == 1 || c->med.type == 2 ? 1 : 0));
+                std::snprintf(c->last_kpaths, sizeof(c->last_kpaths), "k_paths<%s, %s, %d, %d, %s, %s>",
+                              c->med.emissive ? "true" : "false", (c->gray && c->med.type != 4) ? "true" : "false",
+                              sv == 0 ? 0 : (sv == 1 ? 2 : 3), kmed, general_lights ? "true" : "false",
+                              c->render_mode ? "true" : "false");
+            }
             EV_MARK(e1);
             p.rec_mode = 1;   // k_film reads the records k_paths wrote (in slot order)
             p.pix_slot = c->d_pix_slot;
@@ -1701,6 +1716,7 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
             c->timed.push_back({e1, e2, &avr_stats::ms_film, false});
             c->last_base = (int)base;
             c->last_S = S;
+            c->last_order_gen = c->order_gen;
             continue;
         }
         EV_MARK(c0);
@@ -2007,6 +2023,8 @@ int avr_last_pass_samples(avr_context *c, float *L, float *lambda, float *pdf, l
     if (!c || !c->has_film || !L || !lambda || !pdf || !first || !ns) return fail(AVR_ERR_ARG, "null arg");
     const long long n = (long long)c->film.width * c->film.height * c->last_S;
     if (n_max < n) return fail(AVR_ERR_ARG, "buffer too small for the last pass");
+    if (n > 0 && c->last_persistent && c->last_order_gen != c->order_gen)
+        return fail(AVR_ERR_STATE, "the pixel order changed since the last render (its records are in the old order)");
     if (n > 0 && c->last_persistent) {
         // k_paths' records (L) and its camera stage's wavelengths and pdfs, as k_film read them
         HIP_TRY(hipMemcpy(L, c->ps.rec, n * sizeof(float4), hipMemcpyDeviceToHost));
@@ -2032,11 +2050,19 @@ int avr_last_pass_samples(avr_context *c, float *L, float *lambda, float *pdf, l
     return AVR_OK;
 }
 
+int avr_last_kernel(avr_context *c, char *buf, int cap) {
+    if (!c || !buf || cap <= 0) return fail(AVR_ERR_ARG, "null arg");
+    std::snprintf(buf, (size_t)cap, "%s", c->last_kpaths);
+    return AVR_OK;
+}
+
 int avr_last_pass_weights(avr_context *c, float *w, long long n_max) {
     AVR_QUIESCE(c);
     if (!c || !c->has_film || !w) return fail(AVR_ERR_ARG, "null arg");
     const long long n = (long long)c->film.width * c->film.height * c->last_S;
     if (n_max < n) return fail(AVR_ERR_ARG, "buffer too small for the last pass");
+    if (n > 0 && c->last_persistent && c->filter_type != 0 && c->last_order_gen != c->order_gen)
+        return fail(AVR_ERR_STATE, "the pixel order changed since the last render (its records are in the old order)");
     if (c->filter_type == 0) {
         for (long long i = 0; i < n; ++i) w[i] = 1.f;   // BoxFilter::Sample weight
     } else if (n > 0 && c->last_persistent) {

@@ -1793,7 +1793,7 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
     const int xcc = xcc_id();
     // work counters: per lane in 32 bits (a lane traces at most a few thousand segments per
     // launch), the wave-loop counters wave-uniform (scalar registers)
-    uint32_t nLookup = 0, nSteps = 0, nPaths = 0, nShadow = 0, nShadowLookup = 0;
+    uint32_t nLookup = 0, nSteps = 0, nPaths = 0, nShadow = 0, nShadowLookup = 0, nPhase = 0;
     unsigned long long nIter = 0, nActive = 0;
 
     int mode = M_FETCH, ev = EV_NONE;
@@ -1971,6 +1971,7 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
             }
             if (ev == EV_PHASE) {
                 // phase-function sampling (integrators.cpp:1046-1061), then the next segment
+                ++nPhase;
                 float up0, up1;
                 if constexpr (kCoop) {
                     up0 = q0[0];
@@ -2332,6 +2333,7 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
     AVR_SEC_FLUSH
     flush_stat(P.stats, 0, nLookup);
     flush_stat(P.stats, 1, nPaths);
+    flush_stat(P.stats, 2, nPhase);
     flush_stat(P.stats, 3, nShadowLookup);
     flush_stat(P.stats, 4, nShadow);
     flush_stat(P.stats, 5, nSteps);

@@ -52,7 +52,10 @@ def ensure_world(requested, script, argv, env=None):
     sys.exit(rc)
 
 
-def sample_plan(world, steps, warmup, spp_per_step, base_spp=256, pixelsamples=0):
+PLAN_WORLD = 8   # the largest world bench.py is run at (one 8-GPU node)
+
+
+def sample_plan(world, steps, warmup, spp_per_step, base_spp=256, pixelsamples=0, plan_world=PLAN_WORLD):
     """Sample indices of `bench.py --gpus N` (weak scaling: every rank renders spp_per_step
     sample indices of every pixel per step; the sampler is indexed by (pixel, sampleIndex),
     samplers.h:252-254, so disjoint index ranges are disjoint paths).
@@ -60,16 +63,23 @@ def sample_plan(world, steps, warmup, spp_per_step, base_spp=256, pixelsamples=0
     Returns (pixelsamples, warm, timed): warm[r] / timed[r] are rank r's first sample index of
     each warmup / timed step. The timed steps of all ranks cover [0, steps * world * S) once
     — no (pixel, index) pair is rendered twice, so the reduced film is one render at
-    pixelsamples spp — and pixelsamples is the smallest power of two >= that range and
-    >= base_spp (BASELINE config C3: 256), unless given. Warmup steps re-render indices of
-    the same range (their film is cleared before the timed region)."""
+    pixelsamples spp. pixelsamples is the smallest power of two >= steps * max(world,
+    plan_world) * S and >= base_spp (BASELINE config C3: 256), unless given: sized for the
+    largest world (8 GPUs) at EVERY world size, so the N = 1, 2, 4 and 8 lines of one command
+    run the same ZSobol instantiation with the same number of sample digits per draw
+    (samplers.h:250-254: the digit count grows with log2 pixelsamples) and a scaling curve
+    measures scaling, not sampler cost. Warmup steps re-render indices of the same range
+    (their film is cleared before the timed region)."""
     S = int(spp_per_step)
     if S < 1:
         raise ValueError(f"spp per step must be >= 1 (got {S})")
+    if int(world) < 1:
+        raise ValueError(f"world size must be >= 1 (got {world})")
     need = int(steps) * int(world) * S
+    plan = int(steps) * max(int(world), int(plan_world)) * S
     P = int(pixelsamples) if pixelsamples else max(int(base_spp), 1)
     if not pixelsamples:
-        while P < need:
+        while P < plan:
             P *= 2
     if P < need or P % S:
         raise ValueError(f"pixelsamples {P} cannot hold {steps} steps x {world} ranks x {S} distinct sample indices")

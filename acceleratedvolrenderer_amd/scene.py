@@ -31,6 +31,7 @@ class GridMedium:
                  sigma_s=None, scale=1.0, g=0.0, Le=None, Lescale=None, majorant_res=(16, 16, 16), temperature=None,
                  temperaturescale=1.0, temperatureoffset=0.0):
         if hasattr(density, "data_ptr"):
+            check_device_grid(density, "density", 3)
             self.device_density = density
             self.density = None
             nz, ny, nx = (int(s) for s in density.shape)
@@ -176,6 +177,17 @@ class NanoVDBMedium:
         return np.concatenate([self.p0, self.p1]).astype(np.float32)
 
 
+def check_device_grid(t, name, ndim):
+    """A grid handed to the device entry points as a tensor: float32 (the kernels read f32 /
+    float4 elements, so a narrower dtype would be read past its end), contiguous, on a GPU."""
+    if str(getattr(t, "dtype", "")) != "torch.float32":
+        raise ValueError(f"{name} tensor must be float32 (got {getattr(t, 'dtype', None)})")
+    if t.dim() != ndim or not t.is_contiguous():
+        raise ValueError(f"{name} tensor must be contiguous with {ndim} dimensions")
+    if getattr(t.device, "type", None) != "cuda":
+        raise ValueError(f"{name} tensor must live on a GPU (got {t.device}); pass a numpy array for host data")
+
+
 class RGBGridMedium:
     """pbrt "rgbgrid" medium (RGBGridMedium::Create, media.cpp:380-453): per-voxel RGB
     "sigma_a" / "sigma_s" (RGBUnboundedSpectrum) and "Le" (RGBIlluminantSpectrum) arrays
@@ -198,8 +210,9 @@ class RGBGridMedium:
                  sigma_a_coeffs=None, sigma_s_coeffs=None, Le_coeffs=None):
         def conv(rgb, coeffs, name):
             if coeffs is not None and hasattr(coeffs, "data_ptr"):
-                if tuple(coeffs.shape[3:]) != (4,) or coeffs.dim() != 4 or not coeffs.is_contiguous():
+                if tuple(coeffs.shape[3:]) != (4,) or coeffs.dim() != 4:
                     raise ValueError(f"{name}_coeffs must be a contiguous (nz, ny, nx, 4) tensor")
+                check_device_grid(coeffs, f"{name}_coeffs", 4)
                 self.on_device = True
                 return coeffs
             if coeffs is not None:
@@ -219,6 +232,13 @@ class RGBGridMedium:
         self.rgb_sigma_a = conv(sigma_a, sigma_a_coeffs, "sigma_a")
         self.rgb_sigma_s = conv(sigma_s, sigma_s_coeffs, "sigma_s")
         self.rgb_Le = conv(Le, Le_coeffs, "Le")
+        given = [x for x in (self.rgb_sigma_a, self.rgb_sigma_s, self.rgb_Le) if x is not None]
+        if self.on_device:
+            # the device entry point takes device pointers for every grid: no host arrays mixed in
+            if not all(hasattr(x, "data_ptr") for x in given):
+                raise ValueError("RGB grids given as device tensors must all be device tensors (got a host array too)")
+            if len({(x.device.type, x.device.index) for x in given}) != 1:
+                raise ValueError("RGB grids given as device tensors must all live on the same GPU")
         if self.rgb_sigma_a is None and self.rgb_sigma_s is None:
             raise ValueError('RGB grid requires "sigma_a" and/or "sigma_s" parameter values.')
         if self.rgb_Le is not None and self.rgb_sigma_a is None:

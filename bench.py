@@ -37,19 +37,90 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+HBM_ACHIEVABLE_GBPS = 6300.0   # MI355X_MICROARCH.md: ~6.3 TB/s achievable streaming
+HBM_REQUEST_BYTES = 64  # gfx950 memory-side read request (FETCH_SIZE = TCC_EA0_RDREQ x 64 B)
 VALU_SIMDS = 1024       # 256 CUs x 4 SIMDs; a wave64 VALU op issues in 2 cycles (MI355X_MICROARCH.md)
 # SURVEY.md §8d algorithmic bytes: 32 B per trilinear lookup (8 taps x 4 B) and 132 B per
 # work item read / written (ray 24, tMax 4, lambda+pdf 32, beta/r_u/r_l 48, RNG 16, pixel/depth 8).
 BYTES_PER_LOOKUP = 32
 BYTES_PER_ITEM = 132
-BYTES_PER_SAMPLE_RECORD = 32   # k_paths' per-sample record (L, lambda) read later by k_film
+# k_paths' own per-unit bytes (DESIGN.md §4 "Algorithmic bytes"): it writes ONE 16-B record per
+# sample (L; k_film takes the rest from the camera stage) and reads the camera stage's record of
+# every path it starts: cam0..cam3 (4 x 16 B) + the 4-B light-pick draw (ZSobol) or the 16-B
+# PCG32 state (independent sampler)
+BYTES_PER_SAMPLE_RECORD = 16
+BYTES_CAMERA_RECORD_READ = {"zsobol": 68, "independent": 80}
+# ZSobol pixel-table reads (one 4-B entry per draw): 5 draws per phase event in k_paths (phase
+# 2D, the next segment's three 1D, the next light pick); 6 per camera-stage quad of 4 samples
+ZSOBOL_TABLE_BYTES_PER_DRAW = 4
+ZSOBOL_DRAWS_PER_PHASE = 5
+ZSOBOL_CAMERA_DRAWS = 6
+# the camera stage writes cam0, cam1, cam2, cam3, cam4 (5 x 16 B), the 4-B filter weight and cam5
+# (4 B ZSobol light pick / 16 B PCG32 state)
+BYTES_CAMERA_WRITE = {"zsobol": 88, "independent": 100}
+RGB_CPU_MAX_RES = 512   # the rgb-explosion CPU baseline copies its 3 grids to the host (6 GiB at 512^3)
+
+
+def lookup_bytes(medium, emissive=False, rgb_fields=2):
+    """Algorithmic bytes of ONE density lookup of k_paths by medium kind: GridMedium 8 f32 taps
+    (32 B); NanoVDB the apron slot (4 B) + the 32-B stencil entry (+ the same again for
+    the temperature grid of an emissive medium); RGBGridMedium 8 taps x 16 B {c0, c1, c2, scale}
+    per field (sigma_a, sigma_s, and Le when emissive)."""
+    if medium == "rgb":
+        return 8 * 16 * (rgb_fields + (1 if emissive else 0))
+    if medium == "nanovdb":
+        return 36 * (2 if emissive else 1)
+    return BYTES_PER_LOOKUP
+
+
+def kpaths_bytes(agg, sampler, medium="grid", emissive=False, zsobol_table=True):
+    """k_paths' algorithmic bytes over the stats `agg` (counters summed over its launches):
+    density lookups (delta + ratio tracking) + 16 B per sample record + the camera record of every
+    path + the ZSobol pixel-table entries of its phase draws. Returns (total, parts)."""
+    # delta tracking evaluates emission (Le grid / temperature) at its lookups; shadow rays never
+    lk = agg["medium_lookups"] * lookup_bytes(medium, emissive) + agg["shadow_lookups"] * lookup_bytes(medium, False)
+    parts = {
+        "density_lookups": lk,
+        "sample_records_written": BYTES_PER_SAMPLE_RECORD * agg["medium_items_in"],
+        "camera_records_read": BYTES_CAMERA_RECORD_READ[sampler] * agg["medium_items_in"],
+        "zsobol_table_reads": (ZSOBOL_TABLE_BYTES_PER_DRAW * ZSOBOL_DRAWS_PER_PHASE * agg["medium_items_out"]
+                               if sampler == "zsobol" and zsobol_table else 0),
+    }
+    return sum(parts.values()), parts
+
+
+def camera_bytes(samples, sampler, zsobol_table=True):
+    """The camera stage's algorithmic bytes for `samples` samples: its records (88 / 100 B per
+    sample) + the ZSobol pixel-table entries (6 draws per quad of 4 samples of one pixel)."""
+    b = BYTES_CAMERA_WRITE[sampler] * samples
+    if sampler == "zsobol" and zsobol_table:
+        b += ZSOBOL_TABLE_BYTES_PER_DRAW * ZSOBOL_CAMERA_DRAWS * samples // 4
+    return b
+
+
+def kernel_targs(name):
+    """The template arguments of a k_paths kernel name as a tuple of strings: from the demangled
+    form ('void avr::k_paths<false, true, 3, 0, false, false>(avr::Params)', avr_last_kernel's
+    'k_paths<...>') or the Itanium-mangled one ('_ZN3avr7k_pathsILb0ELb1ELi3ELi0ELb0ELb0EEEv...')."""
+    m = re.search(r"k_paths<([^>]*)>", name)
+    if m:
+        return tuple(a.strip() for a in m.group(1).split(","))
+    m = re.search(r"7k_pathsI((?:L[bi]\d+E)+)E", name)
+    if m:
+        out = []
+        for kind, val in re.findall(r"L([bi])(\d+)E", m.group(1)):
+            out.append(("true" if val == "1" else "false") if kind == "b" else val)
+        return tuple(out)
+    return None
+
+
 # rocprofv3 passes (one run each; at most 8 SQ, 4 TCC (FETCH_SIZE 3, WRITE_SIZE 2), 2 GRBM)
 PMC_PASSES = (("fetch", ("FETCH_SIZE",)), ("write", ("WRITE_SIZE",)), ("tcc", ("TCC_HIT_sum", "TCC_MISS_sum")),
               ("sq", ("SQ_INSTS_VALU", "SQ_WAVE_CYCLES", "SQ_ACTIVE_INST_ANY", "SQ_WAIT_INST_ANY", "SQ_WAIT_ANY",
                       "SQ_WAVES", "GRBM_GUI_ACTIVE")))
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=4)
@@ -58,11 +129,12 @@ def parse():
     p.add_argument("--width", type=int, default=1280)
     p.add_argument("--height", type=int, default=720)
     p.add_argument("--spp-per-step", type=int, default=64,
-                   help="sample indices per pass (one step); 64 x 720p = 59M k_paths records, 1.9 GB)")
+                   help="sample indices per pass (one step); 64 x 720p = 59M samples: k_paths' 16-B records and the "
+                        "camera stage's 100 B per sample, 6.8 GB)")
     p.add_argument("--max-paths", type=int, default=0)
     p.add_argument("--pixelsamples", type=int, default=0,
                    help="sampler pixelsamples (0: the smallest power of two >= 256 holding every timed sample index "
-                        "of every rank, launch.sample_plan)")
+                        "of every rank of an 8-GPU world, the same at every N: launch.sample_plan)")
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU-baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--pmc", default="auto", choices=["auto", "on", "off"],
@@ -103,7 +175,7 @@ def parse():
                         "SpectralFilm (pixelsamples >= 4096); rgb-explosion: C5 as an emissive RGB-coefficient RGBGridMedium "
                         "(k_rgb_explosion, 3 x 16 GiB at 1024^3) with a SpectralFilm")
     p.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
-    return p.parse_args()
+    return p.parse_args(argv)
 
 
 def log(msg):
@@ -210,23 +282,35 @@ def cpu_baseline(scene_host, spp_per_step, budget_s, label="S-cloud"):
                       f"scene, {t_used:.1f} s on {cores} threads"}
 
 
-def pmc_passes(args, kernel_re=r"\bk_paths<|\dk_pathsI", timeout_s=240):
-    """rocprofv3 counter passes of this same bench configuration, one child process per
-    pass (--pmc only: no tracing in the same run), each killed after timeout_s. Returns
-    per-launch averages of the dominant kernel's counters, or None. kernel_re matches the
-    kernel name, demangled or mangled (k_paths itself, not the camera stage k_paths_camera)."""
-    exe = shutil.which("rocprofv3")
-    if exe is None:
-        return None, "rocprofv3 not found"
+def pmc_child_argv(args, pixelsamples):
+    """The command of one counter-pass child: this configuration, 2 timed steps after 1 warmup,
+    at the parent's resolved pixelsamples (not re-planned: the plan depends on --steps)."""
     child = [sys.executable, os.path.join(ROOT, "bench.py"), "--pmc-child", "--no-cpu-baseline", "--pmc", "off",
              "--steps", "2", "--warmup", "1"]
-    for k in ("res", "width", "height", "spp_per_step", "max_paths", "pixelsamples", "pixel_order", "kernel", "medium",
+    child += ["--pixelsamples", str(int(pixelsamples))]
+    for k in ("res", "width", "height", "spp_per_step", "max_paths", "pixel_order", "kernel", "medium",
               "refill_min", "grid_layout",
               "dda_budget", "zsobol_table", "sampler", "filter", "mode", "majorant_res", "ray_binning", "occupancy", "nvdb",
               "scene"):
         if getattr(args, k) is not None:
             child += [f"--{k.replace('_', '-')}", str(getattr(args, k))]
+    return child
+
+
+def pmc_passes(args, pixelsamples, kernel_re=r"\bk_paths<|\dk_pathsI", timeout_s=240):
+    """rocprofv3 counter passes of this same bench configuration, one child process per
+    pass (--pmc only: no tracing in the same run), each killed after timeout_s. The child
+    renders with the parent's RESOLVED pixelsamples (so the same k_paths instantiation and
+    ZSobol digit count) and the parent's first timed sample indices (world 1: steps 0 and 1
+    render [0, S) and [S, 2S)). Returns (per-launch averages of the dominant kernel's counters,
+    error, the set of kernel names matched), or None. kernel_re matches the kernel name,
+    demangled or mangled (k_paths itself, not the camera stage k_paths_camera)."""
+    exe = shutil.which("rocprofv3")
+    if exe is None:
+        return None, "rocprofv3 not found", set()
+    child = pmc_child_argv(args, pixelsamples)
     out = {}
+    names = set()
     tmp = tempfile.mkdtemp(prefix="avr_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
     try:
         for name, counters in PMC_PASSES:
@@ -247,18 +331,19 @@ def pmc_passes(args, kernel_re=r"\bk_paths<|\dk_pathsI", timeout_s=240):
                     if el > timeout_s:
                         proc.kill()
                         proc.wait()
-                        return None, f"pmc pass {name} timed out"
+                        return None, f"pmc pass {name} timed out", names
                     log(f"pmc pass {name}: running {el:.0f} s")
             if rc != 0:
                 errf.seek(0)
-                return None, f"pmc pass {name} exited {rc}: {errf.read().decode(errors='replace')[-300:]}"
+                return None, f"pmc pass {name} exited {rc}: {errf.read().decode(errors='replace')[-300:]}", names
             files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
             if not files:
-                return None, f"pmc pass {name}: no counter file"
+                return None, f"pmc pass {name}: no counter file", names
             per = {}
             for fn in files:
                 for row in csv.DictReader(open(fn)):
                     if re.search(kernel_re, row["Kernel_Name"]):
+                        names.add(row["Kernel_Name"])
                         per.setdefault(row["Counter_Name"], {}).setdefault(row.get("Dispatch_Id", ""), 0.0)
                         per[row["Counter_Name"]][row.get("Dispatch_Id", "")] += float(row["Counter_Value"])
             for cn, disp in per.items():
@@ -266,7 +351,7 @@ def pmc_passes(args, kernel_re=r"\bk_paths<|\dk_pathsI", timeout_s=240):
                 vals = [disp[k] for k in sorted(disp, key=lambda x: int(x) if x.isdigit() else 0)]
                 vals = vals[1:] if len(vals) > 1 else vals
                 out[cn] = sum(vals) / len(vals)
-        return out, None
+        return out, None, names
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
 
@@ -434,6 +519,8 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     agg = integ.ctx.stats()   # device counters + per-launch HIP-event times of the timed steps
+    # the k_paths instantiation the timed steps ran (before the fast-mode leg launches another)
+    timed_kernel = integ.ctx.last_kernel() if agg.get("loop_iterations") else "k_medium"
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{dev}")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -491,22 +578,38 @@ def main():
     med_s = agg["ms_medium"] / 1e3
     launches = max(1, agg["medium_launches"])
     persistent = bool(agg.get("loop_iterations"))   # k_paths counts its wave loop iterations
+    medium_kind = "rgb" if args.scene == "rgb-explosion" else ("nanovdb" if vdb is not None else "grid")
+    emissive = "explosion" in args.scene
+    samples_timed = npix * S * args.steps          # this rank's samples in the timed region
+    samples_per_launch = samples_timed / launches
+    bytes_parts = None
     if persistent:
-        # k_paths fuses delta tracking and ratio tracking: 32 B per trilinear lookup (both kinds)
-        # + the 32 B per-sample record it writes; path state never leaves VGPRs.
+        # k_paths fuses delta tracking and ratio tracking: per-unit bytes of kpaths_bytes()
+        # (lookups by medium kind + the 16-B sample record + the camera record it reads per path
+        # + ZSobol table entries); path state never leaves VGPRs / LDS
         kname = "k_paths (persistent: delta + ratio tracking, density fetch)"
-        med_bytes = (BYTES_PER_LOOKUP * (agg["medium_lookups"] + agg["shadow_lookups"]) +
-                     BYTES_PER_SAMPLE_RECORD * agg["medium_items_in"])
+        med_bytes, bytes_parts = kpaths_bytes(agg, args.sampler, medium_kind, emissive, args.zsobol_table > 0)
     else:
         kname = "k_medium (wavefront delta tracking + density fetch)"
         med_bytes = BYTES_PER_LOOKUP * agg["medium_lookups"] + BYTES_PER_ITEM * (agg["medium_items_in"] +
                                                                                 agg["medium_items_out"])
     achieved = med_bytes / med_s / 1e9 if med_s > 0 else 0.0
     avg_launch_ms = agg["ms_medium"] / launches
+    # the camera stage (k_paths_camera), one launch per k_paths launch
+    cam_block = None
+    if persistent and agg["ms_camera"] > 0:
+        cb = camera_bytes(samples_timed, args.sampler, args.zsobol_table > 0)
+        cam_block = {"kernel": "k_paths_camera", "bytes_per_launch": cb / launches,
+                     "avg_launch_ms": round(agg["ms_camera"] / launches, 4),
+                     "achieved": round(cb / (agg["ms_camera"] / 1e3) / 1e9, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                     "frac": round(cb / (agg["ms_camera"] / 1e3) / 1e9 / HBM_PEAK_GBPS, 5),
+                     "bytes_per_sample": round(cb / samples_timed, 2)}
     grid_layout = "fat" if integ.ctx.grid_layout_active() else "linear"
     host_density = host_rgb = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and vdb is None:
-        if args.scene == "rgb-explosion":
+        if args.scene == "rgb-explosion" and n > RGB_CPU_MAX_RES:
+            pass   # no host copy (the CPU baseline is skipped below)
+        elif args.scene == "rgb-explosion":
             host_rgb = [t.cpu().numpy() for t in rgb_grids]
         else:
             host_density = density.cpu().numpy()
@@ -522,6 +625,9 @@ def main():
             # the oracle's own NanoVDB tree for a 1024^3 grid takes over 10 minutes to build
             # on the host: the NanoVDB lines at that size carry no CPU baseline
             cpu = {"value": None, "skipped": f"oracle NanoVDB scene build at {n}^3 exceeds the bench's time budget"}
+        elif args.scene == "rgb-explosion" and n > RGB_CPU_MAX_RES and not args.no_cpu_baseline and world == 1:
+            cpu = {"value": None, "skipped": f"the three RGB-coefficient grids at {n}^3 ({3 * 16 * n ** 3 / 2 ** 30:.0f} GiB) "
+                                             f"exceed the host copy the oracle scene needs (limit {RGB_CPU_MAX_RES}^3)"}
         elif not args.no_cpu_baseline and world == 1:
             if vdb is not None:
                 host_scene = scene
@@ -542,13 +648,22 @@ def main():
         # configuration (child processes; the guide's gfx950 rule: FETCH_SIZE x2 + WRITE_SIZE)
         traffic, limiter, pmc_note, cache = None, None, "pmc off", None
         want_pmc = args.pmc == "on" or (args.pmc == "auto" and world == 1)
+        pmc_kernel = None
         if want_pmc:
-            ctr, err = pmc_passes(args, kernel_re=r"\bk_paths<|\dk_pathsI" if persistent else r"\bk_medium\b|\dk_mediumE")
+            ctr, err, names = pmc_passes(args, spp_total,
+                                         kernel_re=r"\bk_paths<|\dk_pathsI" if persistent else r"\bk_medium\b|\dk_mediumE")
+            if persistent and ctr is not None:
+                # the counters must come from the instantiation the parent timed
+                got = {kernel_targs(nm) for nm in names}
+                pmc_kernel = sorted(names)[0] if len(names) == 1 else sorted(names)
+                if got != {kernel_targs(timed_kernel)}:
+                    ctr, err = None, f"pmc child profiled {sorted(names)}, the timed run launched {timed_kernel}"
             if ctr is None:
                 pmc_note = err
                 log(f"pmc: {err}")
             else:
-                pmc_note = "rocprofv3 --pmc child passes of this configuration (bench.py pmc_passes)"
+                pmc_note = (f"rocprofv3 --pmc child passes of this configuration (bench.py pmc_passes, pixelsamples "
+                            f"{spp_total}, same instantiation)")
                 if "FETCH_SIZE" in ctr and "WRITE_SIZE" in ctr:
                     traffic = round((2 * ctr["FETCH_SIZE"] + ctr["WRITE_SIZE"]) * 1024 / 1e9, 4)
                 lookups_pl = (agg["medium_lookups"] + (agg["shadow_lookups"] if persistent else 0)) / launches
@@ -568,9 +683,11 @@ def main():
                         else "hbm",
                         "valu_issue_frac": round(valu_frac, 4),
                         "valu_wave_insts_per_launch": ctr["SQ_INSTS_VALU"],
-                        "valu_wave_insts_per_sample": round(ctr["SQ_INSTS_VALU"] / (npix * S), 1),
+                        # per launch: the child renders the same pass size (S sample indices per launch)
+                        "valu_wave_insts_per_sample": round(ctr["SQ_INSTS_VALU"] / samples_per_launch, 1),
                         "effective_clock_ghz": round(clk / 1e9, 3),
                         "waves": ctr.get("SQ_WAVES"),
+                        "waves_per_simd": round(ctr["SQ_WAVES"] / VALU_SIMDS, 2) if ctr.get("SQ_WAVES") else None,
                         "wave_cycle_split": {"issuing": round(ctr["SQ_ACTIVE_INST_ANY"] / wc, 4),
                                              "dependency/issue stall": round(ctr["SQ_WAIT_INST_ANY"] / wc, 4),
                                              "s_waitcnt (memory/LDS)": round(ctr["SQ_WAIT_ANY"] / wc, 4)},
@@ -599,6 +716,8 @@ def main():
                        "pixelsamples": spp_total, "sample_indices_distinct": True},
             "roofline": {
                 "kernel": kname,
+                "instantiation": timed_kernel,
+                "pmc_kernel": pmc_kernel,
                 # what limits the kernel, from the counter passes (`limiter`); `achieved` /
                 # `peak` / `frac` stay priced against the HBM roof (no MFMA work on the path)
                 "bound": ("valu" if limiter and limiter["kind"].startswith("valu") else "hbm"),
@@ -610,8 +729,18 @@ def main():
                 "traffic": traffic,
                 "traffic_source": pmc_note,
                 "bytes_per_launch": med_bytes / launches,
+                "bytes_parts_per_launch": ({k: v / launches for k, v in bytes_parts.items()} if bytes_parts else None),
+                "samples_per_launch": samples_per_launch,
                 "avg_launch_ms": avg_launch_ms,
                 "launches": launches,
+                # the ceiling of this access pattern: a random 32-B fat-entry gather moves one whole
+                # memory-side request (64 B) per lookup, so at the achievable 6.3 TB/s at most half of
+                # the bytes are the lookup's own
+                "attainable": {"random_gather_GBps": HBM_ACHIEVABLE_GBPS * BYTES_PER_LOOKUP / HBM_REQUEST_BYTES,
+                               "basis": f"{HBM_ACHIEVABLE_GBPS:.0f} GB/s achievable x {BYTES_PER_LOOKUP} B used per "
+                                        f"{HBM_REQUEST_BYTES}-B request",
+                               "frac": round(achieved / (HBM_ACHIEVABLE_GBPS * BYTES_PER_LOOKUP / HBM_REQUEST_BYTES), 5)},
+                "camera_stage": cam_block,
                 "limiter": limiter,
                 "cache": cache,
             },

@@ -39,7 +39,9 @@ typedef struct avr_context avr_context;
 typedef struct avr_stats {
     unsigned long long medium_lookups;  /* SamplePoint density fetches in k_medium   */
     unsigned long long medium_items_in; /* work items consumed by k_medium           */
-    unsigned long long medium_items_out;/* survivors + shadow rays pushed by k_medium */
+    unsigned long long medium_items_out;/* survivors + shadow rays pushed by k_medium;
+                                           k_paths: phase-function samples (real scatters
+                                           that continue the path)                  */
     unsigned long long shadow_lookups;  /* density fetches in k_shadow               */
     unsigned long long shadow_items;    /* shadow rays traced                        */
     unsigned long long medium_dda_steps;
@@ -58,7 +60,8 @@ const char *avr_last_error(void);
 
 /* Context on HIP device `device` (one process per GPU; no implicit peer access).
  * `max_paths` bounds the paths in flight per pass (0 = default: 64M for the persistent
- * kernel, whose per-path HBM state is one 32-B sample record, 16M for the wavefront
+ * kernel, whose per-sample HBM state is 116 B — the 16-B radiance record plus the camera
+ * stage's 6 x 16 B + 4 B, about 7.4 GB at 64M — 16M for the wavefront
  * kernels; at most 2^31 - 1: path ids are 32-bit, AVR_ERR_ARG above). */
 int avr_context_create(int device, long long max_paths, avr_context **out);
 /* Also releases the RCCL communicators the context shares with the other contexts of its
@@ -477,8 +480,16 @@ int avr_graph_in_node_path_length(avr_graph *g, float *average, long long *count
  * L, lambda, pdf and returns the pass's first sample index and sample count. */
 int avr_last_pass_samples(avr_context *ctx, float *L, float *lambda, float *pdf, long long n_max,
                           int *first_sample, int *n_samples);
-/* Filter weights (CameraSample::filterWeight) of the last pass's samples, same indexing. */
+/* Filter weights (CameraSample::filterWeight) of the last pass's samples, same indexing.
+ * Both readbacks fail with AVR_ERR_STATE once the pixel order (avr_set_pixel_order, or a new
+ * avr_film that drops it) changed after that render: its records are in the old slot order. */
 int avr_last_pass_weights(avr_context *ctx, float *weight, long long n_max);
+/* Template arguments of the last k_paths instantiation avr_render launched, as
+ * "k_paths<emissive, gray, sampler, medium, image, fast>" (sampler 0 independent, 2 / 3 ZSobol
+ * with 32- / 64-bit indices; "" before the first persistent render): lets a profiler pass
+ * (rocprofv3 kernel names) be matched to the configuration that was timed. NUL-terminated,
+ * truncated to cap bytes. */
+int avr_last_kernel(avr_context *ctx, char *buf, int cap);
 
 #ifdef __cplusplus
 }

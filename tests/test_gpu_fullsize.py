@@ -26,6 +26,7 @@ def cloud():
     gen.close()
     scene = scenes.s_cloud(density, sampler="zsobol", spp=256, filter="gaussian")
     integ = VolPathIntegrator(scene, maxdepth=scenes.CLOUD_MAXDEPTH, spp=16, device=0)
+    integ.density_tensor = density   # the device grid, for scenes at other sampler settings
     host = scenes.s_cloud(density.cpu().numpy(), sampler="zsobol", spp=256, filter="gaussian")
     yield integ, host
     integ.close()
@@ -53,6 +54,46 @@ def test_fullsize_majorant_and_replay(cloud):
                          np.array_equal(lam[g].view(np.uint32), lo.view(np.uint32)))
     print(f"full-size replay: {exact}/{total} samples bit-identical")
     assert exact / total >= 0.999
+
+
+def test_fullsize_replay_at_the_driver_headline_configuration(cloud):
+    """The exact configuration the driver times (`python bench.py --steps 20 --warmup 5`):
+    launch.sample_plan gives pixelsamples 16384 at every world size, so at 720p Morton(pixel)
+    (22 bits) << log2 spp (14) needs 36 bits and k_paths runs its 64-bit-index ZSobol
+    GridMedium instantiation (samplers.h:250-254). Strided pixel subset, two 16-index passes
+    (one inside the N = 1 timed range, one at the top of the N = 8 range): >= 99.9 % of the
+    samples bit-identical to the canonical oracle, with the instantiation checked by name."""
+    from acceleratedvolrenderer_amd import VolPathIntegrator, scenes
+    from acceleratedvolrenderer_amd.launch import sample_plan
+    from oracle import binding
+    integ256, host256 = cloud
+    P = sample_plan(1, 20, 5, 64)[0]
+    assert P == sample_plan(8, 20, 5, 64)[0] == 16384
+    scene = scenes.s_cloud(integ256.density_tensor, sampler="zsobol", spp=P, filter="gaussian")
+    integ = VolPathIntegrator(scene, maxdepth=scenes.CLOUD_MAXDEPTH, spp=16, device=0)
+    try:
+        host = scenes.s_cloud(host256.medium.density, sampler="zsobol", spp=P, filter="gaussian")
+        canon = binding.OracleRun(host, max_depth=scenes.CLOUD_MAXDEPTH, seed=0, libm="canonical")
+        f = host.film
+        npix = f.width * f.height
+        pixels = np.arange(0, npix, 4099)
+        exact = total = 0
+        for base in (640, 8 * 20 * 64 - 16):
+            integ.ctx.film_clear()
+            integ.ctx.render(base, base + 16, 0, scenes.CLOUD_MAXDEPTH)
+            assert integ.ctx.last_kernel() == "k_paths<false, true, 3, 0, false, false>"
+            _, _, L, lam, _ = integ.ctx.last_pass_samples(npix, 16)
+            for pix in pixels:
+                for s in range(16):
+                    Lo, lo, _, _ = canon.pixel_sample(int(pix % f.width), int(pix // f.width), base + s)
+                    g = s * npix + int(pix)
+                    total += 1
+                    exact += int(np.array_equal(L[g].view(np.uint32), Lo.view(np.uint32)) and
+                                 np.array_equal(lam[g].view(np.uint32), lo.view(np.uint32)))
+        print(f"headline-config replay (pixelsamples {P}, 64-bit ZSobol): {exact}/{total} samples bit-identical")
+        assert exact / total >= 0.999
+    finally:
+        integ.close()
 
 
 def test_fullsize_multipass_and_determinism(cloud):

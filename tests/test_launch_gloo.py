@@ -51,19 +51,39 @@ def test_launcher_refuses_a_mismatched_world():
 def test_bench_sample_plan_renders_distinct_indices_at_every_world_size():
     """bench.py's step arithmetic (launch.sample_plan): over the timed steps of all ranks every
     (pixel, sample index) pair is rendered exactly once, inside [0, pixelsamples), for the
-    driver's 1/2/4/8-GPU runs; N = 1 with 4 steps of 64 keeps config C3's 256 spp."""
+    driver's 1/2/4/8-GPU runs."""
     from acceleratedvolrenderer_amd.launch import sample_plan
     for world in (1, 2, 4, 8):
-        for steps, warmup, S in ((4, 1, 64), (10, 2, 64), (3, 0, 16)):
+        for steps, warmup, S in ((4, 1, 64), (10, 2, 64), (3, 0, 16), (20, 5, 64)):
             P, warm, timed = sample_plan(world, steps, warmup, S)
             idx = [b + i for r in range(world) for b in timed[r] for i in range(S)]
             assert len(idx) == len(set(idx)) == steps * world * S
             assert min(idx) == 0 and max(idx) < P and P >= 256 and P & (P - 1) == 0
             assert all(0 <= b and b + S <= P for r in range(world) for b in warm[r])
             assert len(warm[0]) == warmup and all(len(t) == steps for t in timed)
-    assert sample_plan(1, 4, 1, 64)[0] == 256
-    assert sample_plan(8, 4, 1, 64)[0] == 2048
     assert sample_plan(1, 4, 1, 64, base_spp=4096)[0] == 4096
     import pytest
     with pytest.raises(ValueError):
         sample_plan(8, 4, 1, 64, pixelsamples=256)
+    with pytest.raises(ValueError):
+        sample_plan(0, 4, 1, 64)
+
+
+def test_bench_sample_plan_pixelsamples_is_invariant_in_the_world_size():
+    """One bench command runs the same sampler at N = 1, 2, 4 and 8: the
+    pixelsamples value, hence the ZSobol index width and the digits per draw (samplers.h:250-254),
+    does not depend on the world size, and is sized for the 8-GPU world."""
+    from acceleratedvolrenderer_amd.launch import sample_plan
+    for steps, warmup, S in ((4, 1, 64), (10, 2, 64), (3, 0, 16), (20, 5, 64), (2, 1, 64)):
+        Ps = {sample_plan(world, steps, warmup, S)[0] for world in (1, 2, 4, 8)}
+        assert len(Ps) == 1, (steps, S, Ps)
+        P = Ps.pop()
+        assert P >= steps * 8 * S
+    # the driver's command: python bench.py --steps 20 --warmup 5 (64 sample indices per step)
+    assert sample_plan(1, 20, 5, 64)[0] == sample_plan(8, 20, 5, 64)[0] == 16384
+    assert sample_plan(1, 4, 1, 64)[0] == 2048
+    # the index ranges of different world sizes are prefixes of one another's sequence: the
+    # timed steps of world N cover [0, steps * N * S)
+    for world in (1, 2, 4, 8):
+        _, _, timed = sample_plan(world, 20, 5, 64)
+        assert sorted(b for r in range(world) for b in timed[r]) == list(range(0, 20 * world * 64, 64))
