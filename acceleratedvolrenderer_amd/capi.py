@@ -153,6 +153,7 @@ SIGNATURES = {
     "avr_set_filter": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, c_float_p, ctypes.c_float]),
     "avr_set_sampler": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]),
     "avr_set_sampler_table": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "avr_set_sampler_pass_table": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "avr_set_pixel_order": (ctypes.c_int, [ctypes.c_void_p, c_int_p, ctypes.c_longlong]),
     "avr_film": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, c_float_p, c_float_p, ctypes.c_float,
                                 ctypes.c_float]),
@@ -317,6 +318,10 @@ class Context:
     def set_sampler_table(self, dims):
         """ZSobol pixel-table dimensions (0 = compute every digit per call)."""
         _check(self.lib.avr_set_sampler_table(self.h, int(dims)))
+
+    def set_sampler_pass_table(self, dims):
+        """ZSobol per-pass table dimensions (avr_set_sampler_pass_table; 0 = off, default 64)."""
+        _check(self.lib.avr_set_sampler_pass_table(self.h, int(dims)))
 
     def set_pixel_order(self, order):
         """avr_set_pixel_order: the persistent kernel's pixel order (a permutation of the film's

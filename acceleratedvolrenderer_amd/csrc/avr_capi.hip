@@ -151,6 +151,11 @@ struct avr_context {
     uint32_t *d_zs_table = nullptr;
     int zs_dims = 256;
     int zs_key[3] = {-1, -1, -1};
+    // ZSobol pass table (zsobol_pass_entry per Morton(pixel) x dimension < zs_pdims), rebuilt
+    // for every k_paths pass: the digits its sample indices share; zs_pdims 0 = no table
+    uint64_t *d_zs_ptab = nullptr;
+    size_t zs_ptab_cap = 0;   // entries allocated
+    int zs_pdims = 64;
     int refill_min = 0;       // 0: the default (32 lanes; 12 for a non-emissive NanoVDB walk, 16 for RGB grids)
     int dda_budget = 0;       // 0: by majorant resolution (12 cells up to 16^3, 32 for NanoVDB's 64^3)
     int grid_layout = 1;
@@ -528,6 +533,8 @@ int medium_common(avr_context *c, const float *d_density, int nx, int ny, int nz
     m.g = g;
     c->gray = true;
     for (int i = 1; i < avr::kNTable; ++i) c->gray &= sigma_a[i] == sigma_a[0] && sigma_s[i] == sigma_s[0];
+    c->med.gray_sigma_a = sigma_a[0];
+    c->med.gray_sigma_s = sigma_s[0];
     // isEmissive = Le_spec.MaxValue() > 0 (media.cpp:238)
     bool emissive = false;
     if (Le) for (int i = 0; i < avr::kNTable; ++i) emissive |= Le[i] > 0;
@@ -717,6 +724,7 @@ int avr_context_destroy(avr_context *c) {
     free_rgb(c);
     for (auto &b : c->d_light_img) if (b) (void)hipFree(b), b = nullptr;
     if (c->d_zs_table) (void)hipFree(c->d_zs_table);
+    if (c->d_zs_ptab) (void)hipFree(c->d_zs_ptab);
     if (c->d_image) (void)hipFree(c->d_image);
     if (c->d_reference) (void)hipFree(c->d_reference);
     if (c->d_metric) (void)hipFree(c->d_metric);
@@ -1463,6 +1471,13 @@ int avr_set_sampler_table(avr_context *c, int dims) {
     return AVR_OK;
 }
 
+int avr_set_sampler_pass_table(avr_context *c, int dims) {
+    AVR_QUIESCE(c);
+    if (!c || dims < 0 || dims > 4096) return fail(AVR_ERR_ARG, "sampler pass table dimensions must be 0..4096");
+    c->zs_pdims = dims;
+    return AVR_OK;
+}
+
 int avr_set_sampler(avr_context *c, int kind, int samples_per_pixel) {
     if (!c || (kind != 0 && kind != 1) || samples_per_pixel < 1)
         return fail(AVR_ERR_ARG, "sampler: kind 0 (independent) or 1 (zsobol), samples_per_pixel >= 1");
@@ -1681,6 +1696,39 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
                     {avr::k_paths_camera<0, false>, avr::k_paths_camera<2, false>, avr::k_paths_camera<3, false>},
                     {avr::k_paths_camera<0, true>, avr::k_paths_camera<2, true>, avr::k_paths_camera<3, true>}};
                 EV_MARK(ec);
+                if (c->sampler_kind == 1 && c->zs_pdims > 0) {
+                    // ZSobol pass table: the digits of GetSampleIndex that the pass's sample
+                    // indices [base, base + S) share (those above their lowest differing bits),
+                    // for the first zs_pdims dimensions; the camera stage and k_paths then
+                    // evaluate only the digits below (two MixBits at 64 indices per pass)
+                    int plo = 0;
+                    while ((base >> plo) != ((base + S - 1) >> plo)) ++plo;
+                    const size_t rows = (size_t)avr::smp::encode_morton2((uint32_t)c->film.width - 1,
+                                                                        (uint32_t)c->film.height - 1) + 1;
+                    const size_t need_e = rows * (size_t)c->zs_pdims;
+                    if (need_e > c->zs_ptab_cap) {
+                        if (c->d_zs_ptab) (void)hipFree(c->d_zs_ptab);
+                        c->d_zs_ptab = nullptr;
+                        c->zs_ptab_cap = 0;
+                        if (hipMalloc((void **)&c->d_zs_ptab, need_e * sizeof(uint64_t)) != hipSuccess) {
+                            (void)hipGetLastError();
+                            c->d_zs_ptab = nullptr;   // no room: the pixel table / every digit per call
+                        } else {
+                            c->zs_ptab_cap = need_e;
+                        }
+                    }
+                    if (c->d_zs_ptab) {
+                        hipLaunchKernelGGL(avr::k_zsobol_pass_table,
+                                           dim3(blocks_for((long long)c->film.width * c->film.height * c->zs_pdims, 256,
+                                                           256 * 64)),
+                                           dim3(256), 0, c->stream, zs, c->film.width, c->film.height, c->zs_pdims, plo,
+                                           base, c->d_zs_ptab);
+                        HIP_TRY(hipGetLastError());
+                        p.zs.ptab = c->d_zs_ptab;
+                        p.zs.pdims = c->zs_pdims;
+                        p.zs.plo = plo;
+                    }
+                }
                 hipLaunchKernelGGL(kcam[c->render_mode ? 1 : 0][sv], dim3(blocks_for(n0, 256, 256 * 8)), dim3(256), 0,
                                    c->stream, p);
                 HIP_TRY(hipGetLastError());

@@ -36,6 +36,7 @@ struct DevMedium {
     Xf render_from_medium, medium_from_render;
     const float *sigma_a, *sigma_s;   // 471-entry densely sampled tables (sigmaScale folded in)
     float g;
+    float gray_sigma_a, gray_sigma_s;   // sigma_a[0], sigma_s[0]: the whole tables when the medium is gray
     int emissive;
     const float *Le;                  // 471
     const float *lescale;
@@ -319,27 +320,40 @@ __device__ __forceinline__ float grid_lookup(const float *__restrict__ v, int nx
     return lerp(dz, lerp(dy, d00, d10), lerp(dy, d01, d11));
 }
 
-// Same value as grid_lookup() bit for bit (same taps, same lerp order) from the fat layout.
-__device__ __forceinline__ float fat_lookup(const float4 *__restrict__ fat, const float *__restrict__ v, int nx, int ny,
-                                            int nz, V3 p) {
+// Same value as grid_lookup() bit for bit (same taps, same lerp order) from the fat layout,
+// in two halves so a caller can issue the gather early and combine it later (k_paths issues
+// it before the DDA walk and consumes it after, hiding the HBM latency behind the walk).
+// fat_issue: false when p's footprint lies outside the fat copy (grid_lookup applies).
+__device__ __forceinline__ bool fat_issue(const float4 *__restrict__ fat, int nx, int ny, int nz, V3 p, float4 &a,
+                                          float4 &b, float &dx, float &dy, float &dz) {
     float psx = p.x * nx - .5f, psy = p.y * ny - .5f, psz = p.z * nz - .5f;
     int ix = (int)__builtin_floorf(psx), iy = (int)__builtin_floorf(psy), iz = (int)__builtin_floorf(psz);
-    if (ix < -1 || ix >= nx || iy < -1 || iy >= ny || iz < -1 || iz >= nz) return grid_lookup(v, nx, ny, nz, p);
-    float dx = psx - (float)ix, dy = psy - (float)iy, dz = psz - (float)iz;
+    if (ix < -1 || ix >= nx || iy < -1 || iy >= ny || iz < -1 || iz >= nz) return false;
+    dx = psx - (float)ix, dy = psy - (float)iy, dz = psz - (float)iz;
     const size_t e = (((size_t)(iz + 1) * (ny + 1) + (iy + 1)) * (nx + 1) + (ix + 1)) * 2;
 #if AVR_NT_FETCH
     typedef float v4f __attribute__((ext_vector_type(4)));
     const v4f va = __builtin_nontemporal_load(reinterpret_cast<const v4f *>(fat + e)),
               vb = __builtin_nontemporal_load(reinterpret_cast<const v4f *>(fat + e + 1));
-    const float4 a = make_float4(va.x, va.y, va.z, va.w), b = make_float4(vb.x, vb.y, vb.z, vb.w);
+    a = make_float4(va.x, va.y, va.z, va.w), b = make_float4(vb.x, vb.y, vb.z, vb.w);
 #else
-    const float4 a = fat[e], b = fat[e + 1];
+    a = fat[e], b = fat[e + 1];
 #endif
+    return true;
+}
+__device__ __forceinline__ float fat_lerp(float4 a, float4 b, float dx, float dy, float dz) {
     float d00 = lerp(dx, a.x, a.y);
     float d10 = lerp(dx, a.z, a.w);
     float d01 = lerp(dx, b.x, b.y);
     float d11 = lerp(dx, b.z, b.w);
     return lerp(dz, lerp(dy, d00, d10), lerp(dy, d01, d11));
+}
+__device__ __forceinline__ float fat_lookup(const float4 *__restrict__ fat, const float *__restrict__ v, int nx, int ny,
+                                            int nz, V3 p) {
+    float4 a, b;
+    float dx, dy, dz;
+    if (!fat_issue(fat, nx, ny, nz, p, a, b, dx, dy, dz)) return grid_lookup(v, nx, ny, nz, p);
+    return fat_lerp(a, b, dx, dy, dz);
 }
 
 #ifndef AVR_KPATHS_TU   // host-launched kernels: compiled in the C-ABI translation unit only
@@ -805,7 +819,7 @@ __device__ __forceinline__ void camera_sample(const Params &P, Smp &smp, int px,
 // requester pulls its results back with ds_bpermute. Results are bit-identical to the
 // sequential get1d / get2d calls (ZSobol::draw_at: a pure function of sample and dimension);
 // the requesters' dimension then advances by `adv`. s_st: this wave's 64 LDS entries.
-constexpr int kDimHash = 264;   // Hash(d, seed) of the first dimensions, staged in LDS by k_paths
+constexpr int kDimHash = 128;   // Hash(d, seed) of the first dimensions, staged in LDS by k_paths (paths deeper than ~15 bounces hash per draw)
 template <int kW, int N>
 __device__ __forceinline__ void coop_draws(smp::ZSobol &z, const smp::ZSobolParams &zp, bool req, const int (&off)[N],
                                            const bool (&two)[N], int adv, float (&r0)[N], float (&r1)[N], uint3 *s_st,
@@ -849,6 +863,51 @@ __device__ __forceinline__ void coop_draws(smp::ZSobol &z, const smp::ZSobolPara
         }
     }
     if (req) z.dimension += (uint32_t)adv;
+}
+
+// coop_draws with the results in LDS instead of registers: the lane that evaluates draw j of
+// requester rank r writes it to s_res[r * K + slot[j]] (a 2D draw's second value after it), so
+// no requester holds N results in VGPRs through the evaluation loop and no result travels by
+// ds_bpermute; returns the calling lane's rank (its record is s_res + rank * K).
+template <int kW, int N, int K>
+__device__ __forceinline__ int coop_draws_lds(smp::ZSobol &z, const smp::ZSobolParams &zp, bool req, const int (&off)[N],
+                                              const bool (&two)[N], const int (&slot)[N], int adv, float *s_res,
+                                              uint3 *s_st, const uint64_t *dhash = nullptr) {
+    const uint64_t mask = __ballot(req);
+    const int lane = lane_id();
+    const int rank = __popcll(mask & ((1ull << lane) - 1ull));
+    if (req) s_st[rank] = make_uint3(z.morton, z.hi, z.dimension);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int total = __popcll(mask) * N;
+    for (int c = 0; c < total; c += 64) {
+        const int t = c + lane;
+        if (t < total) {
+            const int r = t / N, j = t - r * N;
+            int o = off[0], sl = slot[0];
+            bool tw = two[0];
+            _Pragma("unroll") for (int jj = 1; jj < N; ++jj) {
+                o = j == jj ? off[jj] : o;
+                sl = j == jj ? slot[jj] : sl;
+                tw = j == jj ? two[jj] : tw;
+            }
+            const uint3 st = s_st[r];
+            smp::ZSobol q;
+            q.morton = st.x;
+            q.hi = st.y;
+            q.dimension = 0;
+            float v0, v1;
+            q.template draw_at<kW>(zp, st.z + (uint32_t)o, tw, &v0, &v1, dhash, dhash ? kDimHash : 0);
+            s_res[r * K + sl] = v0;
+            if (tw) s_res[r * K + sl + 1] = v1;
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (req) z.dimension += (uint32_t)adv;
+    return rank;
 }
 
 __device__ __forceinline__ const float *base_of(const smp::FilterTables &t) { return t.f; }
@@ -911,11 +970,12 @@ __device__ __forceinline__ void quad_digit(M morton, const uint32_t (&mine)[2], 
         idx |= smp::zperm(p, (uint32_t)(morton >> shift) & 3u) << shift;
     }
 }
+// digits iLo..iHi (at most 8, log2 spp <= 16) and an odd log2(spp)'s final base-2 digit
 template <typename M>
-__device__ __forceinline__ uint32_t zsobol_lower_quad(M morton, uint32_t dimension, const smp::ZSobolParams &zp) {
+__device__ __forceinline__ uint32_t zsobol_lower_quad(M morton, uint32_t dimension, const smp::ZSobolParams &zp,
+                                                      int iLo, int iHi) {
     constexpr int kBits = 8 * (int)sizeof(M);
     const int pw = zp.log2spp & 1;
-    const int iLo = pw, iHi = smp::zsobol_split(zp) - 1;   // at most 8 digits (log2 spp <= 16)
     const int q = lane_id() & 3;
     const uint32_t dmix = 0x55555555u * dimension;
     uint32_t mine[2] = {0, 0};
@@ -958,15 +1018,42 @@ __device__ __forceinline__ void zsobol_draw_quad(smp::ZSobol &z, const smp::ZSob
                                                  float *u1, const uint64_t *dh = nullptr) {
     uint32_t a, ah = 0;
     const uint32_t pm = kW == 2 ? (uint32_t)((((uint64_t)z.hi << 32) | z.morton) >> zp.log2spp) : z.morton >> zp.log2spp;
-    const uint32_t up = (zp.upper && (int)z.dimension < zp.dmax) ? zp.upper[(size_t)pm * (size_t)zp.dmax + z.dimension]
-                                                                   : smp::zsobol_upper(pm, z.dimension, zp);
-    if constexpr (kW == 2) {
-        const uint64_t m = ((uint64_t)z.hi << 32) | z.morton;
-        const uint64_t idx = ((uint64_t)up << zp.log2spp) | zsobol_lower_quad<uint64_t>(m, z.dimension, zp);
-        a = (uint32_t)idx;
-        ah = (uint32_t)(idx >> 32);
+    const int pw = zp.log2spp & 1;
+    if (zp.ptab && (int)z.dimension < zp.pdims) {
+        // the pass table (zsobol_pass_entry): the quad computes the varying digits only (those
+        // below the perm-fixed digit iTop, the highest one under the pass's plo bits)
+        const uint64_t e = zp.ptab[(size_t)pm * (size_t)zp.pdims + z.dimension];
+        const int iTop = (zp.plo + pw - 1) >> 1;
+        const uint32_t perm = (uint32_t)(e >> 56);
+        const uint64_t fx = (e & 0x00ffffffffffffffull) << zp.plo;
+        if constexpr (kW == 2) {
+            const uint64_t m = ((uint64_t)z.hi << 32) | z.morton;
+            uint64_t idx = fx | zsobol_lower_quad<uint64_t>(m, z.dimension, zp, pw, iTop - 1);
+            if (iTop >= pw) {
+                const int sh = 2 * iTop - pw;
+                idx |= (uint64_t)smp::zperm(perm, (uint32_t)(m >> sh) & 3u) << sh;
+            }
+            a = (uint32_t)idx;
+            ah = (uint32_t)(idx >> 32);
+        } else {
+            a = (uint32_t)fx | zsobol_lower_quad<uint32_t>(z.morton, z.dimension, zp, pw, iTop - 1);
+            if (iTop >= pw) {
+                const int sh = 2 * iTop - pw;
+                a |= smp::zperm(perm, (z.morton >> sh) & 3u) << sh;
+            }
+        }
     } else {
-        a = (up << zp.log2spp) | zsobol_lower_quad<uint32_t>(z.morton, z.dimension, zp);
+        const uint32_t up = (zp.upper && (int)z.dimension < zp.dmax) ? zp.upper[(size_t)pm * (size_t)zp.dmax + z.dimension]
+                                                                       : smp::zsobol_upper(pm, z.dimension, zp);
+        const int iHi = smp::zsobol_split(zp) - 1;
+        if constexpr (kW == 2) {
+            const uint64_t m = ((uint64_t)z.hi << 32) | z.morton;
+            const uint64_t idx = ((uint64_t)up << zp.log2spp) | zsobol_lower_quad<uint64_t>(m, z.dimension, zp, pw, iHi);
+            a = (uint32_t)idx;
+            ah = (uint32_t)(idx >> 32);
+        } else {
+            a = (up << zp.log2spp) | zsobol_lower_quad<uint32_t>(z.morton, z.dimension, zp, pw, iHi);
+        }
     }
     z.dimension += two ? 2 : 1;
     // Hash(dimension, seed): from the caller's staged table when it covers the dimension
@@ -1644,6 +1731,18 @@ __global__ void __launch_bounds__(256) k_bin_scatter(const int *__restrict__ que
 #ifndef AVR_NEE_AHEAD
 #define AVR_NEE_AHEAD 1
 #endif
+#ifndef AVR_COOP_LDS
+#define AVR_COOP_LDS 1
+#endif
+#ifndef AVR_WAVE_COUNTERS
+#define AVR_WAVE_COUNTERS 1
+#endif
+#ifndef AVR_OPAQUE_CONSTS
+#define AVR_OPAQUE_CONSTS 0
+#endif
+#ifndef AVR_FETCH_SPLIT
+#define AVR_FETCH_SPLIT 0   // 1: fetch before the walk, consume after it (measured -19 %)
+#endif
 #ifndef AVR_PATHS_WAVES_SPEC
 #define AVR_PATHS_WAVES_SPEC 2   // 4-wavelength state: ~220 VGPRs without scratch
 #endif
@@ -1744,7 +1843,9 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
     // LDS: majorant grid (16 KiB at pbrt's 16^3) + the 471-entry spectral tables the path
     // samples at path start, NEE and escape (sigma_a, sigma_s, up to 4 light spectra).
     __shared__ float s_maj[kVdb ? 1 : 4096];
-    __shared__ float s_tab[(2 + 4) * kNTable];
+    // (a gray medium's sigma_a / sigma_s are one value each: the kernel takes them as scalars)
+    constexpr int kSigTabs = kGray ? 0 : 2;
+    __shared__ float s_tab[(kSigTabs + 4) * kNTable];
     // ImageInfiniteLight shadow rays (non-delta NEE): the sampled (u, v), p_l and the phase
     // value per lane, parked here while the lane traces its shadow ray (off the VGPR budget)
     __shared__ float4 s_img[kImage ? 256 : 1];
@@ -1776,24 +1877,56 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
     }
     const int nlds = P.lights.n < 4 ? P.lights.n : 4;
     for (int i = threadIdx.x; i < kNTable; i += blockDim.x) {
-        s_tab[i] = P.med.sigma_a[i];
-        s_tab[kNTable + i] = P.med.sigma_s[i];
+        if constexpr (!kGray) {
+            s_tab[i] = P.med.sigma_a[i];
+            s_tab[kNTable + i] = P.med.sigma_s[i];
+        }
         for (int k = 0; k < nlds; ++k)
-            if (P.lights.list[k].type != 2) s_tab[(2 + k) * kNTable + i] = P.lights.list[k].L[i];
+            if (P.lights.list[k].type != 2) s_tab[(kSigTabs + k) * kNTable + i] = P.lights.list[k].L[i];
     }
     __syncthreads();
     const float *tab_sa = s_tab, *tab_ss = s_tab + kNTable;
     auto light_table = [&](int k) -> const float * {
-        return k < 4 ? s_tab + (2 + k) * kNTable : P.lights.list[k].L;
+        return k < 4 ? s_tab + (kSigTabs + k) * kNTable : P.lights.list[k].L;
     };
+#if AVR_OPAQUE_CONSTS
+    // a local copy whose loop-invariant scalars (grid and majorant resolutions, g, bounds) are
+    // passed through an empty asm at the top of the loops (opaque_consts): the compiler then
+    // re-derives float(n), 1 + g^2, bmax - bmin, ... from the scalar registers where they are
+    // used instead of hoisting ~20 derived copies into VGPRs for the kernel's lifetime
+    DevMedium m = P.med;
+    auto opaque_consts = [&]() {
+        asm volatile("" : "+s"(m.nx), "+s"(m.ny), "+s"(m.nz), "+s"(m.mres[0]), "+s"(m.mres[1]), "+s"(m.mres[2]));
+        asm volatile("" : "+s"(m.g), "+s"(m.bmin[0]), "+s"(m.bmin[1]), "+s"(m.bmin[2]), "+s"(m.bmax[0]),
+                     "+s"(m.bmax[1]), "+s"(m.bmax[2]));
+    };
+#else
     const DevMedium &m = P.med;
+    auto opaque_consts = [&]() {};
+#endif
     const int npix = P.pass_pixels;
     const long long N = (long long)npix * P.pass_samples;
     const int lane = lane_id();
     const int xcc = xcc_id();
     // work counters: per lane in 32 bits (a lane traces at most a few thousand segments per
     // launch), the wave-loop counters wave-uniform (scalar registers)
+#if AVR_WAVE_COUNTERS
+    // work counters off the VGPR budget: per wave in LDS, one ds_add by the first active lane
+    // of each event batch (wave_count); DDA steps as a wave-uniform (scalar) sum of ballots
+    __shared__ unsigned s_cnt[4][6];
+    if (threadIdx.x < 24) (&s_cnt[0][0])[threadIdx.x] = 0;
+    __syncthreads();
+    unsigned *const wcnt = s_cnt[threadIdx.x >> 6];
+    auto wave_count = [&](int k) {
+        const uint64_t am = __ballot(1);
+        if (lane_id() == __ffsll((long long)am) - 1) atomicAdd(wcnt + k, (unsigned)__popcll(am));
+    };
+    unsigned long long nStepsW = 0;
+#define AVR_COUNT(var, k) wave_count(k)
+#else
     uint32_t nLookup = 0, nSteps = 0, nPaths = 0, nShadow = 0, nShadowLookup = 0, nPhase = 0;
+#define AVR_COUNT(var, k) ++var
+#endif
     unsigned long long nIter = 0, nActive = 0;
 
     int mode = M_FETCH, ev = EV_NONE;
@@ -1802,12 +1935,20 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
     // path state (Li, integrators.cpp:966-971)
     Spec L{}, lam{}, Le_l{};
     S beta{}, r_u{}, r_l{}, sig_a{}, sig_s{};
+    // gray: the same sigma_a and sigma_s at every wavelength, for every path (host-checked)
+    if constexpr (kGray) {
+        sig_a = P.med.gray_sigma_a;
+        sig_s = P.med.gray_sigma_s;
+    }
     constexpr bool kZSobol = kSmp != 0;   // kSmp: 0 Independent, 2 / 3 ZSobol with 32 / 64-bit index
     // cooperative ZSobol draws (coop_draws) in the phase handler and the refill; the
     // 4-wavelength instantiations may opt out (AVR_COOP_SPEC=0: per-lane draws as pbrt does)
     constexpr bool kCoop = kZSobol && (kGray || AVR_COOP_SPEC);
     // the next light-pick draw evaluated ahead with the phase draws (s_ul)
     constexpr bool kUlAhead = kCoop && AVR_NEE_AHEAD;
+    // ... with the cooperative draws' results in LDS (coop_draws_lds)
+    constexpr bool kCoopLds = kUlAhead && AVR_COOP_LDS;
+    __shared__ float s_res[kCoopLds ? 256 * 6 : 1];
     PathSampler<kSmp> smp{};
     int depth = 0;
     V3 po{}, pd{};         // segment origin (== the path vertex) and the path's ray direction
@@ -1818,6 +1959,12 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
     V3 sd{};               // normalised segment direction
     S T_maj{};
     bool needNext = true, shadowStopped = false;
+    // DDA walk state of the lane: 0 walking, 1 a candidate pending its exact decision (kept
+    // across tracking iterations with kFetchSplit), 2 segments exhausted, 3 collision in flight
+    int walk = 0;
+    // GridMedium with the fat layout: the collision's density gather is issued before the DDA
+    // walk of the other lanes and consumed after it (AVR_FETCH_SPLIT)
+    constexpr bool kFetchSplit = AVR_FETCH_SPLIT && kMed == 0;
     bool segPending = false;      // a segment start is queued for the shared block below
     uint64_t seqA = 0, seqB = 0;  // its RNG SetSequence arguments
     // shadow state (SampleLd, integrators.cpp:1339-1391)
@@ -1832,11 +1979,13 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
         ddal_init(it, m, Ray{o, d}, tMax, majp);
         T_maj = sconst<S>(1.f);
         needNext = true;
+        walk = 0;
     };
 
     AVR_SEC_INIT
     while (true) {
         AVR_SEC(0)
+        opaque_consts();
         // =================== batched event handlers (each runs once per batch) ===========
         if (__ballot(ev == EV_SCATTER)) {
             if (ev == EV_SCATTER) {
@@ -1886,7 +2035,7 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
                                     segPending = true;
                                     mode = M_SHADOW;
                                     ev = EV_NONE;
-                                    ++nShadow;
+                                    AVR_COUNT(nShadow, 4);
                                 }
                             }
                         } else if (lt.type == 0) {
@@ -1907,7 +2056,7 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
                                 segPending = true;
                                 mode = M_SHADOW;
                                 ev = EV_NONE;
-                                ++nShadow;
+                                AVR_COUNT(nShadow, 4);
                             }
                         }
                     }
@@ -1952,7 +2101,18 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
             // EV_PHASE, evaluated cooperatively by the whole wave
             // (and, at offset 5, the next bounce's light-pick draw, parked in s_ul)
             float q0[5], q1[5];
-            if constexpr (kUlAhead) {
+            [[maybe_unused]] const float *qr = nullptr;   // this lane's results in s_res (kCoopLds)
+            if constexpr (kCoopLds) {
+                // [u0, u1] phase 2D, [h0, h1, u] the next segment, [ul] the next light pick
+                constexpr int off[5] = {0, 2, 3, 4, 5};
+                constexpr bool two[5] = {true, false, false, false, false};
+                constexpr int slot[5] = {0, 2, 3, 4, 5};
+                float *sres = s_res + (threadIdx.x & ~63u) * 6;
+                const int rk = coop_draws_lds<PathSampler<kSmp>::kW, 5, 6>(smp.z, P.zs, ev == EV_PHASE, off, two, slot, 5, sres,
+                                                                          s_zst + (threadIdx.x & ~63u), AVR_DIM_HASH ? s_dh : nullptr);
+                qr = sres + rk * 6;
+                if (ev == EV_PHASE) s_ul[threadIdx.x] = qr[5];
+            } else if constexpr (kUlAhead) {
                 constexpr int off[5] = {0, 2, 3, 4, 5};
                 constexpr bool two[5] = {true, false, false, false, false};
                 coop_draws<PathSampler<kSmp>::kW, 5>(smp.z, P.zs, ev == EV_PHASE, off, two, 5, q0, q1,
@@ -1971,9 +2131,12 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
             }
             if (ev == EV_PHASE) {
                 // phase-function sampling (integrators.cpp:1046-1061), then the next segment
-                ++nPhase;
+                AVR_COUNT(nPhase, 2);
                 float up0, up1;
-                if constexpr (kCoop) {
+                if constexpr (kCoopLds) {
+                    up0 = qr[0];
+                    up1 = qr[1];
+                } else if constexpr (kCoop) {
                     up0 = q0[0];
                     up1 = q1[0];
                 } else {
@@ -1987,11 +2150,11 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
                     beta = beta * (phPdf / phPdf);
                     r_l = r_u / phPdf;
                     pd = wi;
-                    const float h0 = kCoop ? q0[1] : smp.get1d(P);
-                    const float h1 = kCoop ? q0[2] : smp.get1d(P);
+                    const float h0 = kCoopLds ? qr[2] : (kCoop ? q0[1] : smp.get1d(P));
+                    const float h1 = kCoopLds ? qr[3] : (kCoop ? q0[2] : smp.get1d(P));
                     seqA = hash_u32(f2u(h0));
                     seqB = hash_u32(f2u(h1));
-                    u = kCoop ? q0[3] : smp.get1d(P);
+                    u = kCoopLds ? qr[4] : (kCoop ? q0[3] : smp.get1d(P));
                     sd = pd;
                     segPending = true;
                     mode = M_MEDIUM;
@@ -2070,7 +2233,7 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
             const bool fresh = mode == M_FETCH && k < granted;
             if (mode == M_FETCH) {
                 if (fresh) {
-                    ++nPaths;
+                    AVR_COUNT(nPaths, 1);
                     // ---- a new path from the camera stage (k_paths_camera) ----
                     const int gn = (int)(base + k);
                     const float4 c0 = P.ps.cam0[gn], c1 = P.ps.cam1[gn], c2 = P.ps.cam2[gn];
@@ -2103,8 +2266,10 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
                     depth = 0;
                     {
                         const LambdaIdx li = lambda_index(lam);
-                        sig_a = sfrom<S>(sample_table(tab_sa, li));
-                        sig_s = sfrom<S>(sample_table(tab_ss, li));
+                        if constexpr (!kGray) {
+                            sig_a = sfrom<S>(sample_table(tab_sa, li));
+                            sig_s = sfrom<S>(sample_table(tab_ss, li));
+                        }
                         if (kEmissive && (kMed == 0 || kMed == 1)) Le_l = sample_table(m.Le, li);
                     }
                     sd = pd;
@@ -2152,17 +2317,55 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
             float t = 0;
             const S sig_t = sig_a + sig_s;
             const float st0 = sv0(sig_t);
+            // A pending candidate is decided exactly (media.h:770-777); an accepted one becomes
+            // this lane's collision: its T_maj factor, and for the fat GridMedium its density
+            // gather is issued here. kFetchSplit runs this stage BEFORE the DDA walk — for the
+            // candidates the previous iteration's walk left pending — so the gather's HBM latency
+            // overlaps the other lanes' walk and the callback below consumes it; otherwise after
+            // the walk, as pbrt orders it. Per lane the operations and RNG draws are the same.
+            bool fetching = false, inFat = false;
+            float4 fa{}, fb{};
+            float fdx = 0, fdy = 0, fdz = 0;
+            auto exact_stage = [&]() {
+                if (walk != 1) return;
+                walk = 0;
+                t = tMin + m_exp_dist<kFast>(u, st0 * mv);
+                u = rng.uniform();
+                if (!(t < segMax)) {   // rejected after all: close the segment (media.h:790-801)
+                    float dt = segMax - tMin;
+                    if (__builtin_isinf(dt)) dt = kFloatMax;
+                    T_maj = T_maj * sexpm<kFast>(-((sig_t * mv) * dt));
+                    needNext = true;
+                    return;
+                }
+                fetching = true;
+                T_maj = T_maj * sexpm<kFast>(-((sig_t * mv) * (t - tMin)));
+                if constexpr (kMed == 0) {
+                    if (m.fat) {
+                        V3 pm = xf_point_pair(m.medium_from_render, po + sd * t);
+                        pm = m.unit_box ? V3{pm.x - m.bmin[0], pm.y - m.bmin[1], pm.z - m.bmin[2]} : box_offset(m.bmin, m.bmax, pm);
+                        inFat = fat_issue(m.fat, m.nx, m.ny, m.nz, pm, fa, fb, fdx, fdy, fdz);
+                    }
+                }
+            };
+            if constexpr (kFetchSplit) exact_stage();
             // walk: 0 walking, 1 candidate pending (accepted or ambiguous), 2 segments exhausted.
             // Each step crosses at most one majorant cell and tests at most one candidate; the
             // loop has one wave-uniform exit so the body stays predicated (no per-exit masks).
-            int walk = 0;
+            // A lane whose collision is being fetched sits the walk out.
+            if (fetching) walk = 3;
             for (int b = 0; b < P.dda_budget; ++b) {
+                [[maybe_unused]] bool stepped = false;
                 if (walk == 0 && needNext) {
                     float s0, s1;
                     if (!ddal_next(it, majp, maj_sy, maj_sz, maj_n, &s0, &s1, &mv)) {
                         walk = 2;
                     } else {
+#if AVR_WAVE_COUNTERS
+                        stepped = true;
+#else
                         ++nSteps;
+#endif
                         // zero-majorant cell: T_maj *= FastExp(-0 * dt); for a gray medium that
                         // factor is exactly 1, so the multiply is skipped
                         const S sigma_maj = sig_t * mv;
@@ -2179,6 +2382,9 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
                         }
                     }
                 }
+#if AVR_WAVE_COUNTERS
+                nStepsW += __popcll(__ballot(stepped));
+#endif
                 // unconditional (all busy lanes): in flight during the candidate test below
                 if (kVdb && useOcc) ddal_prefetch_occ(it, majp, s_occ, maj_n);
                 else ddal_prefetch(it, majp);
@@ -2213,29 +2419,22 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
                 if (__ballot(walk == 0) == 0) break;
             }
             AVR_SEC(4)
-            const bool segEnd = walk == 2, pend = walk == 1;
-            if (segEnd) {
+            if (walk == 3) walk = 0;
+            if (walk == 2) {   // segments exhausted
+                walk = 0;
                 if (mode == M_MEDIUM) ev = EV_ESCAPE;
                 else { ev = EV_SHADOW_DONE; shadowStopped = false; }
                 continue;
             }
-            if (!pend) continue;   // walk budget used up: resume the DDA next iteration
-            // exact candidate (media.h:770-777): t = tMin + SampleExponential(u, sigma_maj[0])
-            t = tMin + m_exp_dist<kFast>(u, st0 * mv);
-            u = rng.uniform();
-            if (!(t < segMax)) {   // rejected after all: close the segment (media.h:790-801)
-                float dt = segMax - tMin;
-                if (__builtin_isinf(dt)) dt = kFloatMax;
-                T_maj = T_maj * sexpm<kFast>(-((sig_t * mv) * dt));
-                needNext = true;
-                continue;
-            }
-            // ---- collision: density fetch for every lane that reached one ----
+            // walk == 1 (kFetchSplit): decided at the next iteration's exact stage; walk == 0:
+            // budget used up, the DDA resumes next iteration
+            if constexpr (!kFetchSplit) exact_stage();
+            if (!fetching) continue;
+            // ---- collision: density for every lane that reached one ----
             const S sigma_maj = sig_t * mv;
-            T_maj = T_maj * sexpm<kFast>(-(sigma_maj * (t - tMin)));
             const V3 pc = po + sd * t;
-            // GridMedium::SamplePoint (media.h:287-319) / NanoVDBMedium::SamplePoint (624-637);
-            // k_paths runs these two (the host sends the other media to the wavefront kernels)
+            // GridMedium::SamplePoint (media.h:287-319) / NanoVDBMedium::SamplePoint (624-637) /
+            // RGBGridMedium / Homogeneous / Cloud
             V3 pm = xf_point_pair(m.medium_from_render, pc);
             S ms_a, ms_s;
             Spec rgbLe{};
@@ -2256,16 +2455,17 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
                 if constexpr (kVdb) {
                     dens = vdb::sample_world(m.vdb, pm.x, pm.y, pm.z);
                 } else {
-                    pm = m.unit_box ? V3{pm.x - m.bmin[0], pm.y - m.bmin[1], pm.z - m.bmin[2]} : box_offset(m.bmin, m.bmax, pm);
-                    dens = m.fat ? fat_lookup(m.fat, m.density, m.nx, m.ny, m.nz, pm)
-                                 : grid_lookup(m.density, m.nx, m.ny, m.nz, pm);
+                    // the gather issued at the exact stage (fat layout), else the linear grid
+                    if (kEmissive || !inFat)
+                        pm = m.unit_box ? V3{pm.x - m.bmin[0], pm.y - m.bmin[1], pm.z - m.bmin[2]} : box_offset(m.bmin, m.bmax, pm);
+                    dens = inFat ? fat_lerp(fa, fb, fdx, fdy, fdz) : grid_lookup(m.density, m.nx, m.ny, m.nz, pm);
                 }
                 ms_a = sig_a * dens;
                 ms_s = sig_s * dens;
             }
             bool stop = false;
             if (mode == M_MEDIUM) {
-                ++nLookup;
+                AVR_COUNT(nLookup, 0);
                 // delta-tracking callback (integrators.cpp:990-1077)
                 if (!snz(beta)) {
                     stop = true;
@@ -2310,7 +2510,7 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
                     }
                 }
             } else {
-                ++nShadowLookup;
+                AVR_COUNT(nShadowLookup, 3);
                 // ratio-tracking callback with Russian roulette (integrators.cpp:1351-1378)
                 const S sigma_n = sclamp0(sigma_maj - ms_a - ms_s);
                 const float pdf = sv0(T_maj) * sv0(sigma_maj);
@@ -2331,12 +2531,21 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
         }
     }
     AVR_SEC_FLUSH
+#if AVR_WAVE_COUNTERS
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (lane < 5 && wcnt[lane]) atomicAdd(P.stats + lane, (unsigned long long)wcnt[lane]);
+    if (lane == 0 && nStepsW) atomicAdd(P.stats + 5, nStepsW);
+#else
     flush_stat(P.stats, 0, nLookup);
     flush_stat(P.stats, 1, nPaths);
     flush_stat(P.stats, 2, nPhase);
     flush_stat(P.stats, 3, nShadowLookup);
     flush_stat(P.stats, 4, nShadow);
     flush_stat(P.stats, 5, nSteps);
+#endif
+#undef AVR_COUNT
     if (lane == 0) {   // wave-uniform counters: one add per wave
         if (nIter) atomicAdd(P.stats + 8, nIter);
         if (nActive) atomicAdd(P.stats + 9, nActive);
@@ -2738,6 +2947,25 @@ __global__ void __launch_bounds__(256) k_zsobol_table(smp::ZSobolParams zp, int 
         const long long pix = k / dmax;
         const uint32_t pm = (uint32_t)smp::encode_morton2((uint32_t)(pix % width), (uint32_t)(pix / width));
         table[(size_t)pm * dmax + d] = smp::zsobol_upper(pm, (uint32_t)d, zp);
+    }
+}
+
+// ZSobol pass table: zsobol_pass_entry for every pixel of the film and the first pdims
+// dimensions, for the pass whose sample indices agree with `base` above their low `plo` bits;
+// row Morton(pixel). The pixel digits come from the pixel table (zp.upper) where it covers
+// the dimension. zp.ptab must be null here. Built once per k_paths pass (a few hundred us).
+__global__ void __launch_bounds__(256) k_zsobol_pass_table(smp::ZSobolParams zp, int width, int height, int pdims,
+                                                           int plo, long long base, uint64_t *__restrict__ table) {
+    const long long n = (long long)width * height * pdims;
+    const bool wide = smp::zsobol_wide(zp);
+    for (long long k = blockIdx.x * (long long)blockDim.x + threadIdx.x; k < n; k += (long long)gridDim.x * blockDim.x) {
+        const int d = (int)(k % pdims);
+        const long long pix = k / pdims;
+        const uint32_t pm = (uint32_t)smp::encode_morton2((uint32_t)(pix % width), (uint32_t)(pix / width));
+        const uint32_t up = (zp.upper && d < zp.dmax) ? zp.upper[(size_t)pm * zp.dmax + d] : smp::zsobol_upper(pm, (uint32_t)d, zp);
+        const uint64_t m = ((uint64_t)pm << zp.log2spp) | (uint64_t)base;
+        table[(size_t)pm * pdims + d] = wide ? smp::zsobol_pass_entry<uint64_t>(m, (uint32_t)d, zp, plo, up)
+                                             : smp::zsobol_pass_entry<uint32_t>((uint32_t)m, (uint32_t)d, zp, plo, up);
     }
 }
 

@@ -105,6 +105,11 @@ struct ZSobolParams {
     // `dmax` dimensions, row (Morton(pixel) * dmax + dimension); null = computed per call
     const uint32_t *upper;
     int dmax;
+    // Optional per-pass table (zsobol_pass_entry) for the first `pdims` dimensions, row
+    // (Morton(pixel) * pdims + dimension): valid only for sample indices that agree with the
+    // pass's above their low `plo` bits (the host builds it per pass; null = not used)
+    const uint64_t *ptab;
+    int pdims, plo;
 };
 
 // Morton(pixel) << log2(spp) | sampleIndex fits 32 bits (nBase4Digits <= 16: e.g. 1024 spp
@@ -187,9 +192,76 @@ AVR_HD uint32_t zsobol_lower(M morton, uint32_t dimension, const ZSobolParams &z
     return sampleIndex;
 }
 
-// GetSampleIndex of (morton, dimension): upper digits from the table when present
+// The part of GetSampleIndex shared by a PASS of sample indices that differ only in their low
+// `plo` bits (plo <= log2spp), for one (pixel, dimension): digit i (shift s = 2i - pw) is
+//   fixed      when s >= plo      — its value bits and its permutation (MixBits of the bits
+//                                   above s + 2 and the dimension) lie above plo;
+//   perm-fixed when s < plo <= s + 2 — its permutation reads bits >= plo only, its value varies;
+//   varying    when s + 2 < plo   — the permutation reads varying bits: computed per draw.
+// Returns the fixed digits' permuted bits shifted down by plo (bits 0..55; < 2^52 since the
+// index is) and the perm-fixed digit's permutation (0..23) in bits 56..63, 0xFF if none.
+// `morton`: the index of any sample of the pass; `up`: zsobol_upper of the pixel (the
+// digits above log2spp). A pass of S consecutive indices from `base` has plo = the lowest
+// bit count at which base and base + S - 1 agree.
+template <typename M>
+AVR_HD uint64_t zsobol_pass_entry(M morton, uint32_t dimension, const ZSobolParams &zp, int plo, uint32_t up) {
+    const int pw = zp.log2spp & 1;
+    const uint32_t dmix = 0x55555555u * dimension;
+    constexpr int kBits = 8 * (int)sizeof(M);
+    uint64_t fixed = (uint64_t)up << zp.log2spp;
+    uint32_t perm = 0xFFu;
+    for (int i = zsobol_split(zp) - 1; i >= pw; --i) {
+        const int shift = 2 * i - pw;
+        if (shift + 2 < plo) break;   // this and every lower digit: varying
+        const M higher = shift + 2 >= kBits ? M(0) : M(morton >> (shift + 2));
+        const uint32_t p = mix_perm24<M>((M)(higher ^ (M)dmix));
+        if (shift >= plo) fixed |= (uint64_t)zperm(p, (uint32_t)(morton >> shift) & 3u) << shift;
+        else perm = p;
+    }
+    return (fixed >> plo) | ((uint64_t)perm << 56);
+}
+
+// GetSampleIndex of (morton, dimension) from the sample's pass entry e: the varying digits
+// computed, the perm-fixed digit from e's permutation, the rest from e; an odd log2(spp)'s
+// final base-2 digit as zsobol_lower. Bit-identical to zsobol_index without tables.
+template <typename M>
+AVR_HD M zsobol_index_pass(M morton, uint32_t dimension, const ZSobolParams &zp, uint64_t e) {
+    const int pw = zp.log2spp & 1, plo = zp.plo;
+    const uint32_t dmix = 0x55555555u * dimension;
+    constexpr int kBits = 8 * (int)sizeof(M);
+    M idx = (M)((e & 0x00ffffffffffffffull) << plo);
+    const uint32_t perm = (uint32_t)(e >> 56);
+    for (int i = (plo + pw - 1) >> 1; i >= pw; --i) {   // digits with shift < plo
+        const int shift = 2 * i - pw;
+        uint32_t p = perm;
+        if (shift + 2 < plo) {
+            const M higher = shift + 2 >= kBits ? M(0) : M(morton >> (shift + 2));
+            p = mix_perm24<M>((M)(higher ^ (M)dmix));
+        }
+        idx |= (M)zperm(p, (uint32_t)(morton >> shift) & 3u) << shift;
+    }
+    if (pw) {
+        const uint32_t digit = (uint32_t)morton & 1u;
+        const M x = (M)(morton >> 1) ^ (M)dmix;
+        uint64_t v = (uint64_t)x;
+        v ^= v >> 31;
+        v *= 0x7fb5d329728ea185ull;
+        v ^= v >> 27;
+        v *= 0x81dadef4bc2dd44dull;
+        v ^= v >> 33;
+        idx |= (M)(digit ^ (uint32_t)(v & 1));
+    }
+    return idx;
+}
+
+// GetSampleIndex of (morton, dimension): from the pass table, else the upper digits from the
+// pixel table when present
 template <typename M>
 AVR_HD M zsobol_index(M morton, uint32_t dimension, const ZSobolParams &zp) {
+    if (zp.ptab && (int)dimension < zp.pdims) {
+        const uint32_t pm = (uint32_t)(morton >> zp.log2spp);
+        return zsobol_index_pass<M>(morton, dimension, zp, zp.ptab[(size_t)pm * (size_t)zp.pdims + dimension]);
+    }
     uint32_t up;
     const uint32_t pm = (uint32_t)(morton >> zp.log2spp);
     if (zp.upper && (int)dimension < zp.dmax)
@@ -281,6 +353,9 @@ inline ZSobolParams zsobol_params(int spp, int width, int height, int seed) {
     zp.seed = seed;
     zp.upper = nullptr;
     zp.dmax = 0;
+    zp.ptab = nullptr;
+    zp.pdims = 0;
+    zp.plo = 0;
     return zp;
 }
 

@@ -53,6 +53,7 @@ BYTES_CAMERA_RECORD_READ = {"zsobol": 68, "independent": 80}
 # ZSobol pixel-table reads (one 4-B entry per draw): 5 draws per phase event in k_paths (phase
 # 2D, the next segment's three 1D, the next light pick); 6 per camera-stage quad of 4 samples
 ZSOBOL_TABLE_BYTES_PER_DRAW = 4
+ZSOBOL_PASS_BYTES_PER_DRAW = 8   # the per-pass table's entries (avr_set_sampler_pass_table)
 ZSOBOL_DRAWS_PER_PHASE = 5
 ZSOBOL_CAMERA_DRAWS = 6
 # the camera stage writes cam0, cam1, cam2, cam3, cam4 (5 x 16 B), the 4-B filter weight and cam5
@@ -73,28 +74,34 @@ def lookup_bytes(medium, emissive=False, rgb_fields=2):
     return BYTES_PER_LOOKUP
 
 
-def kpaths_bytes(agg, sampler, medium="grid", emissive=False, zsobol_table=True):
+def kpaths_bytes(agg, sampler, medium="grid", emissive=False, zsobol_table=True, pass_table=False):
     """k_paths' algorithmic bytes over the stats `agg` (counters summed over its launches):
     density lookups (delta + ratio tracking) + 16 B per sample record + the camera record of every
-    path + the ZSobol pixel-table entries of its phase draws. Returns (total, parts)."""
+    path + the ZSobol table entries of its phase draws (4-B pixel-table or 8-B pass-table
+    entries). Returns (total, parts)."""
     # delta tracking evaluates emission (Le grid / temperature) at its lookups; shadow rays never
     lk = agg["medium_lookups"] * lookup_bytes(medium, emissive) + agg["shadow_lookups"] * lookup_bytes(medium, False)
     parts = {
         "density_lookups": lk,
         "sample_records_written": BYTES_PER_SAMPLE_RECORD * agg["medium_items_in"],
         "camera_records_read": BYTES_CAMERA_RECORD_READ[sampler] * agg["medium_items_in"],
-        "zsobol_table_reads": (ZSOBOL_TABLE_BYTES_PER_DRAW * ZSOBOL_DRAWS_PER_PHASE * agg["medium_items_out"]
-                               if sampler == "zsobol" and zsobol_table else 0),
+        "zsobol_table_reads": ((ZSOBOL_PASS_BYTES_PER_DRAW if pass_table else ZSOBOL_TABLE_BYTES_PER_DRAW) *
+                               ZSOBOL_DRAWS_PER_PHASE * agg["medium_items_out"]
+                               if sampler == "zsobol" and (zsobol_table or pass_table) else 0),
     }
     return sum(parts.values()), parts
 
 
-def camera_bytes(samples, sampler, zsobol_table=True):
+def camera_bytes(samples, sampler, zsobol_table=True, pass_dims=0, pixels=0, launches=1):
     """The camera stage's algorithmic bytes for `samples` samples: its records (88 / 100 B per
-    sample) + the ZSobol pixel-table entries (6 draws per quad of 4 samples of one pixel)."""
+    sample) + the ZSobol table entries (6 draws per quad of 4 samples of one pixel) + with the
+    pass table, its per-pass build (an 8-B entry written and a 4-B pixel-table entry read per
+    pixel and dimension, once per launch)."""
     b = BYTES_CAMERA_WRITE[sampler] * samples
-    if sampler == "zsobol" and zsobol_table:
-        b += ZSOBOL_TABLE_BYTES_PER_DRAW * ZSOBOL_CAMERA_DRAWS * samples // 4
+    if sampler == "zsobol" and (zsobol_table or pass_dims):
+        b += (ZSOBOL_PASS_BYTES_PER_DRAW if pass_dims else ZSOBOL_TABLE_BYTES_PER_DRAW) * ZSOBOL_CAMERA_DRAWS * samples // 4
+    if sampler == "zsobol" and pass_dims:
+        b += launches * pixels * pass_dims * (ZSOBOL_PASS_BYTES_PER_DRAW + (ZSOBOL_TABLE_BYTES_PER_DRAW if zsobol_table else 0))
     return b
 
 
@@ -147,6 +154,8 @@ def parse(argv=None):
     p.add_argument("--dda-budget", type=int, default=0, help="k_paths DDA cells per iteration (0 = default)")
     p.add_argument("--zsobol-table", type=int, default=256,
                    help="ZSobol pixel-table dimensions (0 = every digit per sampler call)")
+    p.add_argument("--zsobol-pass-table", type=int, default=64,
+                   help="ZSobol per-pass table dimensions (0 = off): the digits a pass's sample indices share")
     p.add_argument("--sampler", default="zsobol", choices=["zsobol", "independent"],
                    help="pixel sampler (BASELINE.md S-cloud: zsobol, pbrt's default)")
     p.add_argument("--filter", default="gaussian", choices=["gaussian", "box"],
@@ -290,7 +299,7 @@ def pmc_child_argv(args, pixelsamples):
     child += ["--pixelsamples", str(int(pixelsamples))]
     for k in ("res", "width", "height", "spp_per_step", "max_paths", "pixel_order", "kernel", "medium",
               "refill_min", "grid_layout",
-              "dda_budget", "zsobol_table", "sampler", "filter", "mode", "majorant_res", "ray_binning", "occupancy", "nvdb",
+              "dda_budget", "zsobol_table", "zsobol_pass_table", "sampler", "filter", "mode", "majorant_res", "ray_binning", "occupancy", "nvdb",
               "scene"):
         if getattr(args, k) is not None:
             child += [f"--{k.replace('_', '-')}", str(getattr(args, k))]
@@ -466,6 +475,7 @@ def main():
     if args.dda_budget:
         integ.ctx.set_dda_budget(args.dda_budget)
     integ.ctx.set_sampler_table(args.zsobol_table)
+    integ.ctx.set_sampler_pass_table(args.zsobol_pass_table)
     if args.ray_binning:
         integ.ctx.set_ray_binning(1)
     if args.pixel_order == "entry-cell":
@@ -588,7 +598,8 @@ def main():
         # (lookups by medium kind + the 16-B sample record + the camera record it reads per path
         # + ZSobol table entries); path state never leaves VGPRs / LDS
         kname = "k_paths (persistent: delta + ratio tracking, density fetch)"
-        med_bytes, bytes_parts = kpaths_bytes(agg, args.sampler, medium_kind, emissive, args.zsobol_table > 0)
+        med_bytes, bytes_parts = kpaths_bytes(agg, args.sampler, medium_kind, emissive, args.zsobol_table > 0,
+                                              args.zsobol_pass_table > 0)
     else:
         kname = "k_medium (wavefront delta tracking + density fetch)"
         med_bytes = BYTES_PER_LOOKUP * agg["medium_lookups"] + BYTES_PER_ITEM * (agg["medium_items_in"] +
@@ -598,7 +609,7 @@ def main():
     # the camera stage (k_paths_camera), one launch per k_paths launch
     cam_block = None
     if persistent and agg["ms_camera"] > 0:
-        cb = camera_bytes(samples_timed, args.sampler, args.zsobol_table > 0)
+        cb = camera_bytes(samples_timed, args.sampler, args.zsobol_table > 0, args.zsobol_pass_table, npix, launches)
         cam_block = {"kernel": "k_paths_camera", "bytes_per_launch": cb / launches,
                      "avg_launch_ms": round(agg["ms_camera"] / launches, 4),
                      "achieved": round(cb / (agg["ms_camera"] / 1e3) / 1e9, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",

@@ -320,6 +320,14 @@ int avr_set_sampler(avr_context *ctx, int kind, int samples_per_pixel);
  * dimensions (4 B per pixel-Morton row and dimension; default 256, 0 = compute every digit
  * per call). Results are identical either way. */
 int avr_set_sampler_table(avr_context *ctx, int dims);
+/* ZSobolSampler in the persistent kernel: a pass renders sample indices [b, b + S) that agree
+ * above their lowest L differing bits, so every digit of GetSampleIndex above them — and the
+ * permutation of the one just below, whose hash reads only those bits — is shared by the
+ * pass's samples of one pixel. Each pass tabulates them for the first `dims` dimensions
+ * (8 B per pixel-Morton row and dimension; default 64, 0 = off) and a sampler call then
+ * evaluates only the digits below (2 base-4 digits for 64-index passes instead of
+ * log2(spp)/2). Results are identical either way. */
+int avr_set_sampler_pass_table(avr_context *ctx, int dims);
 
 /* Render sample indices [spp_begin, spp_end) of every pixel (the avr_set_sampler sampler,
  * seed), VolPathIntegrator maxdepth. Asynchronous on the context stream. */

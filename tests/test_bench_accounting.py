@@ -43,6 +43,13 @@ def test_camera_bytes():
     assert bench.camera_bytes(4, "zsobol") == 4 * 88 + 6 * 4
     assert bench.camera_bytes(4, "zsobol", zsobol_table=False) == 4 * 88
     assert bench.camera_bytes(4, "independent") == 400
+    # the per-pass ZSobol table: 8-B entries per draw, and its build (8 B written + 4 B of the
+    # pixel table read per pixel and dimension) once per launch
+    assert bench.camera_bytes(4, "zsobol", pass_dims=64, pixels=2, launches=1) == 4 * 88 + 6 * 8 + 2 * 64 * 12
+    assert bench.camera_bytes(8, "zsobol", zsobol_table=False, pass_dims=16, pixels=2, launches=2) == \
+        8 * 88 + 12 * 8 + 2 * 2 * 16 * 8
+    agg = {"medium_lookups": 0, "shadow_lookups": 0, "medium_items_in": 0, "medium_items_out": 1000}
+    assert bench.kpaths_bytes(agg, "zsobol", pass_table=True)[1]["zsobol_table_reads"] == 40 * 1000
 
 
 def test_kernel_names_match_across_demangled_mangled_and_the_abi_string():

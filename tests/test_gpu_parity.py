@@ -613,6 +613,33 @@ def test_zsobol_pixel_table_identical(kernel):
             assert np.array_equal(a, b)
 
 
+@pytest.mark.parametrize("pixelsamples", [2048, 4096])
+def test_zsobol_pass_table_identical(pixelsamples):
+    """The per-pass ZSobol table (avr_set_sampler_pass_table: the digits a k_paths pass's sample
+    indices share) changes nothing: films and per-sample records equal the renders without it,
+    for aligned and unaligned index ranges, several passes per render (different low-bit counts
+    plo), odd and even log2(pixelsamples) and paths running past the table's dimensions."""
+    from acceleratedvolrenderer_amd import scenes, ZSobolSampler, GaussianFilter
+    from acceleratedvolrenderer_amd.scene import Scene, RGBFilm
+    n, W, H = 12, 33, 21
+    dens = (0.5 + np.random.default_rng(19).random((n, n, n), dtype=np.float32)).astype(np.float32)
+    base = scenes.s_uniform(n=n, width=W, height=H, variant="scatter", density=dens)
+    scene = Scene(base.camera, RGBFilm(W, H, filter=GaussianFilter()), base.medium, base.lights,
+                  sampler=ZSobolSampler(pixelsamples))
+    for lo, hi, per_pass in ((64, 128, 64), (5, 71, 24), (1000, 1040, 7)):
+        out = []
+        for dims in (0, 8, 64):
+            integ = _integrator(scene, maxdepth=30, spp=pixelsamples, kernel="persistent", max_paths=W * H * per_pass)
+            integ.ctx.set_sampler_pass_table(dims)
+            rgb, w = integ.render(lo, hi)
+            first, ns, L, lam, _ = integ.ctx.last_pass_samples(W * H, per_pass)
+            out.append((rgb, w, L[:W * H * ns], lam[:W * H * ns]))
+            integ.close()
+        for o in out[1:]:
+            for a, b in zip(out[0], o):
+                assert np.array_equal(a, b), (lo, hi, per_pass)
+
+
 @pytest.mark.parametrize("with_distant", [False, True])
 @pytest.mark.parametrize("kernel", ["persistent", "wavefront"])
 @pytest.mark.parametrize("variant", ["chromatic", "scatter"])

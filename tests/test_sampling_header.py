@@ -40,6 +40,21 @@ def hdr(tmp_path_factory):
         "    else { full[i] = zsobol_index<unsigned>((unsigned)m, q[4 * i + 3], zp);\n"
         "      tab[i] = zsobol_index<unsigned>((unsigned)m, q[4 * i + 3], zt); } }\n"
         "  delete[] t; return zsobol_split(zp); }\n"
+        "void zs_pass(int spp, int rx, int ry, int n, const int *q, unsigned long long *full,\n"
+        "             unsigned long long *pass) {\n"
+        "  ZSobolParams zp = zsobol_params(spp, rx, ry, 0);\n"
+        "  for (int i = 0; i < n; ++i) {\n"
+        "    const int *r = q + 6 * i; int base = r[4], S = r[5], plo = 0;\n"
+        "    while ((base >> plo) != ((base + S - 1) >> plo)) ++plo;\n"
+        "    unsigned pm = (unsigned)encode_morton2(r[0], r[1]); unsigned d = (unsigned)r[3];\n"
+        "    unsigned long long mb = ((unsigned long long)pm << zp.log2spp) | (unsigned)base;\n"
+        "    unsigned long long ms = ((unsigned long long)pm << zp.log2spp) | (unsigned)r[2];\n"
+        "    unsigned up = zsobol_upper(pm, d, zp);\n"
+        "    ZSobolParams zt = zp; zt.plo = plo;\n"
+        "    if (zsobol_wide(zp)) { full[i] = zsobol_index<unsigned long long>(ms, d, zp);\n"
+        "      pass[i] = zsobol_index_pass<unsigned long long>(ms, d, zt, zsobol_pass_entry<unsigned long long>(mb, d, zp, plo, up)); }\n"
+        "    else { full[i] = zsobol_index<unsigned>((unsigned)ms, d, zp);\n"
+        "      pass[i] = zsobol_index_pass<unsigned>((unsigned)ms, d, zt, zsobol_pass_entry<unsigned>((unsigned)mb, d, zp, plo, up)); } } }\n"
         "float sob(unsigned long long a, int dim, unsigned seed, int scr) {\n"
         "  unsigned v = sobol_bits64((unsigned)a, (unsigned)(a >> 32), dim);\n"
         "  return u32_to_unit(scr ? fast_owen(v, seed) : v); }\n"
@@ -87,3 +102,32 @@ def test_zsobol_pixel_table_split(hdr, spp, rx, ry):
                          full.ctypes.data_as(U), tab.ctypes.data_as(U))
     assert np.array_equal(full, tab)
     assert split == (int(np.log2(spp)) + (int(np.log2(spp)) & 1)) // 2
+
+
+@pytest.mark.parametrize("spp,rx,ry", [(1, 37, 21), (2, 37, 21), (8, 37, 21), (128, 37, 21), (256, 37, 21),
+                                        (2048, 1280, 720), (16384, 1280, 720), (8192, 300, 200), (65536, 1100, 900)])
+def test_zsobol_pass_table(hdr, spp, rx, ry):
+    """The per-pass table (avr_set_sampler_pass_table): a pass of S sample indices from `base`
+    shares the digits above its lowest differing bits (and the permutation of the digit just
+    below); the index rebuilt from its entry plus the digits computed per draw equals the
+    untabulated GetSampleIndex for every sample of the pass — aligned passes (the bench's 64),
+    unaligned ranges straddling digit boundaries, single indices and whole-pixel passes."""
+    rng = np.random.default_rng(spp + 7)
+    n = 6000
+    rows = []
+    for _ in range(n):
+        S = int(rng.choice([1, 2, 3, 4, 16, 64, 100, spp]))
+        S = min(S, spp)
+        if rng.random() < 0.5 and spp % S == 0:
+            base = int(rng.integers(0, spp // S)) * S            # aligned pass
+        else:
+            base = int(rng.integers(0, spp - S + 1))             # any range
+        s = base + int(rng.integers(0, S))
+        rows.append((int(rng.integers(0, rx)), int(rng.integers(0, ry)), s, int(rng.integers(0, 40)), base, S))
+    q = np.array(rows, np.int32)
+    full = np.zeros(n, np.uint64)
+    pas = np.zeros(n, np.uint64)
+    U = ctypes.POINTER(ctypes.c_ulonglong)
+    hdr.zs_pass(spp, rx, ry, n, q.ctypes.data_as(ctypes.POINTER(ctypes.c_int)), full.ctypes.data_as(U),
+                pas.ctypes.data_as(U))
+    assert np.array_equal(full, pas)
