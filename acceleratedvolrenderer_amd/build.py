@@ -29,6 +29,11 @@ KP_UNITS = [(m, f) for f in (0, 1) for m in (0, 1, 3, 4)]
 # so a device sample replays the CPU oracle's sample.
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC",
          "-I" + os.path.join(ROOT, "include")]
+# k_paths units only: no MachineLICM. The persistent kernel's main loop would otherwise keep
+# ~40 hoisted loop invariants (f32 literals for VOP3 operands, float(n), 1 + g^2, ...) in VGPRs
+# for its whole lifetime; without the hoisting it fits 4 waves/SIMD (128 VGPRs, DESIGN §6:
+# 1926 -> 2029 Msamples/s at the driver's command).
+KP_FLAGS = ["-mllvm", "-disable-machine-licm"]
 # RCCL for avr_film_reduce_rccl (in-process multi-GPU film reduce)
 LIBS = ["-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"]
 
@@ -41,7 +46,7 @@ def source_hash(defines=()):
         h.update(os.path.basename(d).encode() + b"\0")
         with open(d, "rb") as f:
             h.update(f.read())
-    h.update(repr((FLAGS, LIBS, KP_UNITS, list(defines))).encode())
+    h.update(repr((FLAGS, KP_FLAGS, LIBS, KP_UNITS, list(defines))).encode())
     return h.hexdigest()
 
 
@@ -77,7 +82,7 @@ def build(force=False, verbose=False, jobs=None, variant=None, defines=()):
     units = [(SRC, os.path.join(objdir, "avr_capi.o"), ["-DAVR_KP_SPLIT"] + defines, verbose)]
     for med, fast in KP_UNITS:
         units.append((KPATHS, os.path.join(objdir, f"avr_kpaths_m{med}_f{fast}.o"),
-                      [f"-DAVR_KP_MED={med}", f"-DAVR_KP_FAST={fast}"] + defines, verbose))
+                      KP_FLAGS + [f"-DAVR_KP_MED={med}", f"-DAVR_KP_FAST={fast}"] + defines, verbose))
     jobs = jobs or max(1, min(len(units), int(os.environ.get("MAX_JOBS", os.cpu_count() or 4))))
     with ThreadPoolExecutor(jobs) as ex:
         objs = list(ex.map(_compile, units))

@@ -161,6 +161,7 @@ struct avr_context {
     int grid_layout = 1;
     bool gray = false;        // sigma_a and sigma_s constant over 360..830 nm      // 1: build the fat (footprint) copy when memory allows, 0: linear only
     float4 *d_fat = nullptr;
+    float *d_brick = nullptr;   // bricked GridMedium copy (grid_layout 2)
     uint64_t *d_advance = nullptr;  // per-pass PCG advance table {A, H}
     long long advance_cap = 0;
     // avr_film_reduce_rccl: this context's communicator and the clique (contexts in rank
@@ -544,7 +545,28 @@ int medium_common(avr_context *c, const float *d_density, int nx, int ny, int nz
     m.lnx = lnx; m.lny = lny; m.lnz = lnz;
     if ((rc = build_majorant(c, mres))) return rc;
     if (c->d_fat) { (void)hipFree(c->d_fat); c->d_fat = nullptr; }
+    if (c->d_brick) { (void)hipFree(c->d_brick); c->d_brick = nullptr; }
     m.fat = nullptr;
+    m.brick = nullptr;
+    m.nb[0] = m.nb[1] = m.nb[2] = 0;
+    if (c->grid_layout == 2 && type == 0) {
+        // bricked copy: 8^3 base voxels + apron per brick (k_brickify), 1.42x the grid
+        const int nb[3] = {(nx + 8) / 8, (ny + 8) / 8, (nz + 8) / 8};
+        const long long nbricks = (long long)nb[0] * nb[1] * nb[2];
+        const size_t bytes = (size_t)nbricks * avr::kBrickFloats * sizeof(float);
+        size_t freeB = 0, totalB = 0;
+        HIP_TRY(hipMemGetInfo(&freeB, &totalB));
+        if (bytes + (8ull << 30) < freeB && hipMalloc((void **)&c->d_brick, bytes) == hipSuccess) {
+            hipLaunchKernelGGL(avr::k_brickify, dim3(blocks_for(nbricks * avr::kBrickFloats, 256, 256 * 64)), dim3(256), 0,
+                               c->stream, d_density, nx, ny, nz, nb[0], nb[1], nbricks, c->d_brick);
+            HIP_TRY(hipGetLastError());
+            m.brick = c->d_brick;
+            for (int a = 0; a < 3; ++a) m.nb[a] = nb[a];
+        } else {
+            (void)hipGetLastError();
+            c->d_brick = nullptr;
+        }
+    }
     if (c->grid_layout == 1 && type == 0) {
         const size_t nfat = (size_t)(nx + 1) * (ny + 1) * (nz + 1);
         size_t freeB = 0, totalB = 0;
@@ -647,12 +669,12 @@ int avr_context_create(int device, long long max_paths, avr_context **out) {
 
 int avr_set_grid_layout(avr_context *c, int layout) {
     AVR_QUIESCE(c);
-    if (!c || (layout != 0 && layout != 1)) return fail(AVR_ERR_ARG, "grid layout must be 0 (linear) or 1 (fat)");
+    if (!c || layout < 0 || layout > 2) return fail(AVR_ERR_ARG, "grid layout must be 0 (linear), 1 (fat) or 2 (bricked)");
     c->grid_layout = layout;
     return AVR_OK;
 }
 
-int avr_grid_layout_active(avr_context *c) { return (c && c->d_fat) ? 1 : 0; }
+int avr_grid_layout_active(avr_context *c) { return !c ? 0 : (c->d_fat ? 1 : (c->med.brick ? 2 : 0)); }
 
 int avr_set_dda_budget(avr_context *c, int cells) {
     if (!c || cells < 0) return fail(AVR_ERR_ARG, "DDA budget must be >= 1 cell (0: default)");
@@ -729,6 +751,7 @@ int avr_context_destroy(avr_context *c) {
     if (c->d_reference) (void)hipFree(c->d_reference);
     if (c->d_metric) (void)hipFree(c->d_metric);
     if (c->d_fat) (void)hipFree(c->d_fat);
+    if (c->d_brick) (void)hipFree(c->d_brick);
     free_pixel_order(c);
     if (c->d_stats) (void)hipFree(c->d_stats);
     if (c->h_count) (void)hipHostFree(c->h_count);

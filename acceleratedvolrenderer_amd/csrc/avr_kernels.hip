@@ -53,6 +53,13 @@ struct DevMedium {
     // lookup is ONE 32-B-aligned access inside one cache line instead of 8 scattered taps
     // in 2-4 lines. 8x the grid's memory ((n+1)^3 x 32 B; 34 GB at 1024^3 of the 288 GB).
     const float4 *fat;
+    // bricked copy (avr_set_grid_layout 2): 8^3 base voxels per brick with a
+    // +1 apron, i.e. the 9^3 values v(8b-1 .. 8b+7) per axis (zero outside the grid) stored x
+    // fastest in kBrickFloats floats, bricks in x-fastest order over (nb[0], nb[1], nb[2]) =
+    // ceil((n + 1) / 8): every trilinear footprint lies inside ONE brick (offsets 0, 1, 9, 10,
+    // 81, 82, 90, 91 floats from its base tap). 1.42x the grid instead of the fat copy's 8x.
+    const float *brick;
+    int nb[3];
     // medium interface (f3): 0 = the bounds box (the default scene model), 1 = a sphere
     // {cx, cy, cz, r} in render space, 2 = a convex polyhedron (n_planes half-spaces
     // {nx, ny, nz, h}: n.p <= h inside; a convex triangle mesh's face planes) — shapes with no
@@ -348,6 +355,26 @@ __device__ __forceinline__ float fat_lerp(float4 a, float4 b, float dx, float dy
     float d11 = lerp(dx, b.z, b.w);
     return lerp(dz, lerp(dy, d00, d10), lerp(dy, d01, d11));
 }
+// Same value as grid_lookup() bit for bit from the bricked layout (DevMedium::brick).
+constexpr int kBrickFloats = 736;   // 9^3 = 729 apron values, padded to 23 x 128-B lines
+__device__ __forceinline__ float brick_lookup(const float *__restrict__ brick, const int nb[3],
+                                              const float *__restrict__ v, int nx, int ny, int nz, V3 p) {
+    float psx = p.x * nx - .5f, psy = p.y * ny - .5f, psz = p.z * nz - .5f;
+    int ix = (int)__builtin_floorf(psx), iy = (int)__builtin_floorf(psy), iz = (int)__builtin_floorf(psz);
+    if (ix < -1 || ix >= nx || iy < -1 || iy >= ny || iz < -1 || iz >= nz) return grid_lookup(v, nx, ny, nz, p);
+    float dx = psx - (float)ix, dy = psy - (float)iy, dz = psz - (float)iz;
+    const int ux = ix + 1, uy = iy + 1, uz = iz + 1;   // 0 .. n: brick u >> 3, apron-local u & 7
+    const size_t b = ((size_t)(uz >> 3) * nb[1] + (uy >> 3)) * nb[0] + (ux >> 3);
+    const float *q = brick + b * kBrickFloats + ((uz & 7) * 9 + (uy & 7)) * 9 + (ux & 7);
+    float d00 = lerp(dx, q[0], q[1]);
+    float d10 = lerp(dx, q[9], q[10]);
+    float d01 = lerp(dx, q[81], q[82]);
+    float d11 = lerp(dx, q[90], q[91]);
+    return lerp(dz, lerp(dy, d00, d10), lerp(dy, d01, d11));
+}
+// GridMedium density in the medium's layout: fat, bricked, or pbrt's linear SampledGrid
+__device__ __forceinline__ float grid_density(const DevMedium &m, V3 p);
+
 __device__ __forceinline__ float fat_lookup(const float4 *__restrict__ fat, const float *__restrict__ v, int nx, int ny,
                                             int nz, V3 p) {
     float4 a, b;
@@ -356,7 +383,29 @@ __device__ __forceinline__ float fat_lookup(const float4 *__restrict__ fat, cons
     return fat_lerp(a, b, dx, dy, dz);
 }
 
+__device__ __forceinline__ float grid_density(const DevMedium &m, V3 p) {
+    if (m.fat) return fat_lookup(m.fat, m.density, m.nx, m.ny, m.nz, p);
+    if (m.brick) return brick_lookup(m.brick, m.nb, m.density, m.nx, m.ny, m.nz, p);
+    return grid_lookup(m.density, m.nx, m.ny, m.nz, p);
+}
+
 #ifndef AVR_KPATHS_TU   // host-launched kernels: compiled in the C-ABI translation unit only
+// the bricked copy (DevMedium::brick): one thread per stored float (pad floats zero)
+__global__ void __launch_bounds__(256) k_brickify(const float *__restrict__ v, int nx, int ny, int nz, int nbx, int nby,
+                                                  long long nbricks, float *brick) {
+    const long long n = nbricks * kBrickFloats;
+    for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x) {
+        const long long b = e / kBrickFloats;
+        const int l = (int)(e - b * kBrickFloats);
+        float val = 0.f;
+        if (l < 729) {
+            const int lx = l % 9, ly = (l / 9) % 9, lz = l / 81;
+            const int bx = (int)(b % nbx), by = (int)((b / nbx) % nby), bz = (int)(b / ((long long)nbx * nby));
+            val = grid_at(v, nx, ny, nz, 8 * bx + lx - 1, 8 * by + ly - 1, 8 * bz + lz - 1);
+        }
+        brick[e] = val;
+    }
+}
 __global__ void __launch_bounds__(256) k_fatten(const float *__restrict__ v, int nx, int ny, int nz, float4 *fat) {
     const size_t n = (size_t)(nx + 1) * (ny + 1) * (nz + 1);
     for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < n; e += (size_t)gridDim.x * blockDim.x) {
@@ -602,7 +651,7 @@ __device__ __forceinline__ MediumSample sample_point(const DevMedium &m, V3 p, c
         const unsigned long long k = atomicAdd(m.trace_count, 1ull);
         if ((long long)k < m.trace_cap) m.trace[k] = make_float4(p.x, p.y, p.z, 0.f);
     }
-    float d = m.fat ? fat_lookup(m.fat, m.density, m.nx, m.ny, m.nz, p) : grid_lookup(m.density, m.nx, m.ny, m.nz, p);
+    float d = grid_density(m, p);
     ms.sigma_a = sig_a * d;
     ms.sigma_s = sig_s * d;
     if (emissive && m.emissive) ms.Le = grid_emission(m, p, lam, Le_l);
@@ -1720,7 +1769,7 @@ __global__ void __launch_bounds__(256) k_bin_scatter(const int *__restrict__ que
 #endif
 
 #ifndef AVR_PATHS_WAVES_GRAY
-#define AVR_PATHS_WAVES_GRAY 3   // 168 VGPRs, no scratch (4 waves -> 128 VGPRs spills ~100 B/lane)
+#define AVR_PATHS_WAVES_GRAY 4   // 128 VGPRs (with the k_paths units' -disable-machine-licm: ~44 B/lane of scratch, reloaded outside the tracking loop)
 #endif
 #ifndef AVR_COOP_SPEC
 #define AVR_COOP_SPEC 1
@@ -1739,9 +1788,6 @@ __global__ void __launch_bounds__(256) k_bin_scatter(const int *__restrict__ que
 #endif
 #ifndef AVR_OPAQUE_CONSTS
 #define AVR_OPAQUE_CONSTS 0
-#endif
-#ifndef AVR_FETCH_SPLIT
-#define AVR_FETCH_SPLIT 0   // 1: fetch before the walk, consume after it (measured -19 %)
 #endif
 #ifndef AVR_PATHS_WAVES_SPEC
 #define AVR_PATHS_WAVES_SPEC 2   // 4-wavelength state: ~220 VGPRs without scratch
@@ -1834,7 +1880,7 @@ struct SecProf {
 // escapes); a separate instantiation so the other kernels keep their register budget.
 // kFast: the "fast" render mode (hardware transcendentals, statistical parity); replay otherwise.
 template <bool kEmissive, bool kGray, int kSmp, int kMed, bool kImage, bool kFast>
-__global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_WAVES_SPEC) k_paths(Params P) {
+__global__ void __launch_bounds__(256, kGray ? (kMed == 1 ? 3 : AVR_PATHS_WAVES_GRAY) : AVR_PATHS_WAVES_SPEC) k_paths(Params P) {
     // kMed 1: HomogeneousMedium or CloudMedium — dda_init gives their single
     // HomogeneousMajorantIterator segment over a 1^3 majorant of 1.0; properties from sample_point
     constexpr bool kVdb = kMed == 3, kRgb = kMed == 4, kAnalytic = kMed == 1;
@@ -1959,12 +2005,6 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
     V3 sd{};               // normalised segment direction
     S T_maj{};
     bool needNext = true, shadowStopped = false;
-    // DDA walk state of the lane: 0 walking, 1 a candidate pending its exact decision (kept
-    // across tracking iterations with kFetchSplit), 2 segments exhausted, 3 collision in flight
-    int walk = 0;
-    // GridMedium with the fat layout: the collision's density gather is issued before the DDA
-    // walk of the other lanes and consumed after it (AVR_FETCH_SPLIT)
-    constexpr bool kFetchSplit = AVR_FETCH_SPLIT && kMed == 0;
     bool segPending = false;      // a segment start is queued for the shared block below
     uint64_t seqA = 0, seqB = 0;  // its RNG SetSequence arguments
     // shadow state (SampleLd, integrators.cpp:1339-1391)
@@ -1979,7 +2019,6 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
         ddal_init(it, m, Ray{o, d}, tMax, majp);
         T_maj = sconst<S>(1.f);
         needNext = true;
-        walk = 0;
     };
 
     AVR_SEC_INIT
@@ -2317,43 +2356,10 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
             float t = 0;
             const S sig_t = sig_a + sig_s;
             const float st0 = sv0(sig_t);
-            // A pending candidate is decided exactly (media.h:770-777); an accepted one becomes
-            // this lane's collision: its T_maj factor, and for the fat GridMedium its density
-            // gather is issued here. kFetchSplit runs this stage BEFORE the DDA walk — for the
-            // candidates the previous iteration's walk left pending — so the gather's HBM latency
-            // overlaps the other lanes' walk and the callback below consumes it; otherwise after
-            // the walk, as pbrt orders it. Per lane the operations and RNG draws are the same.
-            bool fetching = false, inFat = false;
-            float4 fa{}, fb{};
-            float fdx = 0, fdy = 0, fdz = 0;
-            auto exact_stage = [&]() {
-                if (walk != 1) return;
-                walk = 0;
-                t = tMin + m_exp_dist<kFast>(u, st0 * mv);
-                u = rng.uniform();
-                if (!(t < segMax)) {   // rejected after all: close the segment (media.h:790-801)
-                    float dt = segMax - tMin;
-                    if (__builtin_isinf(dt)) dt = kFloatMax;
-                    T_maj = T_maj * sexpm<kFast>(-((sig_t * mv) * dt));
-                    needNext = true;
-                    return;
-                }
-                fetching = true;
-                T_maj = T_maj * sexpm<kFast>(-((sig_t * mv) * (t - tMin)));
-                if constexpr (kMed == 0) {
-                    if (m.fat) {
-                        V3 pm = xf_point_pair(m.medium_from_render, po + sd * t);
-                        pm = m.unit_box ? V3{pm.x - m.bmin[0], pm.y - m.bmin[1], pm.z - m.bmin[2]} : box_offset(m.bmin, m.bmax, pm);
-                        inFat = fat_issue(m.fat, m.nx, m.ny, m.nz, pm, fa, fb, fdx, fdy, fdz);
-                    }
-                }
-            };
-            if constexpr (kFetchSplit) exact_stage();
             // walk: 0 walking, 1 candidate pending (accepted or ambiguous), 2 segments exhausted.
             // Each step crosses at most one majorant cell and tests at most one candidate; the
             // loop has one wave-uniform exit so the body stays predicated (no per-exit masks).
-            // A lane whose collision is being fetched sits the walk out.
-            if (fetching) walk = 3;
+            int walk = 0;
             for (int b = 0; b < P.dda_budget; ++b) {
                 [[maybe_unused]] bool stepped = false;
                 if (walk == 0 && needNext) {
@@ -2419,19 +2425,26 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
                 if (__ballot(walk == 0) == 0) break;
             }
             AVR_SEC(4)
-            if (walk == 3) walk = 0;
-            if (walk == 2) {   // segments exhausted
-                walk = 0;
+            const bool segEnd = walk == 2, pend = walk == 1;
+            if (segEnd) {
                 if (mode == M_MEDIUM) ev = EV_ESCAPE;
                 else { ev = EV_SHADOW_DONE; shadowStopped = false; }
                 continue;
             }
-            // walk == 1 (kFetchSplit): decided at the next iteration's exact stage; walk == 0:
-            // budget used up, the DDA resumes next iteration
-            if constexpr (!kFetchSplit) exact_stage();
-            if (!fetching) continue;
-            // ---- collision: density for every lane that reached one ----
+            if (!pend) continue;   // walk budget used up: resume the DDA next iteration
+            // exact candidate (media.h:770-777): t = tMin + SampleExponential(u, sigma_maj[0])
+            t = tMin + m_exp_dist<kFast>(u, st0 * mv);
+            u = rng.uniform();
+            if (!(t < segMax)) {   // rejected after all: close the segment (media.h:790-801)
+                float dt = segMax - tMin;
+                if (__builtin_isinf(dt)) dt = kFloatMax;
+                T_maj = T_maj * sexpm<kFast>(-((sig_t * mv) * dt));
+                needNext = true;
+                continue;
+            }
+            // ---- collision: density fetch for every lane that reached one ----
             const S sigma_maj = sig_t * mv;
+            T_maj = T_maj * sexpm<kFast>(-(sigma_maj * (t - tMin)));
             const V3 pc = po + sd * t;
             // GridMedium::SamplePoint (media.h:287-319) / NanoVDBMedium::SamplePoint (624-637) /
             // RGBGridMedium / Homogeneous / Cloud
@@ -2455,10 +2468,8 @@ __global__ void __launch_bounds__(256, kGray ? AVR_PATHS_WAVES_GRAY : AVR_PATHS_
                 if constexpr (kVdb) {
                     dens = vdb::sample_world(m.vdb, pm.x, pm.y, pm.z);
                 } else {
-                    // the gather issued at the exact stage (fat layout), else the linear grid
-                    if (kEmissive || !inFat)
-                        pm = m.unit_box ? V3{pm.x - m.bmin[0], pm.y - m.bmin[1], pm.z - m.bmin[2]} : box_offset(m.bmin, m.bmax, pm);
-                    dens = inFat ? fat_lerp(fa, fb, fdx, fdy, fdz) : grid_lookup(m.density, m.nx, m.ny, m.nz, pm);
+                    pm = m.unit_box ? V3{pm.x - m.bmin[0], pm.y - m.bmin[1], pm.z - m.bmin[2]} : box_offset(m.bmin, m.bmax, pm);
+                    dens = grid_density(m, pm);
                 }
                 ms_a = sig_a * dens;
                 ms_s = sig_s * dens;
@@ -2709,7 +2720,7 @@ __global__ void __launch_bounds__(256) k_density_fetch(DevMedium m, const float4
         // clamped to the footprint's valid range: a stray point reads the zero border, never
         // past the grid (the layouts' own bounds checks assume finite coordinates)
         const V3 q{fminf_(fmaxf_(p.x, -1.f), 2.f), fminf_(fmaxf_(p.y, -1.f), 2.f), fminf_(fmaxf_(p.z, -1.f), 2.f)};
-        out[i] = m.fat ? fat_lookup(m.fat, m.density, m.nx, m.ny, m.nz, q) : grid_lookup(m.density, m.nx, m.ny, m.nz, q);
+        out[i] = grid_density(m, q);
     }
 }
 

@@ -52,6 +52,10 @@ def reduce_film(buf, npix, nbuckets, rank, group=None):
     return out
 
 
+# avr_set_grid_layout: pbrt's linear SampledGrid, the fat footprint copy (8x), 8^3 apron bricks (1.42x)
+GRID_LAYOUTS = {"linear": 0, "fat": 1, "brick": 2}
+GRID_LAYOUT_NAMES = {v: k for k, v in GRID_LAYOUTS.items()}
+
 class VolPathIntegrator:
     def __init__(self, scene, maxdepth=5, spp=16, seed=0, device=0, max_paths=0, lightsampler="bvh",
                  regularize=False, name="volpath", kernel="persistent", grid_layout="fat", mode="replay"):
@@ -72,9 +76,9 @@ class VolPathIntegrator:
         if kernel not in ("persistent", "wavefront"):
             raise ValueError("kernel must be 'persistent' or 'wavefront'")
         self.ctx.set_kernel_mode(0 if kernel == "persistent" else 1)
-        if grid_layout not in ("fat", "linear"):
-            raise ValueError("grid_layout must be 'fat' or 'linear'")
-        self.ctx.set_grid_layout(1 if grid_layout == "fat" else 0)
+        if grid_layout not in GRID_LAYOUTS:
+            raise ValueError(f"grid_layout must be one of {sorted(GRID_LAYOUTS)}")
+        self.ctx.set_grid_layout(GRID_LAYOUTS[grid_layout])
         if mode not in ("replay", "fast"):
             raise ValueError("mode must be 'replay' (per-sample parity) or 'fast' (statistical parity)")
         self.mode = mode

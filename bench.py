@@ -150,7 +150,7 @@ def parse(argv=None):
     p.add_argument("--medium", default="grid", choices=["grid", "nanovdb"],
                    help="S-cloud as GridMedium (default) or as a NanoVDBMedium tree (disney-cloud's type)")
     p.add_argument("--refill-min", type=int, default=0, help="k_paths refill threshold (0 = library default)")
-    p.add_argument("--grid-layout", default="fat", choices=["fat", "linear"])
+    p.add_argument("--grid-layout", default="fat", choices=["fat", "linear", "brick"])
     p.add_argument("--dda-budget", type=int, default=0, help="k_paths DDA cells per iteration (0 = default)")
     p.add_argument("--zsobol-table", type=int, default=256,
                    help="ZSobol pixel-table dimensions (0 = every digit per sampler call)")
@@ -475,7 +475,8 @@ def main():
     if args.dda_budget:
         integ.ctx.set_dda_budget(args.dda_budget)
     integ.ctx.set_sampler_table(args.zsobol_table)
-    integ.ctx.set_sampler_pass_table(args.zsobol_pass_table)
+    if args.zsobol_pass_table != 64:   # (64: the library default; older libraries lack the call)
+        integ.ctx.set_sampler_pass_table(args.zsobol_pass_table)
     if args.ray_binning:
         integ.ctx.set_ray_binning(1)
     if args.pixel_order == "entry-cell":
@@ -615,7 +616,7 @@ def main():
                      "achieved": round(cb / (agg["ms_camera"] / 1e3) / 1e9, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(cb / (agg["ms_camera"] / 1e3) / 1e9 / HBM_PEAK_GBPS, 5),
                      "bytes_per_sample": round(cb / samples_timed, 2)}
-    grid_layout = "fat" if integ.ctx.grid_layout_active() else "linear"
+    grid_layout = {0: "linear", 1: "fat", 2: "brick"}[integ.ctx.grid_layout_active()]
     host_density = host_rgb = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and vdb is None:
         if args.scene == "rgb-explosion" and n > RGB_CPU_MAX_RES:

@@ -116,10 +116,12 @@ int avr_set_dda_budget(avr_context *ctx, int cells);
  * 32 contiguous bytes, (n+1)^3 x 32 B; NanoVDBMedium: the same 32 B per base voxel of every
  * 9^3 apron block of the density grid (512 x 32 B per block) — built on device if it fits in
  * free HBM with 8 GiB to spare, so a density fetch is one 32-B access in one cache line; 0
- * keeps only pbrt's linear layout (containers.h:834) / the apron blocks. Results are
- * bit-identical either way. */
+ * keeps only pbrt's linear layout (containers.h:834) / the apron blocks; 2 (GridMedium) builds a
+ * bricked copy instead — 8^3 base voxels per brick with a +1 apron (9^3 floats, padded to 736),
+ * bricks x-fastest, so a footprint's 8 taps lie in one brick (4 x 8 B within 368 B), 1.42x the
+ * grid. Results are bit-identical in every layout. */
 int avr_set_grid_layout(avr_context *ctx, int layout);
-/* 1 if the current medium uses the fat layout, else 0. */
+/* The current medium's density copy: 1 fat, 2 bricked, 0 none (pbrt's linear layout only). */
 int avr_grid_layout_active(avr_context *ctx);
 /* The persistent kernel's pixel order (SURVEY §7 step 6 / north star "density-grid fetches
  * coalesced along sorted ray packets"): `order` lists every pixel of the current film once

@@ -286,7 +286,7 @@ def test_density_fetch_kernel_and_lookup_trace():
     from acceleratedvolrenderer_amd import VolPathIntegrator, scenes
     from oracle import binding
     dens = binding.cloud_grid(24)
-    for layout in ("fat", "linear"):
+    for layout in ("fat", "linear", "brick"):
         scene = scenes.s_cloud(dens, width=40, height=24)
         integ = VolPathIntegrator(scene, maxdepth=scenes.CLOUD_MAXDEPTH, spp=4, seed=0, device=0, kernel="wavefront",
                                   grid_layout=layout)

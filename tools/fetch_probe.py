@@ -22,7 +22,7 @@ def main():
     ap.add_argument("--res", type=int, default=1024)
     ap.add_argument("--spp", type=int, default=16)
     ap.add_argument("--cap", type=int, default=48 * 1024 * 1024)
-    ap.add_argument("--layout", default="fat", choices=["fat", "linear"])
+    ap.add_argument("--layout", default="fat", choices=["fat", "linear", "brick"])
     a = ap.parse_args()
     import torch
     from acceleratedvolrenderer_amd import VolPathIntegrator, scenes, capi
@@ -55,7 +55,7 @@ def main():
     out = torch.empty(nl, dtype=torch.float32, device="cuda:0")
     torch.cuda.synchronize()
     fb = 32 + 16 + 4
-    res = {"lookups": nl, "bytes_per_lookup": fb, "layout": "fat" if integ.ctx.grid_layout_active() else "linear",
+    res = {"lookups": nl, "bytes_per_lookup": fb, "layout": {0: "linear", 1: "fat", 2: "brick"}[integ.ctx.grid_layout_active()],
            "peak_GBps": 8000.0}
 
     def run(name, arr):
