@@ -457,7 +457,11 @@ int build_majorant(avr_context *c, const int mres[3]) {
     // nm cells + one trailing 0: the read target of empty cells under the occupancy level
     HIP_TRY(dalloc(&c->d_majorant, (size_t)nm + 1));
     HIP_TRY(hipMemsetAsync(c->d_majorant + nm, 0, sizeof(float), c->stream));
-    for (int i = 0; i < 3; ++i) m.mres[i] = mres[i];
+    for (int i = 0; i < 3; ++i) {
+        m.mres[i] = mres[i];
+        m.fres[i] = (float)mres[i];
+        m.fresm1[i] = (float)(mres[i] - 1);
+    }
     if (type == 0) {
         hipLaunchKernelGGL(avr::k_majorant, dim3(nm), dim3(256), 0, c->stream, m.density, m.nx, m.ny, m.nz, mres[0],
                            mres[1], mres[2], c->d_majorant);
@@ -532,6 +536,10 @@ int medium_common(avr_context *c, const float *d_density, int nx, int ny, int nz
     m.sigma_a = c->d_sigma_a;
     m.sigma_s = c->d_sigma_s;
     m.g = g;
+    m.hg = avr::hg_consts(g);
+    m.fn[0] = (float)nx;
+    m.fn[1] = (float)ny;
+    m.fn[2] = (float)nz;
     c->gray = true;
     for (int i = 1; i < avr::kNTable; ++i) c->gray &= sigma_a[i] == sigma_a[0] && sigma_s[i] == sigma_s[0];
     c->med.gray_sigma_a = sigma_a[0];

@@ -36,6 +36,10 @@ struct DevMedium {
     Xf render_from_medium, medium_from_render;
     const float *sigma_a, *sigma_s;   // 471-entry densely sampled tables (sigmaScale folded in)
     float g;
+    HgC hg;                             // g's Henyey-Greenstein terms (hg_consts(g)), host-computed
+    // float(nx, ny, nz) and float(mres), float(mres - 1): host-converted, so the persistent
+    // kernel takes them from scalar kernel arguments (each the exact int -> float conversion)
+    float fn[3], fres[3], fresm1[3];
     float gray_sigma_a, gray_sigma_s;   // sigma_a[0], sigma_s[0]: the whole tables when the medium is gray
     int emissive;
     const float *Le;                  // 471
@@ -316,8 +320,11 @@ __device__ __forceinline__ float grid_at(const float *__restrict__ v, int nx, in
     if (x < 0 || x >= nx || y < 0 || y >= ny || z < 0 || z >= nz) return 0.f;
     return v[(z * ny + y) * nx + x];
 }
-__device__ __forceinline__ float grid_lookup(const float *__restrict__ v, int nx, int ny, int nz, V3 p) {
-    float psx = p.x * nx - .5f, psy = p.y * ny - .5f, psz = p.z * nz - .5f;
+// fn: float(nx, ny, nz) when the caller has them (the same value as the int -> float conversion)
+__device__ __forceinline__ float grid_lookup(const float *__restrict__ v, int nx, int ny, int nz, V3 p,
+                                             const float *fn = nullptr) {
+    const float fx = fn ? fn[0] : (float)nx, fy = fn ? fn[1] : (float)ny, fz = fn ? fn[2] : (float)nz;
+    float psx = p.x * fx - .5f, psy = p.y * fy - .5f, psz = p.z * fz - .5f;
     int ix = (int)__builtin_floorf(psx), iy = (int)__builtin_floorf(psy), iz = (int)__builtin_floorf(psz);
     float dx = psx - (float)ix, dy = psy - (float)iy, dz = psz - (float)iz;
     float d00 = lerp(dx, grid_at(v, nx, ny, nz, ix, iy, iz), grid_at(v, nx, ny, nz, ix + 1, iy, iz));
@@ -332,8 +339,9 @@ __device__ __forceinline__ float grid_lookup(const float *__restrict__ v, int nx
 // it before the DDA walk and consumes it after, hiding the HBM latency behind the walk).
 // fat_issue: false when p's footprint lies outside the fat copy (grid_lookup applies).
 __device__ __forceinline__ bool fat_issue(const float4 *__restrict__ fat, int nx, int ny, int nz, V3 p, float4 &a,
-                                          float4 &b, float &dx, float &dy, float &dz) {
-    float psx = p.x * nx - .5f, psy = p.y * ny - .5f, psz = p.z * nz - .5f;
+                                          float4 &b, float &dx, float &dy, float &dz, const float *fn = nullptr) {
+    const float fx = fn ? fn[0] : (float)nx, fy = fn ? fn[1] : (float)ny, fz = fn ? fn[2] : (float)nz;
+    float psx = p.x * fx - .5f, psy = p.y * fy - .5f, psz = p.z * fz - .5f;
     int ix = (int)__builtin_floorf(psx), iy = (int)__builtin_floorf(psy), iz = (int)__builtin_floorf(psz);
     if (ix < -1 || ix >= nx || iy < -1 || iy >= ny || iz < -1 || iz >= nz) return false;
     dx = psx - (float)ix, dy = psy - (float)iy, dz = psz - (float)iz;
@@ -358,10 +366,12 @@ __device__ __forceinline__ float fat_lerp(float4 a, float4 b, float dx, float dy
 // Same value as grid_lookup() bit for bit from the bricked layout (DevMedium::brick).
 constexpr int kBrickFloats = 736;   // 9^3 = 729 apron values, padded to 23 x 128-B lines
 __device__ __forceinline__ float brick_lookup(const float *__restrict__ brick, const int nb[3],
-                                              const float *__restrict__ v, int nx, int ny, int nz, V3 p) {
-    float psx = p.x * nx - .5f, psy = p.y * ny - .5f, psz = p.z * nz - .5f;
+                                              const float *__restrict__ v, int nx, int ny, int nz, V3 p,
+                                              const float *fn = nullptr) {
+    const float fx = fn ? fn[0] : (float)nx, fy = fn ? fn[1] : (float)ny, fz = fn ? fn[2] : (float)nz;
+    float psx = p.x * fx - .5f, psy = p.y * fy - .5f, psz = p.z * fz - .5f;
     int ix = (int)__builtin_floorf(psx), iy = (int)__builtin_floorf(psy), iz = (int)__builtin_floorf(psz);
-    if (ix < -1 || ix >= nx || iy < -1 || iy >= ny || iz < -1 || iz >= nz) return grid_lookup(v, nx, ny, nz, p);
+    if (ix < -1 || ix >= nx || iy < -1 || iy >= ny || iz < -1 || iz >= nz) return grid_lookup(v, nx, ny, nz, p, fn);
     float dx = psx - (float)ix, dy = psy - (float)iy, dz = psz - (float)iz;
     const int ux = ix + 1, uy = iy + 1, uz = iz + 1;   // 0 .. n: brick u >> 3, apron-local u & 7
     const size_t b = ((size_t)(uz >> 3) * nb[1] + (uy >> 3)) * nb[0] + (ux >> 3);
@@ -376,17 +386,17 @@ __device__ __forceinline__ float brick_lookup(const float *__restrict__ brick, c
 __device__ __forceinline__ float grid_density(const DevMedium &m, V3 p);
 
 __device__ __forceinline__ float fat_lookup(const float4 *__restrict__ fat, const float *__restrict__ v, int nx, int ny,
-                                            int nz, V3 p) {
+                                            int nz, V3 p, const float *fn = nullptr) {
     float4 a, b;
     float dx, dy, dz;
-    if (!fat_issue(fat, nx, ny, nz, p, a, b, dx, dy, dz)) return grid_lookup(v, nx, ny, nz, p);
+    if (!fat_issue(fat, nx, ny, nz, p, a, b, dx, dy, dz, fn)) return grid_lookup(v, nx, ny, nz, p, fn);
     return fat_lerp(a, b, dx, dy, dz);
 }
 
 __device__ __forceinline__ float grid_density(const DevMedium &m, V3 p) {
-    if (m.fat) return fat_lookup(m.fat, m.density, m.nx, m.ny, m.nz, p);
-    if (m.brick) return brick_lookup(m.brick, m.nb, m.density, m.nx, m.ny, m.nz, p);
-    return grid_lookup(m.density, m.nx, m.ny, m.nz, p);
+    if (m.fat) return fat_lookup(m.fat, m.density, m.nx, m.ny, m.nz, p, m.fn);
+    if (m.brick) return brick_lookup(m.brick, m.nb, m.density, m.nx, m.ny, m.nz, p, m.fn);
+    return grid_lookup(m.density, m.nx, m.ny, m.nz, p, m.fn);
 }
 
 #ifndef AVR_KPATHS_TU   // host-launched kernels: compiled in the C-ABI translation unit only
@@ -667,9 +677,10 @@ struct Dda {
     int vx, vy, vz;        // voxel
     int sx, sy, sz;        // step (+1/-1); voxelLimit = step > 0 ? res : -1
 };
-__device__ __forceinline__ void dda_axis(float gia, float gda, int res, float tMin, int &voxel, float &next,
+// res: the axis' majorant resolution as a float (exact), resm1 = float(res - 1)
+__device__ __forceinline__ void dda_axis(float gia, float gda, float res, float resm1, float tMin, int &voxel, float &next,
                                          float &delta, int &step) {
-    voxel = (int)clampf(gia * res, 0.f, (float)(res - 1));
+    voxel = (int)clampf(gia * res, 0.f, resm1);
     delta = 1 / (__builtin_fabsf(gda) * res);
     if (gda == -0.f) gda = 0.f;
     if (gda >= 0) {
@@ -702,9 +713,9 @@ __device__ __forceinline__ bool dda_init(Dda &it, const DevMedium &m, Ray ray, f
         gd = {ray.d.x / diag0, ray.d.y / diag1, ray.d.z / diag2};
     }
     V3 gi = go + gd * tMin;
-    dda_axis(gi.x, gd.x, m.mres[0], tMin, it.vx, it.nx, it.dx, it.sx);
-    dda_axis(gi.y, gd.y, m.mres[1], tMin, it.vy, it.ny, it.dy, it.sy);
-    dda_axis(gi.z, gd.z, m.mres[2], tMin, it.vz, it.nz, it.dz, it.sz);
+    dda_axis(gi.x, gd.x, m.fres[0], m.fresm1[0], tMin, it.vx, it.nx, it.dx, it.sx);
+    dda_axis(gi.y, gd.y, m.fres[1], m.fresm1[1], tMin, it.vy, it.ny, it.dy, it.sy);
+    dda_axis(gi.z, gd.z, m.fres[2], m.fresm1[2], tMin, it.vz, it.nz, it.dz, it.sz);
     if (m.type == 1 || m.type == 2) {   // HomogeneousMajorantIterator(tMin, tMax, sigma_t): one segment
         it.vx = it.vy = it.vz = 0;
         it.nx = it.ny = it.nz = kInf;
@@ -2061,7 +2072,7 @@ __global__ void __launch_bounds__(256, kGray ? (kMed == 1 ? 3 : AVR_PATHS_WAVES_
                                 const V3 wi = xf_vec3(lt.rfl, wl);
                                 lsPdf = lsPdf / (4 * kPi);
                                 const Spec Ls = image_le(lt, su, sv, lam);
-                                const float fval = hg_eval(dot(wo, wi), m.g);
+                                const float fval = hg_eval_c(dot(wo, wi), m.hg);
                                 if (Ls.nonzero() && fval != 0) {
                                     const V3 pOut = po + wi * (2 * P.lights.scene_radius);
                                     const V3 d = pOut - po;
@@ -2080,7 +2091,7 @@ __global__ void __launch_bounds__(256, kGray ? (kMed == 1 ? 3 : AVR_PATHS_WAVES_
                         } else if (lt.type == 0) {
                             const V3 wi = {lt.w[0], lt.w[1], lt.w[2]};
                             const Spec Ls = sample_table(light_table(idx), lambda_index(lam)) * lt.scale;
-                            const float fval = hg_eval(dot(wo, wi), m.g);
+                            const float fval = hg_eval_c(dot(wo, wi), m.hg);
                             if (Ls.nonzero() && fval != 0) {
                                 s_ls[threadIdx.x] = to4(Ls);
                                 s_fhat[threadIdx.x] = fval;
@@ -2182,7 +2193,7 @@ __global__ void __launch_bounds__(256, kGray ? (kMed == 1 ? 3 : AVR_PATHS_WAVES_
                     smp.get2d(P, &up0, &up1);
                 }
                 float phPdf;
-                const V3 wi = hg_sample<kFast>(-pd, m.g, up0, up1, &phPdf);
+                const V3 wi = hg_sample_c<kFast>(-pd, m.hg, up0, up1, &phPdf);
                 if (phPdf == 0) {
                     ev = EV_END;
                 } else {

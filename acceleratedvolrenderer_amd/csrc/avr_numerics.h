@@ -318,6 +318,27 @@ AVR_HD int sample_discrete3(float w0, float w1, float w2, float u) {
 }
 
 // HG phase function — scattering.h:49-58, sampling.cpp:348-372, vecmath.h:1007-1013,1666-1672,1916
+// Henyey-Greenstein's g-only terms, evaluated once per medium on the host with the same float
+// operations hg_eval / hg_sample apply (so hg_eval_c / hg_sample_c return the same bits): the
+// persistent kernel reads them as scalar kernel arguments instead of keeping hoisted copies in
+// VGPRs. a = 1 + g^2, b = 2g, k = Inv4Pi (1 - g^2), c = 1 - g^2, m = -1 / (2g), d = 1 + g.
+struct HgC {
+    float g, a, b, k, c, m, d;
+    int iso;   // |g| < 1e-3: uniform cosTheta
+};
+AVR_HD HgC hg_consts(float g) {
+    HgC h;
+    g = clampf(g, -.99f, .99f);
+    h.g = g;
+    h.a = 1 + sqr(g);
+    h.b = 2 * g;
+    h.c = 1 - sqr(g);
+    h.k = kInv4Pi * h.c;
+    h.m = -1 / (2 * g);
+    h.d = 1 + g;
+    h.iso = __builtin_fabsf(g) < 1e-3f ? 1 : 0;
+    return h;
+}
 AVR_HD float hg_eval(float cosTheta, float g) {
     g = clampf(g, -.99f, .99f);
     float denom = 1 + sqr(g) + 2 * g * cosTheta;
@@ -343,6 +364,33 @@ AVR_HD V3 hg_sample(V3 wo, float g, float u0, float u1, float *pdf) {
     V3 s = {st * cosPhi, st * sinPhi, clampf(cosTheta, -1, 1)};
     V3 wi = s.x * fx + s.y * fy + s.z * wo;
     *pdf = hg_eval(cosTheta, g);
+    return wi;
+}
+
+// hg_eval / hg_sample from the precomputed terms (HgC): bit-identical results
+AVR_HD float hg_eval_c(float cosTheta, const HgC &h) {
+    float denom = h.a + h.b * cosTheta;
+    return h.k / (denom * __builtin_sqrtf(fmaxf_(0.f, denom)));
+}
+template <bool kFast = false>
+AVR_HD V3 hg_sample_c(V3 wo, const HgC &h, float u0, float u1, float *pdf) {
+    float cosTheta;
+    if (h.iso) cosTheta = 1 - 2 * u0;
+    else cosTheta = h.m * (h.a - sqr(h.c / (h.d - h.b * u0)));
+    float sinTheta = __builtin_sqrtf(fmaxf_(0.f, 1 - sqr(cosTheta)));
+    float phi = 2 * kPi * u1;
+    float sign = __builtin_copysignf(1.f, wo.z);
+    float a = -1 / (sign + wo.z);
+    float b = wo.x * wo.y * a;
+    V3 fx = {1 + sign * sqr(wo.x) * a, sign * b, -sign * wo.x};
+    V3 fy = {b, sign + sqr(wo.y) * a, -wo.y};
+    float st = clampf(sinTheta, -1, 1);
+    float sinPhi, cosPhi;
+    if (kFast) hw_sincos_turns(u1, &sinPhi, &cosPhi);
+    else cr_sincos(phi, &sinPhi, &cosPhi);
+    V3 s = {st * cosPhi, st * sinPhi, clampf(cosTheta, -1, 1)};
+    V3 wi = s.x * fx + s.y * fy + s.z * wo;
+    *pdf = hg_eval_c(cosTheta, h);
     return wi;
 }
 
