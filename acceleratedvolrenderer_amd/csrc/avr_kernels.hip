@@ -1791,6 +1791,9 @@ __global__ void __launch_bounds__(256) k_bin_scatter(const int *__restrict__ que
 #ifndef AVR_NEE_AHEAD
 #define AVR_NEE_AHEAD 1
 #endif
+#ifndef AVR_REJECT_BY_EXP
+#define AVR_REJECT_BY_EXP 1   // replay's fast reject from T_maj's FastExp factor instead of v_log_f32 + v_rcp_f32
+#endif
 #ifndef AVR_COOP_LDS
 #define AVR_COOP_LDS 1
 #endif
@@ -2413,9 +2416,21 @@ __global__ void __launch_bounds__(256, kGray ? (kMed == 1 ? 3 : AVR_PATHS_WAVES_
                     // "pending" and are decided exactly, once per wave, after the walk.
                     const float sm0 = st0 * mv;
                     bool pending;
+                    float dt = segMax - tMin;
+                    if (__builtin_isinf(dt)) dt = kFloatMax;
+                    // T_maj's factor should the candidate be rejected (media.h:790-801)
+                    const S fac = sexpm<kFast>(-((sig_t * mv) * dt));
                     if constexpr (kFast) {
                         // fast mode: the hardware candidate is the candidate (decided once)
                         pending = tMin + m_exp_dist<true>(u, sm0) < segMax;
+                    } else if constexpr (AVR_REJECT_BY_EXP) {
+                        // t = tMin + (-log(1-u) / sm0) >= segMax  <=>  1-u <= exp(-sm0 (segMax - tMin))
+                        // in real arithmetic; FastExp(-A) (relative error < 1.2e-4 for A < 40, the
+                        // rounding of A = sm0 * dt and of pbrt's log / division / add all inside
+                        // the 1e-3 + 5e-7 A margin) decides it for sure outside the margin: no
+                        // transcendental of its own — the factor is T_maj's anyway
+                        const float A = sm0 * dt;
+                        pending = !(A < 40.f && (1 - u) <= sv0(fac) * (1 - 1e-3f - 5e-7f * A));
                     } else {
                         const float rs = __builtin_amdgcn_rcpf(sm0);
                         const float eFast = -__builtin_amdgcn_logf(1 - u) * (kLn2 * rs);
@@ -2427,9 +2442,7 @@ __global__ void __launch_bounds__(256, kGray ? (kMed == 1 ? 3 : AVR_PATHS_WAVES_
                         walk = 1;
                     } else {
                         u = rng.uniform();
-                        float dt = segMax - tMin;
-                        if (__builtin_isinf(dt)) dt = kFloatMax;
-                        T_maj = T_maj * sexpm<kFast>(-((sig_t * mv) * dt));
+                        T_maj = T_maj * fac;
                         needNext = true;
                     }
                 }
