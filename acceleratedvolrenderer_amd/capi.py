@@ -101,6 +101,8 @@ SIGNATURES = {
     "avr_medium_boundary_convex": (ctypes.c_int, [ctypes.c_void_p, c_float_p, ctypes.c_int]),
     "avr_tune_majorant": (ctypes.c_int, [ctypes.c_void_p, c_int_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                          ctypes.c_int, ctypes.c_int, c_int_p, c_float_p]),
+    "avr_tune_walk": (ctypes.c_int, [ctypes.c_void_p, c_int_p, ctypes.c_int, c_int_p, ctypes.c_int, ctypes.c_int,
+                                     ctypes.c_int, ctypes.c_int, ctypes.c_int, c_int_p, c_float_p]),
     "avr_set_refill_min": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "avr_light_sampler": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "avr_set_dda_budget": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
@@ -279,6 +281,17 @@ class Context:
                                           int(spp_end), int(seed), int(max_depth), chosen.ctypes.data_as(c_int_p),
                                           ms.ctypes.data_as(c_float_p)))
         return tuple(int(v) for v in chosen), ms
+
+    def tune_walk(self, refill, dda, spp_begin, spp_end, seed, max_depth):
+        """avr_tune_walk: returns ((refill, dda) chosen, probe ms as a len(refill) x len(dda) array)."""
+        r = np.ascontiguousarray(np.asarray(refill, np.int32).ravel())
+        d = np.ascontiguousarray(np.asarray(dda, np.int32).ravel())
+        chosen = np.zeros(2, np.int32)
+        ms = np.zeros(len(r) * len(d), np.float32)
+        _check(self.lib.avr_tune_walk(self.h, r.ctypes.data_as(c_int_p), len(r), d.ctypes.data_as(c_int_p), len(d),
+                                      int(spp_begin), int(spp_end), int(seed), int(max_depth),
+                                      chosen.ctypes.data_as(c_int_p), ms.ctypes.data_as(c_float_p)))
+        return (int(chosen[0]), int(chosen[1])), ms.reshape(len(r), len(d))
 
     def set_ray_binning(self, on):
         _check(self.lib.avr_set_ray_binning(self.h, 1 if on else 0))

@@ -1085,20 +1085,17 @@ int avr_set_majorant_res(avr_context *c, const int res[3]) {
     return AVR_OK;
 }
 
-int avr_tune_majorant(avr_context *c, const int *candidates, int n, int spp_begin, int spp_end, int seed,
-                      int max_depth, int chosen[3], float *ms) {
-    AVR_QUIESCE(c);
-    if (!c || !candidates || n < 1 || !chosen) return fail(AVR_ERR_ARG, "null argument");
-    if (!c->has_medium || !c->has_film || !c->has_camera) return fail(AVR_ERR_STATE, "scene incomplete");
-    if (c->med.type == 1 || c->med.type == 2)
-        return fail(AVR_ERR_ARG, "homogeneous / cloud media have a single majorant segment");
-    if (spp_end <= spp_begin) return fail(AVR_ERR_ARG, "empty probe sample range");
-    for (int k = 0; k < 3 * n; ++k)
-        if (candidates[k] < 1 || candidates[k] > 255) return fail(AVR_ERR_ARG, "majorant resolution must be 1..255");
+// The probe loop of the device-side tuners (avr_tune_majorant, avr_tune_walk): render
+// [spp_begin, spp_end) once after setup(k) for each k < n — plus one untimed render after
+// setup(0) first (the first render after a scene change builds one-off tables) — timed with
+// HIP events on the context stream; *bestk = the fastest, ms[k] the times when non-null. The
+// film sums are saved before and restored after (also when a probe fails; the first error is
+// kept); restore() then re-applies the chosen (or, after a failure, the original) setting.
+extern "C++" {
+template <typename Setup, typename Restore>
+static int probe_loop(avr_context *c, int n, Setup setup, Restore restore, int spp_begin, int spp_end, int seed,
+                      int max_depth, int *bestk, float *ms) {
     HIP_TRY(hipSetDevice(c->device));
-    // the probes render into the film: keep its sums and put them back afterwards — also when
-    // a probe fails, together with the majorant resolution the medium had before
-    const int mres0[3] = {c->med.mres[0], c->med.mres[1], c->med.mres[2]};
     const size_t np = (size_t)c->film.width * c->film.height;
     const size_t nd = (4 + 2 * (size_t)std::max(0, c->film.nbuckets)) * np;
     double *saved = nullptr;
@@ -1108,11 +1105,9 @@ int avr_tune_majorant(avr_context *c, const int *candidates, int n, int spp_begi
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (!rc && (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess)) rc = fail(AVR_ERR_HIP, "event");
     float best = -1.f;
-    int bestk = 0;
-    // one untimed probe first: the first render after a scene change builds one-off tables
+    *bestk = 0;
     for (int k = -1; k < n && !rc; ++k) {
-        const int *r = candidates + 3 * (k < 0 ? 0 : k);
-        if ((rc = build_majorant(c, r))) break;
+        if ((rc = setup(k < 0 ? 0 : k))) break;
         if (hipEventRecord(e0, c->stream) != hipSuccess) { rc = fail(AVR_ERR_HIP, "event record"); break; }
         if ((rc = avr_render(c, spp_begin, spp_end, seed, max_depth))) break;
         if (hipEventRecord(e1, c->stream) != hipSuccess || hipEventSynchronize(e1) != hipSuccess) {
@@ -1123,14 +1118,12 @@ int avr_tune_majorant(avr_context *c, const int *candidates, int n, int spp_begi
         (void)hipEventElapsedTime(&t, e0, e1);
         if (k < 0) continue;
         if (ms) ms[k] = t;
-        if (best < 0 || t < best) { best = t; bestk = k; }
+        if (best < 0 || t < best) { best = t; *bestk = k; }
     }
-    // the chosen resolution, or after a failure the original one (the first error is kept)
     const std::string err = g_err;
     const int rcProbe = rc;
-    int rcRestore = build_majorant(c, rc ? mres0 : candidates + 3 * bestk);
+    int rcRestore = restore(rc != 0, *bestk);
     if (haveSaved) {
-        // restore the film sums
         const double *d = saved;
         hipError_t e = hipMemcpyAsync(c->film.rgb_sum, d, 3 * np * sizeof(double), hipMemcpyDeviceToDevice, c->stream);
         if (e == hipSuccess)
@@ -1147,12 +1140,64 @@ int avr_tune_majorant(avr_context *c, const int *candidates, int n, int spp_begi
     } else {
         rc = rcRestore;
     }
-    if (!rc)
-        for (int i = 0; i < 3; ++i) chosen[i] = candidates[3 * bestk + i];
     if (e0) (void)hipEventDestroy(e0);
     if (e1) (void)hipEventDestroy(e1);
     (void)hipFree(saved);
     if (!rc) rc = avr_reset_stats(c);
+    return rc;
+}
+}  // extern "C++"
+
+int avr_tune_majorant(avr_context *c, const int *candidates, int n, int spp_begin, int spp_end, int seed,
+                      int max_depth, int chosen[3], float *ms) {
+    AVR_QUIESCE(c);
+    if (!c || !candidates || n < 1 || !chosen) return fail(AVR_ERR_ARG, "null argument");
+    if (!c->has_medium || !c->has_film || !c->has_camera) return fail(AVR_ERR_STATE, "scene incomplete");
+    if (c->med.type == 1 || c->med.type == 2)
+        return fail(AVR_ERR_ARG, "homogeneous / cloud media have a single majorant segment");
+    if (spp_end <= spp_begin) return fail(AVR_ERR_ARG, "empty probe sample range");
+    for (int k = 0; k < 3 * n; ++k)
+        if (candidates[k] < 1 || candidates[k] > 255) return fail(AVR_ERR_ARG, "majorant resolution must be 1..255");
+    const int mres0[3] = {c->med.mres[0], c->med.mres[1], c->med.mres[2]};
+    int bestk = 0;
+    const int rc = probe_loop(
+        c, n, [&](int k) { return build_majorant(c, candidates + 3 * k); },
+        [&](bool failed, int b) { return build_majorant(c, failed ? mres0 : candidates + 3 * b); }, spp_begin, spp_end,
+        seed, max_depth, &bestk, ms);
+    if (!rc)
+        for (int i = 0; i < 3; ++i) chosen[i] = candidates[3 * bestk + i];
+    return rc;
+}
+
+int avr_tune_walk(avr_context *c, const int *refill, int nr, const int *dda, int nd, int spp_begin, int spp_end,
+                  int seed, int max_depth, int chosen[2], float *ms) {
+    AVR_QUIESCE(c);
+    if (!c || !refill || !dda || nr < 1 || nd < 1 || !chosen) return fail(AVR_ERR_ARG, "null argument");
+    if (!c->has_medium || !c->has_film || !c->has_camera) return fail(AVR_ERR_STATE, "scene incomplete");
+    if (spp_end <= spp_begin) return fail(AVR_ERR_ARG, "empty probe sample range");
+    for (int k = 0; k < nr; ++k)
+        if (refill[k] < 0 || refill[k] > 64) return fail(AVR_ERR_ARG, "refill candidates must be 0..64 lanes");
+    for (int k = 0; k < nd; ++k)
+        if (dda[k] < 0) return fail(AVR_ERR_ARG, "DDA budget candidates must be >= 0 cells");
+    const int r0 = c->refill_min, d0 = c->dda_budget;
+    int bestk = 0;
+    const int rc = probe_loop(
+        c, nr * nd,
+        [&](int k) {
+            c->refill_min = refill[k / nd];
+            c->dda_budget = dda[k % nd];
+            return AVR_OK;
+        },
+        [&](bool failed, int b) {
+            c->refill_min = failed ? r0 : refill[b / nd];
+            c->dda_budget = failed ? d0 : dda[b % nd];
+            return AVR_OK;
+        },
+        spp_begin, spp_end, seed, max_depth, &bestk, ms);
+    if (!rc) {
+        chosen[0] = refill[bestk / nd];
+        chosen[1] = dda[bestk % nd];
+    }
     return rc;
 }
 

@@ -152,6 +152,9 @@ def parse(argv=None):
     p.add_argument("--refill-min", type=int, default=0, help="k_paths refill threshold (0 = library default)")
     p.add_argument("--grid-layout", default="fat", choices=["fat", "linear", "brick"])
     p.add_argument("--dda-budget", type=int, default=0, help="k_paths DDA cells per iteration (0 = default)")
+    p.add_argument("--tune-walk", default="on", choices=["on", "off"],
+                   help="choose k_paths' refill / DDA budget for this scene by on-device probe renders (avr_tune_walk, "
+                        "outside the timed region); off: --refill-min / --dda-budget or the library defaults")
     p.add_argument("--zsobol-table", type=int, default=256,
                    help="ZSobol pixel-table dimensions (0 = every digit per sampler call)")
     p.add_argument("--zsobol-pass-table", type=int, default=64,
@@ -295,7 +298,7 @@ def pmc_child_argv(args, pixelsamples):
     """The command of one counter-pass child: this configuration, 2 timed steps after 1 warmup,
     at the parent's resolved pixelsamples (not re-planned: the plan depends on --steps)."""
     child = [sys.executable, os.path.join(ROOT, "bench.py"), "--pmc-child", "--no-cpu-baseline", "--pmc", "off",
-             "--steps", "2", "--warmup", "1"]
+             "--steps", "2", "--warmup", "1", "--tune-walk", "off"]
     child += ["--pixelsamples", str(int(pixelsamples))]
     for k in ("res", "width", "height", "spp_per_step", "max_paths", "pixel_order", "kernel", "medium",
               "refill_min", "grid_layout",
@@ -483,6 +486,24 @@ def main():
         integ.ctx.set_pixel_order(integ.entry_cell_order())
     if args.occupancy:
         integ.ctx.set_majorant_occupancy(1)
+    walk_tuned = None
+    if args.tune_walk == "on" and args.kernel == "persistent" and not (args.refill_min or args.dda_budget):
+        # k_paths' lane schedule for this scene (avr_tune_walk): refill lanes x DDA cells per
+        # iteration, 0 = the library default, probe = 8 sample indices of every pixel
+        fine = vdb is not None or (scene.medium.majorant_res[0] > 16)
+        rc = (0, 12, 16, 24, 32, 40)
+        dc = (0, 16, 24, 28, 32, 40) if fine else (0, 8, 10, 12, 16, 24)
+        (r_best, d_best), wms = integ.ctx.tune_walk(rc, dc, 0, 8, 0, maxdepth)
+        if world > 1:   # every rank renders with rank 0's choice
+            t = torch.tensor([r_best, d_best], dtype=torch.int64, device=f"cuda:{dev}")
+            dist.broadcast(t, src=0)
+            r_best, d_best = (int(v) for v in t.tolist())
+        integ.ctx.set_refill_min(r_best)
+        integ.ctx.set_dda_budget(d_best)
+        walk_tuned = {"refill_min": r_best, "dda_budget": d_best, "refill_candidates": list(rc), "dda_candidates": list(dc),
+                      "probe_ms": [[round(float(x), 3) for x in row] for row in wms]}
+        args.refill_min, args.dda_budget = r_best, d_best   # the counter passes render the same schedule
+        log(f"tuned walk: refill {r_best}, DDA {d_best} (0 = default)")
     maj_res = tuple(scene.medium.majorant_res)
     tune_ms = None
     if args.majorant_res == -1 or (args.majorant_res is None and args.mode == "fast"):
@@ -724,6 +745,7 @@ def main():
                                    f"{S} spp/step/GPU, maxdepth {maxdepth}, {args.sampler} sampler "
                                    f"(pixelsamples {spp_total}), {args.filter} filter, {args.mode} mode",
                        "majorant_res": list(maj_res), "majorant_tuning_ms": tune_ms,
+                       "walk_schedule": walk_tuned or {"refill_min": args.refill_min, "dda_budget": args.dda_budget},
                        "global_batch": samples // args.steps, "parallelism": f"sample-shard x{world}",
                        "pixelsamples": spp_total, "sample_indices_distinct": True},
             "roofline": {

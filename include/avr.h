@@ -266,6 +266,15 @@ int avr_set_majorant_res(avr_context *ctx, const int res[3]);
  * film sums are restored and the work counters reset afterwards. */
 int avr_tune_majorant(avr_context *ctx, const int *candidates, int n, int spp_begin, int spp_end, int seed,
                       int max_depth, int chosen[3], float *ms);
+/* k_paths' lane schedule chosen on the device for the current scene (replaces fixed
+ * per-medium defaults): render the probe sample range once per (refill lanes, DDA cells)
+ * candidate pair, refill[i] x dda[j] (0 = the library default for either), timed with HIP
+ * events on the context stream, and keep the fastest (chosen[2] = {refill, dda}; the nr*nd
+ * probe times in ms[i * nd + j] when non-null). Film sums restored and work counters reset
+ * afterwards, as avr_tune_majorant. The schedule never changes results, only how a wave
+ * batches its lanes' events and walks. */
+int avr_tune_walk(avr_context *ctx, const int *refill, int nr, const int *dda, int nd, int spp_begin, int spp_end,
+                  int seed, int max_depth, int chosen[2], float *ms);
 
 /* Lights (lights.h:244-305 DistantLight, lights.cpp:950-972 UniformInfiniteLight).
  * type 0 = distant: w = render-space unit vector towards the light

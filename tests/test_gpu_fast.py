@@ -202,3 +202,34 @@ def test_tune_majorant_refuses_single_segment_media():
     with pytest.raises(RuntimeError, match="single majorant segment"):
         integ.ctx.set_majorant_res((2, 2, 2))
     integ.close()
+
+
+def test_tune_walk_keeps_the_film_and_changes_no_result():
+    """avr_tune_walk (k_paths' refill / DDA-budget schedule chosen by on-device probes): the film
+    is restored, the choice is the fastest probe, the counters are reset, and renders under the
+    chosen schedule — and under every candidate — are bit-identical to the default schedule."""
+    from acceleratedvolrenderer_amd import scenes, VolPathIntegrator
+    from oracle import binding
+    dens = binding.cloud_grid(32)
+    scene = scenes.s_cloud(dens, width=64, height=36, sampler="zsobol", spp=64, filter="gaussian")
+    integ = VolPathIntegrator(scene, maxdepth=scenes.CLOUD_MAXDEPTH, spp=4, seed=0, device=0)
+    rgb, w = integ.render()
+    refill, dda = (0, 8, 32, 48), (0, 4, 12)
+    chosen, ms = integ.ctx.tune_walk(refill, dda, 4, 8, 0, scenes.CLOUD_MAXDEPTH)
+    rgb2, w2 = integ.film_sums()
+    assert np.array_equal(rgb, rgb2) and np.array_equal(w, w2)
+    assert ms.shape == (4, 3) and (ms > 0).all()
+    i, j = np.unravel_index(int(np.argmin(ms)), ms.shape)
+    assert chosen == (refill[i], dda[j])
+    assert integ.stats()["medium_lookups"] == 0
+    rgb3, w3 = integ.render()
+    assert np.array_equal(rgb3, rgb) and np.array_equal(w3, w)
+    for r in refill[1:]:
+        for d in dda[1:]:
+            integ.ctx.set_refill_min(r)
+            integ.ctx.set_dda_budget(d)
+            rgb4, w4 = integ.render()
+            assert np.array_equal(rgb4, rgb) and np.array_equal(w4, w), (r, d)
+    with pytest.raises(RuntimeError, match="refill candidates"):
+        integ.ctx.tune_walk((65,), (0,), 0, 1, 0, 5)
+    integ.close()

@@ -15,8 +15,7 @@ timeout -k 10 600 python bench.py --steps 20 --warmup 2 > $O/bench_line.json 2> 
 cat $O/bench_line.json | cut -c1-400
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 bench.py --steps 20 --warmup 2 --pmc off --no-cpu-baseline --fast-leg 0 > $O/bench_prof.json 2> $O/bench_prof.err || { tail -10 $O/bench_prof.err; exit 4; }
 A="--steps 20 --warmup 2 --pmc off"
-bash tools/gpu_ab.sh "gc8f|AVR_LIB=variants/c8f/libavr_hip.so|$A" "gcur||$A" "grj|AVR_LIB=variants/rj/libavr_hip.so|$A" || exit 5
-AVR_LIB=variants/rj/libavr_hip.so timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/gpu_tests_rj.log 2>&1 || { tail -30 $O/gpu_tests_rj.log; exit 6; }
-tail -1 $O/gpu_tests_rj.log
+bash tools/gpu_ab.sh "gc8f|AVR_LIB=variants/c8f/libavr_hip.so|$A --tune-walk off" "gcur||$A --tune-walk off" "gcurt||$A" \
+  "gcam5l|AVR_LIB=variants/cam5l/libavr_hip.so|$A --tune-walk off" || exit 5
 A="--medium nanovdb --steps 20 --warmup 2 --pmc off"
-bash tools/gpu_ab.sh "vdbbase|AVR_LIB=variants/base/libavr_hip.so|$A" "vdbc3|AVR_LIB=variants/c3/libavr_hip.so|$A" "vdbc8f|AVR_LIB=variants/c8f/libavr_hip.so|$A" "vdbcur||$A" || exit 5
+bash tools/gpu_ab.sh "vdbbase|AVR_LIB=variants/base/libavr_hip.so|$A --tune-walk off" "vdbc3|AVR_LIB=variants/c3/libavr_hip.so|$A --tune-walk off" "vdbc8f|AVR_LIB=variants/c8f/libavr_hip.so|$A --tune-walk off" "vdbcur||$A --tune-walk off" "vdbcurt||$A" || exit 6
