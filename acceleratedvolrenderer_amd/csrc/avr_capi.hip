@@ -1772,7 +1772,8 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
                     {avr::k_paths_camera<0, false>, avr::k_paths_camera<2, false>, avr::k_paths_camera<3, false>},
                     {avr::k_paths_camera<0, true>, avr::k_paths_camera<2, true>, avr::k_paths_camera<3, true>}};
                 EV_MARK(ec);
-                if (c->sampler_kind == 1 && c->zs_pdims > 0) {
+                if (c->sampler_kind == 1 && c->zs_pdims > 0 &&
+                    (long long)c->film.width * c->film.height * c->zs_pdims < (1ll << 31)) {
                     // ZSobol pass table: the digits of GetSampleIndex that the pass's sample
                     // indices [base, base + S) share (those above their lowest differing bits),
                     // for the first zs_pdims dimensions; the camera stage and k_paths then

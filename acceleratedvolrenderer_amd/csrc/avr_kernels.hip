@@ -2991,12 +2991,15 @@ __global__ void __launch_bounds__(256) k_zsobol_table(smp::ZSobolParams zp, int 
 // the dimension. zp.ptab must be null here. Built once per k_paths pass (a few hundred us).
 __global__ void __launch_bounds__(256) k_zsobol_pass_table(smp::ZSobolParams zp, int width, int height, int pdims,
                                                            int plo, long long base, uint64_t *__restrict__ table) {
-    const long long n = (long long)width * height * pdims;
+    // 32-bit indices (the host checks width * height * pdims < 2^31): 64-bit divisions by a
+    // run-time divisor are ~100 instructions each, more than the entry's own digits
+    const uint32_t n = (uint32_t)width * (uint32_t)height * (uint32_t)pdims;
     const bool wide = smp::zsobol_wide(zp);
-    for (long long k = blockIdx.x * (long long)blockDim.x + threadIdx.x; k < n; k += (long long)gridDim.x * blockDim.x) {
-        const int d = (int)(k % pdims);
-        const long long pix = k / pdims;
-        const uint32_t pm = (uint32_t)smp::encode_morton2((uint32_t)(pix % width), (uint32_t)(pix / width));
+    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
+        const uint32_t pix = k / (uint32_t)pdims;
+        const int d = (int)(k - pix * (uint32_t)pdims);
+        const uint32_t py = pix / (uint32_t)width;
+        const uint32_t pm = (uint32_t)smp::encode_morton2(pix - py * (uint32_t)width, py);
         const uint32_t up = (zp.upper && d < zp.dmax) ? zp.upper[(size_t)pm * zp.dmax + d] : smp::zsobol_upper(pm, (uint32_t)d, zp);
         const uint64_t m = ((uint64_t)pm << zp.log2spp) | (uint64_t)base;
         table[(size_t)pm * pdims + d] = wide ? smp::zsobol_pass_entry<uint64_t>(m, (uint32_t)d, zp, plo, up)

@@ -13,7 +13,7 @@ timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.
 tail -1 $O/smoke.log
 timeout -k 10 600 python bench.py --steps 20 --warmup 2 > $O/bench_line.json 2> $O/bench_line.err || { tail -10 $O/bench_line.err; exit 3; }
 cat $O/bench_line.json | cut -c1-400
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 bench.py --steps 20 --warmup 2 --pmc off --no-cpu-baseline --fast-leg 0 > $O/bench_prof.json 2> $O/bench_prof.err || { tail -10 $O/bench_prof.err; exit 4; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 bench.py --steps 20 --warmup 2 --pmc off --no-cpu-baseline --fast-leg 0 --tune-walk off > $O/bench_prof.json 2> $O/bench_prof.err || { tail -10 $O/bench_prof.err; exit 4; }
 A="--steps 20 --warmup 2 --pmc off"
 bash tools/gpu_ab.sh "gc8f|AVR_LIB=variants/c8f/libavr_hip.so|$A --tune-walk off" "gcur||$A --tune-walk off" "gcurt||$A" \
   "gcam5l|AVR_LIB=variants/cam5l/libavr_hip.so|$A --tune-walk off" || exit 5

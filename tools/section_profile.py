@@ -37,6 +37,8 @@ def main():
     p.add_argument("--steps", type=int, default=3)
     p.add_argument("--sampler", default="zsobol")
     p.add_argument("--filter", default="gaussian")
+    p.add_argument("--pixelsamples", type=int, default=16384, help="sampler pixelsamples (bench.py --steps 20: 16384)")
+    p.add_argument("--pass-size", type=int, default=64, help="sample indices per pass (bench.py: 64)")
     a = p.parse_args()
     if a.build:
         return build()
@@ -53,27 +55,30 @@ def main():
     gen.sync()
     gen.close()
     if a.medium == "nanovdb":
-        scene = scenes.s_cloud_vdb(scenes.vdb_grid(density.cpu().numpy()), sampler=a.sampler, spp=256, filter=a.filter)
+        scene = scenes.s_cloud_vdb(scenes.vdb_grid(density.cpu().numpy()), sampler=a.sampler, spp=a.pixelsamples,
+                                   filter=a.filter)
         del density
     else:
-        scene = scenes.s_cloud(density, sampler=a.sampler, spp=256, filter=a.filter)
-    integ = VolPathIntegrator(scene, maxdepth=scenes.CLOUD_MAXDEPTH, spp=16, device=0)
+        scene = scenes.s_cloud(density, sampler=a.sampler, spp=a.pixelsamples, filter=a.filter)
+    S = a.pass_size
+    integ = VolPathIntegrator(scene, maxdepth=scenes.CLOUD_MAXDEPTH, spp=S, device=0)
     lib = capi.load()
     lib.avr_debug_sections.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_ulonglong)]
     out = (ctypes.c_ulonglong * 8)()
-    integ.ctx.render(0, 16, 0, scenes.CLOUD_MAXDEPTH)   # warmup (pixel tables)
+    integ.ctx.render(0, S, 0, scenes.CLOUD_MAXDEPTH)   # warmup (pixel tables)
     integ.ctx.sync()
     lib.avr_debug_sections(integ.ctx.h, out)
     t0 = time.perf_counter()
     for k in range(1, 1 + a.steps):
-        integ.ctx.render(16 * k, 16 * (k + 1), 0, scenes.CLOUD_MAXDEPTH)
+        integ.ctx.render(S * k, S * (k + 1), 0, scenes.CLOUD_MAXDEPTH)
     integ.ctx.sync()
     dt = time.perf_counter() - t0
     lib.avr_debug_sections(integ.ctx.h, out)
     tot = sum(out[i] for i in range(8))
     res = {NAMES[i]: round(out[i] / tot, 4) for i in range(8)}
     st = integ.stats()
-    print(json.dumps({"medium": a.medium, "res": n, "Msamples_per_s": 1280 * 720 * 16 * a.steps / dt / 1e6,
+    print(json.dumps({"medium": a.medium, "res": n, "pixelsamples": a.pixelsamples, "pass_size": S,
+                      "Msamples_per_s": 1280 * 720 * S * a.steps / dt / 1e6,
                       "section_share": res, "wave_cycles": tot, "loop_iterations": st.get("loop_iterations"),
                       "dda_steps": st.get("medium_dda_steps")}))
     integ.close()
