@@ -309,14 +309,18 @@ def pmc_child_argv(args, pixelsamples):
     return child
 
 
-def pmc_passes(args, pixelsamples, kernel_re=r"\bk_paths<|\dk_pathsI", timeout_s=240):
+CAMERA_RE = r"\bk_paths_camera<|k_paths_cameraI"
+
+
+def pmc_passes(args, pixelsamples, kernel_re=r"\bk_paths<|\dk_pathsI", timeout_s=240, side=None):
     """rocprofv3 counter passes of this same bench configuration, one child process per
     pass (--pmc only: no tracing in the same run), each killed after timeout_s. The child
     renders with the parent's RESOLVED pixelsamples (so the same k_paths instantiation and
     ZSobol digit count) and the parent's first timed sample indices (world 1: steps 0 and 1
     render [0, S) and [S, 2S)). Returns (per-launch averages of the dominant kernel's counters,
     error, the set of kernel names matched), or None. kernel_re matches the kernel name,
-    demangled or mangled (k_paths itself, not the camera stage k_paths_camera)."""
+    demangled or mangled (k_paths itself, not the camera stage k_paths_camera). `side`: an
+    optional dict filled with the same per-launch averages of the camera stage (CAMERA_RE)."""
     exe = shutil.which("rocprofv3")
     if exe is None:
         return None, "rocprofv3 not found", set()
@@ -351,18 +355,24 @@ def pmc_passes(args, pixelsamples, kernel_re=r"\bk_paths<|\dk_pathsI", timeout_s
             files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
             if not files:
                 return None, f"pmc pass {name}: no counter file", names
-            per = {}
+            per, per_cam = {}, {}
             for fn in files:
                 for row in csv.DictReader(open(fn)):
+                    tgt = None
                     if re.search(kernel_re, row["Kernel_Name"]):
                         names.add(row["Kernel_Name"])
-                        per.setdefault(row["Counter_Name"], {}).setdefault(row.get("Dispatch_Id", ""), 0.0)
-                        per[row["Counter_Name"]][row.get("Dispatch_Id", "")] += float(row["Counter_Value"])
-            for cn, disp in per.items():
-                # the child's first launch is its warmup; average the timed launches
-                vals = [disp[k] for k in sorted(disp, key=lambda x: int(x) if x.isdigit() else 0)]
-                vals = vals[1:] if len(vals) > 1 else vals
-                out[cn] = sum(vals) / len(vals)
+                        tgt = per
+                    elif side is not None and re.search(CAMERA_RE, row["Kernel_Name"]):
+                        tgt = per_cam
+                    if tgt is not None:
+                        tgt.setdefault(row["Counter_Name"], {}).setdefault(row.get("Dispatch_Id", ""), 0.0)
+                        tgt[row["Counter_Name"]][row.get("Dispatch_Id", "")] += float(row["Counter_Value"])
+            for dst, src in ((out, per), (side, per_cam)):
+                for cn, disp in src.items():
+                    # the child's first launch is its warmup; average the timed launches
+                    vals = [disp[k] for k in sorted(disp, key=lambda x: int(x) if x.isdigit() else 0)]
+                    vals = vals[1:] if len(vals) > 1 else vals
+                    dst[cn] = sum(vals) / len(vals)
         return out, None, names
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
@@ -683,8 +693,10 @@ def main():
         want_pmc = args.pmc == "on" or (args.pmc == "auto" and world == 1)
         pmc_kernel = None
         if want_pmc:
+            cam_ctr = {}
             ctr, err, names = pmc_passes(args, spp_total,
-                                         kernel_re=r"\bk_paths<|\dk_pathsI" if persistent else r"\bk_medium\b|\dk_mediumE")
+                                         kernel_re=r"\bk_paths<|\dk_pathsI" if persistent else r"\bk_medium\b|\dk_mediumE",
+                                         side=cam_ctr if persistent else None)
             if persistent and ctr is not None:
                 # the counters must come from the instantiation the parent timed
                 got = {kernel_targs(nm) for nm in names}
@@ -724,6 +736,21 @@ def main():
                         "wave_cycle_split": {"issuing": round(ctr["SQ_ACTIVE_INST_ANY"] / wc, 4),
                                              "dependency/issue stall": round(ctr["SQ_WAIT_INST_ANY"] / wc, 4),
                                              "s_waitcnt (memory/LDS)": round(ctr["SQ_WAIT_ANY"] / wc, 4)},
+                    }
+                if cam_block is not None and "SQ_INSTS_VALU" in cam_ctr and cam_ctr.get("SQ_WAVE_CYCLES"):
+                    # the camera stage's own limiter (the same passes count k_paths_camera separately)
+                    cms = cam_block["avg_launch_ms"]
+                    cclk = (cam_ctr["GRBM_GUI_ACTIVE"] / 8 / (cms / 1e3)) if cam_ctr.get("GRBM_GUI_ACTIVE") else 2.4e9
+                    cwc = cam_ctr["SQ_WAVE_CYCLES"]
+                    cam_block["limiter"] = {
+                        "valu_issue_frac": round(cam_ctr["SQ_INSTS_VALU"] * 2 / (VALU_SIMDS * cclk * cms / 1e3), 4),
+                        "valu_wave_insts_per_sample": round(cam_ctr["SQ_INSTS_VALU"] / samples_per_launch, 2),
+                        "waves_per_simd_launched": round(cam_ctr["SQ_WAVES"] / VALU_SIMDS, 2) if cam_ctr.get("SQ_WAVES") else None,
+                        "wave_cycle_split": {"issuing": round(cam_ctr["SQ_ACTIVE_INST_ANY"] / cwc, 4),
+                                             "dependency/issue stall": round(cam_ctr["SQ_WAIT_INST_ANY"] / cwc, 4),
+                                             "s_waitcnt (memory/LDS)": round(cam_ctr["SQ_WAIT_ANY"] / cwc, 4)},
+                        "hbm_traffic_GB": (round((2 * cam_ctr["FETCH_SIZE"] + cam_ctr["WRITE_SIZE"]) * 1024 / 1e9, 4)
+                                           if "FETCH_SIZE" in cam_ctr and "WRITE_SIZE" in cam_ctr else None),
                     }
         out = {
             "metric": "Msamples/s (whole node) on synthetic S-cloud-1024 720p (disney-cloud stand-in)",
