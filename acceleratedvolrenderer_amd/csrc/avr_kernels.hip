@@ -1074,15 +1074,17 @@ __device__ __forceinline__ uint32_t zsobol_lower_quad(M morton, uint32_t dimensi
 // ZSobol::get1d / get2d with the quad-shared lower digits (kW: 1 32-bit, 2 64-bit index)
 constexpr uint32_t kCamDimHash = 16;   // the camera stage's draws end at dimension 10
 template <int kW>
+// pe: the dimension's pass-table entry when the caller loaded it ahead (pe_ok), else it is read here
 __device__ __forceinline__ void zsobol_draw_quad(smp::ZSobol &z, const smp::ZSobolParams &zp, bool two, float *u0,
-                                                 float *u1, const uint64_t *dh = nullptr) {
+                                                 float *u1, const uint64_t *dh = nullptr, uint64_t pe = 0,
+                                                 bool pe_ok = false) {
     uint32_t a, ah = 0;
     const uint32_t pm = kW == 2 ? (uint32_t)((((uint64_t)z.hi << 32) | z.morton) >> zp.log2spp) : z.morton >> zp.log2spp;
     const int pw = zp.log2spp & 1;
-    if (zp.ptab && (int)z.dimension < zp.pdims) {
+    if (pe_ok || (zp.ptab && (int)z.dimension < zp.pdims)) {
         // the pass table (zsobol_pass_entry): the quad computes the varying digits only (those
         // below the perm-fixed digit iTop, the highest one under the pass's plo bits)
-        const uint64_t e = zp.ptab[(size_t)pm * (size_t)zp.pdims + z.dimension];
+        const uint64_t e = pe_ok ? pe : zp.ptab[(size_t)pm * (size_t)zp.pdims + z.dimension];
         const int iTop = (zp.plo + pw - 1) >> 1;
         const uint32_t perm = (uint32_t)(e >> 56);
         const uint64_t fx = (e & 0x00ffffffffffffffull) << zp.plo;
@@ -1187,8 +1189,25 @@ __global__ void __launch_bounds__(256, AVR_CAM_WAVES) k_paths_camera(Params P) {
         } else {
             smp.start(P, px, py, P.sample_base + s);
         }
+        // ZSobol with the pass table: the entries of the stage's six draws (dimensions 0, 1 and
+        // 6..9) loaded up front by three 16-B loads of the pixel's row, so the draws wait for
+        // one memory round trip instead of six in sequence
+        [[maybe_unused]] uint64_t pe0 = 0, pe1 = 0, pe6 = 0, pe7 = 0, pe8 = 0, pe9 = 0;
+        [[maybe_unused]] bool pe_ok = false;
+        if constexpr (kSmp != 0) {
+            if (quad && P.zs.ptab && P.zs.pdims >= 10) {
+                const uint32_t pmk = PathSampler<kSmp>::kW == 2
+                                         ? (uint32_t)((((uint64_t)smp.z.hi << 32) | smp.z.morton) >> P.zs.log2spp)
+                                         : smp.z.morton >> P.zs.log2spp;
+                const ulonglong2 *row = reinterpret_cast<const ulonglong2 *>(P.zs.ptab + (size_t)pmk * (size_t)P.zs.pdims);
+                const ulonglong2 r01 = row[0], r67 = row[3], r89 = row[4];
+                pe0 = r01.x; pe1 = r01.y; pe6 = r67.x; pe7 = r67.y; pe8 = r89.x; pe9 = r89.y;
+                pe_ok = true;
+            }
+        }
         // the sampler's draws: a ZSobol quad shares its digit permutations
-        auto get1 = [&]() -> float {
+        // pe: the draw's preloaded pass-table entry (used when pe_ok)
+        auto get1 = [&](uint64_t pe) -> float {
 #if AVR_CAM_EXPERIMENT == 2   // measurement only: no sampler work (breaks replay)
             static_assert(kSmp >= 0, "");
             if constexpr (kSmp != 0) return u32_to_unit_exp((uint32_t)(id * 2654435761u + smp.z.dimension++ * 40503u));
@@ -1196,13 +1215,14 @@ __global__ void __launch_bounds__(256, AVR_CAM_WAVES) k_paths_camera(Params P) {
             if constexpr (kSmp != 0) {
                 if (quad) {
                     float a, b;
-                    zsobol_draw_quad<PathSampler<kSmp>::kW>(smp.z, P.zs, false, &a, &b, AVR_CAM_DIM_HASH ? s_cdh : nullptr);
+                    zsobol_draw_quad<PathSampler<kSmp>::kW>(smp.z, P.zs, false, &a, &b, AVR_CAM_DIM_HASH ? s_cdh : nullptr,
+                                                            pe, pe_ok);
                     return a;
                 }
             }
             return smp.get1d(P);
         };
-        const float ulam = get1();
+        const float ulam = get1(pe0);
 #if AVR_CAM_EXPERIMENT == 1   // measurement only: wavelengths without transcendentals (breaks replay)
         const Spec lam = {360 + 470 * ulam, 360 + 470 * (1 - ulam), 400 + 400 * ulam, 600 - 200 * ulam};
         const Spec pdf = Spec::c(1.f / 470);
@@ -1221,10 +1241,11 @@ __global__ void __launch_bounds__(256, AVR_CAM_WAVES) k_paths_camera(Params P) {
         if constexpr (kSmp != 0) {
             float fu0, fu1;
 #if AVR_CAM_EXPERIMENT == 2
-            fu0 = get1();
-            fu1 = get1();
+            fu0 = get1(0);
+            fu1 = get1(0);
 #else
-            if (quad) zsobol_draw_quad<PathSampler<kSmp>::kW>(smp.z, P.zs, true, &fu0, &fu1, AVR_CAM_DIM_HASH ? s_cdh : nullptr);
+            if (quad) zsobol_draw_quad<PathSampler<kSmp>::kW>(smp.z, P.zs, true, &fu0, &fu1, AVR_CAM_DIM_HASH ? s_cdh : nullptr,
+                                                              pe1, pe_ok);
             else smp.get2d(P, &fu0, &fu1);
 #endif
             camera_filter(P, px, py, fu0, fu1, &pFilmX, &pFilmY, &fweight, &s_ftab);
@@ -1243,13 +1264,13 @@ __global__ void __launch_bounds__(256, AVR_CAM_WAVES) k_paths_camera(Params P) {
         ray = xf_ray(P.cam.render_from_camera, ray, nullptr, /*forward=*/true);
         const V3 o = P.med.boundary ? interface_entry(P.med, ray.o, ray.d) : ray.o;
         // first medium segment: RNG from two sampler dims, u from a third (984-989)
-        const float h0 = get1();
-        const float h1 = get1();
-        const float u = get1();
+        const float h0 = get1(pe6);
+        const float h1 = get1(pe7);
+        const float u = get1(pe8);
         const uint64_t seqA = hash_u32(f2u(h0)), seqB = hash_u32(f2u(h1));
         // ZSobol: the first scatter's light-pick draw (dimension 9) ahead of time (k_paths' NEE
         // handler reads it instead of evaluating the sampler for its lanes)
-        const float ulight = kSmp != 0 ? get1() : 0.f;
+        const float ulight = kSmp != 0 ? get1(pe9) : 0.f;
         P.ps.cam0[id] = make_float4(o.x, o.y, o.z, u);
         P.ps.cam1[id] = make_float4(ray.d.x, ray.d.y, ray.d.z, fweight);
         P.ps.cam2[id] = to4(lam);
