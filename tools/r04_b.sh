@@ -15,3 +15,6 @@ timeout -k 10 300 python tools/section_profile.py --steps 3 > $O/sections_grid.j
 cat $O/sections_grid.json
 timeout -k 10 400 python tools/section_profile.py --steps 3 --medium nanovdb > $O/sections_vdb.json 2> $O/sections_vdb.err || { tail -10 $O/sections_vdb.err; exit 5; }
 cat $O/sections_vdb.json
+# camera-stage decomposition (measurement-only variants; replay broken by design)
+bash tools/gpu_ab.sh "camx1|AVR_LIB=variants/camx1/libavr_hip.so|$A" "camx2|AVR_LIB=variants/camx2/libavr_hip.so|$A" || exit 6
+timeout -k 10 600 python bench.py --steps 20 --warmup 2 --fast-leg 0 --no-cpu-baseline > $O/bench_pmc.json 2> $O/bench_pmc.err || { tail -10 $O/bench_pmc.err; exit 7; }
