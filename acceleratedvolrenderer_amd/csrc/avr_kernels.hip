@@ -1071,6 +1071,59 @@ __device__ __forceinline__ uint32_t zsobol_lower_quad(M morton, uint32_t dimensi
     }
     return idx;
 }
+// Two GetSampleIndex values of a quad's samples, at dimensions dA and dB, from their pass-table
+// entries, for passes with at most two varying base-4 digits (a 64-index pass: digits 0 and 1):
+// lane q of the quad evaluates the MixBits of digit pw + (q & 1) for dA (q < 2) or dB (q >= 2),
+// so one round of MixBits serves both draws (zsobol_draw_quad spends a round per draw with two
+// of its four lanes busy). Same bits as zsobol_index_pass / zsobol_index.
+template <typename M>
+__device__ __forceinline__ void zsobol_index_quad_pair(M morton, const smp::ZSobolParams &zp, uint32_t dA, uint64_t eA,
+                                                       uint32_t dB, uint64_t eB, M *ia, M *ib) {
+    constexpr int kBits = 8 * (int)sizeof(M);
+    const int pw = zp.log2spp & 1, plo = zp.plo;
+    const int iTop = (plo + pw - 1) >> 1;   // the perm-fixed digit (when >= pw); digits below it vary
+    const int q = lane_id() & 3;
+    const int i = pw + (q & 1);
+    uint32_t p = 0;
+    if (i < iTop) {
+        const int shift = 2 * i - pw;
+        const M higher = shift + 2 >= kBits ? M(0) : M(morton >> (shift + 2));
+        p = smp::mix_perm24<M>((M)(higher ^ (M)(0x55555555u * (q < 2 ? dA : dB))));
+    }
+    const uint32_t pA0 = quad_bcast<0>(p), pA1 = quad_bcast<1>(p), pB0 = quad_bcast<2>(p), pB1 = quad_bcast<3>(p);
+    auto assemble = [&](uint64_t e, uint32_t d, uint32_t p0, uint32_t p1) -> M {
+        M idx = (M)((e & 0x00ffffffffffffffull) << plo);
+        if (iTop >= pw) {
+            const int sh = 2 * iTop - pw;
+            idx |= (M)smp::zperm((uint32_t)(e >> 56), (uint32_t)(morton >> sh) & 3u) << sh;
+        }
+        if (pw < iTop) idx |= (M)smp::zperm(p0, (uint32_t)(morton >> pw) & 3u) << pw;
+        if (pw + 1 < iTop) idx |= (M)smp::zperm(p1, (uint32_t)(morton >> (pw + 2)) & 3u) << (pw + 2);
+        if (pw) {   // the final base-2 digit (as zsobol_lower)
+            const M x = (M)(morton >> 1) ^ (M)(0x55555555u * d);
+            uint64_t v = (uint64_t)x;
+            v ^= v >> 31;
+            v *= 0x7fb5d329728ea185ull;
+            v ^= v >> 27;
+            v *= 0x81dadef4bc2dd44dull;
+            v ^= v >> 33;
+            idx |= (M)(((uint32_t)morton & 1u) ^ (uint32_t)(v & 1));
+        }
+        return idx;
+    };
+    *ia = assemble(eA, dA, pA0, pA1);
+    *ib = assemble(eB, dB, pB0, pB1);
+}
+// A ZSobol draw from its index (ZSobol::get1d / get2d after GetSampleIndex): `dnext` = the
+// dimension after the draw (the FastOwen seed is Hash(dnext, seed))
+template <typename M>
+__device__ __forceinline__ void zsobol_finish(M idx, uint32_t dnext, const smp::ZSobolParams &zp, bool two, float *u0,
+                                              float *u1, const uint64_t *dh) {
+    const uint64_t h = (dh && dnext < 16) ? dh[dnext] : smp::hash_2u32(dnext, (uint32_t)zp.seed);
+    const uint32_t a = (uint32_t)idx, ah = sizeof(M) == 8 ? (uint32_t)((uint64_t)idx >> 32) : 0u;
+    *u0 = smp::u32_to_unit(smp::fast_owen(smp::sobol_bits(a, 0), (uint32_t)h));
+    if (two) *u1 = smp::u32_to_unit(smp::fast_owen(smp::sobol_bits64(a, ah, 1), (uint32_t)(h >> 32)));
+}
 // ZSobol::get1d / get2d with the quad-shared lower digits (kW: 1 32-bit, 2 64-bit index)
 constexpr uint32_t kCamDimHash = 16;   // the camera stage's draws end at dimension 10
 template <int kW>
@@ -1222,7 +1275,33 @@ __global__ void __launch_bounds__(256, AVR_CAM_WAVES) k_paths_camera(Params P) {
             }
             return smp.get1d(P);
         };
-        const float ulam = get1(pe0);
+        // ZSobol quads whose pass varies at most two base-4 digits: the six draws as three pairs
+        // of indices (zsobol_index_quad_pair), each pair one round of MixBits for the quad
+        [[maybe_unused]] float pu[7] = {};   // ulam, fu0, fu1, h0, h1, u, ulight
+        bool paired = false;
+#if AVR_CAM_EXPERIMENT != 2
+        if constexpr (kSmp != 0) {
+            if (pe_ok && ((P.zs.plo + (P.zs.log2spp & 1) - 1) >> 1) - (P.zs.log2spp & 1) <= 2) {
+                using M = typename std::conditional<PathSampler<kSmp>::kW == 2, uint64_t, uint32_t>::type;
+                const M m = PathSampler<kSmp>::kW == 2 ? (M)(((uint64_t)smp.z.hi << 32) | smp.z.morton) : (M)smp.z.morton;
+                const uint64_t *dh = AVR_CAM_DIM_HASH ? s_cdh : nullptr;
+                M i0, i1, i6, i7, i8, i9;
+                zsobol_index_quad_pair<M>(m, P.zs, 0, pe0, 1, pe1, &i0, &i1);
+                zsobol_index_quad_pair<M>(m, P.zs, 6, pe6, 7, pe7, &i6, &i7);
+                zsobol_index_quad_pair<M>(m, P.zs, 8, pe8, 9, pe9, &i8, &i9);
+                float dummy;
+                zsobol_finish<M>(i0, 1, P.zs, false, &pu[0], &dummy, dh);
+                zsobol_finish<M>(i1, 3, P.zs, true, &pu[1], &pu[2], dh);
+                zsobol_finish<M>(i6, 7, P.zs, false, &pu[3], &dummy, dh);
+                zsobol_finish<M>(i7, 8, P.zs, false, &pu[4], &dummy, dh);
+                zsobol_finish<M>(i8, 9, P.zs, false, &pu[5], &dummy, dh);
+                zsobol_finish<M>(i9, 10, P.zs, false, &pu[6], &dummy, dh);
+                smp.z.dimension = 10;
+                paired = true;
+            }
+        }
+#endif
+        const float ulam = paired ? pu[0] : get1(pe0);
 #if AVR_CAM_EXPERIMENT == 1   // measurement only: wavelengths without transcendentals (breaks replay)
         const Spec lam = {360 + 470 * ulam, 360 + 470 * (1 - ulam), 400 + 400 * ulam, 600 - 200 * ulam};
         const Spec pdf = Spec::c(1.f / 470);
@@ -1244,12 +1323,18 @@ __global__ void __launch_bounds__(256, AVR_CAM_WAVES) k_paths_camera(Params P) {
             fu0 = get1(0);
             fu1 = get1(0);
 #else
-            if (quad) zsobol_draw_quad<PathSampler<kSmp>::kW>(smp.z, P.zs, true, &fu0, &fu1, AVR_CAM_DIM_HASH ? s_cdh : nullptr,
-                                                              pe1, pe_ok);
-            else smp.get2d(P, &fu0, &fu1);
+            if (paired) {
+                fu0 = pu[1];
+                fu1 = pu[2];
+            } else if (quad) {
+                zsobol_draw_quad<PathSampler<kSmp>::kW>(smp.z, P.zs, true, &fu0, &fu1, AVR_CAM_DIM_HASH ? s_cdh : nullptr,
+                                                        pe1, pe_ok);
+            } else {
+                smp.get2d(P, &fu0, &fu1);
+            }
 #endif
             camera_filter(P, px, py, fu0, fu1, &pFilmX, &pFilmY, &fweight, &s_ftab);
-            smp.z.dimension += 3;   // time (1D) and lens (2D): drawn by pbrt, unused by pinholes
+            if (!paired) smp.z.dimension += 3;   // time (1D) and lens (2D): drawn by pbrt, unused by pinholes
         } else {
             camera_sample(P, smp, px, py, &pFilmX, &pFilmY, &fweight, &s_ftab);
         }
@@ -1264,13 +1349,13 @@ __global__ void __launch_bounds__(256, AVR_CAM_WAVES) k_paths_camera(Params P) {
         ray = xf_ray(P.cam.render_from_camera, ray, nullptr, /*forward=*/true);
         const V3 o = P.med.boundary ? interface_entry(P.med, ray.o, ray.d) : ray.o;
         // first medium segment: RNG from two sampler dims, u from a third (984-989)
-        const float h0 = get1(pe6);
-        const float h1 = get1(pe7);
-        const float u = get1(pe8);
+        const float h0 = paired ? pu[3] : get1(pe6);
+        const float h1 = paired ? pu[4] : get1(pe7);
+        const float u = paired ? pu[5] : get1(pe8);
         const uint64_t seqA = hash_u32(f2u(h0)), seqB = hash_u32(f2u(h1));
         // ZSobol: the first scatter's light-pick draw (dimension 9) ahead of time (k_paths' NEE
         // handler reads it instead of evaluating the sampler for its lanes)
-        const float ulight = kSmp != 0 ? get1(pe9) : 0.f;
+        const float ulight = kSmp != 0 ? (paired ? pu[6] : get1(pe9)) : 0.f;
         P.ps.cam0[id] = make_float4(o.x, o.y, o.z, u);
         P.ps.cam1[id] = make_float4(ray.d.x, ray.d.y, ray.d.z, fweight);
         P.ps.cam2[id] = to4(lam);

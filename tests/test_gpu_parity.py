@@ -653,7 +653,7 @@ def test_zsobol_pass_table_identical(pixelsamples):
     base = scenes.s_uniform(n=n, width=W, height=H, variant="scatter", density=dens)
     scene = Scene(base.camera, RGBFilm(W, H, filter=GaussianFilter()), base.medium, base.lights,
                   sampler=ZSobolSampler(pixelsamples))
-    for lo, hi, per_pass in ((64, 128, 64), (5, 71, 24), (1000, 1040, 7)):
+    for lo, hi, per_pass in ((64, 128, 64), (5, 71, 24), (1000, 1040, 7), (512, 544, 8), (0, 64, 16)):
         out = []
         for dims in (0, 8, 64):
             integ = _integrator(scene, maxdepth=30, spp=pixelsamples, kernel="persistent", max_paths=W * H * per_pass)
