@@ -48,6 +48,10 @@ int fail(int code, const std::string &msg) {
             return fail(AVR_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));       \
     } while (0)
 
+#ifndef AVR_ZS_TWO_LEVEL
+#define AVR_ZS_TWO_LEVEL 1   // build the ZSobol pass table from a level-A table shared by 4 passes
+#endif
+
 template <typename T>
 hipError_t dalloc(T **p, size_t n) { return hipMalloc((void **)p, std::max<size_t>(n, 1) * sizeof(T)); }
 
@@ -156,6 +160,12 @@ struct avr_context {
     uint64_t *d_zs_ptab = nullptr;
     size_t zs_ptab_cap = 0;   // entries allocated
     int zs_pdims = 64;
+    // Level-A pass table (the same table for plo + 2, shared by four consecutive passes);
+    // zs_akey names the build it holds (rebuilt when any field changes), zs_two_level 0 = off
+    uint64_t *d_zs_atab = nullptr;
+    size_t zs_atab_cap = 0;
+    long long zs_akey[6] = {-1, -1, -1, -1, -1, -1};
+    int zs_two_level = AVR_ZS_TWO_LEVEL;
     int refill_min = 0;       // 0: the default (32 lanes; 12 for a non-emissive NanoVDB walk, 16 for RGB grids)
     int dda_budget = 0;       // 0: by majorant resolution (12 cells up to 16^3, 32 for NanoVDB's 64^3)
     int grid_layout = 1;
@@ -755,6 +765,7 @@ int avr_context_destroy(avr_context *c) {
     for (auto &b : c->d_light_img) if (b) (void)hipFree(b), b = nullptr;
     if (c->d_zs_table) (void)hipFree(c->d_zs_table);
     if (c->d_zs_ptab) (void)hipFree(c->d_zs_ptab);
+    if (c->d_zs_atab) (void)hipFree(c->d_zs_atab);
     if (c->d_image) (void)hipFree(c->d_image);
     if (c->d_reference) (void)hipFree(c->d_reference);
     if (c->d_metric) (void)hipFree(c->d_metric);
@@ -1794,12 +1805,46 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
                             c->zs_ptab_cap = need_e;
                         }
                     }
+                    // two-level build: the plo + 2 table is shared by the four passes whose
+                    // indices agree above plo + 2 bits; each pass then derives its own from it
+                    const uint64_t *atab = nullptr;
+                    if (c->d_zs_ptab && c->zs_two_level && plo + 2 <= zs.log2spp) {
+                        if (need_e > c->zs_atab_cap) {
+                            if (c->d_zs_atab) (void)hipFree(c->d_zs_atab);
+                            c->d_zs_atab = nullptr;
+                            c->zs_atab_cap = 0;
+                            for (long long &k : c->zs_akey) k = -1;
+                            if (hipMalloc((void **)&c->d_zs_atab, need_e * sizeof(uint64_t)) != hipSuccess) {
+                                (void)hipGetLastError();
+                                c->d_zs_atab = nullptr;   // no room: one-level build
+                            } else {
+                                c->zs_atab_cap = need_e;
+                            }
+                        }
+                        if (c->d_zs_atab) {
+                            const long long key[6] = {base >> (plo + 2), plo, (long long)zs.log2spp, zs.seed,
+                                                      (long long)c->film.width * 65536 + c->film.height, c->zs_pdims};
+                            bool same = true;
+                            for (int k = 0; k < 6; ++k) same = same && key[k] == c->zs_akey[k];
+                            if (!same) {
+                                hipLaunchKernelGGL(avr::k_zsobol_pass_table,
+                                                   dim3(blocks_for((long long)c->film.width * c->film.height * c->zs_pdims,
+                                                                   256, 256 * 64)),
+                                                   dim3(256), 0, c->stream, zs, c->film.width, c->film.height, c->zs_pdims,
+                                                   plo + 2, (base >> (plo + 2)) << (plo + 2), c->d_zs_atab,
+                                                   (const uint64_t *)nullptr);
+                                HIP_TRY(hipGetLastError());
+                                for (int k = 0; k < 6; ++k) c->zs_akey[k] = key[k];
+                            }
+                            atab = c->d_zs_atab;
+                        }
+                    }
                     if (c->d_zs_ptab) {
                         hipLaunchKernelGGL(avr::k_zsobol_pass_table,
                                            dim3(blocks_for((long long)c->film.width * c->film.height * c->zs_pdims, 256,
                                                            256 * 64)),
                                            dim3(256), 0, c->stream, zs, c->film.width, c->film.height, c->zs_pdims, plo,
-                                           base, c->d_zs_ptab);
+                                           base, c->d_zs_ptab, atab);
                         HIP_TRY(hipGetLastError());
                         p.zs.ptab = c->d_zs_ptab;
                         p.zs.pdims = c->zs_pdims;

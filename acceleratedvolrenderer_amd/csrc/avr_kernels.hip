@@ -3094,9 +3094,12 @@ __global__ void __launch_bounds__(256) k_zsobol_table(smp::ZSobolParams zp, int 
 // ZSobol pass table: zsobol_pass_entry for every pixel of the film and the first pdims
 // dimensions, for the pass whose sample indices agree with `base` above their low `plo` bits;
 // row Morton(pixel). The pixel digits come from the pixel table (zp.upper) where it covers
-// the dimension. zp.ptab must be null here. Built once per k_paths pass (a few hundred us).
+// the dimension. zp.ptab must be null here. Built once per k_paths pass (a few hundred us);
+// with `atab` (the same table built for plo + 2, plo + 2 <= log2spp) each entry is derived
+// from its level-A entry by zsobol_pass_entry_from (one MixBits instead of ~5).
 __global__ void __launch_bounds__(256) k_zsobol_pass_table(smp::ZSobolParams zp, int width, int height, int pdims,
-                                                           int plo, long long base, uint64_t *__restrict__ table) {
+                                                           int plo, long long base, uint64_t *__restrict__ table,
+                                                           const uint64_t *__restrict__ atab) {
     // 32-bit indices (the host checks width * height * pdims < 2^31): 64-bit divisions by a
     // run-time divisor are ~100 instructions each, more than the entry's own digits
     const uint32_t n = (uint32_t)width * (uint32_t)height * (uint32_t)pdims;
@@ -3106,9 +3109,16 @@ __global__ void __launch_bounds__(256) k_zsobol_pass_table(smp::ZSobolParams zp,
         const int d = (int)(k - pix * (uint32_t)pdims);
         const uint32_t py = pix / (uint32_t)width;
         const uint32_t pm = (uint32_t)smp::encode_morton2(pix - py * (uint32_t)width, py);
-        const uint32_t up = (zp.upper && d < zp.dmax) ? zp.upper[(size_t)pm * zp.dmax + d] : smp::zsobol_upper(pm, (uint32_t)d, zp);
         const uint64_t m = ((uint64_t)pm << zp.log2spp) | (uint64_t)base;
-        table[(size_t)pm * pdims + d] = wide ? smp::zsobol_pass_entry<uint64_t>(m, (uint32_t)d, zp, plo, up)
+        const size_t row = (size_t)pm * pdims + d;
+        if (atab) {
+            const uint64_t eA = atab[row];
+            table[row] = wide ? smp::zsobol_pass_entry_from<uint64_t>(m, (uint32_t)d, zp, plo, eA)
+                              : smp::zsobol_pass_entry_from<uint32_t>((uint32_t)m, (uint32_t)d, zp, plo, eA);
+            continue;
+        }
+        const uint32_t up = (zp.upper && d < zp.dmax) ? zp.upper[(size_t)pm * zp.dmax + d] : smp::zsobol_upper(pm, (uint32_t)d, zp);
+        table[row] = wide ? smp::zsobol_pass_entry<uint64_t>(m, (uint32_t)d, zp, plo, up)
                                              : smp::zsobol_pass_entry<uint32_t>((uint32_t)m, (uint32_t)d, zp, plo, up);
     }
 }

@@ -221,6 +221,34 @@ AVR_HD uint64_t zsobol_pass_entry(M morton, uint32_t dimension, const ZSobolPara
     return (fixed >> plo) | ((uint64_t)perm << 56);
 }
 
+// The entry for `plo` from the entry eA the same pixel, dimension and pass prefix have for
+// plo + 2 (plo + 2 <= log2spp): eA's fixed digits, its perm-fixed digit — whose value bits now
+// lie at or above plo, so it is fixed too — and the permutation of the digit under plo (one
+// MixBits instead of the log2(spp)/2 - plo/2 + 1 a fresh entry takes). A pass of 64 indices
+// shares eA with the three passes after it (bits >= plo + 2 agree), so eA is built once per
+// four passes.
+template <typename M>
+AVR_HD uint64_t zsobol_pass_entry_from(M morton, uint32_t dimension, const ZSobolParams &zp, int plo, uint64_t eA) {
+    const int pw = zp.log2spp & 1;
+    const int ploA = plo + 2;
+    constexpr int kBits = 8 * (int)sizeof(M);
+    uint64_t fixed = (eA & 0x00ffffffffffffffull) << ploA;
+    const uint32_t permA = (uint32_t)(eA >> 56);
+    const int iTopA = (ploA + pw - 1) >> 1;
+    if (permA != 0xFFu) {
+        const int sh = 2 * iTopA - pw;
+        fixed |= (uint64_t)zperm(permA, (uint32_t)(morton >> sh) & 3u) << sh;
+    }
+    uint32_t perm = 0xFFu;
+    const int iTop = iTopA - 1;   // (plo + pw - 1) >> 1
+    if (iTop >= pw) {
+        const int shift = 2 * iTop - pw;
+        const M higher = shift + 2 >= kBits ? M(0) : M(morton >> (shift + 2));
+        perm = mix_perm24<M>((M)(higher ^ (M)(0x55555555u * dimension)));
+    }
+    return (fixed >> plo) | ((uint64_t)perm << 56);
+}
+
 // GetSampleIndex of (morton, dimension) from the sample's pass entry e: the varying digits
 // computed, the perm-fixed digit from e's permutation, the rest from e; an odd log2(spp)'s
 // final base-2 digit as zsobol_lower. Bit-identical to zsobol_index without tables.

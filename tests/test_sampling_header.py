@@ -55,6 +55,20 @@ def hdr(tmp_path_factory):
         "      pass[i] = zsobol_index_pass<unsigned long long>(ms, d, zt, zsobol_pass_entry<unsigned long long>(mb, d, zp, plo, up)); }\n"
         "    else { full[i] = zsobol_index<unsigned>((unsigned)ms, d, zp);\n"
         "      pass[i] = zsobol_index_pass<unsigned>((unsigned)ms, d, zt, zsobol_pass_entry<unsigned>((unsigned)mb, d, zp, plo, up)); } } }\n"
+        "int zs_pass_from(int spp, int rx, int ry, int n, const int *q) {\n"
+        "  ZSobolParams zp = zsobol_params(spp, rx, ry, 0); int bad = 0;\n"
+        "  for (int i = 0; i < n; ++i) {\n"
+        "    const int *r = q + 6 * i; int base = r[4], S = r[5], plo = 0;\n"
+        "    while ((base >> plo) != ((base + S - 1) >> plo)) ++plo;\n"
+        "    if (plo + 2 > zp.log2spp) continue;\n"
+        "    unsigned pm = (unsigned)encode_morton2(r[0], r[1]); unsigned d = (unsigned)r[3];\n"
+        "    unsigned long long mb = ((unsigned long long)pm << zp.log2spp) | (unsigned)base;\n"
+        "    unsigned up = zsobol_upper(pm, d, zp);\n"
+        "    if (zsobol_wide(zp)) bad += zsobol_pass_entry_from<unsigned long long>(mb, d, zp, plo,\n"
+        "        zsobol_pass_entry<unsigned long long>(mb, d, zp, plo + 2, up)) != zsobol_pass_entry<unsigned long long>(mb, d, zp, plo, up);\n"
+        "    else bad += zsobol_pass_entry_from<unsigned>((unsigned)mb, d, zp, plo,\n"
+        "        zsobol_pass_entry<unsigned>((unsigned)mb, d, zp, plo + 2, up)) != zsobol_pass_entry<unsigned>((unsigned)mb, d, zp, plo, up); }\n"
+        "  return bad; }\n"
         "float sob(unsigned long long a, int dim, unsigned seed, int scr) {\n"
         "  unsigned v = sobol_bits64((unsigned)a, (unsigned)(a >> 32), dim);\n"
         "  return u32_to_unit(scr ? fast_owen(v, seed) : v); }\n"
@@ -131,3 +145,5 @@ def test_zsobol_pass_table(hdr, spp, rx, ry):
     hdr.zs_pass(spp, rx, ry, n, q.ctypes.data_as(ctypes.POINTER(ctypes.c_int)), full.ctypes.data_as(U),
                 pas.ctypes.data_as(U))
     assert np.array_equal(full, pas)
+    # the two-level build: the entry for plo from the one for plo + 2 (built once per 4 passes)
+    assert hdr.zs_pass_from(spp, rx, ry, n, q.ctypes.data_as(ctypes.POINTER(ctypes.c_int))) == 0
