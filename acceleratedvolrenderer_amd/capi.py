@@ -337,7 +337,7 @@ class Context:
         _check(self.lib.avr_set_sampler_table(self.h, int(dims)))
 
     def set_sampler_pass_table(self, dims):
-        """ZSobol per-pass table dimensions (avr_set_sampler_pass_table; 0 = off, default 64)."""
+        """ZSobol per-pass table dimensions (avr_set_sampler_pass_table; 0 = off, default 96)."""
         _check(self.lib.avr_set_sampler_pass_table(self.h, int(dims)))
 
     def set_pixel_order(self, order):

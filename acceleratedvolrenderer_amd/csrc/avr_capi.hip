@@ -159,7 +159,7 @@ struct avr_context {
     // for every k_paths pass: the digits its sample indices share; zs_pdims 0 = no table
     uint64_t *d_zs_ptab = nullptr;
     size_t zs_ptab_cap = 0;   // entries allocated
-    int zs_pdims = 64;
+    int zs_pdims = 96;
     // Level-A pass table (the same table for plo + 2, shared by four consecutive passes);
     // zs_akey names the build it holds (rebuilt when any field changes), zs_two_level 0 = off
     uint64_t *d_zs_atab = nullptr;
@@ -1510,6 +1510,15 @@ int avr_set_filter(avr_context *c, int type, const float radius[2], float sigma)
         }
     for (int y = 0; y < ny; ++y) pc1d_build(f + (size_t)y * nx, nx, -radius[0], radius[0], ccdf + (size_t)y * (nx + 1), cint + y);
     pc1d_build(cint, ny, -radius[1], radius[1], mcdf, mint);
+    // the search guides (camera stage): one row per conditional CDF, then the marginal's
+    t.resize((size_t)avr::smp::filter_blob_floats(nx, ny), 0.f);
+    f = t.data();
+    ccdf = f + nx * ny;
+    mcdf = ccdf + ny * (nx + 1) + ny;
+    uint8_t *guide = (uint8_t *)(t.data() + avr::smp::filter_table_floats(nx, ny));
+    for (int y = 0; y < ny; ++y)
+        avr::smp::filter_guide_build(ccdf + (size_t)y * (nx + 1), nx, guide + (size_t)y * (avr::smp::kFilterGuideK + 1));
+    avr::smp::filter_guide_build(mcdf, ny, guide + (size_t)ny * (avr::smp::kFilterGuideK + 1));
     if (c->d_filter) (void)hipFree(c->d_filter);
     c->d_filter = nullptr;
     HIP_TRY(dalloc(&c->d_filter, t.size()));
@@ -1522,7 +1531,8 @@ int avr_set_filter(avr_context *c, int type, const float radius[2], float sigma)
     c->ftab.ccdf = c->d_filter + nx * ny;
     c->ftab.cint = c->ftab.ccdf + ny * (nx + 1);
     c->ftab.mcdf = c->ftab.cint + ny;
-    c->ftab.mint = *mint;
+    c->ftab.mint = t[(size_t)avr::smp::filter_table_floats(nx, ny) - 1];
+    c->ftab.guide = (const uint8_t *)(c->d_filter + avr::smp::filter_table_floats(nx, ny));
     c->filter_type = 1;
     return AVR_OK;
 }

@@ -985,29 +985,34 @@ __device__ __forceinline__ const float *stage_majorant(const DevMedium &m, float
 }
 
 // GaussianFilter's FilterSampler tables (pbrt's default radius 1.5: 48 x 48 function + CDFs,
-// ~19 KB) staged in LDS when they fit, so the camera sample's two binary searches run on LDS;
-// the descriptor pointing at them is published in *s_ftab. Returns after a block barrier.
-constexpr int kFiltLds = 4864;
-__device__ __forceinline__ void stage_filter(const Params &P, float *s_filt, smp::FilterTables *s_ftab) {
+// ~19 KB, and their 6.3 KB of search guides) staged in LDS when they fit, so the camera
+// sample's two guided searches run on LDS. Returns (after a block barrier) whether they were
+// staged; filter_lds_tables then describes the copy. The descriptor is built in registers from
+// the kernel arguments, not read back from LDS: its pointers then stay LDS-typed (ds_read, not
+// flat loads) and the first table read does not wait for a descriptor read.
+constexpr int kFiltLds = 6400;
+__device__ __forceinline__ bool stage_filter(const Params &P, float *s_filt) {
+    bool staged = false;
     if (P.film.filter_type != 0) {
         const smp::FilterTables &g = P.film.gauss;
-        const int nf = smp::filter_table_floats(g.nx, g.ny);
-        if (nf <= kFiltLds) {
+        const int nf = smp::filter_blob_floats(g.nx, g.ny);
+        if (g.guide && nf <= kFiltLds) {
             const float *base = g.f;
             for (int i = threadIdx.x; i < nf; i += blockDim.x) s_filt[i] = base[i];
-        }
-        if (threadIdx.x == 0) {
-            smp::FilterTables t = g;
-            if (nf <= kFiltLds) {
-                t.f = s_filt;
-                t.ccdf = s_filt + (g.ccdf - g.f);
-                t.cint = s_filt + (g.cint - g.f);
-                t.mcdf = s_filt + (g.mcdf - g.f);
-            }
-            *s_ftab = t;
+            staged = true;
         }
     }
     __syncthreads();
+    return staged;
+}
+__device__ __forceinline__ smp::FilterTables filter_lds_tables(const smp::FilterTables &g, const float *s_filt) {
+    smp::FilterTables t = g;
+    t.f = s_filt;
+    t.ccdf = s_filt + g.nx * g.ny;
+    t.cint = t.ccdf + g.ny * (g.nx + 1);
+    t.mcdf = t.cint + g.ny;
+    t.guide = reinterpret_cast<const uint8_t *>(s_filt + smp::filter_table_floats(g.nx, g.ny));
+    return t;
 }
 
 // ZSobol draws shared by a QUAD of lanes holding samples 4m .. 4m+3 of one pixel (the camera
@@ -1204,7 +1209,6 @@ __device__ __forceinline__ float u32_to_unit_exp(uint32_t v) { return (float)(v 
 template <int kSmp, bool kFast>
 __global__ void __launch_bounds__(256, AVR_CAM_WAVES) k_paths_camera(Params P) {
     __shared__ float s_filt[kFiltLds];
-    __shared__ smp::FilterTables s_ftab;
     __shared__ double s_canon[canon::kCanonTabDoubles];
     if constexpr (AVR_CAM_CANON_LDS)   // (fast mode too: the pdfs stay canonical)
         for (int i = threadIdx.x; i < canon::kCanonTabDoubles; i += blockDim.x)
@@ -1212,7 +1216,7 @@ __global__ void __launch_bounds__(256, AVR_CAM_WAVES) k_paths_camera(Params P) {
     __shared__ uint64_t s_cdh[kCamDimHash];
     if constexpr (kSmp != 0)
         if (threadIdx.x < kCamDimHash) s_cdh[threadIdx.x] = smp::hash_2u32(threadIdx.x, (uint32_t)P.zs.seed);
-    stage_filter(P, s_filt, &s_ftab);   // (its barrier covers s_canon and s_cdh)
+    const bool ftab_lds = stage_filter(P, s_filt);   // (its barrier covers s_canon and s_cdh)
     const int npix = P.pass_pixels;
     const long long n = (long long)npix * P.pass_samples;
     // ZSobol quads (zsobol_draw_quad): lanes 4a .. 4a+3 take samples 4m .. 4m+3 of one pixel
@@ -1333,10 +1337,26 @@ __global__ void __launch_bounds__(256, AVR_CAM_WAVES) k_paths_camera(Params P) {
                 smp.get2d(P, &fu0, &fu1);
             }
 #endif
-            camera_filter(P, px, py, fu0, fu1, &pFilmX, &pFilmY, &fweight, &s_ftab);
+#if AVR_CAM_EXPERIMENT == 3   // measurement only: no filter-table sampling (breaks replay)
+            pFilmX = (float)px + fu0;
+            pFilmY = (float)py + fu1;
+            fweight = 1.f;
+#else
+            if (ftab_lds) {
+                const smp::FilterTables ft = filter_lds_tables(P.film.gauss, s_filt);
+                camera_filter(P, px, py, fu0, fu1, &pFilmX, &pFilmY, &fweight, &ft);
+            } else {
+                camera_filter(P, px, py, fu0, fu1, &pFilmX, &pFilmY, &fweight, nullptr);
+            }
+#endif
             if (!paired) smp.z.dimension += 3;   // time (1D) and lens (2D): drawn by pbrt, unused by pinholes
         } else {
-            camera_sample(P, smp, px, py, &pFilmX, &pFilmY, &fweight, &s_ftab);
+            if (ftab_lds) {
+                const smp::FilterTables ft = filter_lds_tables(P.film.gauss, s_filt);
+                camera_sample(P, smp, px, py, &pFilmX, &pFilmY, &fweight, &ft);
+            } else {
+                camera_sample(P, smp, px, py, &pFilmX, &pFilmY, &fweight, nullptr);
+            }
         }
         const float *r = P.cam.raster;
         V3 pCam = {r[0] * pFilmX + r[1] * pFilmY + r[2] * 0.f + r[3], r[4] * pFilmX + r[5] * pFilmY + r[6] * 0.f + r[7],

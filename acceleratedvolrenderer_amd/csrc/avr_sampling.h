@@ -390,18 +390,25 @@ inline ZSobolParams zsobol_params(int spp, int width, int height, int seed) {
 // ---------------------------------------------------------------------------
 // FilterSampler tables of a GaussianFilter: nx = int(32 rx) by ny = int(32 ry) cells.
 // Layout (floats): f[ny*nx] | ccdf[ny*(nx+1)] | cint[ny] | mcdf[ny+1] | {mint}
+// Optional guide (null = none): for each of the ny conditional CDFs and then the marginal one,
+// kFilterGuideK + 1 bytes g[k] = FindInterval's answer at u = k / K (filter_guide_build), so a
+// search for u starts from [g[k], g[k + 1]] with k = floor(u K) instead of the whole CDF.
+constexpr int kFilterGuideK = 128;
 struct FilterTables {
     int nx, ny;
     float rx, ry;
     const float *f, *ccdf, *cint, *mcdf;
     float mint;
+    const uint8_t *guide;
 };
 AVR_HD int filter_table_floats(int nx, int ny) { return nx * ny + ny * (nx + 1) + ny + (ny + 1) + 1; }
+AVR_HD int filter_guide_bytes(int ny) { return (ny + 1) * (kFilterGuideK + 1); }
+// tables + guide, in floats (the guide's bytes follow the tables, padded to a float)
+AVR_HD int filter_blob_floats(int nx, int ny) { return filter_table_floats(nx, ny) + (filter_guide_bytes(ny) + 3) / 4; }
 
-// Sample one PiecewiseConstant1D given as (cdf[n+1], func[n], funcInt) over [mn, mx]
-AVR_HD float pc1d_sample(const float *cdf, const float *func, int n, float funcInt, float mn, float mx, float u,
-                         float *pdf, int *off) {
-    // FindInterval(n + 1, cdf[i] <= u), util/math.h:508-519
+// FindInterval(n + 1, cdf[i] <= u), util/math.h:508-519, clamped to [0, n - 1] as pc1d_sample
+// uses it: for a non-decreasing cdf, the number of i in [1, n - 1] with cdf[i] <= u
+AVR_HD int find_interval(const float *cdf, int n, float u) {
     int size = (n + 1) - 2, first = 1;
     while (size > 0) {
         const int half = size >> 1, middle = first + half;
@@ -409,8 +416,35 @@ AVR_HD float pc1d_sample(const float *cdf, const float *func, int n, float funcI
         first = pr ? middle + 1 : first;
         size = pr ? size - (half + 1) : half;
     }
-    int o = first - 1;
-    o = o < 0 ? 0 : (o > n - 1 ? n - 1 : o);
+    const int o = first - 1;
+    return o < 0 ? 0 : (o > n - 1 ? n - 1 : o);
+}
+// The same answer from a guide row g (K + 1 entries, g[k] = find_interval(cdf, n, k / K)): the
+// count is monotone in u, so for k / K <= u < (k + 1) / K (u K is exact: K is a power of two)
+// it lies in [g[k], g[k + 1]], and the indices there are searched for the last cdf[i] <= u.
+// n <= 256 (the guide's entries are bytes); u outside [0, 1) takes the full search.
+AVR_HD int find_interval_guided(const float *cdf, int n, const uint8_t *g, float u) {
+    if (!(u >= 0.f && u < 1.f)) return find_interval(cdf, n, u);
+    const int k = (int)(u * (float)kFilterGuideK);
+    int lo = g[k], hi = g[k + 1];
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        const bool pr = cdf[mid] <= u;
+        lo = pr ? mid : lo;
+        hi = pr ? hi : mid - 1;
+    }
+    return lo;
+}
+// the guide row of one CDF (host side of the build)
+inline void filter_guide_build(const float *cdf, int n, uint8_t *g) {
+    for (int k = 0; k <= kFilterGuideK; ++k) g[k] = (uint8_t)find_interval(cdf, n, (float)k / (float)kFilterGuideK);
+}
+
+// Sample one PiecewiseConstant1D given as (cdf[n+1], func[n], funcInt) over [mn, mx]
+// (guide: the CDF's guide row, or null)
+AVR_HD float pc1d_sample(const float *cdf, const float *func, int n, float funcInt, float mn, float mx, float u,
+                         float *pdf, int *off, const uint8_t *guide = nullptr) {
+    const int o = guide ? find_interval_guided(cdf, n, guide, u) : find_interval(cdf, n, u);
     *off = o;
     float du = u - cdf[o];
     if (cdf[o + 1] - cdf[o] > 0) du /= cdf[o + 1] - cdf[o];
@@ -423,9 +457,11 @@ AVR_HD float pc1d_sample(const float *cdf, const float *func, int n, float funcI
 AVR_HD void gaussian_filter_sample(const FilterTables &T, float u0, float u1, float *px, float *py, float *weight) {
     float pdf1, pdf0;
     int v, uo;
-    *py = pc1d_sample(T.mcdf, T.cint, T.ny, T.mint, -T.ry, T.ry, u1, &pdf1, &v);
+    const uint8_t *gm = T.guide ? T.guide + (std::size_t)T.ny * (kFilterGuideK + 1) : nullptr;
+    *py = pc1d_sample(T.mcdf, T.cint, T.ny, T.mint, -T.ry, T.ry, u1, &pdf1, &v, gm);
+    const uint8_t *gc = T.guide ? T.guide + (std::size_t)v * (kFilterGuideK + 1) : nullptr;
     *px = pc1d_sample(T.ccdf + (std::size_t)v * (T.nx + 1), T.f + (std::size_t)v * T.nx, T.nx, T.cint[v], -T.rx, T.rx, u0,
-                      &pdf0, &uo);
+                      &pdf0, &uo, gc);
     *weight = T.f[(std::size_t)v * T.nx + uo] / (pdf0 * pdf1);
 }
 

@@ -157,7 +157,7 @@ def parse(argv=None):
                         "outside the timed region); off: --refill-min / --dda-budget or the library defaults")
     p.add_argument("--zsobol-table", type=int, default=256,
                    help="ZSobol pixel-table dimensions (0 = every digit per sampler call)")
-    p.add_argument("--zsobol-pass-table", type=int, default=64,
+    p.add_argument("--zsobol-pass-table", type=int, default=96,
                    help="ZSobol per-pass table dimensions (0 = off): the digits a pass's sample indices share")
     p.add_argument("--sampler", default="zsobol", choices=["zsobol", "independent"],
                    help="pixel sampler (BASELINE.md S-cloud: zsobol, pbrt's default)")
@@ -488,7 +488,7 @@ def main():
     if args.dda_budget:
         integ.ctx.set_dda_budget(args.dda_budget)
     integ.ctx.set_sampler_table(args.zsobol_table)
-    if args.zsobol_pass_table != 64:   # (64: the library default; older libraries lack the call)
+    if args.zsobol_pass_table != 96:   # (96: the library default; older libraries lack the call)
         integ.ctx.set_sampler_pass_table(args.zsobol_pass_table)
     if args.ray_binning:
         integ.ctx.set_ray_binning(1)

@@ -335,7 +335,7 @@ int avr_set_sampler_table(avr_context *ctx, int dims);
  * above their lowest L differing bits, so every digit of GetSampleIndex above them — and the
  * permutation of the one just below, whose hash reads only those bits — is shared by the
  * pass's samples of one pixel. Each pass tabulates them for the first `dims` dimensions
- * (8 B per pixel-Morton row and dimension; default 64, 0 = off) and a sampler call then
+ * (8 B per pixel-Morton row and dimension; default 96, 0 = off) and a sampler call then
  * evaluates only the digits below (2 base-4 digits for 64-index passes instead of
  * log2(spp)/2). Results are identical either way. */
 int avr_set_sampler_pass_table(avr_context *ctx, int dims);

@@ -69,6 +69,10 @@ def hdr(tmp_path_factory):
         "    else bad += zsobol_pass_entry_from<unsigned>((unsigned)mb, d, zp, plo,\n"
         "        zsobol_pass_entry<unsigned>((unsigned)mb, d, zp, plo + 2, up)) != zsobol_pass_entry<unsigned>((unsigned)mb, d, zp, plo, up); }\n"
         "  return bad; }\n"
+        "int fi_check(const float *cdf, int n, int nu, const float *u) {\n"
+        "  unsigned char g[kFilterGuideK + 1]; filter_guide_build(cdf, n, g); int bad = 0;\n"
+        "  for (int i = 0; i < nu; ++i) bad += find_interval_guided(cdf, n, g, u[i]) != find_interval(cdf, n, u[i]);\n"
+        "  return bad; }\n"
         "float sob(unsigned long long a, int dim, unsigned seed, int scr) {\n"
         "  unsigned v = sobol_bits64((unsigned)a, (unsigned)(a >> 32), dim);\n"
         "  return u32_to_unit(scr ? fast_owen(v, seed) : v); }\n"
@@ -147,3 +151,43 @@ def test_zsobol_pass_table(hdr, spp, rx, ry):
     assert np.array_equal(full, pas)
     # the two-level build: the entry for plo from the one for plo + 2 (built once per 4 passes)
     assert hdr.zs_pass_from(spp, rx, ry, n, q.ctypes.data_as(ctypes.POINTER(ctypes.c_int))) == 0
+
+
+def _pc1d_cdf(f, lo, hi):
+    """pc1d_build in float32, in the host build's operation order"""
+    n = len(f)
+    cdf = np.zeros(n + 1, np.float32)
+    w = np.float32(hi) - np.float32(lo)
+    for i in range(1, n + 1):
+        cdf[i] = np.float32(cdf[i - 1] + np.float32(np.float32(abs(f[i - 1])) * w) / np.float32(n))
+    tot = cdf[n]
+    if tot == 0:
+        return np.array([np.float32(i) / np.float32(n) for i in range(n + 1)], np.float32)
+    return (cdf / tot).astype(np.float32)
+
+
+def test_filter_guided_find_interval_identical(hdr):
+    """The camera stage's guided FindInterval (a 128-bucket guide per CDF) returns the binary
+    search's interval for every u: Gaussian-filter rows, random CDFs with empty cells and ties,
+    an all-zero function (cdf = i / n), n = 1 .. 128; u at every CDF value and its neighbours,
+    at every bucket edge k / 128 and its neighbours, and at random points (plus u = 1 and
+    negative u, which take the full search)."""
+    rng = np.random.default_rng(5)
+    F = ctypes.POINTER(ctypes.c_float)
+    x = (np.arange(48, dtype=np.float32) + np.float32(0.5)) / np.float32(48)
+    g = np.maximum(0, np.exp(-((-1.5 + 3 * x) ** 2) / 0.5) - np.exp(-4.5)).astype(np.float32)
+    cases = [g, g * np.float32(1e-3), np.outer(g, g)[7]]
+    for n in (1, 2, 3, 7, 48, 64, 127, 128):
+        f = rng.random(n).astype(np.float32)
+        f[rng.random(n) < 0.3] = 0
+        cases.append(f)
+        cases.append(np.zeros(n, np.float32))
+        cases.append(np.round(rng.random(n) * 3).astype(np.float32))   # ties
+    edges = np.arange(129, dtype=np.float32) / np.float32(128)
+    for f in cases:
+        cdf = _pc1d_cdf(f, -1.5, 1.5)
+        pts = np.concatenate([cdf, edges]).astype(np.float32)
+        u = np.concatenate([pts, np.nextafter(pts, np.float32(2)), np.nextafter(pts, np.float32(-1)),
+                            rng.random(4000).astype(np.float32), np.array([0, np.nextafter(np.float32(1), np.float32(0)), 1, -0.25], np.float32)])
+        u = np.ascontiguousarray(u.astype(np.float32))
+        assert hdr.fi_check(cdf.ctypes.data_as(F), len(f), len(u), u.ctypes.data_as(F)) == 0, len(f)
