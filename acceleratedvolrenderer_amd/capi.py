@@ -219,14 +219,20 @@ def load():
     if not os.path.exists(LIB_PATH):
         raise RuntimeError(f"{LIB_PATH} not built: run __graft_entry__.build() (hipcc --offload-arch=gfx950)")
     lib = ctypes.CDLL(LIB_PATH)
+    # a variant library named by AVR_LIB (A/B runs against older builds) may lack the newest
+    # entry points (calling one then raises AttributeError); the in-tree library must export
+    # every one, so a stale build fails here, at load, naming what is missing
+    variant = os.path.abspath(LIB_PATH) != os.path.join(_HERE, "libavr_hip.so")
+    missing = []
     for name, (res, args) in SIGNATURES.items():
-        # an older library (AVR_LIB A/B runs) may lack the newest entry points: calling one
-        # then raises AttributeError; tests/test_capi_abi.py checks the in-tree library exports all
         fn = getattr(lib, name, None)
         if fn is None:
+            missing.append(name)
             continue
         fn.restype = res
         fn.argtypes = args
+    if missing and not variant:
+        raise RuntimeError(f"{LIB_PATH} is stale: it lacks {', '.join(missing)} — rebuild it (__graft_entry__.build())")
     _lib = lib
     return lib
 

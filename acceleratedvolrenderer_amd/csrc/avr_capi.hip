@@ -1102,10 +1102,13 @@ int avr_set_majorant_res(avr_context *c, const int res[3]) {
 // HIP events on the context stream; *bestk = the fastest, ms[k] the times when non-null. The
 // film sums are saved before and restored after (also when a probe fails; the first error is
 // kept); restore() then re-applies the chosen (or, after a failure, the original) setting.
+// prefer >= 0: that candidate (the default schedule) is kept unless the fastest probe beats it
+// by more than kProbeNoise — the probes' run-to-run spread — so the choice is reproducible.
+constexpr float kProbeNoise = 0.02f;
 extern "C++" {
 template <typename Setup, typename Restore>
 static int probe_loop(avr_context *c, int n, Setup setup, Restore restore, int spp_begin, int spp_end, int seed,
-                      int max_depth, int *bestk, float *ms) {
+                      int max_depth, int *bestk, float *ms, int prefer = -1) {
     HIP_TRY(hipSetDevice(c->device));
     const size_t np = (size_t)c->film.width * c->film.height;
     const size_t nd = (4 + 2 * (size_t)std::max(0, c->film.nbuckets)) * np;
@@ -1115,7 +1118,7 @@ static int probe_loop(avr_context *c, int n, Setup setup, Restore restore, int s
     const bool haveSaved = rc == AVR_OK;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (!rc && (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess)) rc = fail(AVR_ERR_HIP, "event");
-    float best = -1.f;
+    float best = -1.f, tPrefer = -1.f;
     *bestk = 0;
     for (int k = -1; k < n && !rc; ++k) {
         if ((rc = setup(k < 0 ? 0 : k))) break;
@@ -1129,8 +1132,10 @@ static int probe_loop(avr_context *c, int n, Setup setup, Restore restore, int s
         (void)hipEventElapsedTime(&t, e0, e1);
         if (k < 0) continue;
         if (ms) ms[k] = t;
+        if (k == prefer) tPrefer = t;
         if (best < 0 || t < best) { best = t; *bestk = k; }
     }
+    if (!rc && prefer >= 0 && tPrefer >= 0 && tPrefer <= best * (1 + kProbeNoise)) *bestk = prefer;
     const std::string err = g_err;
     const int rcProbe = rc;
     int rcRestore = restore(rc != 0, *bestk);
@@ -1191,6 +1196,12 @@ int avr_tune_walk(avr_context *c, const int *refill, int nr, const int *dda, int
     for (int k = 0; k < nd; ++k)
         if (dda[k] < 0) return fail(AVR_ERR_ARG, "DDA budget candidates must be >= 0 cells");
     const int r0 = c->refill_min, d0 = c->dda_budget;
+    // the default schedule (0, 0) when listed, else the current one, wins ties within the noise
+    int prefer = -1;
+    for (int k = 0; k < nr * nd && prefer < 0; ++k)
+        if (refill[k / nd] == 0 && dda[k % nd] == 0) prefer = k;
+    for (int k = 0; k < nr * nd && prefer < 0; ++k)
+        if (refill[k / nd] == r0 && dda[k % nd] == d0) prefer = k;
     int bestk = 0;
     const int rc = probe_loop(
         c, nr * nd,
@@ -1204,7 +1215,7 @@ int avr_tune_walk(avr_context *c, const int *refill, int nr, const int *dda, int
             c->dda_budget = failed ? d0 : dda[b % nd];
             return AVR_OK;
         },
-        spp_begin, spp_end, seed, max_depth, &bestk, ms);
+        spp_begin, spp_end, seed, max_depth, &bestk, ms, prefer);
     if (!rc) {
         chosen[0] = refill[bestk / nd];
         chosen[1] = dda[bestk % nd];
@@ -1571,7 +1582,10 @@ int avr_set_sampler_table(avr_context *c, int dims) {
 int avr_set_sampler_pass_table(avr_context *c, int dims) {
     AVR_QUIESCE(c);
     if (!c || dims < 0 || dims > 4096) return fail(AVR_ERR_ARG, "sampler pass table dimensions must be 0..4096");
-    c->zs_pdims = dims;
+    // rows of an even number of 8-B entries: the camera stage loads a draw pair's entries as one
+    // 16-B ulonglong2 at ptab + row * dims, aligned only for even dims (the extra dimension is
+    // never read — same results)
+    c->zs_pdims = (dims + 1) & ~1;
     return AVR_OK;
 }
 
@@ -1793,22 +1807,32 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
                     {avr::k_paths_camera<0, false>, avr::k_paths_camera<2, false>, avr::k_paths_camera<3, false>},
                     {avr::k_paths_camera<0, true>, avr::k_paths_camera<2, true>, avr::k_paths_camera<3, true>}};
                 EV_MARK(ec);
+                // rows = Morton(w-1, h-1) + 1 (up to ~4x the pixels of a non-square film): the
+                // table kernel indexes entries with 32 bits
+                const long long prow = (long long)avr::smp::encode_morton2((uint32_t)c->film.width - 1,
+                                                                           (uint32_t)c->film.height - 1) + 1;
                 if (c->sampler_kind == 1 && c->zs_pdims > 0 &&
-                    (long long)c->film.width * c->film.height * c->zs_pdims < (1ll << 31)) {
+                    (long long)c->film.width * c->film.height * c->zs_pdims < (1ll << 31) &&
+                    prow * c->zs_pdims < (1ll << 31)) {
                     // ZSobol pass table: the digits of GetSampleIndex that the pass's sample
                     // indices [base, base + S) share (those above their lowest differing bits),
                     // for the first zs_pdims dimensions; the camera stage and k_paths then
                     // evaluate only the digits below (two MixBits at 64 indices per pass)
                     int plo = 0;
                     while ((base >> plo) != ((base + S - 1) >> plo)) ++plo;
-                    const size_t rows = (size_t)avr::smp::encode_morton2((uint32_t)c->film.width - 1,
-                                                                        (uint32_t)c->film.height - 1) + 1;
-                    const size_t need_e = rows * (size_t)c->zs_pdims;
+                    const size_t need_e = (size_t)prow * (size_t)c->zs_pdims;
+                    // the same headroom policy as the fat / bricked density copies: allocate only
+                    // with >= 8 GiB of HBM to spare (else the pixel table serves every draw)
+                    auto fits = [](size_t bytes) {
+                        size_t freeB = 0, totalB = 0;
+                        return hipMemGetInfo(&freeB, &totalB) == hipSuccess && bytes + (8ull << 30) < freeB;
+                    };
                     if (need_e > c->zs_ptab_cap) {
                         if (c->d_zs_ptab) (void)hipFree(c->d_zs_ptab);
                         c->d_zs_ptab = nullptr;
                         c->zs_ptab_cap = 0;
-                        if (hipMalloc((void **)&c->d_zs_ptab, need_e * sizeof(uint64_t)) != hipSuccess) {
+                        if (!fits(need_e * sizeof(uint64_t)) ||
+                            hipMalloc((void **)&c->d_zs_ptab, need_e * sizeof(uint64_t)) != hipSuccess) {
                             (void)hipGetLastError();
                             c->d_zs_ptab = nullptr;   // no room: the pixel table / every digit per call
                         } else {
@@ -1824,7 +1848,8 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
                             c->d_zs_atab = nullptr;
                             c->zs_atab_cap = 0;
                             for (long long &k : c->zs_akey) k = -1;
-                            if (hipMalloc((void **)&c->d_zs_atab, need_e * sizeof(uint64_t)) != hipSuccess) {
+                            if (!fits(need_e * sizeof(uint64_t)) ||
+                                hipMalloc((void **)&c->d_zs_atab, need_e * sizeof(uint64_t)) != hipSuccess) {
                                 (void)hipGetLastError();
                                 c->d_zs_atab = nullptr;   // no room: one-level build
                             } else {

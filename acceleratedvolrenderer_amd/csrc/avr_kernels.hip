@@ -1906,7 +1906,7 @@ __global__ void __launch_bounds__(256) k_bin_scatter(const int *__restrict__ que
 #endif
 
 #ifndef AVR_PATHS_WAVES_GRAY
-#define AVR_PATHS_WAVES_GRAY 4   // 128 VGPRs (with the k_paths units' -disable-machine-licm: ~44 B/lane of scratch, reloaded outside the tracking loop)
+#define AVR_PATHS_WAVES_GRAY 4   // <= 128 VGPRs: with the k_paths units' -disable-machine-licm and the host-computed constants, 126 (ZSobol-64 GridMedium) / 127 (NanoVDB) and no scratch (tools/kres.py on the -Rpass-analysis log)
 #endif
 #ifndef AVR_COOP_SPEC
 #define AVR_COOP_SPEC 1

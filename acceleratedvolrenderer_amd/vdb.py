@@ -71,14 +71,16 @@ class NanoVDBGrid:
         Blocks equal to the background everywhere are dropped; with `tiles`, blocks of one
         other constant become 8^3 tiles. The map is `index_to_world`, or a uniform scale
         `voxel_size` plus translation `origin` (identity when neither is given)."""
-        v = np.asarray(values, np.float32)
-        if v.ndim != 3:
-            raise ValueError("values must be (nz, ny, nx)")
         if index_to_world is None:
             index_to_world = np.eye(4)
             if voxel_size is not None:
                 index_to_world[:3, :3] *= float(voxel_size)
             index_to_world[:3, 3] = np.asarray(origin, np.float64)
+        if hasattr(values, "data_ptr"):
+            return cls._from_dense_torch(values, index_min, index_to_world, background, tiles)
+        v = np.asarray(values, np.float32)
+        if v.ndim != 3:
+            raise ValueError("values must be (nz, ny, nx)")
         bg = np.float32(background)
         mn = np.asarray(index_min, np.int64)[::-1]   # (z, y, x)
         base = (mn // 8) * 8
@@ -104,6 +106,57 @@ class NanoVDBGrid:
         hi = active.max(axis=0)[::-1] + np.asarray(index_min)
         return cls(org[is_leaf], flat[is_leaf].reshape(-1, 8, 8, 8), bg, org[is_tile],
                    np.full(int(is_tile.sum()), 8, np.int32), mx[is_tile], np.concatenate([lo, hi]), index_to_world)
+
+    @classmethod
+    def _from_dense_torch(cls, t, index_min, index_to_world, background, tiles):
+        """from_dense for a torch tensor (e.g. a 1024^3 grid generated on the device): the same
+        block classification with torch ops where the tensor lives, so only the leaf values
+        (and the small origin / tile arrays) come back to the host. Scene construction, not
+        the render path."""
+        import torch
+        if t.dim() != 3:
+            raise ValueError("values must be (nz, ny, nx)")
+        t = t.to(torch.float32)
+        bg = float(np.float32(background))
+        mn = np.asarray(index_min, np.int64)[::-1]   # (z, y, x)
+        base = (mn // 8) * 8
+        pad_lo = mn - base
+        shape = np.asarray(t.shape, np.int64)
+        ext = pad_lo + shape
+        nb = (ext + 7) // 8
+        if np.any(pad_lo) or np.any(nb * 8 != ext):
+            full = torch.full(tuple(int(x) for x in nb * 8), bg, dtype=torch.float32, device=t.device)
+            full[pad_lo[0]:pad_lo[0] + shape[0], pad_lo[1]:pad_lo[1] + shape[1], pad_lo[2]:pad_lo[2] + shape[2]] = t
+        else:
+            full = t
+        nbz, nby, nbx = (int(x) for x in nb)
+        # blocks[bz, by, bx, lx, ly, lz] (a leaf stores x-major values), one row of 512 per block
+        flat = full.reshape(nbz, 8, nby, 8, nbx, 8).permute(0, 2, 4, 5, 3, 1).reshape(-1, 512)
+        mx, mnv = flat.amax(dim=1), flat.amin(dim=1)
+        const = mx == mnv
+        empty = const & (mx == bg)
+        is_tile = (const & ~empty) if tiles else torch.zeros_like(const)
+        is_leaf = ~empty & ~is_tile
+        active = full != bg
+        if not bool(active.any()):
+            raise ValueError("grid has no active voxels")
+        # active-voxel bbox per axis from the reductions over the other two axes
+        lo, hi = [], []
+        for dims, off, n in (((0, 1), pad_lo[2], shape[2]), ((0, 2), pad_lo[1], shape[1]), ((1, 2), pad_lo[0], shape[0])):
+            idx = torch.nonzero(active.any(dim=dims[1]).any(dim=dims[0])).flatten()
+            lo.append(int(idx.min()) - int(off))
+            hi.append(int(idx.max()) - int(off))
+        del active
+        ids = torch.arange(nbz * nby * nbx, device=t.device, dtype=torch.int64)
+        bx, by, bz = ids % nbx, (ids // nbx) % nby, ids // (nbx * nby)
+        org = torch.stack([base[2] + 8 * bx, base[1] + 8 * by, base[0] + 8 * bz], 1)
+        leaf_org = org[is_leaf].cpu().numpy()
+        leaf_val = flat[is_leaf].cpu().numpy().reshape(-1, 8, 8, 8)
+        tile_org = org[is_tile].cpu().numpy()
+        tile_val = mx[is_tile].cpu().numpy()
+        bbox = np.concatenate([np.asarray(lo) + np.asarray(index_min), np.asarray(hi) + np.asarray(index_min)])
+        return cls(leaf_org, leaf_val, np.float32(bg), tile_org, np.full(len(tile_org), 8, np.int32), tile_val, bbox,
+                   index_to_world)
 
     def values(self, ijk):
         """ReadAccessor::getValue for integer index coordinates ijk (n, 3)."""

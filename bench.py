@@ -63,33 +63,73 @@ RGB_CPU_MAX_RES = 512   # the rgb-explosion CPU baseline copies its 3 grids to t
 
 
 def lookup_bytes(medium, emissive=False, rgb_fields=2):
-    """Algorithmic bytes of ONE density lookup of k_paths by medium kind: GridMedium 8 f32 taps
-    (32 B); NanoVDB the apron slot (4 B) + the 32-B stencil entry (+ the same again for
-    the temperature grid of an emissive medium); RGBGridMedium 8 taps x 16 B {c0, c1, c2, scale}
-    per field (sigma_a, sigma_s, and Le when emissive)."""
+    """SURVEY §8(d) algorithmic bytes of ONE density lookup of k_paths by medium kind: a trilinear
+    lookup is 8 f32 taps = 32 B (GridMedium; NanoVDB likewise, plus the same again for the
+    temperature grid of an emissive medium); RGBGridMedium 8 taps x 16 B {c0, c1, c2, scale} per
+    field (sigma_a, sigma_s, and Le when emissive)."""
     if medium == "rgb":
         return 8 * 16 * (rgb_fields + (1 if emissive else 0))
     if medium == "nanovdb":
-        return 36 * (2 if emissive else 1)
+        return BYTES_PER_LOOKUP * (2 if emissive else 1)
     return BYTES_PER_LOOKUP
 
 
-def kpaths_bytes(agg, sampler, medium="grid", emissive=False, zsobol_table=True, pass_table=False):
-    """k_paths' algorithmic bytes over the stats `agg` (counters summed over its launches):
-    density lookups (delta + ratio tracking) + 16 B per sample record + the camera record of every
-    path + the ZSobol table entries of its phase draws (4-B pixel-table or 8-B pass-table
-    entries). Returns (total, parts)."""
+# NanoVDB's apron layout reads one 4-B slot index per grid lookup before the 32-B stencil entry:
+# a cost of this implementation's sparse layout, not a §8(d) algorithmic byte
+VDB_SLOT_BYTES = 4
+# §8(d): "4 B per majorant DDA step (counted as 0 HBM if LDS-staged; report it separately)"
+BYTES_PER_MAJORANT_STEP = 4
+
+
+def kpaths_bytes(agg, sampler, medium="grid", emissive=False, zsobol_table=True, pass_table=False,
+                 majorant_in_lds=True):
+    """k_paths' bytes over the stats `agg` (counters summed over its launches), split as SURVEY
+    §8(d) prices them. Algorithmic: 32 B per trilinear lookup (delta + ratio tracking), 4 B per
+    majorant DDA step where the majorant is NOT staged in LDS (NanoVDB's 64^3 grid, read through
+    L2; 0 for the LDS-staged 16^3 grids), and the per-work-item state k_paths moves through HBM —
+    its 16-B sample record and the camera record it reads per path (68 B ZSobol / 80 B
+    independent). Implementation (reported apart, not in `frac`): the ZSobol table entries of the
+    phase draws (they replace register arithmetic pbrt does in samplers.h:225-330) and NanoVDB's
+    4-B apron slot per lookup. Returns (algorithmic total, parts, implementation parts)."""
     # delta tracking evaluates emission (Le grid / temperature) at its lookups; shadow rays never
     lk = agg["medium_lookups"] * lookup_bytes(medium, emissive) + agg["shadow_lookups"] * lookup_bytes(medium, False)
     parts = {
         "density_lookups": lk,
+        "majorant_steps": 0 if majorant_in_lds else BYTES_PER_MAJORANT_STEP * agg["medium_dda_steps"],
         "sample_records_written": BYTES_PER_SAMPLE_RECORD * agg["medium_items_in"],
         "camera_records_read": BYTES_CAMERA_RECORD_READ[sampler] * agg["medium_items_in"],
+    }
+    impl = {
         "zsobol_table_reads": ((ZSOBOL_PASS_BYTES_PER_DRAW if pass_table else ZSOBOL_TABLE_BYTES_PER_DRAW) *
                                ZSOBOL_DRAWS_PER_PHASE * agg["medium_items_out"]
                                if sampler == "zsobol" and (zsobol_table or pass_table) else 0),
+        "vdb_slot_reads": (VDB_SLOT_BYTES * (agg["medium_lookups"] * (2 if emissive else 1) + agg["shadow_lookups"])
+                           if medium == "nanovdb" else 0),
     }
-    return sum(parts.values()), parts
+    return sum(parts.values()), parts, impl
+
+
+def roofline_block(agg, launches, sampler, medium, emissive, zsobol_table, pass_table):
+    """The §8(d) numbers of one k_paths configuration from its stats: per-launch algorithmic bytes
+    over the average HIP-event launch time, and the density-fetch share the north star prices
+    (`density_fetch`: lookup bytes only)."""
+    alg, parts, impl = kpaths_bytes(agg, sampler, medium, emissive, zsobol_table, pass_table,
+                                    majorant_in_lds=medium != "nanovdb")
+    ms = agg["ms_medium"] / launches
+    s = ms / 1e3
+    lk = parts["density_lookups"] / launches
+    return {
+        "achieved": round(alg / launches / s / 1e9, 2) if s > 0 else 0.0,
+        "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+        "frac": round(alg / launches / s / 1e9 / HBM_PEAK_GBPS, 5) if s > 0 else 0.0,
+        "bytes_per_launch": alg / launches,
+        "bytes_parts_per_launch": {k: v / launches for k, v in parts.items()},
+        "implementation_bytes_per_launch": {k: v / launches for k, v in impl.items()},
+        "avg_launch_ms": ms,
+        "density_fetch": {"bytes_per_launch": lk, "GBps": round(lk / s / 1e9, 2) if s > 0 else 0.0,
+                          "frac": round(lk / s / 1e9 / HBM_PEAK_GBPS, 5) if s > 0 else 0.0,
+                          "basis": "32 B per trilinear lookup (SURVEY §8d) x lookups per launch / avg launch time"},
+    }
 
 
 def camera_bytes(samples, sampler, zsobol_table=True, pass_dims=0, pixels=0, launches=1):
@@ -186,6 +226,10 @@ def parse(argv=None):
                         "use --res 256 --width 512 --height 512); explosion: C5's emissive NanoVDB stand-in with a "
                         "SpectralFilm (pixelsamples >= 4096); rgb-explosion: C5 as an emissive RGB-coefficient RGBGridMedium "
                         "(k_rgb_explosion, 3 x 16 GiB at 1024^3) with a SpectralFilm")
+    p.add_argument("--nanovdb-leg", type=int, default=1,
+                   help="after the headline (S-cloud GridMedium), time the same sample indices over the same cloud as a "
+                        "NanoVDBMedium (disney-cloud's medium type; tree built on the device), reported as `nanovdb`")
+    p.add_argument("--nanovdb-steps", type=int, default=4, help="timed steps of the NanoVDB leg (at most --steps)")
     p.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     return p.parse_args(argv)
 
@@ -378,6 +422,77 @@ def pmc_passes(args, pixelsamples, kernel_re=r"\bk_paths<|\dk_pathsI", timeout_s
         shutil.rmtree(tmp, ignore_errors=True)
 
 
+def timed_steps(integ, bases, S, maxdepth, world, buf):
+    """Render the sample ranges [b, b + S) for b in bases back to back on the context stream,
+    then export the film (and SUM-reduce it over the world), bracketed by barrier + sync;
+    returns the max-over-ranks wall time in s."""
+    import torch
+    import torch.distributed as dist
+    integ.ctx.sync()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for b in bases:
+        integ.ctx.render(b, b + S, 0, maxdepth)
+    integ.ctx.film_export_device(buf.data_ptr())
+    if world > 1:
+        dist.reduce(buf, dst=0, op=dist.ReduceOp.SUM)
+    integ.ctx.sync()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=buf.device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    return el
+
+
+def nanovdb_leg(args, density, dev, world, rank, S, warm_bases, timed_bases, spp_total, buf):
+    """The headline's sample indices over the same S-cloud as a NanoVDBMedium (disney-cloud's
+    medium type; media.h:602-685): the sparse tree is classified from the device grid
+    (NanoVDBGrid.from_dense on the tensor), uploaded, its 64^3 majorant built on the device
+    (pbrt's resolution: replay), library-default walk schedule, then `--nanovdb-steps` timed
+    steps like the headline's. Returns the `nanovdb` block of the line."""
+    from acceleratedvolrenderer_amd import VolPathIntegrator, scenes
+    tb = time.perf_counter()
+    grid = scenes.vdb_grid(density)
+    scene = scenes.s_cloud_vdb(grid, width=args.width, height=args.height, sampler=args.sampler, spp=spp_total,
+                               filter=args.filter)
+    integ = VolPathIntegrator(scene, maxdepth=scenes.CLOUD_MAXDEPTH, spp=S, seed=0, device=dev, mode="replay")
+    nleaves, ntiles = len(grid.leaf_origins), len(grid.tile_values)
+    del grid
+    try:
+        integ.ctx.set_sampler_table(args.zsobol_table)
+        if args.zsobol_pass_table != 96:
+            integ.ctx.set_sampler_pass_table(args.zsobol_pass_table)
+        for b in (list(warm_bases[rank]) or list(timed_bases[rank]))[:1]:   # one-off tables, untimed
+            integ.ctx.render(b, b + S, 0, scenes.CLOUD_MAXDEPTH)
+        integ.ctx.film_clear()
+        integ.ctx.reset_stats()
+        build_s = time.perf_counter() - tb
+        steps = max(1, min(args.steps, args.nanovdb_steps))
+        el = timed_steps(integ, timed_bases[rank][:steps], S, scenes.CLOUD_MAXDEPTH, world, buf)
+        agg = integ.ctx.stats()
+        kernel = integ.ctx.last_kernel()
+        launches = max(1, agg["medium_launches"])
+        rb = roofline_block(agg, launches, args.sampler, "nanovdb", False, args.zsobol_table > 0,
+                            args.zsobol_pass_table > 0)
+    finally:
+        integ.close()
+    npix = args.width * args.height
+    return {"workload": f"S-cloud-{args.res} as NanoVDBMedium ({nleaves} leaves, {ntiles} tiles; pbrt's 64^3 majorant, "
+                        f"read through L2), same camera / film / sampler / sample indices as the headline, replay mode",
+            "value": round(npix * S * steps * world / el / 1e6, 4), "unit": "Msamples/s", "steps": steps,
+            "ms_per_step": round(1e3 * el / steps, 3), "instantiation": kernel, "build_s": round(build_s, 2),
+            "parity": "tests/test_gpu_fullsize.py::test_fullsize_nanovdb_replay_at_the_driver_configuration",
+            "roofline": rb, "dda_steps_per_sample": round(agg["medium_dda_steps"] / (npix * S * steps), 2)}
+
+
 def main():
     args = parse()
     from acceleratedvolrenderer_amd import launch
@@ -511,6 +626,7 @@ def main():
         integ.ctx.set_refill_min(r_best)
         integ.ctx.set_dda_budget(d_best)
         walk_tuned = {"refill_min": r_best, "dda_budget": d_best, "refill_candidates": list(rc), "dda_candidates": list(dc),
+                      "tie_break": "the default (0, 0) is kept unless a candidate's probe is > 2 % faster (avr_tune_walk)",
                       "probe_ms": [[round(float(x), 3) for x in row] for row in wms]}
         args.refill_min, args.dda_budget = r_best, d_best   # the counter passes render the same schedule
         log(f"tuned walk: refill {r_best}, DDA {d_best} (0 = default)")
@@ -624,14 +740,19 @@ def main():
     emissive = "explosion" in args.scene
     samples_timed = npix * S * args.steps          # this rank's samples in the timed region
     samples_per_launch = samples_timed / launches
-    bytes_parts = None
+    bytes_parts = impl_parts = None
+    rb = None
     if persistent:
         # k_paths fuses delta tracking and ratio tracking: per-unit bytes of kpaths_bytes()
-        # (lookups by medium kind + the 16-B sample record + the camera record it reads per path
-        # + ZSobol table entries); path state never leaves VGPRs / LDS
+        # (lookups by medium kind + majorant steps read outside LDS + the 16-B sample record + the
+        # camera record it reads per path; ZSobol table entries and NanoVDB slots apart as
+        # implementation bytes); path state never leaves VGPRs / LDS
         kname = "k_paths (persistent: delta + ratio tracking, density fetch)"
-        med_bytes, bytes_parts = kpaths_bytes(agg, args.sampler, medium_kind, emissive, args.zsobol_table > 0,
-                                              args.zsobol_pass_table > 0)
+        med_bytes, bytes_parts, impl_parts = kpaths_bytes(agg, args.sampler, medium_kind, emissive,
+                                                          args.zsobol_table > 0, args.zsobol_pass_table > 0,
+                                                          majorant_in_lds=medium_kind != "nanovdb")
+        rb = roofline_block(agg, launches, args.sampler, medium_kind, emissive, args.zsobol_table > 0,
+                            args.zsobol_pass_table > 0)
     else:
         kname = "k_medium (wavefront delta tracking + density fetch)"
         med_bytes = BYTES_PER_LOOKUP * agg["medium_lookups"] + BYTES_PER_ITEM * (agg["medium_items_in"] +
@@ -657,6 +778,13 @@ def main():
         else:
             host_density = density.cpu().numpy()
     integ.close()
+    vdb_line = None
+    if (args.nanovdb_leg and args.scene == "cloud" and vdb is None and args.kernel == "persistent"
+            and args.mode == "replay"):
+        torch.cuda.empty_cache()
+        log("nanovdb leg: tree from the device grid")
+        vdb_line = nanovdb_leg(args, density, dev, world, rank, S, warm_bases, timed_bases, spp_total, buf)
+        log(f"nanovdb leg: {vdb_line['value']} Msamples/s ({vdb_line['instantiation']})")
     del density
     rgb_grids = None
     torch.cuda.empty_cache()
@@ -690,6 +818,7 @@ def main():
         # HBM traffic and the VALU limiter from rocprofv3 counter passes of this same
         # configuration (child processes; the guide's gfx950 rule: FETCH_SIZE x2 + WRITE_SIZE)
         traffic, limiter, pmc_note, cache = None, None, "pmc off", None
+        traffic_raw = None
         want_pmc = args.pmc == "on" or (args.pmc == "auto" and world == 1)
         pmc_kernel = None
         if want_pmc:
@@ -711,6 +840,7 @@ def main():
                             f"{spp_total}, same instantiation)")
                 if "FETCH_SIZE" in ctr and "WRITE_SIZE" in ctr:
                     traffic = round((2 * ctr["FETCH_SIZE"] + ctr["WRITE_SIZE"]) * 1024 / 1e9, 4)
+                    traffic_raw = round((ctr["FETCH_SIZE"] + ctr["WRITE_SIZE"]) * 1024 / 1e9, 4)
                 lookups_pl = (agg["medium_lookups"] + (agg["shadow_lookups"] if persistent else 0)) / launches
                 cache = {
                     "fetch_bytes_per_lookup": (round(2 * ctr["FETCH_SIZE"] * 1024 / lookups_pl, 2)
@@ -789,8 +919,18 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBPS, 5),
                 "traffic": traffic,
                 "traffic_source": pmc_note,
+                # counter bytes over §8(d) bytes: > 1 is over-fetch (whole lines per 32-B gather,
+                # ZSobol tables, NanoVDB slots). FETCH_SIZE is doubled per MI355X_MICROARCH.md's
+                # gfx950 rule, calibrated there on 16-B/lane streaming reads; for 32-B random
+                # gathers the factor is uncalibrated, so traffic_fetch_raw keeps the undoubled reads
+                "traffic_over_algorithmic": (round(traffic * 1e9 / (med_bytes / launches), 3)
+                                             if traffic and med_bytes else None),
+                "traffic_fetch_raw": traffic_raw,
                 "bytes_per_launch": med_bytes / launches,
                 "bytes_parts_per_launch": ({k: v / launches for k, v in bytes_parts.items()} if bytes_parts else None),
+                "implementation_bytes_per_launch": ({k: v / launches for k, v in impl_parts.items()}
+                                                    if impl_parts else None),
+                "density_fetch": rb["density_fetch"] if rb else None,
                 "samples_per_launch": samples_per_launch,
                 "avg_launch_ms": avg_launch_ms,
                 "launches": launches,
@@ -806,6 +946,7 @@ def main():
                 "cache": cache,
             },
             "fast_mode": fast_line,
+            "nanovdb": vdb_line,
             "grid_layout": grid_layout,
             "majorant_occupancy": bool(args.occupancy) if vdb is not None else None,
             "simd_utilisation": (agg["active_lane_iterations"] / (64.0 * agg["loop_iterations"])

@@ -270,7 +270,10 @@ int avr_tune_majorant(avr_context *ctx, const int *candidates, int n, int spp_be
  * per-medium defaults): render the probe sample range once per (refill lanes, DDA cells)
  * candidate pair, refill[i] x dda[j] (0 = the library default for either), timed with HIP
  * events on the context stream, and keep the fastest (chosen[2] = {refill, dda}; the nr*nd
- * probe times in ms[i * nd + j] when non-null). Film sums restored and work counters reset
+ * probe times in ms[i * nd + j] when non-null) — except that the default pair (0, 0), when
+ * listed (else the current schedule, when listed), is kept unless the fastest probe beats it
+ * by more than 2 % (the probes' run-to-run spread), so repeated runs choose the same
+ * schedule. Film sums restored and work counters reset
  * afterwards, as avr_tune_majorant. The schedule never changes results, only how a wave
  * batches its lanes' events and walks. */
 int avr_tune_walk(avr_context *ctx, const int *refill, int nr, const int *dda, int nd, int spp_begin, int spp_end,
@@ -337,7 +340,12 @@ int avr_set_sampler_table(avr_context *ctx, int dims);
  * pass's samples of one pixel. Each pass tabulates them for the first `dims` dimensions
  * (8 B per pixel-Morton row and dimension; default 96, 0 = off) and a sampler call then
  * evaluates only the digits below (2 base-4 digits for 64-index passes instead of
- * log2(spp)/2). Results are identical either way. */
+ * log2(spp)/2). Results are identical either way. Odd `dims` are rounded up to even (rows
+ * of 16-B aligned entry pairs). Memory: two tables of rows x dims x 8 B (the pass's and the
+ * level-A table it is derived from), rows = Morton(width - 1, height - 1) + 1 — 1.64 M rows at
+ * 720p, 1.26 GB per table at 96 dimensions, up to ~4x the pixel count for non-square films —
+ * allocated lazily by the first render, only with >= 8 GiB of HBM to spare (else the pixel
+ * table serves every draw), next to max_paths' records. */
 int avr_set_sampler_pass_table(avr_context *ctx, int dims);
 
 /* Render sample indices [spp_begin, spp_end) of every pixel (the avr_set_sampler sampler,

@@ -751,6 +751,10 @@ struct VdbTree {
     std::vector<float> leafStore;
     std::vector<int> tileBox;      // ox, oy, oz, size per tile
     std::vector<float> tileValue;
+    // 8^3 tiles by origin (a dense grid's constant blocks: ~10^5 of them at 1024^3); larger
+    // tiles (128^3 / 4096^3 internal-node tiles, few) are searched in tileBox order
+    std::unordered_map<uint64_t, float> tile8;
+    std::vector<int> bigTiles;     // indices into tileValue of tiles larger than 8^3
     float background = 0;
     int ibbox[6] = {0, 0, 0, -1, -1, -1};
     double matD[12] = {};          // index -> world (3x3 row-major, translation in column 3)
@@ -762,7 +766,10 @@ struct VdbTree {
     float GetValue(int x, int y, int z) const {
         auto it = leaves.find(Key(x, y, z));
         if (it != leaves.end()) return it->second[(x & 7) * 64 + (y & 7) * 8 + (z & 7)];
-        for (int t = (int)tileValue.size() - 1; t >= 0; --t) {   // tiles do not overlap in a valid tree
+        // tiles do not overlap in a valid tree: at most one contains (x, y, z)
+        auto t8 = tile8.find(Key(x, y, z));
+        if (t8 != tile8.end()) return t8->second;
+        for (int t : bigTiles) {
             const int *b = &tileBox[4 * t];
             if (x >= b[0] && x < b[0] + b[3] && y >= b[1] && y < b[1] + b[3] && z >= b[2] && z < b[2] + b[3])
                 return tileValue[t];
@@ -1963,6 +1970,12 @@ void *oracle_vdb_create(int nLeaves, const int *leafOrigin, const float *leafVal
         for (int a = 0; a < 3; ++a) g->tileBox.push_back(tileOrigin[3 * t + a]);
         g->tileBox.push_back(tileSize[t]);
         g->tileValue.push_back(tileValue[t]);
+        if (tileSize[t] == 8) {
+            const int *o = tileOrigin + 3 * t;
+            g->tile8[VdbTree::Key(o[0], o[1], o[2])] = tileValue[t];
+        } else {
+            g->bigTiles.push_back(t);
+        }
     }
     g->background = background;
     for (int a = 0; a < 6; ++a) g->ibbox[a] = ibbox[a];

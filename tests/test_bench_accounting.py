@@ -15,26 +15,46 @@ import bench  # noqa: E402
 def test_kpaths_bytes_follow_the_per_unit_figures():
     # BENCH_r03's counters (20 launches): VERDICT r3's recomputation, 8.90 GB per launch
     agg = {"medium_lookups": 1813622114, "shadow_lookups": 652134642, "medium_items_in": 1179648000,
-           "medium_items_out": 0}
-    tot, parts = bench.kpaths_bytes(agg, "zsobol", "grid", False, zsobol_table=True)
+           "medium_items_out": 0, "medium_dda_steps": 19127199408}
+    tot, parts, impl = bench.kpaths_bytes(agg, "zsobol", "grid", False, zsobol_table=True)
     assert parts["density_lookups"] == 32 * (1813622114 + 652134642)
     assert parts["sample_records_written"] == 16 * 1179648000
     assert parts["camera_records_read"] == 68 * 1179648000
+    assert parts["majorant_steps"] == 0          # the 16^3 majorant is staged in LDS
     assert tot / 20 / 1e9 == pytest.approx(8.90, abs=0.01)
-    # phase events add 5 ZSobol table entries of 4 B each
+    # phase events read 5 ZSobol table entries of 4 B each: implementation bytes, not in the total
     agg["medium_items_out"] = 1000
-    assert bench.kpaths_bytes(agg, "zsobol")[1]["zsobol_table_reads"] == 20 * 1000
-    assert bench.kpaths_bytes(agg, "zsobol", zsobol_table=False)[1]["zsobol_table_reads"] == 0
+    t2, _, impl = bench.kpaths_bytes(agg, "zsobol")
+    assert impl["zsobol_table_reads"] == 20 * 1000 and t2 == tot
+    assert bench.kpaths_bytes(agg, "zsobol", zsobol_table=False)[2]["zsobol_table_reads"] == 0
     assert bench.kpaths_bytes(agg, "independent")[1]["camera_records_read"] == 80 * 1179648000
+    # NanoVDB: 4 B per majorant step read through L2, the 4-B apron slot apart
+    _, pv, iv = bench.kpaths_bytes(agg, "zsobol", "nanovdb", majorant_in_lds=False)
+    assert pv["majorant_steps"] == 4 * 19127199408
+    assert iv["vdb_slot_reads"] == 4 * (1813622114 + 652134642)
+
+
+def test_roofline_block_reproduces_the_r04_recomputation():
+    """BENCH_r04's counters over 20 launches at the rocprof average 24.213 ms give
+    8.90 GB per launch = 0.046 of 8 TB/s, and lookups alone 3.945 GB = 0.020."""
+    agg = {"medium_lookups": 1813755508, "shadow_lookups": 652138892, "medium_items_in": 1179648000,
+           "medium_items_out": 1054911269, "medium_dda_steps": 19127199408, "ms_medium": 20 * 24.213}
+    rb = bench.roofline_block(agg, 20, "zsobol", "grid", False, True, True)
+    assert rb["bytes_per_launch"] / 1e9 == pytest.approx(8.90, abs=0.01)
+    assert rb["frac"] == pytest.approx(0.046, abs=0.0005)
+    assert rb["density_fetch"]["bytes_per_launch"] / 1e9 == pytest.approx(3.945, abs=0.001)
+    assert rb["density_fetch"]["frac"] == pytest.approx(0.020, abs=0.0005)
+    assert rb["implementation_bytes_per_launch"]["zsobol_table_reads"] / 1e9 == pytest.approx(2.11, abs=0.01)
 
 
 def test_lookup_bytes_by_medium():
     assert bench.lookup_bytes("grid") == 32
-    assert bench.lookup_bytes("nanovdb") == 36
-    assert bench.lookup_bytes("nanovdb", emissive=True) == 72     # + the temperature grid
+    assert bench.lookup_bytes("nanovdb") == 32
+    assert bench.lookup_bytes("nanovdb", emissive=True) == 64     # + the temperature grid
     assert bench.lookup_bytes("rgb") == 8 * 16 * 2
     assert bench.lookup_bytes("rgb", emissive=True) == 384       # sigma_a, sigma_s, Le
-    agg = {"medium_lookups": 10, "shadow_lookups": 5, "medium_items_in": 0, "medium_items_out": 0}
+    agg = {"medium_lookups": 10, "shadow_lookups": 5, "medium_items_in": 0, "medium_items_out": 0,
+           "medium_dda_steps": 0}
     # shadow rays evaluate no emission
     assert bench.kpaths_bytes(agg, "zsobol", "rgb", True)[1]["density_lookups"] == 10 * 384 + 5 * 256
 
@@ -48,8 +68,9 @@ def test_camera_bytes():
     assert bench.camera_bytes(4, "zsobol", pass_dims=64, pixels=2, launches=1) == 4 * 88 + 6 * 8 + 2 * 64 * 12
     assert bench.camera_bytes(8, "zsobol", zsobol_table=False, pass_dims=16, pixels=2, launches=2) == \
         8 * 88 + 12 * 8 + 2 * 2 * 16 * 8
-    agg = {"medium_lookups": 0, "shadow_lookups": 0, "medium_items_in": 0, "medium_items_out": 1000}
-    assert bench.kpaths_bytes(agg, "zsobol", pass_table=True)[1]["zsobol_table_reads"] == 40 * 1000
+    agg = {"medium_lookups": 0, "shadow_lookups": 0, "medium_items_in": 0, "medium_items_out": 1000,
+           "medium_dda_steps": 0}
+    assert bench.kpaths_bytes(agg, "zsobol", pass_table=True)[2]["zsobol_table_reads"] == 40 * 1000
 
 
 def test_kernel_names_match_across_demangled_mangled_and_the_abi_string():

@@ -96,6 +96,48 @@ def test_fullsize_replay_at_the_driver_headline_configuration(cloud):
         integ.close()
 
 
+def test_fullsize_nanovdb_replay_at_the_driver_configuration(cloud):
+    """disney-cloud's medium type at the bench's size: the S-cloud-1024 as a
+    NanoVDBMedium (the tree classified from the device grid, pbrt's 64^3 majorant) at 720p with
+    the driver's pixelsamples 16384, so k_paths runs its 64-bit-index ZSobol NanoVDB
+    instantiation (checked by name). The 64^3 majorant is bit-exact against the oracle's
+    (media.cpp:556-613), and a strided pixel subset of two 16-index passes (inside the N = 1
+    timed range and at the top of the N = 8 range) is bit-identical to the canonical oracle,
+    which walks its own hash-map tree (parity against NanoVDB itself unpinned)."""
+    from acceleratedvolrenderer_amd import VolPathIntegrator, scenes
+    from acceleratedvolrenderer_amd.launch import sample_plan
+    from oracle import binding
+    integ256, _ = cloud
+    P = sample_plan(1, 20, 5, 64)[0]
+    grid = scenes.vdb_grid(integ256.density_tensor)
+    scene = scenes.s_cloud_vdb(grid, sampler="zsobol", spp=P, filter="gaussian")
+    integ = VolPathIntegrator(scene, maxdepth=scenes.CLOUD_MAXDEPTH, spp=16, device=0)
+    try:
+        canon = binding.OracleRun(scene, max_depth=scenes.CLOUD_MAXDEPTH, seed=0, libm="canonical")
+        assert integ.ctx.majorant(64 ** 3).view(np.uint32).tolist() == canon.majorant.view(np.uint32).tolist()
+        f = scene.film
+        npix = f.width * f.height
+        pixels = np.arange(0, npix, 4099)
+        exact = total = 0
+        for base in (640, 8 * 20 * 64 - 16):
+            integ.ctx.film_clear()
+            integ.ctx.render(base, base + 16, 0, scenes.CLOUD_MAXDEPTH)
+            assert integ.ctx.last_kernel() == "k_paths<false, true, 3, 3, false, false>"
+            _, _, L, lam, _ = integ.ctx.last_pass_samples(npix, 16)
+            for pix in pixels:
+                for s in range(16):
+                    Lo, lo, _, _ = canon.pixel_sample(int(pix % f.width), int(pix // f.width), base + s)
+                    g = s * npix + int(pix)
+                    total += 1
+                    exact += int(np.array_equal(L[g].view(np.uint32), Lo.view(np.uint32)) and
+                                 np.array_equal(lam[g].view(np.uint32), lo.view(np.uint32)))
+        print(f"NanoVDB S-cloud-1024 replay ({len(grid.leaf_origins)} leaves, {len(grid.tile_values)} tiles, "
+              f"pixelsamples {P}): {exact}/{total} samples bit-identical")
+        assert exact == total
+    finally:
+        integ.close()
+
+
 def test_fullsize_multipass_and_determinism(cloud):
     from acceleratedvolrenderer_amd import scenes
     integ, _ = cloud

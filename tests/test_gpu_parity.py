@@ -645,7 +645,8 @@ def test_zsobol_pass_table_identical(pixelsamples):
     """The per-pass ZSobol table (avr_set_sampler_pass_table: the digits a k_paths pass's sample
     indices share) changes nothing: films and per-sample records equal the renders without it,
     for aligned and unaligned index ranges, several passes per render (different low-bit counts
-    plo), odd and even log2(pixelsamples) and paths running past the table's dimensions."""
+    plo), odd and even log2(pixelsamples) and paths running past the table's dimensions; odd
+    dimension counts (11) are rounded up to even rows (the 16-B entry-pair loads)."""
     from acceleratedvolrenderer_amd import scenes, ZSobolSampler, GaussianFilter
     from acceleratedvolrenderer_amd.scene import Scene, RGBFilm
     n, W, H = 12, 33, 21
@@ -655,7 +656,7 @@ def test_zsobol_pass_table_identical(pixelsamples):
                   sampler=ZSobolSampler(pixelsamples))
     for lo, hi, per_pass in ((64, 128, 64), (5, 71, 24), (1000, 1040, 7), (512, 544, 8), (0, 64, 16)):
         out = []
-        for dims in (0, 8, 64):
+        for dims in (0, 8, 11, 64):
             integ = _integrator(scene, maxdepth=30, spp=pixelsamples, kernel="persistent", max_paths=W * H * per_pass)
             integ.ctx.set_sampler_pass_table(dims)
             rgb, w = integ.render(lo, hi)

@@ -72,6 +72,29 @@ def test_from_dense_values_tiles_and_roundtrip(tmp_path):
     assert h.index_bbox.tolist() == g.index_bbox.tolist()
 
 
+@pytest.mark.parametrize("case", ["offset", "aligned", "background", "notiles"])
+def test_from_dense_torch_equals_numpy(case):
+    """The torch block classification (used for device-generated 1024^3 grids: bench.py's
+    NanoVDB leg, the full-size NanoVDB replay test) builds exactly the tree of the numpy one."""
+    torch = pytest.importorskip("torch")
+    d = _dense(3, (24, 16, 21))
+    d[8:16, 0:8, 0:8] = 0.5       # constant blocks -> tiles (where block-aligned)
+    d[16:24, 8:16, 8:16] = 0.0
+    kw = {"offset": dict(index_min=(-3, 2, 5)), "aligned": dict(index_min=(8, -16, 0)),
+          "background": dict(index_min=(1, 1, 1), background=0.5), "notiles": dict(tiles=False)}[case]
+    a = NanoVDBGrid.from_dense(d, **kw)
+    b = NanoVDBGrid.from_dense(torch.from_numpy(d), **kw)
+    ka = np.lexsort(a.leaf_origins.T[::-1])
+    kb = np.lexsort(b.leaf_origins.T[::-1])
+    assert np.array_equal(a.leaf_origins[ka], b.leaf_origins[kb])
+    assert np.array_equal(a.leaf_values[ka].view(np.uint32), b.leaf_values[kb].view(np.uint32))
+    ta, tb = np.lexsort(a.tile_origins.T[::-1]), np.lexsort(b.tile_origins.T[::-1])
+    assert np.array_equal(a.tile_origins[ta], b.tile_origins[tb])
+    assert np.array_equal(a.tile_values[ta], b.tile_values[tb]) and np.array_equal(a.tile_sizes, b.tile_sizes)
+    assert a.index_bbox.tolist() == b.index_bbox.tolist() and a.background == b.background
+    assert np.array_equal(a.index_to_world, b.index_to_world)
+
+
 def test_world_bbox_python_equals_oracle():
     g = NanoVDBGrid.from_dense(_dense(), index_min=(1, -4, 0), index_to_world=_rotated_map(9))
     t = NanoVDBGrid.from_dense(_dense(3, (5, 5, 5)) * 3000, index_min=(20, 0, 0), index_to_world=_rotated_map(9))
