@@ -281,6 +281,8 @@ struct Params {
     int refill_min;                   // k_paths: refill a wave once this many lanes are idle
     int dda_budget;                   // k_paths: majorant cells a lane may cross per tracking
                                       //   iteration before yielding (bounds DDA divergence)
+    int walk_exit;                    // k_paths: end a DDA walk early once fewer lanes than this
+                                      //   are still walking (they resume next round; <= 1: never)
     int rec_mode;                     // k_film: 1 = read k_paths' records (ps.rec), 0 = wavefront SoA
     const int *sh_perm;               // k_shadow: processing order of the shadow queue (ray binning), or null
     int fast;                         // render mode: 0 replay (canonical math), 1 fast (hardware math)
@@ -2572,7 +2574,10 @@ __global__ void __launch_bounds__(256, kGray ? (kMed == 1 ? 3 : AVR_PATHS_WAVES_
                         needNext = true;
                     }
                 }
-                if (__ballot(walk == 0) == 0) break;
+                // the walk ends when no lane walks, or when only a few long walkers are left: they
+                // resume in the next round, stepping alongside the lanes whose walks start there
+                const uint64_t walking = __ballot(walk == 0);
+                if (walking == 0 || __popcll(walking) < P.walk_exit) break;
             }
             AVR_SEC(4)
             const bool segEnd = walk == 2, pend = walk == 1;
