@@ -15,4 +15,4 @@ timeout -k 10 600 python bench.py --steps 20 --warmup 5 > $O/bench_line.json 2> 
 cut -c1-400 $O/bench_line.json
 timeout -k 10 300 python tools/walk_sweep.py --medium grid --ddas 0,16,32 --exits 0,4,8,12,16,24 --steps 4 --rounds 2 > $O/sweep_grid.json 2> $O/sweep_grid.err || { tail -5 $O/sweep_grid.err; exit 4; }
 timeout -k 10 400 python tools/walk_sweep.py --medium nanovdb --ddas 0,48 --exits 0,4,8,12,16 --steps 4 --rounds 2 > $O/sweep_vdb.json 2> $O/sweep_vdb.err || { tail -5 $O/sweep_vdb.err; exit 5; }
-python tools/summ.py $O/sweep_grid.json 2>/dev/null || cat $O/sweep_grid.json | cut -c1-2000
+cut -c1-1500 $O/sweep_grid.json; cut -c1-800 $O/sweep_vdb.json
