@@ -104,8 +104,8 @@ def s_mesh_interface(n=32, width=64, height=64, variant="scatter", density=None,
 
 def vdb_grid(density, index_to_world=None, index_min=(0, 0, 0), background=0.0):
     """Sparse NanoVDB-style copy of a dense (nz, ny, nx) grid; default map: index i at world
-    i / n per axis."""
-    d = np.asarray(density, np.float32)
+    i / n per axis. A torch tensor (e.g. a device-generated grid) is classified where it lives."""
+    d = density if hasattr(density, "data_ptr") else np.asarray(density, np.float32)
     if index_to_world is None:
         index_to_world = np.eye(4)
         index_to_world[0, 0], index_to_world[1, 1], index_to_world[2, 2] = (1.0 / d.shape[2], 1.0 / d.shape[1],
