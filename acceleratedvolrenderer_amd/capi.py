@@ -106,7 +106,6 @@ SIGNATURES = {
     "avr_set_refill_min": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "avr_light_sampler": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "avr_set_dda_budget": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
-    "avr_set_walk_exit": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "avr_set_grid_layout": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "avr_grid_layout_active": (ctypes.c_int, [ctypes.c_void_p]),
     "avr_medium_grid": (ctypes.c_int, [ctypes.c_void_p, c_float_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
@@ -331,10 +330,6 @@ class Context:
 
     def set_dda_budget(self, cells):
         _check(self.lib.avr_set_dda_budget(self.h, int(cells)))
-
-    def set_walk_exit(self, lanes):
-        """avr_set_walk_exit: end a DDA walk once fewer than `lanes` lanes still walk (-1 default)."""
-        _check(self.lib.avr_set_walk_exit(self.h, int(lanes)))
 
     def set_light_sampler(self, kind):
         """0: "bvh" / "uniform" (identical for infinite lights); 1: "power" (avr_light_sampler)."""

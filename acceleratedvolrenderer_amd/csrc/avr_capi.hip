@@ -168,7 +168,6 @@ struct avr_context {
     int zs_two_level = AVR_ZS_TWO_LEVEL;
     int refill_min = 0;       // 0: the default (32 lanes; 12 for a non-emissive NanoVDB walk, 16 for RGB grids)
     int dda_budget = 0;       // 0: by majorant resolution (12 cells up to 16^3, 32 for NanoVDB's 64^3)
-    int walk_exit = -1;       // -1: the default (see avr_render); 0 / 1: walks run to the budget
     int grid_layout = 1;
     bool gray = false;        // sigma_a and sigma_s constant over 360..830 nm      // 1: build the fat (footprint) copy when memory allows, 0: linear only
     float4 *d_fat = nullptr;
@@ -698,12 +697,6 @@ int avr_grid_layout_active(avr_context *c) { return !c ? 0 : (c->d_fat ? 1 : (c-
 int avr_set_dda_budget(avr_context *c, int cells) {
     if (!c || cells < 0) return fail(AVR_ERR_ARG, "DDA budget must be >= 1 cell (0: default)");
     c->dda_budget = cells;
-    return AVR_OK;
-}
-
-int avr_set_walk_exit(avr_context *c, int lanes) {
-    if (!c || lanes < -1 || lanes > 64) return fail(AVR_ERR_ARG, "walk exit must be -1 (default) or 0..64 lanes");
-    c->walk_exit = lanes;
     return AVR_OK;
 }
 
@@ -1800,7 +1793,6 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
                 const bool rgbWalk = c->med.type == 4;
                 p.refill_min = c->refill_min > 0 ? c->refill_min : (vdbWalk ? 12 : (rgbWalk ? 16 : 32));
                 p.dda_budget = c->dda_budget > 0 ? c->dda_budget : (vdbWalk ? 28 : (rgbWalk || mres > 16 ? 32 : 10));
-                p.walk_exit = c->walk_exit >= 0 ? c->walk_exit : 0;
             }
             p.heads = c->d_heads;
             HIP_TRY(hipMemsetAsync(c->d_heads, 0, 8 * sizeof(int), c->stream));
@@ -2366,8 +2358,9 @@ int avr_film_reduce_rccl(avr_context **ctxs, int n, int root) {
 
 #include "avr_graph_capi.hip"
 
-#ifdef AVR_PROFILE_SECTIONS
+#if defined(AVR_PROFILE_SECTIONS) || defined(AVR_PROBE_STATS)
 // Variant builds only (not part of include/avr.h): read and clear the k_paths section cycles
+// (or, with AVR_PROBE_STATS, the walk / gather probe counters)
 // of this context (stats[kNumStats .. kNumStats + 4], written by every k_paths unit).
 extern "C" int avr_debug_sections(avr_context *c, unsigned long long *out) {
     if (!c || !out) return fail(AVR_ERR_ARG, "null argument");

@@ -281,8 +281,6 @@ struct Params {
     int refill_min;                   // k_paths: refill a wave once this many lanes are idle
     int dda_budget;                   // k_paths: majorant cells a lane may cross per tracking
                                       //   iteration before yielding (bounds DDA divergence)
-    int walk_exit;                    // k_paths: end a DDA walk early once fewer lanes than this
-                                      //   are still walking (they resume next round; <= 1: never)
     int rec_mode;                     // k_film: 1 = read k_paths' records (ps.rec), 0 = wavefront SoA
     const int *sh_perm;               // k_shadow: processing order of the shadow queue (ray binning), or null
     int fast;                         // render mode: 0 replay (canonical math), 1 fast (hardware math)
@@ -2012,6 +2010,45 @@ struct SecProf {
 #define AVR_SEC_FLUSH
 #endif
 
+// Walk / gather probes (variant builds with -DAVR_PROBE_STATS only; tools/probe_stats.py): wave
+// counters of the DDA walk's lane occupancy and of how many distinct cache lines the lanes of one
+// collision round gather from (the coalescing an in-wave sort of the lookups could exploit, N1),
+// summed into stats[kNumStats + 0..7] like the section profile. Results unchanged.
+#ifdef AVR_PROBE_STATS
+struct ProbeStats {
+    // 0 walk trips, 1 walking lanes summed over trips, 2 collision rounds, 3 collision lanes,
+    // 4 distinct 128-B lines, 5 distinct 64-B lines (fat entries), 6 zero-majorant lane steps,
+    // 7 walks ended by the DDA budget with lanes still walking. Per wave in LDS: the first
+    // active lane adds (values are wave-uniform; inactive lanes of a divergent region skip it)
+    unsigned long long *c;
+    __device__ __forceinline__ void add(int k, unsigned long long v) {
+        const uint64_t am = __ballot(1);
+        if (lane_id() == __ffsll((long long)am) - 1) atomicAdd(c + k, v);
+    }
+    // distinct keys among the active lanes (wave-uniform result)
+    __device__ __forceinline__ static unsigned distinct(long long key) {
+        uint64_t rem = __ballot(1);
+        unsigned n = 0;
+        while (rem) {
+            const int l = __ffsll((long long)rem) - 1;
+            const long long k0 = __shfl(key, l);
+            rem &= ~__ballot(key == k0);
+            ++n;
+        }
+        return n;
+    }
+    __device__ __forceinline__ void flush(unsigned long long *stats) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (lane_id() < 8 && c[lane_id()]) atomicAdd(&stats[kNumStats + lane_id()], c[lane_id()]);
+    }
+};
+#define AVR_PROBE(k, v) probe.add(k, v);
+#else
+#define AVR_PROBE(k, v)
+#endif
+
 // NanoVDBMedium (kVdb, media.h:602-685): the same loop over the sparse tree. Its 64^3
 // majorant (1 MiB) does not fit LDS and is read through L2 (per-XCD 4 MiB); the density
 // fetch is NanoVDB's index-space trilinear sampler (avr_vdb.h) and emission comes from the
@@ -2164,6 +2201,12 @@ __global__ void __launch_bounds__(256, kGray ? (kMed == 1 ? 3 : AVR_PATHS_WAVES_
     };
 
     AVR_SEC_INIT
+#ifdef AVR_PROBE_STATS
+    __shared__ unsigned long long s_probe[4][8];
+    if (threadIdx.x < 32) (&s_probe[0][0])[threadIdx.x] = 0;
+    __syncthreads();
+    ProbeStats probe{s_probe[threadIdx.x >> 6]};
+#endif
     while (true) {
         AVR_SEC(0)
         opaque_consts();
@@ -2517,6 +2560,9 @@ __global__ void __launch_bounds__(256, kGray ? (kMed == 1 ? 3 : AVR_PATHS_WAVES_
                         // zero-majorant cell: T_maj *= FastExp(-0 * dt); for a gray medium that
                         // factor is exactly 1, so the multiply is skipped
                         const S sigma_maj = sig_t * mv;
+#ifdef AVR_PROBE_STATS
+                        { const uint64_t z = __ballot(sv0(sigma_maj) == 0); AVR_PROBE(6, __popcll(z)) }
+#endif
                         if (sv0(sigma_maj) == 0) {
                             if (!kGray) {
                                 float dt = s1 - s0;
@@ -2574,12 +2620,15 @@ __global__ void __launch_bounds__(256, kGray ? (kMed == 1 ? 3 : AVR_PATHS_WAVES_
                         needNext = true;
                     }
                 }
-                // the walk ends when no lane walks, or when only a few long walkers are left: they
-                // resume in the next round, stepping alongside the lanes whose walks start there
                 const uint64_t walking = __ballot(walk == 0);
-                if (walking == 0 || __popcll(walking) < P.walk_exit) break;
+                AVR_PROBE(0, 1)
+                AVR_PROBE(1, __popcll(walking))
+                if (walking == 0) break;
             }
             AVR_SEC(4)
+#ifdef AVR_PROBE_STATS
+            { const uint64_t still = __ballot(walk == 0); AVR_PROBE(7, still != 0) }
+#endif
             const bool segEnd = walk == 2, pend = walk == 1;
             if (segEnd) {
                 if (mode == M_MEDIUM) ev = EV_ESCAPE;
@@ -2624,6 +2673,19 @@ __global__ void __launch_bounds__(256, kGray ? (kMed == 1 ? 3 : AVR_PATHS_WAVES_
                     dens = vdb::sample_world(m.vdb, pm.x, pm.y, pm.z);
                 } else {
                     pm = m.unit_box ? V3{pm.x - m.bmin[0], pm.y - m.bmin[1], pm.z - m.bmin[2]} : box_offset(m.bmin, m.bmax, pm);
+#ifdef AVR_PROBE_STATS
+                    {
+                        // the fat entry this lookup reads (fat_issue's index), per 32-B entry
+                        const float psx = pm.x * m.nx - .5f, psy = pm.y * m.ny - .5f, psz = pm.z * m.nz - .5f;
+                        const long long ent = ((long long)((int)__builtin_floorf(psz) + 1) * (m.ny + 1) +
+                                               ((int)__builtin_floorf(psy) + 1)) * (m.nx + 1) +
+                                              ((int)__builtin_floorf(psx) + 1);
+                        AVR_PROBE(2, 1)
+                        AVR_PROBE(3, __popcll(__ballot(1)))
+                        AVR_PROBE(4, ProbeStats::distinct(ent >> 2))
+                        AVR_PROBE(5, ProbeStats::distinct(ent >> 1))
+                    }
+#endif
                     dens = grid_density(m, pm);
                 }
                 ms_a = sig_a * dens;
@@ -2697,6 +2759,9 @@ __global__ void __launch_bounds__(256, kGray ? (kMed == 1 ? 3 : AVR_PATHS_WAVES_
         }
     }
     AVR_SEC_FLUSH
+#ifdef AVR_PROBE_STATS
+    probe.flush(P.stats);
+#endif
 #if AVR_WAVE_COUNTERS
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();

@@ -192,8 +192,6 @@ def parse(argv=None):
     p.add_argument("--refill-min", type=int, default=0, help="k_paths refill threshold (0 = library default)")
     p.add_argument("--grid-layout", default="fat", choices=["fat", "linear", "brick"])
     p.add_argument("--dda-budget", type=int, default=0, help="k_paths DDA cells per iteration (0 = default)")
-    p.add_argument("--walk-exit", type=int, default=-1,
-                   help="k_paths: end a DDA walk once fewer lanes than this still walk (-1 = library default)")
     p.add_argument("--tune-walk", default="on", choices=["on", "off"],
                    help="choose k_paths' refill / DDA budget for this scene by on-device probe renders (avr_tune_walk, "
                         "outside the timed region); off: --refill-min / --dda-budget or the library defaults")
@@ -347,7 +345,7 @@ def pmc_child_argv(args, pixelsamples):
              "--steps", "2", "--warmup", "1", "--tune-walk", "off"]
     child += ["--pixelsamples", str(int(pixelsamples))]
     for k in ("res", "width", "height", "spp_per_step", "max_paths", "pixel_order", "kernel", "medium",
-              "refill_min", "grid_layout", "walk_exit",
+              "refill_min", "grid_layout",
               "dda_budget", "zsobol_table", "zsobol_pass_table", "sampler", "filter", "mode", "majorant_res", "ray_binning", "occupancy", "nvdb",
               "scene"):
         if getattr(args, k) is not None:
@@ -604,8 +602,6 @@ def main():
         integ.ctx.set_refill_min(args.refill_min)
     if args.dda_budget:
         integ.ctx.set_dda_budget(args.dda_budget)
-    if args.walk_exit >= 0:
-        integ.ctx.set_walk_exit(args.walk_exit)
     integ.ctx.set_sampler_table(args.zsobol_table)
     if args.zsobol_pass_table != 96:   # (96: the library default; older libraries lack the call)
         integ.ctx.set_sampler_pass_table(args.zsobol_pass_table)

@@ -111,12 +111,6 @@ int avr_set_refill_min(avr_context *ctx, int lanes);
  * RGBGridMedium, 28 for a non-emissive NanoVDB medium at 64^3 — measured optima); bounds the
  * divergence of the DDA walk. No effect on results. */
 int avr_set_dda_budget(avr_context *ctx, int cells);
-/* k_paths: end a wave's DDA walk early once fewer than `lanes` of its lanes are still walking
- * (the rest have a candidate collision or left the medium); the long walkers resume in the
- * next tracking round, stepping alongside the lanes whose walks start there, instead of
- * running the wave's walk on a few lanes. -1 = default, 0 or 1 = walk until no lane walks or
- * the DDA budget is spent. No effect on results. */
-int avr_set_walk_exit(avr_context *ctx, int lanes);
 /* Density layout for the NEXT avr_medium_grid* / avr_medium_nanovdb call: 1 (default) also
  * builds a "fat" footprint copy — GridMedium: entry (ix,iy,iz) holds the 8 trilinear taps as
  * 32 contiguous bytes, (n+1)^3 x 32 B; NanoVDBMedium: the same 32 B per base voxel of every

@@ -1,12 +1,12 @@
-"""k_paths schedule sweep in ONE process (GPU): the bench's S-cloud-1024 (GridMedium, or the
+"""k_paths schedule sweep (refill lanes x DDA budget) in ONE process (GPU): the bench's S-cloud-1024 (GridMedium, or the
 same cloud as a NanoVDBMedium with --medium nanovdb) at 720p, ZSobol + Gaussian, pixelsamples
-16384 (the driver's plan), built once; then for each (refill, dda budget, walk exit) candidate
+16384 (the driver's plan), built once; then for each (refill, dda budget) candidate
 `--steps` passes of 64 sample indices are timed (HIP events of k_paths, summed, and wall time of
 the steps), candidates interleaved over `--rounds` rounds so box drift averages out. Schedule
 parameters never change results (tests/test_gpu_edges.py).
 
-usage: python tools/walk_sweep.py [--medium grid|nanovdb] [--exits 0,4,8] [--ddas 0,16] [--refills 0]
-prints one JSON line: {"medium", "rows": [{"refill", "dda", "walk_exit", "kpaths_ms", "step_ms", "Msamples_s"}]}"""
+usage: python tools/walk_sweep.py [--medium grid|nanovdb] [--ddas 0,16] [--refills 0,24]
+prints one JSON line: {"medium", "rows": [{"refill", "dda", "kpaths_ms", "step_ms", "Msamples_s"}]}"""
 import argparse
 import json
 import os
@@ -27,7 +27,6 @@ def main():
     p.add_argument("--res", type=int, default=1024)
     p.add_argument("--refills", default="0")
     p.add_argument("--ddas", default="0")
-    p.add_argument("--exits", default="0")
     p.add_argument("--steps", type=int, default=4)
     p.add_argument("--rounds", type=int, default=2)
     p.add_argument("--pixelsamples", type=int, default=16384)
@@ -51,17 +50,16 @@ def main():
     S = 64
     integ = VolPathIntegrator(scene, maxdepth=scenes.CLOUD_MAXDEPTH, spp=S, seed=0, device=0)
     npix = scene.film.width * scene.film.height
-    cands = [(r, d, e) for r in ints(a.refills) for d in ints(a.ddas) for e in ints(a.exits)]
+    cands = [(r, d) for r in ints(a.refills) for d in ints(a.ddas)]
     acc = {c: [0.0, 0.0, 0] for c in cands}
     integ.ctx.render(0, S, 0, scenes.CLOUD_MAXDEPTH)   # one-off tables
     integ.ctx.sync()
     base = S
     for rnd in range(a.rounds):
         for c in (cands if rnd % 2 == 0 else cands[::-1]):
-            r, d, e = c
+            r, d = c
             integ.ctx.set_refill_min(r)
             integ.ctx.set_dda_budget(d)
-            integ.ctx.set_walk_exit(e)
             integ.ctx.render(base, base + S, 0, scenes.CLOUD_MAXDEPTH)   # warm this schedule
             integ.ctx.sync()
             integ.ctx.reset_stats()
@@ -74,10 +72,10 @@ def main():
             acc[c][0] += st["ms_medium"]
             acc[c][1] += el * 1e3
             acc[c][2] += a.steps
-            print(f"[sweep] round {rnd} refill {r} dda {d} exit {e}: k_paths {st['ms_medium'] / a.steps:.3f} ms, "
+            print(f"[sweep] round {rnd} refill {r} dda {d}: k_paths {st['ms_medium'] / a.steps:.3f} ms, "
                   f"step {el * 1e3 / a.steps:.3f} ms", file=sys.stderr, flush=True)
             base = (base + (a.steps + 2) * S) % (a.pixelsamples - (a.steps + 2) * S)
-    rows = [{"refill": c[0], "dda": c[1], "walk_exit": c[2], "kpaths_ms": round(v[0] / v[2], 4),
+    rows = [{"refill": c[0], "dda": c[1], "kpaths_ms": round(v[0] / v[2], 4),
              "step_ms": round(v[1] / v[2], 4), "Msamples_s": round(npix * S / (v[1] / v[2] / 1e3) / 1e6, 2)}
             for c, v in acc.items()]
     integ.close()
