@@ -2271,11 +2271,11 @@ int avr_last_pass_weights(avr_context *c, float *w, long long n_max) {
     if (c->filter_type == 0) {
         for (long long i = 0; i < n; ++i) w[i] = 1.f;   // BoxFilter::Sample weight
     } else if (n > 0 && c->last_persistent) {
-        std::vector<float4> cam1((size_t)n);
-        HIP_TRY(hipMemcpy(cam1.data(), c->ps.cam1, n * sizeof(float4), hipMemcpyDeviceToHost));
+        std::vector<float> camw((size_t)n);
+        HIP_TRY(hipMemcpy(camw.data(), c->ps.camw, n * sizeof(float), hipMemcpyDeviceToHost));
         const long long np = (long long)c->film.width * c->film.height;
         for (long long i = 0; i < n; ++i)
-            w[i] = cam1[c->h_pix_slot.empty() ? i : (i / np) * np + c->h_pix_slot[(size_t)(i % np)]].w;
+            w[i] = camw[c->h_pix_slot.empty() ? i : (i / np) * np + c->h_pix_slot[(size_t)(i % np)]];
     } else if (n > 0) {
         HIP_TRY(hipMemcpy(w, c->ps.weight, n * sizeof(float), hipMemcpyDeviceToHost));
     }

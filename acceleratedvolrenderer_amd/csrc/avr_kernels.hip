@@ -234,11 +234,11 @@ struct PathSoA {
     // k_paths' per-sample record: L (16 B at id), written once at path end
     float4 *rec;
     // k_paths' camera stage (k_paths_camera, one lane per sample of the pass), read by the
-    // refill and by k_film: cam0 {o, u}, cam1 {d, filter weight}, cam2 lambda, cam3 the first
-    // segment's RNG SetSequence arguments {seqA, seqB} (u64 each), cam4 the wavelength pdfs,
-    // cam5 the IndependentSampler's PCG32 {state, inc} after the camera draws (ZSobol: the
-    // first light-pick draw, 4 B per sample packed at the array's start), camw the filter
-    // weight alone (k_film's 4-B read)
+    // refill and by k_film: cam0 {o, u}, cam1 {d, ZSobol: the first light-pick draw /
+    // independent: the filter weight}, cam2 lambda, cam3 the first segment's RNG SetSequence
+    // arguments {seqA, seqB} (u64 each), cam4 the wavelength pdfs, cam5 the IndependentSampler's
+    // PCG32 {state, inc} after the camera draws (unused with ZSobol), camw the filter weight
+    // (k_film's 4-B read)
     float4 *cam0, *cam1, *cam2, *cam4;
     uint4 *cam3, *cam5;
     float *camw;
@@ -253,6 +253,9 @@ struct ShadowSoA {
 // [2] items out k_medium (survivors + shadow pushes), [3] lookups k_shadow, [4] items k_shadow,
 // [5] DDA steps k_medium, [6] DDA steps k_shadow; k_paths: [6] loop iterations (per wave),
 // [7] sum over iterations of active lanes (SIMD utilisation = [7] / (64 * [6]))
+#ifndef AVR_UL_IN_CAM1
+#define AVR_UL_IN_CAM1 1   // ZSobol's first light-pick draw in cam1.w (0: a separate 4-B array, round 4)
+#endif
 constexpr int kNumStats = 10;   // 0-6 wavefront/shared work counters, 8-9 k_paths wave loop
 
 struct Params {
@@ -1377,7 +1380,8 @@ __global__ void __launch_bounds__(256, AVR_CAM_WAVES) k_paths_camera(Params P) {
         // handler reads it instead of evaluating the sampler for its lanes)
         const float ulight = kSmp != 0 ? (paired ? pu[6] : get1(pe9)) : 0.f;
         P.ps.cam0[id] = make_float4(o.x, o.y, o.z, u);
-        P.ps.cam1[id] = make_float4(ray.d.x, ray.d.y, ray.d.z, fweight);
+        // ZSobol: the first light pick rides in cam1.w (k_paths' refill reads 4 x 16 B, no 4-B gather)
+        P.ps.cam1[id] = make_float4(ray.d.x, ray.d.y, ray.d.z, (kSmp != 0 && AVR_UL_IN_CAM1) ? ulight : fweight);
         P.ps.cam2[id] = to4(lam);
         P.ps.cam3[id] = make_uint4((uint32_t)seqA, (uint32_t)(seqA >> 32), (uint32_t)seqB, (uint32_t)(seqB >> 32));
         P.ps.cam4[id] = to4(pdf);
@@ -1385,7 +1389,7 @@ __global__ void __launch_bounds__(256, AVR_CAM_WAVES) k_paths_camera(Params P) {
         if constexpr (kSmp == 0)
             P.ps.cam5[id] = make_uint4((uint32_t)smp.rng.state, (uint32_t)(smp.rng.state >> 32), (uint32_t)smp.rng.inc,
                                        (uint32_t)(smp.rng.inc >> 32));
-        else   // ZSobol: the first light pick (k_paths' refill), packed 4 B per sample
+        else if constexpr (!AVR_UL_IN_CAM1)
             reinterpret_cast<float *>(P.ps.cam5)[id] = ulight;
     }
 }
@@ -2466,7 +2470,7 @@ __global__ void __launch_bounds__(256, kGray ? (kMed == 1 ? 3 : AVR_PATHS_WAVES_
                     [[maybe_unused]] float ul5 = 0.f;
                     [[maybe_unused]] uint4 c5{};
                     if constexpr (!kZSobol) c5 = P.ps.cam5[gn];
-                    else if constexpr (kUlAhead) ul5 = reinterpret_cast<const float *>(P.ps.cam5)[gn];
+                    else if constexpr (kUlAhead) ul5 = AVR_UL_IN_CAM1 ? c1.w : reinterpret_cast<const float *>(P.ps.cam5)[gn];
                     g = gn;
                     if constexpr (kZSobol) {
                         // the sample's ZSobol state past the camera draws and the first segment's three
@@ -2518,7 +2522,13 @@ __global__ void __launch_bounds__(256, kGray ? (kMed == 1 ? 3 : AVR_PATHS_WAVES_
                 segPending = false;
             }
         }
+#ifdef AVR_BLOCK_SYNC
+        // measurement variant: the block's four waves meet at a barrier once per iteration (the
+        // cost of lockstep iterations, the precondition for pooling event handlers across waves)
+        if (!__syncthreads_or(mode != M_DONE)) break;
+#else
         if (__ballot(mode != M_DONE) == 0) break;
+#endif
 
         // =================== tracking: advance every busy lane collision by collision ======
         // until a batch of lanes needs service (events or refill) or none is busy.

@@ -46,19 +46,19 @@ BYTES_PER_LOOKUP = 32
 BYTES_PER_ITEM = 132
 # k_paths' own per-unit bytes (DESIGN.md §4 "Algorithmic bytes"): it writes ONE 16-B record per
 # sample (L; k_film takes the rest from the camera stage) and reads the camera stage's record of
-# every path it starts: cam0..cam3 (4 x 16 B) + the 4-B light-pick draw (ZSobol) or the 16-B
-# PCG32 state (independent sampler)
+# every path it starts: cam0..cam3 (4 x 16 B; ZSobol's first light-pick draw rides in cam1.w) +
+# the 16-B PCG32 state (independent sampler)
 BYTES_PER_SAMPLE_RECORD = 16
-BYTES_CAMERA_RECORD_READ = {"zsobol": 68, "independent": 80}
+BYTES_CAMERA_RECORD_READ = {"zsobol": 64, "independent": 80}
 # ZSobol pixel-table reads (one 4-B entry per draw): 5 draws per phase event in k_paths (phase
 # 2D, the next segment's three 1D, the next light pick); 6 per camera-stage quad of 4 samples
 ZSOBOL_TABLE_BYTES_PER_DRAW = 4
 ZSOBOL_PASS_BYTES_PER_DRAW = 8   # the per-pass table's entries (avr_set_sampler_pass_table)
 ZSOBOL_DRAWS_PER_PHASE = 5
 ZSOBOL_CAMERA_DRAWS = 6
-# the camera stage writes cam0, cam1, cam2, cam3, cam4 (5 x 16 B), the 4-B filter weight and cam5
-# (4 B ZSobol light pick / 16 B PCG32 state)
-BYTES_CAMERA_WRITE = {"zsobol": 88, "independent": 100}
+# the camera stage writes cam0, cam1, cam2, cam3, cam4 (5 x 16 B), the 4-B filter weight and, for
+# the independent sampler, cam5 (16 B PCG32 state)
+BYTES_CAMERA_WRITE = {"zsobol": 84, "independent": 100}
 RGB_CPU_MAX_RES = 512   # the rgb-explosion CPU baseline copies its 3 grids to the host (6 GiB at 512^3)
 
 
