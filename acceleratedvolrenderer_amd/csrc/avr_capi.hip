@@ -1785,13 +1785,14 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
                 // defaults (measured optimum of replay and fast mode): refill at 32 idle
                 // lanes and 10 DDA cells per iteration for 16^3 majorants, 32 cells for finer ones;
                 // a non-emissive NanoVDB medium (pbrt's 64^3 majorant: ~4x the DDA steps of the
-                // grid) refills at 12 lanes with 28 cells (S-cloud-1024: 1239 -> 1352 Msamples/s);
+                // grid) refills at 16 lanes with 28 cells (S-cloud-1024: 1239 -> 1352 Msamples/s at
+                // 12 / 28 in round 3, 1435 -> 1464 at 16 / 28 in round 5, profiles/r05_refill_dda_sweep.json);
                 // an RGBGridMedium (8 sigmoid taps x 4 wavelengths per lookup, 2 waves / SIMD) at
                 // 16 lanes with 32 cells (C5's RGB explosion: 1770 -> 2094 Msamples/s)
                 const int mres = std::max(c->med.mres[0], std::max(c->med.mres[1], c->med.mres[2]));
                 const bool vdbWalk = c->med.type == 3 && !c->med.emissive && mres > 16;
                 const bool rgbWalk = c->med.type == 4;
-                p.refill_min = c->refill_min > 0 ? c->refill_min : (vdbWalk ? 12 : (rgbWalk ? 16 : 32));
+                p.refill_min = c->refill_min > 0 ? c->refill_min : (vdbWalk || rgbWalk ? 16 : 32);
                 p.dda_budget = c->dda_budget > 0 ? c->dda_budget : (vdbWalk ? 28 : (rgbWalk || mres > 16 ? 32 : 10));
             }
             p.heads = c->d_heads;
