@@ -206,7 +206,8 @@ def test_tune_majorant_refuses_single_segment_media():
 
 def test_tune_walk_keeps_the_film_and_changes_no_result():
     """avr_tune_walk (k_paths' refill / DDA-budget schedule chosen by on-device probes): the film
-    is restored, the choice is the fastest probe, the counters are reset, and renders under the
+    is restored, the choice is the fastest probe (the default unless beaten by > 2 %), the counters
+    are reset, and renders under the
     chosen schedule — and under every candidate — are bit-identical to the default schedule."""
     from acceleratedvolrenderer_amd import scenes, VolPathIntegrator
     from oracle import binding
@@ -219,8 +220,10 @@ def test_tune_walk_keeps_the_film_and_changes_no_result():
     rgb2, w2 = integ.film_sums()
     assert np.array_equal(rgb, rgb2) and np.array_equal(w, w2)
     assert ms.shape == (4, 3) and (ms > 0).all()
+    # the fastest probe, except that the default (0, 0) is kept unless beaten by > 2 % (probe noise)
     i, j = np.unravel_index(int(np.argmin(ms)), ms.shape)
-    assert chosen == (refill[i], dda[j])
+    want = (0, 0) if ms[0, 0] <= ms[i, j] * 1.02 else (refill[i], dda[j])
+    assert chosen == want
     assert integ.stats()["medium_lookups"] == 0
     rgb3, w3 = integ.render()
     assert np.array_equal(rgb3, rgb) and np.array_equal(w3, w)
