@@ -69,17 +69,16 @@ struct avr_context {
     bool max_paths_set = false;
     long long rec_cap = 0;   // k_paths records and camera stage allocated (samples)
     hipStream_t own_stream = nullptr, stream = nullptr;
-    // k_film on its own low-priority stream (AVR_FILM_OVERLAP): a pass's film accumulation runs
-    // in the CUs the next pass's camera stage and k_paths leave. film_stream waits for ev_paths
-    // (k_paths of its pass); what k_film reads — rec and the camera stage's cam2 / cam4 / camw — is
-    // double-buffered by pass parity (the *_alt set, pass_par), so the context stream waits for a
-    // film (ev_film_par) only before the pass two later rewrites its set, and for the last one
-    // (ev_film) before anything that touches the film (join_film).
+    // k_film on its own stream (AVR_FILM_OVERLAP): a pass's film accumulation runs beside the next
+    // pass's camera stage. film_stream waits for ev_paths (k_paths of its pass); the context stream
+    // waits for ev_film before the next k_paths (which rewrites the records k_film reads) and
+    // before anything that touches the film (join_film). The camera stage's cam2 / cam4 / camw —
+    // what k_film reads — are double-buffered by pass parity (cam_alt, pass_par).
     hipStream_t film_stream = nullptr;
-    hipEvent_t ev_paths = nullptr, ev_film = nullptr, ev_film_par[2] = {nullptr, nullptr};
-    bool film_pending = false, film_par_pending[2] = {false, false};
+    hipEvent_t ev_paths = nullptr, ev_film = nullptr;
+    bool film_pending = false;
     int pass_par = 0, last_par = 0;
-    float4 *cam2_alt = nullptr, *cam4_alt = nullptr, *rec_alt = nullptr;
+    float4 *cam2_alt = nullptr, *cam4_alt = nullptr;
     float *camw_alt = nullptr;
     // medium
     avr::DevMedium med{};
@@ -218,7 +217,6 @@ void release_comms(avr_context *c) {
 static inline hipError_t join_film(avr_context *c) {
     if (!c || !c->film_pending) return hipSuccess;
     c->film_pending = false;
-    c->film_par_pending[0] = c->film_par_pending[1] = false;
     return hipStreamWaitEvent(c->stream, c->ev_film, 0);
 }
 
@@ -256,12 +254,12 @@ void free_pixel_order(avr_context *c) {
 void free_records(avr_context *c) {
     for (void *p : {(void *)c->ps.rec, (void *)c->ps.cam0, (void *)c->ps.cam1, (void *)c->ps.cam2, (void *)c->ps.cam3,
                     (void *)c->ps.cam4, (void *)c->ps.cam5, (void *)c->ps.camw, (void *)c->cam2_alt,
-                    (void *)c->cam4_alt, (void *)c->camw_alt, (void *)c->rec_alt})
+                    (void *)c->cam4_alt, (void *)c->camw_alt})
         if (p) (void)hipFree(p);
     c->ps.rec = c->ps.cam0 = c->ps.cam1 = c->ps.cam2 = c->ps.cam4 = nullptr;
     c->ps.cam3 = c->ps.cam5 = nullptr;
     c->ps.camw = nullptr;
-    c->cam2_alt = c->cam4_alt = c->rec_alt = nullptr;
+    c->cam2_alt = c->cam4_alt = nullptr;
     c->camw_alt = nullptr;
     c->rec_cap = 0;
 }
@@ -284,7 +282,6 @@ int ensure_records(avr_context *c, long long n) {
     HIP_TRY(dalloc(&c->ps.camw, (size_t)n));
     if (c->film_stream) {   // the second set of what k_film reads (film overlap, by pass parity)
         HIP_TRY(dalloc(&c->cam2_alt, (size_t)n));
-        HIP_TRY(dalloc(&c->rec_alt, (size_t)n));
         HIP_TRY(dalloc(&c->cam4_alt, (size_t)n));
         HIP_TRY(dalloc(&c->camw_alt, (size_t)n));
     }
@@ -675,15 +672,9 @@ int avr_context_create(int device, long long max_paths, avr_context **out) {
     if (e != hipSuccess) { delete c; return fail(AVR_ERR_HIP, hipGetErrorString(e)); }
     c->stream = c->own_stream;
 #if AVR_FILM_OVERLAP
-    // the film stream at the lowest priority: its k_film blocks take CUs the camera stage and
-    // k_paths leave (their tails), instead of stretching the camera stage
-    int prLeast = 0, prGreatest = 0;
-    (void)hipDeviceGetStreamPriorityRange(&prLeast, &prGreatest);
-    if (hipStreamCreateWithPriority(&c->film_stream, hipStreamNonBlocking, prLeast) != hipSuccess ||
+    if (hipStreamCreateWithFlags(&c->film_stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_paths, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_film, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_film_par[0], hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_film_par[1], hipEventDisableTiming) != hipSuccess) {
+        hipEventCreateWithFlags(&c->ev_film, hipEventDisableTiming) != hipSuccess) {
         delete c;
         return fail(AVR_ERR_HIP, "film stream creation failed");
     }
@@ -828,7 +819,7 @@ int avr_context_destroy(avr_context *c) {
     if (c->d_stats) (void)hipFree(c->d_stats);
     if (c->h_count) (void)hipHostFree(c->h_count);
     for (auto e : c->evpool) (void)hipEventDestroy(e);
-    for (auto e : {c->ev_paths, c->ev_film, c->ev_film_par[0], c->ev_film_par[1]}) if (e) (void)hipEventDestroy(e);
+    for (auto e : {c->ev_paths, c->ev_film}) if (e) (void)hipEventDestroy(e);
     if (c->film_stream) (void)hipStreamDestroy(c->film_stream);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     delete c;
@@ -1873,12 +1864,6 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
                 p.ps.cam2 = c->cam2_alt;
                 p.ps.cam4 = c->cam4_alt;
                 p.ps.camw = c->camw_alt;
-                p.ps.rec = c->rec_alt;
-            }
-            // this pass rewrites the set the film of two passes ago read: wait for that film
-            if (overlap && c->film_par_pending[par]) {
-                HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_film_par[par], 0));
-                c->film_par_pending[par] = false;
             }
             // the camera stage: one lane per sample (k_paths_camera)
             {
@@ -1984,6 +1969,8 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
             const bool general_lights = c->n_image_lights > 0 || c->lights.power;
             const int kv = ((((c->render_mode * 2 + (general_lights ? 1 : 0)) * 4 + mk) * 3 + sv) * 2 +
                             (c->med.emissive ? 1 : 0)) * 2 + (c->gray && c->med.type != 4 ? 1 : 0);
+            // k_paths rewrites the records the previous pass's k_film reads: wait for that film
+            if (overlap) HIP_TRY(join_film(c));
             hipLaunchKernelGGL(c->kpaths[kv], dim3(c->paths_grid[kv]), dim3(256), 0, c->stream, p);
             HIP_TRY(hipGetLastError());
             {
@@ -2010,9 +1997,7 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
             EV_MARK_ON(e2, fs);
             if (overlap) {
                 HIP_TRY(hipEventRecord(c->ev_film, c->film_stream));
-                HIP_TRY(hipEventRecord(c->ev_film_par[par], c->film_stream));
                 c->film_pending = true;
-                c->film_par_pending[par] = true;
             }
             c->last_par = par;
             c->timed.push_back({e0, e1, &avr_stats::ms_medium, true});
@@ -2338,7 +2323,7 @@ int avr_last_pass_samples(avr_context *c, float *L, float *lambda, float *pdf, l
         return fail(AVR_ERR_STATE, "the pixel order changed since the last render (its records are in the old order)");
     if (n > 0 && c->last_persistent) {
         // k_paths' records (L) and its camera stage's wavelengths and pdfs, as k_film read them
-        HIP_TRY(hipMemcpy(L, c->last_par ? c->rec_alt : c->ps.rec, n * sizeof(float4), hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(L, c->ps.rec, n * sizeof(float4), hipMemcpyDeviceToHost));
         HIP_TRY(hipMemcpy(lambda, c->last_par ? c->cam2_alt : c->ps.cam2, n * sizeof(float4), hipMemcpyDeviceToHost));
         HIP_TRY(hipMemcpy(pdf, c->last_par ? c->cam4_alt : c->ps.cam4, n * sizeof(float4), hipMemcpyDeviceToHost));
         if (!c->h_pix_slot.empty()) {   // slot order -> pixel order
