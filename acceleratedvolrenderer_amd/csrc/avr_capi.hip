@@ -48,9 +48,6 @@ int fail(int code, const std::string &msg) {
             return fail(AVR_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));       \
     } while (0)
 
-#ifndef AVR_FILM_OVERLAP
-#define AVR_FILM_OVERLAP 1   // k_film on a second stream, beside the next pass's camera stage
-#endif
 #ifndef AVR_ZS_TWO_LEVEL
 #define AVR_ZS_TWO_LEVEL 1   // build the ZSobol pass table from a level-A table shared by 4 passes
 #endif
@@ -69,17 +66,6 @@ struct avr_context {
     bool max_paths_set = false;
     long long rec_cap = 0;   // k_paths records and camera stage allocated (samples)
     hipStream_t own_stream = nullptr, stream = nullptr;
-    // k_film on its own stream (AVR_FILM_OVERLAP): a pass's film accumulation runs beside the next
-    // pass's camera stage. film_stream waits for ev_paths (k_paths of its pass); the context stream
-    // waits for ev_film before the next k_paths (which rewrites the records k_film reads) and
-    // before anything that touches the film (join_film). The camera stage's cam2 / cam4 / camw —
-    // what k_film reads — are double-buffered by pass parity (cam_alt, pass_par).
-    hipStream_t film_stream = nullptr;
-    hipEvent_t ev_paths = nullptr, ev_film = nullptr;
-    bool film_pending = false;
-    int pass_par = 0, last_par = 0;
-    float4 *cam2_alt = nullptr, *cam4_alt = nullptr;
-    float *camw_alt = nullptr;
     // medium
     avr::DevMedium med{};
     float *d_density_owned = nullptr;
@@ -212,14 +198,6 @@ void release_comms(avr_context *c) {
     (void)hipSetDevice(c->device);
 }
 
-// The context stream waits for the last k_film launched on the film stream (no-op otherwise):
-// every call that reads, writes or syncs on the film goes through this first.
-static inline hipError_t join_film(avr_context *c) {
-    if (!c || !c->film_pending) return hipSuccess;
-    c->film_pending = false;
-    return hipStreamWaitEvent(c->stream, c->ev_film, 0);
-}
-
 void free_paths(avr_context *c) {
     float4 *f4[] = {c->ps.o, c->ps.d, c->ps.lambda, c->ps.pdf, c->ps.beta, c->ps.r_u, c->ps.r_l, c->ps.L,
                     c->sh.o, c->sh.d, c->sh.bf, c->sh.Ls, c->sh.rp};
@@ -253,14 +231,11 @@ void free_pixel_order(avr_context *c) {
 
 void free_records(avr_context *c) {
     for (void *p : {(void *)c->ps.rec, (void *)c->ps.cam0, (void *)c->ps.cam1, (void *)c->ps.cam2, (void *)c->ps.cam3,
-                    (void *)c->ps.cam4, (void *)c->ps.cam5, (void *)c->ps.camw, (void *)c->cam2_alt,
-                    (void *)c->cam4_alt, (void *)c->camw_alt})
+                    (void *)c->ps.cam4, (void *)c->ps.cam5, (void *)c->ps.camw})
         if (p) (void)hipFree(p);
     c->ps.rec = c->ps.cam0 = c->ps.cam1 = c->ps.cam2 = c->ps.cam4 = nullptr;
     c->ps.cam3 = c->ps.cam5 = nullptr;
     c->ps.camw = nullptr;
-    c->cam2_alt = c->cam4_alt = nullptr;
-    c->camw_alt = nullptr;
     c->rec_cap = 0;
 }
 
@@ -268,9 +243,6 @@ void free_records(avr_context *c) {
 // 4-B filter weight), independent of the wavefront SoA
 int ensure_records(avr_context *c, long long n) {
     if (n <= c->rec_cap) return AVR_OK;
-    // the film stream may still read the old records: finish everything before freeing them
-    HIP_TRY(join_film(c));
-    HIP_TRY(hipStreamSynchronize(c->stream));
     free_records(c);
     HIP_TRY(dalloc(&c->ps.rec, (size_t)n));
     HIP_TRY(dalloc(&c->ps.cam0, (size_t)n));
@@ -280,11 +252,6 @@ int ensure_records(avr_context *c, long long n) {
     HIP_TRY(dalloc(&c->ps.cam4, (size_t)n));
     HIP_TRY(dalloc(&c->ps.cam5, (size_t)n));
     HIP_TRY(dalloc(&c->ps.camw, (size_t)n));
-    if (c->film_stream) {   // the second set of what k_film reads (film overlap, by pass parity)
-        HIP_TRY(dalloc(&c->cam2_alt, (size_t)n));
-        HIP_TRY(dalloc(&c->cam4_alt, (size_t)n));
-        HIP_TRY(dalloc(&c->camw_alt, (size_t)n));
-    }
     c->rec_cap = n;
     return AVR_OK;
 }
@@ -651,7 +618,6 @@ const char *avr_last_error(void) { return g_err.c_str(); }
 #define AVR_QUIESCE(c)                                                                              \
     do {                                                                                            \
         if ((c) && (c)->stream) {                                                                   \
-            (void)join_film(c);                                                                     \
             const hipError_t qe_ = hipStreamSynchronize((c)->stream);                               \
             if (qe_ != hipSuccess) return fail(AVR_ERR_HIP, std::string("stream: ") + hipGetErrorString(qe_)); \
         }                                                                                           \
@@ -671,14 +637,6 @@ int avr_context_create(int device, long long max_paths, avr_context **out) {
     hipError_t e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
     if (e != hipSuccess) { delete c; return fail(AVR_ERR_HIP, hipGetErrorString(e)); }
     c->stream = c->own_stream;
-#if AVR_FILM_OVERLAP
-    if (hipStreamCreateWithFlags(&c->film_stream, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_paths, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_film, hipEventDisableTiming) != hipSuccess) {
-        delete c;
-        return fail(AVR_ERR_HIP, "film stream creation failed");
-    }
-#endif
     if (dalloc(&c->d_counts, 4) != hipSuccess || dalloc(&c->d_stats, avr::kNumStats + 8) != hipSuccess ||
         hipHostMalloc((void **)&c->h_count, sizeof(int) * 4) != hipSuccess) {
         delete c;
@@ -783,9 +741,7 @@ int avr_set_kernel_mode(avr_context *c, int mode) {
 int avr_context_destroy(avr_context *c) {
     if (!c) return AVR_OK;
     (void)hipSetDevice(c->device);
-    (void)join_film(c);
     (void)hipStreamSynchronize(c->stream);
-    if (c->film_stream) (void)hipStreamSynchronize(c->film_stream);
     release_comms(c);
     free_paths(c);
     free_records(c);
@@ -819,8 +775,6 @@ int avr_context_destroy(avr_context *c) {
     if (c->d_stats) (void)hipFree(c->d_stats);
     if (c->h_count) (void)hipHostFree(c->h_count);
     for (auto e : c->evpool) (void)hipEventDestroy(e);
-    for (auto e : {c->ev_paths, c->ev_film}) if (e) (void)hipEventDestroy(e);
-    if (c->film_stream) (void)hipStreamDestroy(c->film_stream);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     delete c;
     return AVR_OK;
@@ -828,10 +782,6 @@ int avr_context_destroy(avr_context *c) {
 
 int avr_set_stream(avr_context *c, void *s) {
     if (!c) return fail(AVR_ERR_ARG, "null context");
-    // finish what the old stream (and the film stream) hold before switching; with a caller's
-    // stream every kernel runs on it (no film overlap)
-    HIP_TRY(join_film(c));
-    HIP_TRY(hipStreamSynchronize(c->stream));
     c->stream = s ? (hipStream_t)s : c->own_stream;
     return AVR_OK;
 }
@@ -1649,7 +1599,6 @@ int avr_set_sampler(avr_context *c, int kind, int samples_per_pixel) {
 
 int avr_film_clear(avr_context *c) {
     if (!c || !c->has_film) return fail(AVR_ERR_STATE, "no film");
-    HIP_TRY(join_film(c));
     const size_t np = (size_t)c->film.width * c->film.height;
     HIP_TRY(hipMemsetAsync(c->film.rgb_sum, 0, 3 * np * sizeof(double), c->stream));
     HIP_TRY(hipMemsetAsync(c->film.w_sum, 0, np * sizeof(double), c->stream));
@@ -1662,7 +1611,6 @@ int avr_film_clear(avr_context *c) {
 // lambda_max]; n_buckets = 0 returns to RGBFilm. Both sums live in one allocation.
 int avr_film_spectral(avr_context *c, int n_buckets, float lambda_min, float lambda_max) {
     if (!c || !c->has_film) return fail(AVR_ERR_STATE, "no film");
-    HIP_TRY(join_film(c));
     if (n_buckets < 0) return fail(AVR_ERR_ARG, "n_buckets must be >= 0");
     if (n_buckets > 0 && !(360.f <= lambda_min && lambda_min < lambda_max && lambda_max <= 830.f))
         return fail(AVR_ERR_ARG, "SpectralFilm wavelength range must lie within 360..830 nm");
@@ -1685,7 +1633,6 @@ int avr_film_spectral(avr_context *c, int n_buckets, float lambda_min, float lam
 // records two pool events and is folded (one stream sync) when stats are read.
 static int fold_stats(avr_context *c) {
     if (c->timed.empty()) return AVR_OK;
-    HIP_TRY(join_film(c));
     HIP_TRY(hipStreamSynchronize(c->stream));
     for (const auto &t : c->timed) {
         float ms = 0;
@@ -1711,7 +1658,7 @@ static int fold_stats(avr_context *c) {
 }
 
 // next free pool event (folds first when the pool is full)
-static int next_event(avr_context *c, int *idx, hipStream_t on = nullptr) {
+static int next_event(avr_context *c, int *idx) {
     if (c->ev_used >= 512) {
         int rc = fold_stats(c);
         if (rc) return rc;
@@ -1722,7 +1669,7 @@ static int next_event(avr_context *c, int *idx, hipStream_t on = nullptr) {
         c->evpool.push_back(e);
     }
     *idx = (int)c->ev_used++;
-    HIP_TRY(hipEventRecord(c->evpool[*idx], on ? on : c->stream));
+    HIP_TRY(hipEventRecord(c->evpool[*idx], c->stream));
     return AVR_OK;
 }
 #define EV_MARK(var)                      \
@@ -1730,12 +1677,6 @@ static int next_event(avr_context *c, int *idx, hipStream_t on = nullptr) {
     do {                                  \
         int rc_ = next_event(c, &var);    \
         if (rc_) return rc_;              \
-    } while (0)
-#define EV_MARK_ON(var, strm)                   \
-    int var;                                    \
-    do {                                        \
-        int rc_ = next_event(c, &var, (strm));  \
-        if (rc_) return rc_;                    \
     } while (0)
 
 int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_depth) {
@@ -1856,15 +1797,6 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
             }
             p.heads = c->d_heads;
             HIP_TRY(hipMemsetAsync(c->d_heads, 0, 8 * sizeof(int), c->stream));
-            // film overlap: this pass's k_film runs on the film stream beside the next pass's
-            // camera stage, which then writes the other set of cam2 / cam4 / camw
-            const bool overlap = c->film_stream && c->stream == c->own_stream && c->cam2_alt;
-            const int par = overlap ? (c->pass_par ^= 1) : 0;
-            if (par) {
-                p.ps.cam2 = c->cam2_alt;
-                p.ps.cam4 = c->cam4_alt;
-                p.ps.camw = c->camw_alt;
-            }
             // the camera stage: one lane per sample (k_paths_camera)
             {
                 const int sv = c->sampler_kind == 0 ? 0 : (avr::smp::zsobol_wide(p.zs) ? 2 : 1);
@@ -1969,8 +1901,6 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
             const bool general_lights = c->n_image_lights > 0 || c->lights.power;
             const int kv = ((((c->render_mode * 2 + (general_lights ? 1 : 0)) * 4 + mk) * 3 + sv) * 2 +
                             (c->med.emissive ? 1 : 0)) * 2 + (c->gray && c->med.type != 4 ? 1 : 0);
-            // k_paths rewrites the records the previous pass's k_film reads: wait for that film
-            if (overlap) HIP_TRY(join_film(c));
             hipLaunchKernelGGL(c->kpaths[kv], dim3(c->paths_grid[kv]), dim3(256), 0, c->stream, p);
             HIP_TRY(hipGetLastError());
             {
@@ -1984,24 +1914,12 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
             p.rec_mode = 1;   // k_film reads the records k_paths wrote (in slot order)
             p.pix_slot = c->d_pix_slot;
             p.fast = c->render_mode;
-            hipStream_t fs = c->stream;
-            if (overlap) {
-                HIP_TRY(hipEventRecord(c->ev_paths, c->stream));
-                HIP_TRY(hipStreamWaitEvent(c->film_stream, c->ev_paths, 0));
-                fs = c->film_stream;
-            }
-            EV_MARK_ON(f1, fs);
             hipLaunchKernelGGL((c->film.nbuckets > 0 ? avr::k_film<true> : avr::k_film<false>), dim3(blocks_for(P)), dim3(256), avr::film_lds_bytes(c->film.nbuckets),
-                               fs, p);
+                               c->stream, p);
             HIP_TRY(hipGetLastError());
-            EV_MARK_ON(e2, fs);
-            if (overlap) {
-                HIP_TRY(hipEventRecord(c->ev_film, c->film_stream));
-                c->film_pending = true;
-            }
-            c->last_par = par;
+            EV_MARK(e2);
             c->timed.push_back({e0, e1, &avr_stats::ms_medium, true});
-            c->timed.push_back({f1, e2, &avr_stats::ms_film, false});
+            c->timed.push_back({e1, e2, &avr_stats::ms_film, false});
             c->last_base = (int)base;
             c->last_S = S;
             c->last_order_gen = c->order_gen;
@@ -2141,7 +2059,6 @@ int avr_transmittance(avr_context *c, long long n, const float *p0, const float 
 
 int avr_sync(avr_context *c) {
     if (!c) return fail(AVR_ERR_ARG, "null context");
-    HIP_TRY(join_film(c));
     HIP_TRY(hipStreamSynchronize(c->stream));
     return AVR_OK;
 }
@@ -2178,7 +2095,6 @@ static int film_image(avr_context *c, const avr::Mat3 &M, int fp16, float *d_out
 
 int avr_film_image_device(avr_context *c, const float out_from_sensor[9], int fp16, float *d_out) {
     if (!c || !c->has_film || !out_from_sensor || !d_out) return fail(AVR_ERR_STATE, "no film or null argument");
-    HIP_TRY(join_film(c));
     HIP_TRY(hipSetDevice(c->device));
     avr::Mat3 M;
     for (int i = 0; i < 9; ++i) M.m[i] = out_from_sensor[i];
@@ -2187,7 +2103,6 @@ int avr_film_image_device(avr_context *c, const float out_from_sensor[9], int fp
 
 int avr_film_set_reference(avr_context *c, const float *reference_rgb, const float out_from_sensor[9], int fp16) {
     if (!c || !c->has_film || !reference_rgb || !out_from_sensor) return fail(AVR_ERR_STATE, "no film or null argument");
-    HIP_TRY(join_film(c));
     HIP_TRY(hipSetDevice(c->device));
     const size_t np = (size_t)c->film.width * c->film.height;
     if (c->d_reference) (void)hipFree(c->d_reference);
@@ -2206,7 +2121,6 @@ int avr_film_set_reference(avr_context *c, const float *reference_rgb, const flo
 
 int avr_film_metric(avr_context *c, int metric, float *out) {
     if (!c || !c->has_film || !out) return fail(AVR_ERR_STATE, "no film");
-    HIP_TRY(join_film(c));
     if (!c->d_reference) return fail(AVR_ERR_STATE, "no reference image (avr_film_set_reference)");
     if (metric < 0 || metric > 3) return fail(AVR_ERR_ARG, "metric must be 0 MSE, 1 MAE, 2 MRSE, 3 ME");
     HIP_TRY(hipSetDevice(c->device));
@@ -2277,7 +2191,6 @@ int avr_flip(avr_context *c, const float *test, const float *ref, int width, int
 
 int avr_film_read(avr_context *c, double *rgb, double *w) {
     if (!c || !c->has_film || !rgb || !w) return fail(AVR_ERR_STATE, "no film");
-    HIP_TRY(join_film(c));
     const size_t np = (size_t)c->film.width * c->film.height;
     HIP_TRY(hipMemcpyAsync(rgb, c->film.rgb_sum, 3 * np * sizeof(double), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipMemcpyAsync(w, c->film.w_sum, np * sizeof(double), hipMemcpyDeviceToHost, c->stream));
@@ -2287,7 +2200,6 @@ int avr_film_read(avr_context *c, double *rgb, double *w) {
 
 int avr_film_read_spectral(avr_context *c, double *bucket_sums, double *weight_sums) {
     if (!c || !c->has_film || c->film.nbuckets <= 0) return fail(AVR_ERR_STATE, "no spectral film");
-    HIP_TRY(join_film(c));
     if (!bucket_sums || !weight_sums) return fail(AVR_ERR_ARG, "null buffer");
     const size_t nb = (size_t)c->film.width * c->film.height * c->film.nbuckets;
     HIP_TRY(hipMemcpyAsync(bucket_sums, c->film.bucket_sum, nb * sizeof(double), hipMemcpyDeviceToHost, c->stream));
@@ -2299,7 +2211,6 @@ int avr_film_read_spectral(avr_context *c, double *bucket_sums, double *weight_s
 int avr_film_spectral_device_ptrs(avr_context *c, void **bucket_sums, void **weight_sums) {
     if (!c || !c->has_film || c->film.nbuckets <= 0 || !bucket_sums || !weight_sums)
         return fail(AVR_ERR_STATE, "no spectral film");
-    HIP_TRY(join_film(c));
     *bucket_sums = c->film.bucket_sum;
     *weight_sums = c->film.bucket_w;
     return AVR_OK;
@@ -2307,7 +2218,6 @@ int avr_film_spectral_device_ptrs(avr_context *c, void **bucket_sums, void **wei
 
 int avr_film_device_ptrs(avr_context *c, void **rgb, void **w) {
     if (!c || !c->has_film || !rgb || !w) return fail(AVR_ERR_STATE, "no film");
-    HIP_TRY(join_film(c));
     *rgb = c->film.rgb_sum;
     *w = c->film.w_sum;
     return AVR_OK;
@@ -2324,8 +2234,8 @@ int avr_last_pass_samples(avr_context *c, float *L, float *lambda, float *pdf, l
     if (n > 0 && c->last_persistent) {
         // k_paths' records (L) and its camera stage's wavelengths and pdfs, as k_film read them
         HIP_TRY(hipMemcpy(L, c->ps.rec, n * sizeof(float4), hipMemcpyDeviceToHost));
-        HIP_TRY(hipMemcpy(lambda, c->last_par ? c->cam2_alt : c->ps.cam2, n * sizeof(float4), hipMemcpyDeviceToHost));
-        HIP_TRY(hipMemcpy(pdf, c->last_par ? c->cam4_alt : c->ps.cam4, n * sizeof(float4), hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(lambda, c->ps.cam2, n * sizeof(float4), hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(pdf, c->ps.cam4, n * sizeof(float4), hipMemcpyDeviceToHost));
         if (!c->h_pix_slot.empty()) {   // slot order -> pixel order
             const long long np = (long long)c->film.width * c->film.height;
             std::vector<float> tmp(4 * (size_t)np);
@@ -2363,7 +2273,7 @@ int avr_last_pass_weights(avr_context *c, float *w, long long n_max) {
         for (long long i = 0; i < n; ++i) w[i] = 1.f;   // BoxFilter::Sample weight
     } else if (n > 0 && c->last_persistent) {
         std::vector<float> camw((size_t)n);
-        HIP_TRY(hipMemcpy(camw.data(), c->last_par ? c->camw_alt : c->ps.camw, n * sizeof(float), hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(camw.data(), c->ps.camw, n * sizeof(float), hipMemcpyDeviceToHost));
         const long long np = (long long)c->film.width * c->film.height;
         for (long long i = 0; i < n; ++i)
             w[i] = camw[c->h_pix_slot.empty() ? i : (i / np) * np + c->h_pix_slot[(size_t)(i % np)]];
@@ -2375,7 +2285,6 @@ int avr_last_pass_weights(avr_context *c, float *w, long long n_max) {
 
 int avr_film_export_device(avr_context *c, void *dst) {
     if (!c || !c->has_film || !dst) return fail(AVR_ERR_STATE, "no film");
-    HIP_TRY(join_film(c));
     const size_t np = (size_t)c->film.width * c->film.height;
     double *d = (double *)dst;
     HIP_TRY(hipMemcpyAsync(d, c->film.rgb_sum, 3 * np * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
@@ -2394,7 +2303,6 @@ int avr_film_reduce_rccl(avr_context **ctxs, int n, int root) {
     if (!ctxs || n < 1 || root < 0 || root >= n) return fail(AVR_ERR_ARG, "film reduce: bad context list");
     for (int i = 0; i < n; ++i) {
         if (!ctxs[i] || !ctxs[i]->has_film) return fail(AVR_ERR_STATE, "film reduce: context without a film");
-        HIP_TRY(join_film(ctxs[i]));
         const avr::DevFilm &a = ctxs[i]->film, &b = ctxs[root]->film;
         if (a.width != b.width || a.height != b.height || a.nbuckets != b.nbuckets)
             return fail(AVR_ERR_ARG, "film reduce: films differ in resolution or buckets");
