@@ -55,7 +55,7 @@ def main():
     gen.sync()
     gen.close()
     if a.medium == "nanovdb":
-        scene = scenes.s_cloud_vdb(scenes.vdb_grid(density.cpu().numpy()), sampler=a.sampler, spp=a.pixelsamples,
+        scene = scenes.s_cloud_vdb(scenes.vdb_grid(density), sampler=a.sampler, spp=a.pixelsamples,
                                    filter=a.filter)
         del density
     else:
