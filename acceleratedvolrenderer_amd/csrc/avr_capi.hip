@@ -1103,12 +1103,14 @@ int avr_set_majorant_res(avr_context *c, const int res[3]) {
 // film sums are saved before and restored after (also when a probe fails; the first error is
 // kept); restore() then re-applies the chosen (or, after a failure, the original) setting.
 // prefer >= 0: that candidate (the default schedule) is kept unless the fastest probe beats it
-// by more than kProbeNoise — the probes' run-to-run spread — so the choice is reproducible.
+// by more than kProbeNoise — the probes' run-to-run spread — so the choice is reproducible. Its
+// time is the fastest probe of every candidate marked in `same` (those that run the very same
+// schedule, e.g. refill 0 and refill 32 when 32 is the default), not one noisy probe.
 constexpr float kProbeNoise = 0.02f;
 extern "C++" {
 template <typename Setup, typename Restore>
 static int probe_loop(avr_context *c, int n, Setup setup, Restore restore, int spp_begin, int spp_end, int seed,
-                      int max_depth, int *bestk, float *ms, int prefer = -1) {
+                      int max_depth, int *bestk, float *ms, int prefer = -1, const std::vector<char> *same = nullptr) {
     HIP_TRY(hipSetDevice(c->device));
     const size_t np = (size_t)c->film.width * c->film.height;
     const size_t nd = (4 + 2 * (size_t)std::max(0, c->film.nbuckets)) * np;
@@ -1132,7 +1134,7 @@ static int probe_loop(avr_context *c, int n, Setup setup, Restore restore, int s
         (void)hipEventElapsedTime(&t, e0, e1);
         if (k < 0) continue;
         if (ms) ms[k] = t;
-        if (k == prefer) tPrefer = t;
+        if ((k == prefer || (same && (*same)[k])) && (tPrefer < 0 || t < tPrefer)) tPrefer = t;
         if (best < 0 || t < best) { best = t; *bestk = k; }
     }
     if (!rc && prefer >= 0 && tPrefer >= 0 && tPrefer <= best * (1 + kProbeNoise)) *bestk = prefer;
@@ -1185,6 +1187,21 @@ int avr_tune_majorant(avr_context *c, const int *candidates, int n, int spp_begi
     return rc;
 }
 
+// k_paths' effective walk schedule for requested (refill lanes, DDA cells), 0 = the defaults —
+// measured optima: refill at 32 idle lanes and 10 DDA cells per iteration for 16^3
+// majorants, 32 cells for finer ones; a non-emissive NanoVDB medium (pbrt's 64^3 majorant: ~4x the
+// DDA steps of the grid) refills at 16 lanes with 28 cells (S-cloud-1024: 1239 -> 1352
+// Msamples/s at 12 / 28 in round 3, 1435 -> 1464 at 16 / 28 in round 5,
+// profiles/r05_refill_dda_sweep.json); an RGBGridMedium (8 sigmoid taps x 4 wavelengths per
+// lookup, 2 waves / SIMD) at 16 lanes with 32 cells (C5's RGB explosion: 1770 -> 2094 Msamples/s)
+static void walk_schedule(const avr_context *c, int refill, int dda, int *r_eff, int *d_eff) {
+    const int mres = std::max(c->med.mres[0], std::max(c->med.mres[1], c->med.mres[2]));
+    const bool vdbWalk = c->med.type == 3 && !c->med.emissive && mres > 16;
+    const bool rgbWalk = c->med.type == 4;
+    *r_eff = refill > 0 ? refill : (vdbWalk || rgbWalk ? 16 : 32);
+    *d_eff = dda > 0 ? dda : (vdbWalk ? 28 : (rgbWalk || mres > 16 ? 32 : 10));
+}
+
 int avr_tune_walk(avr_context *c, const int *refill, int nr, const int *dda, int nd, int spp_begin, int spp_end,
                   int seed, int max_depth, int chosen[2], float *ms) {
     AVR_QUIESCE(c);
@@ -1202,6 +1219,17 @@ int avr_tune_walk(avr_context *c, const int *refill, int nr, const int *dda, int
         if (refill[k / nd] == 0 && dda[k % nd] == 0) prefer = k;
     for (int k = 0; k < nr * nd && prefer < 0; ++k)
         if (refill[k / nd] == r0 && dda[k % nd] == d0) prefer = k;
+    // every candidate that resolves to the preferred schedule counts as the same probe
+    std::vector<char> same((size_t)nr * nd, 0);
+    if (prefer >= 0) {
+        int rp, dp;
+        walk_schedule(c, refill[prefer / nd], dda[prefer % nd], &rp, &dp);
+        for (int k = 0; k < nr * nd; ++k) {
+            int rk, dk;
+            walk_schedule(c, refill[k / nd], dda[k % nd], &rk, &dk);
+            same[(size_t)k] = rk == rp && dk == dp;
+        }
+    }
     int bestk = 0;
     const int rc = probe_loop(
         c, nr * nd,
@@ -1215,7 +1243,7 @@ int avr_tune_walk(avr_context *c, const int *refill, int nr, const int *dda, int
             c->dda_budget = failed ? d0 : dda[b % nd];
             return AVR_OK;
         },
-        spp_begin, spp_end, seed, max_depth, &bestk, ms, prefer);
+        spp_begin, spp_end, seed, max_depth, &bestk, ms, prefer, &same);
     if (!rc) {
         chosen[0] = refill[bestk / nd];
         chosen[1] = dda[bestk % nd];
@@ -1781,20 +1809,7 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
                                (long long)base, S);
             HIP_TRY(hipGetLastError());
             p.advance = c->d_advance;
-            {
-                // defaults (measured optimum of replay and fast mode): refill at 32 idle
-                // lanes and 10 DDA cells per iteration for 16^3 majorants, 32 cells for finer ones;
-                // a non-emissive NanoVDB medium (pbrt's 64^3 majorant: ~4x the DDA steps of the
-                // grid) refills at 16 lanes with 28 cells (S-cloud-1024: 1239 -> 1352 Msamples/s at
-                // 12 / 28 in round 3, 1435 -> 1464 at 16 / 28 in round 5, profiles/r05_refill_dda_sweep.json);
-                // an RGBGridMedium (8 sigmoid taps x 4 wavelengths per lookup, 2 waves / SIMD) at
-                // 16 lanes with 32 cells (C5's RGB explosion: 1770 -> 2094 Msamples/s)
-                const int mres = std::max(c->med.mres[0], std::max(c->med.mres[1], c->med.mres[2]));
-                const bool vdbWalk = c->med.type == 3 && !c->med.emissive && mres > 16;
-                const bool rgbWalk = c->med.type == 4;
-                p.refill_min = c->refill_min > 0 ? c->refill_min : (vdbWalk || rgbWalk ? 16 : 32);
-                p.dda_budget = c->dda_budget > 0 ? c->dda_budget : (vdbWalk ? 28 : (rgbWalk || mres > 16 ? 32 : 10));
-            }
+            walk_schedule(c, c->refill_min, c->dda_budget, &p.refill_min, &p.dda_budget);   // defaults: measured optima
             p.heads = c->d_heads;
             HIP_TRY(hipMemsetAsync(c->d_heads, 0, 8 * sizeof(int), c->stream));
             // the camera stage: one lane per sample (k_paths_camera)

@@ -626,7 +626,8 @@ def main():
         integ.ctx.set_refill_min(r_best)
         integ.ctx.set_dda_budget(d_best)
         walk_tuned = {"refill_min": r_best, "dda_budget": d_best, "refill_candidates": list(rc), "dda_candidates": list(dc),
-                      "tie_break": "the default (0, 0) is kept unless a candidate's probe is > 2 % faster (avr_tune_walk)",
+                      "tie_break": "the default (0, 0) is kept unless a candidate's probe is > 2 % faster than every probe of the "
+                                   "default's effective schedule (avr_tune_walk)",
                       "probe_ms": [[round(float(x), 3) for x in row] for row in wms]}
         args.refill_min, args.dda_budget = r_best, d_best   # the counter passes render the same schedule
         log(f"tuned walk: refill {r_best}, DDA {d_best} (0 = default)")

@@ -271,8 +271,9 @@ int avr_tune_majorant(avr_context *ctx, const int *candidates, int n, int spp_be
  * candidate pair, refill[i] x dda[j] (0 = the library default for either), timed with HIP
  * events on the context stream, and keep the fastest (chosen[2] = {refill, dda}; the nr*nd
  * probe times in ms[i * nd + j] when non-null) — except that the default pair (0, 0), when
- * listed (else the current schedule, when listed), is kept unless the fastest probe beats it
- * by more than 2 % (the probes' run-to-run spread), so repeated runs choose the same
+ * listed (else the current schedule, when listed), is kept unless the fastest probe beats
+ * every probe of that same effective schedule (e.g. refill 0 and refill 32 where 32 is the
+ * default) by more than 2 % (the probes' run-to-run spread), so repeated runs choose the same
  * schedule. Film sums restored and work counters reset
  * afterwards, as avr_tune_majorant. The schedule never changes results, only how a wave
  * batches its lanes' events and walks. */
