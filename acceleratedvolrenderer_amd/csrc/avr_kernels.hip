@@ -1949,6 +1949,15 @@ enum : int { EV_NONE = 0, EV_SCATTER = 1, EV_SHADOW_DONE = 2, EV_PHASE = 3, EV_E
 // yields exactly the bits each component would get: the overloads below restate Spec's
 // operations on one component (Spec::avg of four equal values is (((x+x)+x)+x)/4, NOT x).
 __device__ __forceinline__ float sv0(float x) { return x; }
+// x / x as IEEE division computes it: exactly 1 for a finite nonzero x, NaN for 0, inf or NaN.
+// pbrt's ratios T_maj / T_maj[0] and T_maj * sigma / (T_maj[0] * sigma[0]) are such quotients in
+// a gray medium (the same float products on both sides); the division itself runs only when a
+// lane of the wave has a special x, so the result (NaN bits included) is the division's.
+__device__ __forceinline__ float unit_quot(float x) {
+    const bool plain = __builtin_isfinite(x) && x != 0.f;
+    if (__ballot(!plain) == 0) return 1.f;
+    return plain ? 1.f : x / x;
+}
 __device__ __forceinline__ float sv0(const Spec &x) { return x.v0; }
 __device__ __forceinline__ bool snz(float x) { return x != 0; }
 __device__ __forceinline__ bool snz(const Spec &x) { return x.nonzero(); }
@@ -2296,9 +2305,16 @@ __global__ void __launch_bounds__(256, kGray ? (kMed == 1 ? 3 : AVR_PATHS_WAVES_
             if (ev == EV_SHADOW_DONE) {
                 // finish SampleLd (1379-1398); SampleT_maj returned 1 if the callback stopped
                 const S Tm = shadowStopped ? sconst<S>(1.f) : T_maj;
-                T_ray = T_ray * (Tm / sv0(Tm));
-                sr_l = sr_l * (Tm / sv0(Tm));
-                sr_u = sr_u * (Tm / sv0(Tm));
+                if constexpr (kGray) {
+                    const float q = unit_quot(Tm);
+                    T_ray = T_ray * q;
+                    sr_l = sr_l * q;
+                    sr_u = sr_u * q;
+                } else {
+                    T_ray = T_ray * (Tm / sv0(Tm));
+                    sr_l = sr_l * (Tm / sv0(Tm));
+                    sr_u = sr_u * (Tm / sv0(Tm));
+                }
                 Spec contrib = Spec::c(0.f);
                 if (snz(T_ray)) {
                     const DevLight &lt = P.lights.list[light];
@@ -2375,7 +2391,7 @@ __global__ void __launch_bounds__(256, kGray ? (kMed == 1 ? 3 : AVR_PATHS_WAVES_
                 if (phPdf == 0) {
                     ev = EV_END;
                 } else {
-                    beta = beta * (phPdf / phPdf);
+                    beta = beta * unit_quot(phPdf);
                     r_l = r_u / phPdf;
                     pd = wi;
                     const float h0 = kCoopLds ? qr[2] : (kCoop ? q0[1] : smp.get1d(P));
@@ -2394,9 +2410,16 @@ __global__ void __launch_bounds__(256, kGray ? (kMed == 1 ? 3 : AVR_PATHS_WAVES_
         if (__ballot(ev == EV_ESCAPE)) {
             if (ev == EV_ESCAPE) {
                 // escaped (integrators.cpp:1078-1107)
-                beta = beta * (T_maj / sv0(T_maj));
-                r_u = r_u * (T_maj / sv0(T_maj));
-                r_l = r_l * (T_maj / sv0(T_maj));
+                if constexpr (kGray) {
+                    const float q = unit_quot(T_maj);
+                    beta = beta * q;
+                    r_u = r_u * q;
+                    r_l = r_l * q;
+                } else {
+                    beta = beta * (T_maj / sv0(T_maj));
+                    r_u = r_u * (T_maj / sv0(T_maj));
+                    r_l = r_l * (T_maj / sv0(T_maj));
+                }
                 for (int k = 0; k < P.lights.n; ++k) {
                     const DevLight &lt = P.lights.list[k];
                     if (lt.type == 0 || (!kImage && lt.type == 2)) continue;
@@ -2730,8 +2753,14 @@ __global__ void __launch_bounds__(256, kGray ? (kMed == 1 ? 3 : AVR_PATHS_WAVES_
                         ev = EV_END;
                         if (depth++ < P.max_depth) {
                             const float pdf = sv0(T_maj) * sv0(ms_s);
-                            beta = beta * (T_maj * ms_s / pdf);
-                            r_u = r_u * (T_maj * ms_s / pdf);
+                            if constexpr (kGray) {   // T_maj * ms_s is pdf's product
+                                const float q = unit_quot(pdf);
+                                beta = beta * q;
+                                r_u = r_u * q;
+                            } else {
+                                beta = beta * (T_maj * ms_s / pdf);
+                                r_u = r_u * (T_maj * ms_s / pdf);
+                            }
                             if (snz(beta) && snz(r_u)) {
                                 po = pc;     // the scatter vertex: shadow-ray and next-segment origin
                                 ev = EV_SCATTER;
@@ -2740,9 +2769,10 @@ __global__ void __launch_bounds__(256, kGray ? (kMed == 1 ? 3 : AVR_PATHS_WAVES_
                     } else {
                         const S sigma_n = sclamp0(sigma_maj - ms_a - ms_s);
                         const float pdf = sv0(T_maj) * sv0(sigma_n);
-                        beta = beta * (T_maj * sigma_n / pdf);
+                        const S qn = kGray ? sconst<S>(unit_quot(pdf)) : T_maj * sigma_n / pdf;   // gray: pdf's product
+                        beta = beta * qn;
                         if (pdf == 0) beta = sconst<S>(0.f);
-                        r_u = r_u * (T_maj * sigma_n / pdf);
+                        r_u = r_u * qn;
                         r_l = r_l * (T_maj * sigma_maj / pdf);
                         if (!(snz(beta) && snz(r_u))) { stop = true; ev = EV_END; }
                     }
@@ -2753,7 +2783,8 @@ __global__ void __launch_bounds__(256, kGray ? (kMed == 1 ? 3 : AVR_PATHS_WAVES_
                 const S sigma_n = sclamp0(sigma_maj - ms_a - ms_s);
                 const float pdf = sv0(T_maj) * sv0(sigma_maj);
                 T_ray = T_ray * (T_maj * sigma_n / pdf);
-                sr_l = sr_l * (T_maj * sigma_maj / pdf);
+                if constexpr (kGray) sr_l = sr_l * unit_quot(pdf);   // T_maj * sigma_maj is pdf's product
+                else sr_l = sr_l * (T_maj * sigma_maj / pdf);
                 sr_u = sr_u * (T_maj * sigma_n / pdf);
                 const S Tr = T_ray / savg(sr_l + sr_u);
                 if (smaxc(Tr) < 0.05f) {
