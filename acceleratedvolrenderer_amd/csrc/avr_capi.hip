@@ -1791,6 +1791,8 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
         p.max_depth = max_depth;
         p.seed = seed;
         p.pass_pixels = (int)P;
+        p.div_pixels = avr::fastdiv_make((uint32_t)P);
+        p.div_width = avr::fastdiv_make((uint32_t)c->film.width);
         p.pass_samples = S;
         p.sample_base = (int)base;
         p.stats = c->d_stats;

@@ -292,6 +292,8 @@ struct Params {
     // index holds pixel pix_order[j]; pix_slot is the inverse (pixel -> slot, read by k_film)
     const int *pix_order;
     const int *pix_slot;
+    FastDiv div_pixels;               // by pass_pixels
+    FastDiv div_width;                // by film.width
 };
 
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
@@ -1226,20 +1228,22 @@ __global__ void __launch_bounds__(256, AVR_CAM_WAVES) k_paths_camera(Params P) {
     // when the pass is quad-aligned (sample_base and pass_samples multiples of 4, log2 spp <=
     // 16; the host sets P.cam_quad), so each store still writes 16 consecutive pixels per wave
     const bool quad = kSmp != 0 && P.cam_quad;
-    for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < n; t += (long long)gridDim.x * blockDim.x) {
+    // (n < 2^31: the host bounds a pass by max_paths; 32-bit index arithmetic, FastDiv splits)
+    for (uint32_t tu = blockIdx.x * blockDim.x + threadIdx.x; tu < (uint32_t)n; tu += gridDim.x * blockDim.x) {
+        const int t = (int)tu;
         int slot, s;
         if (quad) {
-            const long long qd = t >> 2;
-            slot = (int)(qd % npix);
-            s = (int)(qd / npix) * 4 + (int)(t & 3);
+            const int qd = t >> 2, qs = fdiv(qd, P.div_pixels);
+            slot = fmod_(qd, qs, P.div_pixels);
+            s = qs * 4 + (t & 3);
         } else {
-            slot = (int)(t % npix);
-            s = (int)(t / npix);
+            s = fdiv(t, P.div_pixels);
+            slot = fmod_(t, s, P.div_pixels);
         }
         // the camera stage and k_paths walk the pass in slot order; slot -> pixel by pix_order
-        const long long id = (long long)s * npix + slot;
+        const int id = s * npix + slot;
         const int pix = P.pix_order ? P.pix_order[slot] : slot;
-        const int px = pix % P.film.width, py = pix / P.film.width;
+        const int py = fdiv(pix, P.div_width), px = fmod_(pix, py, P.div_width);
         PathSampler<kSmp> smp;
         if constexpr (kSmp == 0) {
             const uint64_t seq = hash_3u32((uint32_t)px, (uint32_t)py, (uint32_t)P.seed);
@@ -2497,9 +2501,10 @@ __global__ void __launch_bounds__(256, kGray ? (kMed == 1 ? 3 : AVR_PATHS_WAVES_
                     g = gn;
                     if constexpr (kZSobol) {
                         // the sample's ZSobol state past the camera draws and the first segment's three
-                        const int slot = g % npix, sIdx = g / npix;
+                        const int sIdx = fdiv(g, P.div_pixels), slot = fmod_(g, sIdx, P.div_pixels);
                         const int pix = P.pix_order ? P.pix_order[slot] : slot;
-                        smp.start(P, pix % P.film.width, pix / P.film.width, P.sample_base + sIdx);
+                        const int py = fdiv(pix, P.div_width);
+                        smp.start(P, fmod_(pix, py, P.div_width), py, P.sample_base + sIdx);
                         if constexpr (kUlAhead) s_ul[threadIdx.x] = ul5;
                         smp.z.dimension = 9;
                     } else {

@@ -16,6 +16,7 @@
 
 #define AVR_HD __host__ __device__ __forceinline__
 #include "avr_canon.h"
+#include "avr_fastdiv.h"
 
 namespace avr {
 
@@ -52,6 +53,7 @@ AVR_HD float fmaxf_(float a, float b) { return a < b ? b : a; }   // std::max se
 AVR_HD float lerp(float x, float a, float b) { return (1 - x) * a + x * b; }
 AVR_HD float sqr(float v) { return v * v; }
 AVR_HD float clampf(float v, float lo, float hi) { return v < lo ? lo : (v > hi ? hi : v); }
+
 
 // util/math.h:450-471, CPU branch (EvaluatePolynomial = nested std::fma)
 AVR_HD float fast_exp(float x) {
