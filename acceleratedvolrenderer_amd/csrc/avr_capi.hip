@@ -1553,11 +1553,17 @@ int avr_set_filter(avr_context *c, int type, const float radius[2], float sigma)
     t.resize((size_t)avr::smp::filter_blob_floats(nx, ny), 0.f);
     f = t.data();
     ccdf = f + nx * ny;
-    mcdf = ccdf + ny * (nx + 1) + ny;
+    cint = ccdf + ny * (nx + 1);
+    mcdf = cint + ny;
+    const float mint_v = t[(size_t)avr::smp::filter_table_floats(nx, ny) - 1];
     uint8_t *guide = (uint8_t *)(t.data() + avr::smp::filter_table_floats(nx, ny));
     for (int y = 0; y < ny; ++y)
         avr::smp::filter_guide_build(ccdf + (size_t)y * (nx + 1), nx, guide + (size_t)y * (avr::smp::kFilterGuideK + 1));
     avr::smp::filter_guide_build(mcdf, ny, guide + (size_t)ny * (avr::smp::kFilterGuideK + 1));
+    // the cell weights (after the guides)
+    float *wt = t.data() + avr::smp::filter_table_floats(nx, ny) + avr::smp::filter_guide_floats(ny);
+    for (int y = 0; y < ny; ++y)
+        for (int x = 0; x < nx; ++x) wt[(size_t)y * nx + x] = avr::smp::filter_cell_weight(f, cint, mint_v, nx, y, x);
     if (c->d_filter) (void)hipFree(c->d_filter);
     c->d_filter = nullptr;
     HIP_TRY(dalloc(&c->d_filter, t.size()));
@@ -1570,8 +1576,9 @@ int avr_set_filter(avr_context *c, int type, const float radius[2], float sigma)
     c->ftab.ccdf = c->d_filter + nx * ny;
     c->ftab.cint = c->ftab.ccdf + ny * (nx + 1);
     c->ftab.mcdf = c->ftab.cint + ny;
-    c->ftab.mint = t[(size_t)avr::smp::filter_table_floats(nx, ny) - 1];
+    c->ftab.mint = mint_v;
     c->ftab.guide = (const uint8_t *)(c->d_filter + avr::smp::filter_table_floats(nx, ny));
+    c->ftab.wt = c->d_filter + avr::smp::filter_table_floats(nx, ny) + avr::smp::filter_guide_floats(ny);
     c->filter_type = 1;
     return AVR_OK;
 }

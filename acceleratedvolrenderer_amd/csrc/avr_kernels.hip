@@ -990,18 +990,18 @@ __device__ __forceinline__ const float *stage_majorant(const DevMedium &m, float
 }
 
 // GaussianFilter's FilterSampler tables (pbrt's default radius 1.5: 48 x 48 function + CDFs,
-// ~19 KB, and their 6.3 KB of search guides) staged in LDS when they fit, so the camera
+// ~19 KB, their 6.3 KB of search guides and 9.2 KB of cell weights) staged in LDS when they fit, so the camera
 // sample's two guided searches run on LDS. Returns (after a block barrier) whether they were
 // staged; filter_lds_tables then describes the copy. The descriptor is built in registers from
 // the kernel arguments, not read back from LDS: its pointers then stay LDS-typed (ds_read, not
 // flat loads) and the first table read does not wait for a descriptor read.
-constexpr int kFiltLds = 6400;
+constexpr int kFiltLds = 8704;
 __device__ __forceinline__ bool stage_filter(const Params &P, float *s_filt) {
     bool staged = false;
     if (P.film.filter_type != 0) {
         const smp::FilterTables &g = P.film.gauss;
         const int nf = smp::filter_blob_floats(g.nx, g.ny);
-        if (g.guide && nf <= kFiltLds) {
+        if (g.guide && g.wt && nf <= kFiltLds) {
             const float *base = g.f;
             for (int i = threadIdx.x; i < nf; i += blockDim.x) s_filt[i] = base[i];
             staged = true;
@@ -1017,6 +1017,7 @@ __device__ __forceinline__ smp::FilterTables filter_lds_tables(const smp::Filter
     t.cint = t.ccdf + g.ny * (g.nx + 1);
     t.mcdf = t.cint + g.ny;
     t.guide = reinterpret_cast<const uint8_t *>(s_filt + smp::filter_table_floats(g.nx, g.ny));
+    t.wt = s_filt + smp::filter_table_floats(g.nx, g.ny) + smp::filter_guide_floats(g.ny);
     return t;
 }
 

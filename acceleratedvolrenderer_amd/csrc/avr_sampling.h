@@ -400,11 +400,24 @@ struct FilterTables {
     const float *f, *ccdf, *cint, *mcdf;
     float mint;
     const uint8_t *guide;
+    // Optional (null = none): the sample weight of every cell, f / (pdf0 * pdf1) evaluated on
+    // the host with the same float operations (filter_cell_weight), so a sample reads it
+    // instead of dividing three times
+    const float *wt;
 };
 AVR_HD int filter_table_floats(int nx, int ny) { return nx * ny + ny * (nx + 1) + ny + (ny + 1) + 1; }
 AVR_HD int filter_guide_bytes(int ny) { return (ny + 1) * (kFilterGuideK + 1); }
-// tables + guide, in floats (the guide's bytes follow the tables, padded to a float)
-AVR_HD int filter_blob_floats(int nx, int ny) { return filter_table_floats(nx, ny) + (filter_guide_bytes(ny) + 3) / 4; }
+AVR_HD int filter_guide_floats(int ny) { return (filter_guide_bytes(ny) + 3) / 4; }
+// tables | guide bytes (padded to a float) | cell weights, in floats
+AVR_HD int filter_blob_floats(int nx, int ny) { return filter_table_floats(nx, ny) + filter_guide_floats(ny) + nx * ny; }
+// GaussianFilter::Sample's weight for cell (v, u): f / (pdf0 * pdf1) with pdf1 = cint[v] / mint
+// and pdf0 = f / cint[v] (0 where the integral is 0), as pc1d_sample computes them
+AVR_HD float filter_cell_weight(const float *f, const float *cint, float mint, int nx, int v, int u) {
+    const float fv = f[(std::size_t)v * nx + u];
+    const float pdf1 = (mint > 0) ? cint[v] / mint : 0;
+    const float pdf0 = (cint[v] > 0) ? fv / cint[v] : 0;
+    return fv / (pdf0 * pdf1);
+}
 
 // FindInterval(n + 1, cdf[i] <= u), util/math.h:508-519, clamped to [0, n - 1] as pc1d_sample
 // uses it: for a non-decreasing cdf, the number of i in [1, n - 1] with cdf[i] <= u
@@ -440,23 +453,37 @@ inline void filter_guide_build(const float *cdf, int n, uint8_t *g) {
     for (int k = 0; k <= kFilterGuideK; ++k) g[k] = (uint8_t)find_interval(cdf, n, (float)k / (float)kFilterGuideK);
 }
 
-// Sample one PiecewiseConstant1D given as (cdf[n+1], func[n], funcInt) over [mn, mx]
+// The sample point of one PiecewiseConstant1D (cdf[n+1]) over [mn, mx] and its interval
 // (guide: the CDF's guide row, or null)
-AVR_HD float pc1d_sample(const float *cdf, const float *func, int n, float funcInt, float mn, float mx, float u,
-                         float *pdf, int *off, const uint8_t *guide = nullptr) {
+AVR_HD float pc1d_point(const float *cdf, int n, float mn, float mx, float u, int *off, const uint8_t *guide = nullptr) {
     const int o = guide ? find_interval_guided(cdf, n, guide, u) : find_interval(cdf, n, u);
     *off = o;
     float du = u - cdf[o];
     if (cdf[o + 1] - cdf[o] > 0) du /= cdf[o + 1] - cdf[o];
-    *pdf = (funcInt > 0) ? func[o] / funcInt : 0;
     const float t = (o + du) / (float)n;
     return (1 - t) * mn + t * mx;   // Lerp
+}
+// Sample one PiecewiseConstant1D given as (cdf[n+1], func[n], funcInt) over [mn, mx]
+AVR_HD float pc1d_sample(const float *cdf, const float *func, int n, float funcInt, float mn, float mx, float u,
+                         float *pdf, int *off, const uint8_t *guide = nullptr) {
+    const float x = pc1d_point(cdf, n, mn, mx, u, off, guide);
+    *pdf = (funcInt > 0) ? func[*off] / funcInt : 0;
+    return x;
 }
 
 // GaussianFilter::Sample(u) -> (p, weight = f[cell] / pdf)
 AVR_HD void gaussian_filter_sample(const FilterTables &T, float u0, float u1, float *px, float *py, float *weight) {
     float pdf1, pdf0;
     int v, uo;
+    if (T.wt) {   // the cell's weight from the table (a NaN entry: recomputed, its bits are the device's)
+        const uint8_t *gm = T.guide ? T.guide + (std::size_t)T.ny * (kFilterGuideK + 1) : nullptr;
+        *py = pc1d_point(T.mcdf, T.ny, -T.ry, T.ry, u1, &v, gm);
+        const uint8_t *gc = T.guide ? T.guide + (std::size_t)v * (kFilterGuideK + 1) : nullptr;
+        *px = pc1d_point(T.ccdf + (std::size_t)v * (T.nx + 1), T.nx, -T.rx, T.rx, u0, &uo, gc);
+        const float w = T.wt[(std::size_t)v * T.nx + uo];
+        *weight = w == w ? w : filter_cell_weight(T.f, T.cint, T.mint, T.nx, v, uo);
+        return;
+    }
     const uint8_t *gm = T.guide ? T.guide + (std::size_t)T.ny * (kFilterGuideK + 1) : nullptr;
     *py = pc1d_sample(T.mcdf, T.cint, T.ny, T.mint, -T.ry, T.ry, u1, &pdf1, &v, gm);
     const uint8_t *gc = T.guide ? T.guide + (std::size_t)v * (kFilterGuideK + 1) : nullptr;

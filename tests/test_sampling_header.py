@@ -73,6 +73,25 @@ def hdr(tmp_path_factory):
         "  unsigned char g[kFilterGuideK + 1]; filter_guide_build(cdf, n, g); int bad = 0;\n"
         "  for (int i = 0; i < nu; ++i) bad += find_interval_guided(cdf, n, g, u[i]) != find_interval(cdf, n, u[i]);\n"
         "  return bad; }\n"
+        "static void pcb(const float *f, int n, float mn, float mx, float *cdf, float *fi) {\n"
+        "  cdf[0] = 0; for (int i = 1; i <= n; ++i) cdf[i] = cdf[i - 1] + __builtin_fabsf(f[i - 1]) * (mx - mn) / n;\n"
+        "  *fi = cdf[n]; if (*fi == 0) for (int i = 1; i <= n; ++i) cdf[i] = float(i) / float(n);\n"
+        "  else for (int i = 1; i <= n; ++i) cdf[i] /= *fi; }\n"
+        "int fs_check(int nx, int ny, float rx, float ry, const float *f, int nu, const float *u) {\n"
+        "  float *cc = new float[ny * (nx + 1)], *ci = new float[ny], *mc = new float[ny + 1], mi;\n"
+        "  for (int y = 0; y < ny; ++y) pcb(f + y * nx, nx, -rx, rx, cc + y * (nx + 1), ci + y);\n"
+        "  pcb(ci, ny, -ry, ry, mc, &mi);\n"
+        "  unsigned char *g = new unsigned char[(ny + 1) * (kFilterGuideK + 1)]; float *w = new float[nx * ny];\n"
+        "  for (int y = 0; y < ny; ++y) filter_guide_build(cc + y * (nx + 1), nx, g + y * (kFilterGuideK + 1));\n"
+        "  filter_guide_build(mc, ny, g + ny * (kFilterGuideK + 1));\n"
+        "  for (int y = 0; y < ny; ++y) for (int x = 0; x < nx; ++x) w[y * nx + x] = filter_cell_weight(f, ci, mi, nx, y, x);\n"
+        "  FilterTables a{nx, ny, rx, ry, f, cc, ci, mc, mi, nullptr, nullptr}, b = a; b.guide = g; b.wt = w;\n"
+        "  int bad = 0;\n"
+        "  for (int i = 0; i < nu; ++i) { float p[3], q[3];\n"
+        "    gaussian_filter_sample(a, u[2 * i], u[2 * i + 1], p, p + 1, p + 2);\n"
+        "    gaussian_filter_sample(b, u[2 * i], u[2 * i + 1], q, q + 1, q + 2);\n"
+        "    bad += __builtin_memcmp(p, q, sizeof p) != 0; }\n"
+        "  delete[] cc; delete[] ci; delete[] mc; delete[] g; delete[] w; return bad; }\n"
         "float sob(unsigned long long a, int dim, unsigned seed, int scr) {\n"
         "  unsigned v = sobol_bits64((unsigned)a, (unsigned)(a >> 32), dim);\n"
         "  return u32_to_unit(scr ? fast_owen(v, seed) : v); }\n"
@@ -191,3 +210,24 @@ def test_filter_guided_find_interval_identical(hdr):
                             rng.random(4000).astype(np.float32), np.array([0, np.nextafter(np.float32(1), np.float32(0)), 1, -0.25], np.float32)])
         u = np.ascontiguousarray(u.astype(np.float32))
         assert hdr.fi_check(cdf.ctypes.data_as(F), len(f), len(u), u.ctypes.data_as(F)) == 0, len(f)
+
+
+@pytest.mark.parametrize("r,sigma", [(1.5, 0.5), (0.5, 0.5), (2.0, 0.3), (1.0, 1.0)])
+def test_filter_guided_weighted_sample_identical(hdr, r, sigma):
+    """GaussianFilter::Sample through the camera stage's tables (128-bucket guides + the cell
+    weights f / (pdf0 pdf1) evaluated on the host) returns the point and weight of the plain
+    binary-search, divide-per-sample path bit for bit: pbrt's default radius and others, random
+    u pairs plus u at 0 and just below 1."""
+    n = int(32 * r)
+    x = (np.arange(n, dtype=np.float32) + np.float32(0.5)) / np.float32(n)
+    p = ((np.float32(1) - x) * np.float32(-r) + x * np.float32(r)).astype(np.float32)
+    g1 = np.maximum(0, np.exp(-p.astype(np.float64) ** 2 / (2 * sigma ** 2)) - np.exp(-r * r / (2 * sigma ** 2)))
+    f = np.ascontiguousarray(np.outer(g1, g1).astype(np.float32))
+    rng = np.random.default_rng(3)
+    u = rng.random((20000, 2)).astype(np.float32)
+    u[:4] = [[0, 0], [0, np.nextafter(np.float32(1), np.float32(0))], [np.nextafter(np.float32(1), np.float32(0)), 0.5],
+             [0.5, 0.5]]
+    u = np.ascontiguousarray(u)
+    F = ctypes.POINTER(ctypes.c_float)
+    hdr.fs_check.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_float, ctypes.c_float, F, ctypes.c_int, F]
+    assert hdr.fs_check(n, n, r, r, f.ctypes.data_as(F), len(u), u.ctypes.data_as(F)) == 0

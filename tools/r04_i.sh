@@ -1,5 +1,6 @@
 #!/bin/bash
-# FastDiv index splits (camera stage + k_paths refill): the GPU suite, then bench lines at the
+# FastDiv index splits (camera stage + k_paths refill) and the Gaussian filter cell weights
+# precomputed on the host: the GPU suite, then bench lines at the
 # driver command; pass size 64 vs 128 / 32 sample indices (the drain's share of k_paths)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
