@@ -2502,10 +2502,11 @@ __global__ void __launch_bounds__(256, kGray ? (kMed == 1 ? 3 : AVR_PATHS_WAVES_
                     g = gn;
                     if constexpr (kZSobol) {
                         // the sample's ZSobol state past the camera draws and the first segment's three
-                        const int sIdx = fdiv(g, P.div_pixels), slot = fmod_(g, sIdx, P.div_pixels);
+                        // (hardware-sequence divisions: FastDiv splits here measured 1.2 % slower in
+                        // k_paths, profiles/r05_ab_unit_quot_fastdiv.json; the camera stage keeps them)
+                        const int slot = g % npix, sIdx = g / npix;
                         const int pix = P.pix_order ? P.pix_order[slot] : slot;
-                        const int py = fdiv(pix, P.div_width);
-                        smp.start(P, fmod_(pix, py, P.div_width), py, P.sample_base + sIdx);
+                        smp.start(P, pix % P.film.width, pix / P.film.width, P.sample_base + sIdx);
                         if constexpr (kUlAhead) s_ul[threadIdx.x] = ul5;
                         smp.z.dimension = 9;
                     } else {
