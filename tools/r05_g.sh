@@ -3,7 +3,7 @@
 # leg), its rocprofv3 kernel stats, and the section profiles (grid, NanoVDB) at the current build
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
-O=$GRAFT_REPO_ROOT/gpurun_out/r05/g
+O=$GRAFT_REPO_ROOT/gpurun_out/r05/${R05_PASS:-g}
 mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 600 python bench.py --steps 20 --warmup 5 > $O/bench_line.json 2> $O/bench_line.err || { tail -10 $O/bench_line.err; exit 1; }
