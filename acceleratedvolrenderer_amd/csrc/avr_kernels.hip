@@ -2109,11 +2109,26 @@ __global__ void __launch_bounds__(256, kGray ? (kMed == 1 ? 3 : AVR_PATHS_WAVES_
     __shared__ float s_ul[kSmp != 0 ? 256 : 1];
     // the host routes GridMedium majorant grids of more than 4096 cells to the wavefront kernels
     if constexpr (!kVdb) stage_majorant(P.med, s_maj);
+#ifndef AVR_VDB_MAJ_LDS
     const float *__restrict__ majp = kVdb ? P.med.majorant : s_maj;
+#endif
     // NanoVDB: the majorant's coarse occupancy level (one bit per cell pair, 16 KiB at 64^3;
     // 33 + 16 KiB per block keeps three blocks of 256 lanes per CU)
     __shared__ unsigned s_occ[kVdb ? kOccWords : 1];
     const bool useOcc = kVdb && P.med.occ != nullptr;
+#ifdef AVR_VDB_MAJ_LDS
+    // measurement variant (tools/vdb_maj_lds.py): a NanoVDB majorant of at most 4096 cells (a
+    // non-pbrt resolution, avr_set_majorant_res 16; the variant assumes it) read from LDS — staged
+    // in the occupancy level's 16 KiB, unused without it — instead of through L2: the same walk,
+    // only the majorant's memory path differs
+    float *const s_vmaj = reinterpret_cast<float *>(s_occ);
+    if constexpr (kVdb) {
+        for (int i = threadIdx.x; i < 4096; i += blockDim.x)
+            s_vmaj[i] = i < P.med.mres[0] * P.med.mres[1] * P.med.mres[2] + 1 ? P.med.majorant[i] : 0.f;
+        __syncthreads();
+    }
+    const float *__restrict__ majp = kVdb ? s_vmaj : s_maj;
+#endif
     if (useOcc) {
         const int nw = (P.med.mres[0] * P.med.mres[1] * P.med.mres[2] + 63) >> 6;
         for (int i = threadIdx.x; i < nw; i += blockDim.x) s_occ[i] = P.med.occ[i];

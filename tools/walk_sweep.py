@@ -30,6 +30,7 @@ def main():
     p.add_argument("--steps", type=int, default=4)
     p.add_argument("--rounds", type=int, default=2)
     p.add_argument("--pixelsamples", type=int, default=16384)
+    p.add_argument("--majorant-res", type=int, default=0, help="r^3 majorant instead of pbrt's (0)")
     a = p.parse_args()
     import torch
     from acceleratedvolrenderer_amd import VolPathIntegrator, scenes, capi
@@ -49,6 +50,8 @@ def main():
         scene = scenes.s_cloud(density, sampler="zsobol", spp=a.pixelsamples, filter="gaussian")
     S = 64
     integ = VolPathIntegrator(scene, maxdepth=scenes.CLOUD_MAXDEPTH, spp=S, seed=0, device=0)
+    if a.majorant_res:
+        integ.ctx.set_majorant_res((a.majorant_res,) * 3)
     npix = scene.film.width * scene.film.height
     cands = [(r, d) for r in ints(a.refills) for d in ints(a.ddas)]
     acc = {c: [0.0, 0.0, 0] for c in cands}
@@ -79,7 +82,7 @@ def main():
              "step_ms": round(v[1] / v[2], 4), "Msamples_s": round(npix * S / (v[1] / v[2] / 1e3) / 1e6, 2)}
             for c, v in acc.items()]
     integ.close()
-    print(json.dumps({"medium": a.medium, "res": n, "pixelsamples": a.pixelsamples, "steps_per_round": a.steps,
+    print(json.dumps({"medium": a.medium, "res": n, "majorant_res": a.majorant_res or None, "lib": os.environ.get("AVR_LIB"), "pixelsamples": a.pixelsamples, "steps_per_round": a.steps,
                       "rounds": a.rounds, "rows": rows}))
 
 
