@@ -2307,8 +2307,15 @@ __global__ void __launch_bounds__(256, kGray ? (kMed == 1 ? 3 : AVR_PATHS_WAVES_
                                 light = idx;
                                 T_ray = sr_l = sr_u = sconst<S>(1.f);
                                 // shadow-ray RNG (integrators.cpp:1338); u is its first draw
+#ifdef AVR_MEASURE_CHEAP_HASH
+                                // measurement only (other shadow-ray streams, statistically the
+                                // same work): a multiply-xor instead of the two MurmurHash64A
+                                seqA = ((uint64_t)f2u(po.x) * 0x9E3779B97F4A7C15ull) ^ f2u(po.y) ^ ((uint64_t)f2u(po.z) << 29);
+                                seqB = ((uint64_t)f2u(d.x) * 0xC2B2AE3D27D4EB4Full) ^ f2u(d.y) ^ ((uint64_t)f2u(d.z) << 29);
+#else
                                 seqA = hash_3u32(f2u(po.x), f2u(po.y), f2u(po.z));
                                 seqB = hash_3u32(f2u(d.x), f2u(d.y), f2u(d.z));
+#endif
                                 sd = d;
                                 segPending = true;
                                 mode = M_SHADOW;

@@ -288,7 +288,14 @@ template <typename M>
 AVR_HD M zsobol_index(M morton, uint32_t dimension, const ZSobolParams &zp) {
     if (zp.ptab && (int)dimension < zp.pdims) {
         const uint32_t pm = (uint32_t)(morton >> zp.log2spp);
+#if defined(AVR_MEASURE_NO_PTAB) && defined(AVR_KPATHS_TU)
+        // measurement only (wrong samples, statistically the same work): the pass-table entry
+        // from registers instead of its HBM / L2 read — the read's latency cost in k_paths
+        const uint64_t fake = ((uint64_t)pm * 0x9E3779B97F4A7C15ull) ^ ((uint64_t)dimension << 40);
+        return zsobol_index_pass<M>(morton, dimension, zp, fake);
+#else
         return zsobol_index_pass<M>(morton, dimension, zp, zp.ptab[(size_t)pm * (size_t)zp.pdims + dimension]);
+#endif
     }
     uint32_t up;
     const uint32_t pm = (uint32_t)(morton >> zp.log2spp);
