@@ -2400,6 +2400,9 @@ __global__ void __launch_bounds__(256, kGray ? (kMed == 1 ? 3 : AVR_PATHS_WAVES_
                     q1[j] = r1[j];
                 }
             }
+#ifdef AVR_SEC_SPLIT_PHASE
+            AVR_SEC(7)   // profiling variant: section 6 = the cooperative draws only, the rest of the phase handler into 7
+#endif
             if (ev == EV_PHASE) {
                 // phase-function sampling (integrators.cpp:1046-1061), then the next segment
                 AVR_COUNT(nPhase, 2);
@@ -2414,7 +2417,13 @@ __global__ void __launch_bounds__(256, kGray ? (kMed == 1 ? 3 : AVR_PATHS_WAVES_
                     smp.get2d(P, &up0, &up1);
                 }
                 float phPdf;
+#ifdef AVR_MEASURE_CHEAP_PHASE
+                // measurement only (other directions, statistically the same work): the hardware
+                // transcendentals of fast mode and multiply-xor seeds instead of two MurmurHash64A
+                const V3 wi = hg_sample_c<true>(-pd, m.hg, up0, up1, &phPdf);
+#else
                 const V3 wi = hg_sample_c<kFast>(-pd, m.hg, up0, up1, &phPdf);
+#endif
                 if (phPdf == 0) {
                     ev = EV_END;
                 } else {
@@ -2423,8 +2432,13 @@ __global__ void __launch_bounds__(256, kGray ? (kMed == 1 ? 3 : AVR_PATHS_WAVES_
                     pd = wi;
                     const float h0 = kCoopLds ? qr[2] : (kCoop ? q0[1] : smp.get1d(P));
                     const float h1 = kCoopLds ? qr[3] : (kCoop ? q0[2] : smp.get1d(P));
+#ifdef AVR_MEASURE_CHEAP_PHASE
+                    seqA = (uint64_t)f2u(h0) * 0x9E3779B97F4A7C15ull;
+                    seqB = (uint64_t)f2u(h1) * 0xC2B2AE3D27D4EB4Full;
+#else
                     seqA = hash_u32(f2u(h0));
                     seqB = hash_u32(f2u(h1));
+#endif
                     u = kCoopLds ? qr[4] : (kCoop ? q0[3] : smp.get1d(P));
                     sd = pd;
                     segPending = true;

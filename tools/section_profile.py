@@ -18,15 +18,14 @@ import sys
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-VARIANT = os.path.join(ROOT, "variants", "prof", "libavr_hip.so")
 NAMES = ["nee spawn", "refill", "segment starts", "dda walk", "collision", "shadow done", "phase sampling",
          "escape+end"]
 
 
-def build():
+def build(variant="prof", extra=()):
     sys.path.insert(0, ROOT)
     from acceleratedvolrenderer_amd import build as b
-    print(b.build(variant="prof", defines=["-DAVR_PROFILE_SECTIONS"]))
+    print(b.build(variant=variant, defines=["-DAVR_PROFILE_SECTIONS"] + list(extra)))
 
 
 def main():
@@ -39,10 +38,14 @@ def main():
     p.add_argument("--filter", default="gaussian")
     p.add_argument("--pixelsamples", type=int, default=16384, help="sampler pixelsamples (bench.py --steps 20: 16384)")
     p.add_argument("--pass-size", type=int, default=64, help="sample indices per pass (bench.py: 64)")
+    p.add_argument("--variant", default="prof", help="variants/<name> (e.g. profsplit)")
+    p.add_argument("--define", action="append", default=[],
+                   help="extra -D for --build (-DAVR_SEC_SPLIT_PHASE: section 'phase sampling' = its cooperative draws only, "
+                        "the rest of the phase handler counted under 'escape+end')")
     a = p.parse_args()
     if a.build:
-        return build()
-    os.environ["AVR_LIB"] = VARIANT
+        return build(a.variant, a.define)
+    os.environ["AVR_LIB"] = os.path.join(ROOT, "variants", a.variant, "libavr_hip.so")
     sys.path.insert(0, ROOT)
     import torch
     from acceleratedvolrenderer_amd import VolPathIntegrator, scenes, capi
@@ -77,7 +80,7 @@ def main():
     tot = sum(out[i] for i in range(8))
     res = {NAMES[i]: round(out[i] / tot, 4) for i in range(8)}
     st = integ.stats()
-    print(json.dumps({"medium": a.medium, "res": n, "pixelsamples": a.pixelsamples, "pass_size": S,
+    print(json.dumps({"variant": a.variant, "medium": a.medium, "res": n, "pixelsamples": a.pixelsamples, "pass_size": S,
                       "Msamples_per_s": 1280 * 720 * S * a.steps / dt / 1e6,
                       "section_share": res, "wave_cycles": tot, "loop_iterations": st.get("loop_iterations"),
                       "dda_steps": st.get("medium_dda_steps")}))
