@@ -1945,7 +1945,19 @@ __global__ void __launch_bounds__(256) k_bin_scatter(const int *__restrict__ que
 // enough lanes of its wave need service, so each event handler runs once per batch
 // instead of once per tracking iteration (SQ_INSTS_VALU showed the per-iteration union
 // of all branches, ~8k wave-instructions, dominating an eager state machine).
-enum : int { EV_NONE = 0, EV_SCATTER = 1, EV_SHADOW_DONE = 2, EV_PHASE = 3, EV_ESCAPE = 4, EV_END = 5 };
+enum : int { EV_NONE = 0, EV_SCATTER = 1, EV_SHADOW_DONE = 2, EV_PHASE = 3, EV_ESCAPE = 4, EV_END = 5, EV_PHASE_WAIT = 6 };
+// Phase requests pooled across the block's four waves (variant, -DAVR_POOL_PHASE=1): a lane that
+// needs phase sampling publishes its sampler state and wo to a per-thread LDS slot and parks
+// (EV_PHASE_WAIT); a wave serves every request pending in the block once at least
+// AVR_POOL_MIN are pending (or none of its own lanes is tracking), evaluating the draws and the
+// phase sample for all of them at once, and flags them done; each owner picks its results up.
+// No barrier: the waves meet only through LDS atomics on the pending / done masks.
+#ifndef AVR_POOL_PHASE
+#define AVR_POOL_PHASE 0
+#endif
+#ifndef AVR_POOL_MIN
+#define AVR_POOL_MIN 32
+#endif
 
 // Spectral-state type of k_paths: Spec (4 wavelengths) in general; float for a GRAY medium
 // (sigma_a and sigma_s tables constant over 360..830 nm, decided on the host). In a gray
@@ -2088,12 +2100,15 @@ __global__ void __launch_bounds__(256, kGray ? (kMed == 1 ? 3 : AVR_PATHS_WAVES_
     __shared__ float s_maj[kVdb ? 1 : 4096];
     // (a gray medium's sigma_a / sigma_s are one value each: the kernel takes them as scalars)
     constexpr int kSigTabs = kGray ? 0 : 2;
-    __shared__ float s_tab[(kSigTabs + 4) * kNTable];
+    // pooled phase requests: two LDS light tables instead of four (the slots below need the room)
+    constexpr bool kPoolDecl = kSmp != 0 && (kGray || AVR_COOP_SPEC) && AVR_NEE_AHEAD && AVR_COOP_LDS && AVR_POOL_PHASE;
+    constexpr int kLdsLights = kPoolDecl ? 2 : 4;
+    __shared__ float s_tab[(kSigTabs + kLdsLights) * kNTable];
     // ImageInfiniteLight shadow rays (non-delta NEE): the sampled (u, v), p_l and the phase
     // value per lane, parked here while the lane traces its shadow ray (off the VGPR budget)
     __shared__ float4 s_img[kImage ? 256 : 1];
     // ZSobol: the requesters' sampler state for the cooperative draws (coop_draws), 64 per wave
-    __shared__ uint3 s_zst[kSmp != 0 ? 256 : 1];
+    __shared__ uint3 s_zst[(kSmp != 0 && !kPoolDecl) ? 256 : 1];
     // NEE toward a delta light: the light's spectrum at the path's wavelengths and the phase
     // value f_hat, computed when the shadow ray is spawned and read back when it finishes
     // (SampleLd evaluates them once, integrators.cpp:1311-1331)
@@ -2106,7 +2121,17 @@ __global__ void __launch_bounds__(256, kGray ? (kMed == 1 ? 3 : AVR_PATHS_WAVES_
         for (int i = threadIdx.x; i < kDimHash; i += blockDim.x) s_dh[i] = smp::hash_2u32((uint32_t)i, (uint32_t)P.zs.seed);
     // ZSobol: each lane's next light-pick draw (SampleLd's 1D, integrators.cpp:1302), evaluated
     // ahead with the previous bounce's cooperative phase draws (or by the camera stage)
-    __shared__ float s_ul[kSmp != 0 ? 256 : 1];
+    __shared__ float s_ul[(kSmp != 0 && !kPoolDecl) ? 256 : 1];
+    // pooled phase requests, word-major (slot word k of thread t at s_pslot[k * 256 + t]):
+    // 0-2 sampler state (morton, hi, dimension) then wi, 3-5 wo then [3] phPdf [4-7] seqA / seqB,
+    // 6-9 the draws u0 u1 h0 h1, 10 the next segment's u, 11 the next light-pick draw (s_ul's role)
+    __shared__ float s_pslot[kPoolDecl ? 12 * 256 : 1];
+    __shared__ unsigned long long s_ppend[kPoolDecl ? 4 : 1], s_pdone[kPoolDecl ? 4 : 1];
+    __shared__ unsigned char s_plist[kPoolDecl ? 4 * 256 : 1];   // a serving wave's requester list
+    if constexpr (kPoolDecl) {
+        if (threadIdx.x < 4) s_ppend[threadIdx.x] = s_pdone[threadIdx.x] = 0;
+    }
+    float *const ul_slot = kPoolDecl ? s_pslot + 11 * 256 : s_ul;
     // the host routes GridMedium majorant grids of more than 4096 cells to the wavefront kernels
     if constexpr (!kVdb) stage_majorant(P.med, s_maj);
 #ifndef AVR_VDB_MAJ_LDS
@@ -2133,7 +2158,7 @@ __global__ void __launch_bounds__(256, kGray ? (kMed == 1 ? 3 : AVR_PATHS_WAVES_
         const int nw = (P.med.mres[0] * P.med.mres[1] * P.med.mres[2] + 63) >> 6;
         for (int i = threadIdx.x; i < nw; i += blockDim.x) s_occ[i] = P.med.occ[i];
     }
-    const int nlds = P.lights.n < 4 ? P.lights.n : 4;
+    const int nlds = P.lights.n < kLdsLights ? P.lights.n : kLdsLights;
     for (int i = threadIdx.x; i < kNTable; i += blockDim.x) {
         if constexpr (!kGray) {
             s_tab[i] = P.med.sigma_a[i];
@@ -2145,7 +2170,7 @@ __global__ void __launch_bounds__(256, kGray ? (kMed == 1 ? 3 : AVR_PATHS_WAVES_
     __syncthreads();
     const float *tab_sa = s_tab, *tab_ss = s_tab + kNTable;
     auto light_table = [&](int k) -> const float * {
-        return k < 4 ? s_tab + (kSigTabs + k) * kNTable : P.lights.list[k].L;
+        return k < kLdsLights ? s_tab + (kSigTabs + k) * kNTable : P.lights.list[k].L;
     };
 #if AVR_OPAQUE_CONSTS
     // a local copy whose loop-invariant scalars (grid and majorant resolutions, g, bounds) are
@@ -2206,7 +2231,9 @@ __global__ void __launch_bounds__(256, kGray ? (kMed == 1 ? 3 : AVR_PATHS_WAVES_
     constexpr bool kUlAhead = kCoop && AVR_NEE_AHEAD;
     // ... with the cooperative draws' results in LDS (coop_draws_lds)
     constexpr bool kCoopLds = kUlAhead && AVR_COOP_LDS;
-    __shared__ float s_res[kCoopLds ? 256 * 6 : 1];
+    __shared__ float s_res[(kCoopLds && !kPoolDecl) ? 256 * 6 : 1];
+    constexpr bool kPool = kPoolDecl;
+    static_assert(!kPool || kCoopLds, "pooled phase requests build on the LDS cooperative draws");
     PathSampler<kSmp> smp{};
     int depth = 0;
     V3 po{}, pd{};         // segment origin (== the path vertex) and the path's ray direction
@@ -2250,7 +2277,7 @@ __global__ void __launch_bounds__(256, kGray ? (kMed == 1 ? 3 : AVR_PATHS_WAVES_
                 const V3 wo = -pd;
                 float ul;
                 if constexpr (kUlAhead) {
-                    ul = s_ul[threadIdx.x];   // drawn ahead (same sampler dimension)
+                    ul = ul_slot[threadIdx.x];   // drawn ahead (same sampler dimension)
                     smp.z.dimension += 1;
                 } else {
                     ul = smp.get1d(P);
@@ -2367,6 +2394,127 @@ __global__ void __launch_bounds__(256, kGray ? (kMed == 1 ? 3 : AVR_PATHS_WAVES_
             }
         }
         AVR_SEC(6)
+        if constexpr (kPool) {
+            constexpr auto WG = __HIP_MEMORY_SCOPE_WORKGROUP;
+            const int wv = threadIdx.x >> 6, tid = threadIdx.x;
+            // (1) publish: the sampler state and wo of every lane that needs phase sampling
+            const uint64_t pub = __ballot(ev == EV_PHASE);
+            if (pub) {
+                if (ev == EV_PHASE) {
+                    AVR_COUNT(nPhase, 2);
+                    s_pslot[tid] = __uint_as_float(smp.z.morton);
+                    s_pslot[256 + tid] = __uint_as_float(smp.z.hi);
+                    s_pslot[512 + tid] = __uint_as_float(smp.z.dimension);
+                    s_pslot[768 + tid] = -pd.x;
+                    s_pslot[1024 + tid] = -pd.y;
+                    s_pslot[1280 + tid] = -pd.z;
+                    smp.z.dimension += 5;
+                    ev = EV_PHASE_WAIT;
+                }
+                if (lane == __ffsll((long long)pub) - 1) __hip_atomic_fetch_or(&s_ppend[wv], pub, __ATOMIC_RELEASE, WG);
+            }
+            // (2) serve every pending request of the block once enough are pending, or when none
+            // of this wave's lanes is tracking (nothing else to run)
+            if (__ballot(ev == EV_PHASE_WAIT)) {
+                int total = 0;
+                _Pragma("unroll") for (int k = 0; k < 4; ++k)
+                    total += __popcll(__hip_atomic_load(&s_ppend[k], __ATOMIC_RELAXED, WG));
+                const uint64_t tracking = __ballot((mode == M_MEDIUM || mode == M_SHADOW) && ev == EV_NONE);
+                if (total >= AVR_POOL_MIN || (total > 0 && tracking == 0)) {
+                    uint64_t take[4];
+                    _Pragma("unroll") for (int k = 0; k < 4; ++k) {
+                        unsigned long long tk = 0;
+                        if (lane == 0) tk = __hip_atomic_exchange(&s_ppend[k], 0ull, __ATOMIC_ACQ_REL, WG);
+                        take[k] = __shfl(tk, 0);
+                    }
+                    const int c0 = __popcll(take[0]), c1 = __popcll(take[1]), c2 = __popcll(take[2]);
+                    const int n = c0 + c1 + c2 + __popcll(take[3]);
+                    unsigned char *lst = s_plist + wv * 256;
+                    const uint64_t lt = lane == 0 ? 0ull : ((~0ull) >> (64 - lane));
+                    if ((take[0] >> lane) & 1ull) lst[__popcll(take[0] & lt)] = (unsigned char)lane;
+                    if ((take[1] >> lane) & 1ull) lst[c0 + __popcll(take[1] & lt)] = (unsigned char)(64 + lane);
+                    if ((take[2] >> lane) & 1ull) lst[c0 + c1 + __popcll(take[2] & lt)] = (unsigned char)(128 + lane);
+                    if ((take[3] >> lane) & 1ull) lst[c0 + c1 + c2 + __popcll(take[3] & lt)] = (unsigned char)(192 + lane);
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                    // the five draws of every requester (phase 2D at +0, h0 h1 u at +2..4, the next
+                    // light pick at +5), spread over the wave as coop_draws_lds does for one wave
+                    for (int c = 0; c < 5 * n; c += 64) {
+                        const int t5 = c + lane;
+                        if (t5 < 5 * n) {
+                            const int r = t5 / 5, j = t5 - r * 5;
+                            const int R = lst[r];
+                            smp::ZSobol q;
+                            q.morton = __float_as_uint(s_pslot[R]);
+                            q.hi = __float_as_uint(s_pslot[256 + R]);
+                            q.dimension = 0;
+                            const uint32_t d0 = __float_as_uint(s_pslot[512 + R]);
+                            const int o = j == 0 ? 0 : j + 1;   // dimension offsets 0, 2, 3, 4, 5
+                            const int w = 6 + o;                // slot words 6-7, 8, 9, 10, 11
+                            float v0, v1;
+                            q.template draw_at<PathSampler<kSmp>::kW>(P.zs, d0 + (uint32_t)o, j == 0, &v0, &v1,
+                                                                        AVR_DIM_HASH ? s_dh : nullptr, AVR_DIM_HASH ? kDimHash : 0);
+                            s_pslot[w * 256 + R] = v0;
+                            if (j == 0) s_pslot[(w + 1) * 256 + R] = v1;
+                        }
+                    }
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                    // phase-function sampling (integrators.cpp:1046-1061) and the next segment's
+                    // RNG seeds, one lane per requester
+                    for (int c = 0; c < n; c += 64) {
+                        const int r = c + lane;
+                        if (r < n) {
+                            const int R = lst[r];
+                            const V3 wo = {s_pslot[768 + R], s_pslot[1024 + R], s_pslot[1280 + R]};
+                            const float up0 = s_pslot[1536 + R], up1 = s_pslot[1792 + R];
+                            const float h0 = s_pslot[2048 + R], h1 = s_pslot[2304 + R];
+                            float phPdf;
+                            const V3 wi = hg_sample_c<kFast>(wo, m.hg, up0, up1, &phPdf);
+                            const uint64_t a = hash_u32(f2u(h0)), b = hash_u32(f2u(h1));
+                            s_pslot[R] = wi.x;
+                            s_pslot[256 + R] = wi.y;
+                            s_pslot[512 + R] = wi.z;
+                            s_pslot[768 + R] = phPdf;
+                            s_pslot[1024 + R] = __uint_as_float((uint32_t)a);
+                            s_pslot[1280 + R] = __uint_as_float((uint32_t)(a >> 32));
+                            s_pslot[1536 + R] = __uint_as_float((uint32_t)b);
+                            s_pslot[1792 + R] = __uint_as_float((uint32_t)(b >> 32));
+                        }
+                    }
+                    if (lane == 0) {
+                        _Pragma("unroll") for (int k = 0; k < 4; ++k)
+                            if (take[k]) __hip_atomic_fetch_or(&s_pdone[k], take[k], __ATOMIC_RELEASE, WG);
+                    }
+                }
+                // (3) pick up this wave's finished requests (served here or by another wave)
+                const uint64_t dn = __shfl(lane == 0 ? __hip_atomic_load(&s_pdone[wv], __ATOMIC_ACQUIRE, WG) : 0ull, 0);
+                const bool fin = ev == EV_PHASE_WAIT && ((dn >> lane) & 1ull);
+                const uint64_t finMask = __ballot(fin);
+                if (finMask) {
+                    if (lane == 0) __hip_atomic_fetch_and(&s_pdone[wv], ~finMask, __ATOMIC_RELAXED, WG);
+                    if (fin) {
+                        const float phPdf = s_pslot[768 + tid];
+                        if (phPdf == 0) {
+                            ev = EV_END;
+                        } else {
+                            beta = beta * unit_quot(phPdf);
+                            r_l = r_u / phPdf;
+                            pd = {s_pslot[tid], s_pslot[256 + tid], s_pslot[512 + tid]};
+                            seqA = ((uint64_t)__float_as_uint(s_pslot[1280 + tid]) << 32) | __float_as_uint(s_pslot[1024 + tid]);
+                            seqB = ((uint64_t)__float_as_uint(s_pslot[1792 + tid]) << 32) | __float_as_uint(s_pslot[1536 + tid]);
+                            u = s_pslot[2560 + tid];
+                            sd = pd;
+                            segPending = true;
+                            mode = M_MEDIUM;
+                            ev = EV_NONE;
+                        }
+                    }
+                }
+            }
+        } else
         if (__ballot(ev == EV_PHASE)) {
             // ZSobol: the phase 2D draw and the next segment's three 1D draws of every lane in
             // EV_PHASE, evaluated cooperatively by the whole wave
@@ -2543,7 +2691,7 @@ __global__ void __launch_bounds__(256, kGray ? (kMed == 1 ? 3 : AVR_PATHS_WAVES_
                         const int slot = g % npix, sIdx = g / npix;
                         const int pix = P.pix_order ? P.pix_order[slot] : slot;
                         smp.start(P, pix % P.film.width, pix / P.film.width, P.sample_base + sIdx);
-                        if constexpr (kUlAhead) s_ul[threadIdx.x] = ul5;
+                        if constexpr (kUlAhead) ul_slot[threadIdx.x] = ul5;
                         smp.z.dimension = 9;
                     } else {
                         smp.rng.state = ((uint64_t)c5.y << 32) | c5.x;
@@ -2602,7 +2750,7 @@ __global__ void __launch_bounds__(256, kGray ? (kMed == 1 ? 3 : AVR_PATHS_WAVES_
             AVR_SEC(3)
             const bool busy = (mode == M_MEDIUM || mode == M_SHADOW) && ev == EV_NONE;
             const uint64_t busyNow = __ballot(busy);
-            const uint64_t service = __ballot(mode != M_DONE && !busy);
+            const uint64_t service = __ballot(mode != M_DONE && !busy && (!kPool || ev != EV_PHASE_WAIT));
             if (busyNow == 0 || __popcll(service) >= P.refill_min) break;
             ++nIter;
             nActive += __popcll(busyNow);
