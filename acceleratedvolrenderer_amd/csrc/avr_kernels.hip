@@ -1945,7 +1945,8 @@ __global__ void __launch_bounds__(256) k_bin_scatter(const int *__restrict__ que
 // enough lanes of its wave need service, so each event handler runs once per batch
 // instead of once per tracking iteration (SQ_INSTS_VALU showed the per-iteration union
 // of all branches, ~8k wave-instructions, dominating an eager state machine).
-enum : int { EV_NONE = 0, EV_SCATTER = 1, EV_SHADOW_DONE = 2, EV_PHASE = 3, EV_ESCAPE = 4, EV_END = 5, EV_PHASE_WAIT = 6 };
+enum : int { EV_NONE = 0, EV_SCATTER = 1, EV_SHADOW_DONE = 2, EV_PHASE = 3, EV_ESCAPE = 4, EV_END = 5, EV_PHASE_WAIT = 6,
+              EV_NEE_WAIT = 7 };
 // Phase requests pooled across the block's four waves (variant, -DAVR_POOL_PHASE=1): a lane that
 // needs phase sampling publishes its sampler state and wo to a per-thread LDS slot and parks
 // (EV_PHASE_WAIT); a wave serves every request pending in the block once at least
@@ -1957,6 +1958,10 @@ enum : int { EV_NONE = 0, EV_SCATTER = 1, EV_SHADOW_DONE = 2, EV_PHASE = 3, EV_E
 #endif
 #ifndef AVR_POOL_MIN
 #define AVR_POOL_MIN 32
+#endif
+// ... and the NEE spawns toward delta lights the same way (-DAVR_POOL_NEE=1, with AVR_POOL_PHASE)
+#ifndef AVR_POOL_NEE
+#define AVR_POOL_NEE 0
 #endif
 
 // Spectral-state type of k_paths: Spec (4 wavelengths) in general; float for a GRAY medium
@@ -2127,9 +2132,13 @@ __global__ void __launch_bounds__(256, kGray ? (kMed == 1 ? 3 : AVR_PATHS_WAVES_
     // 6-9 the draws u0 u1 h0 h1, 10 the next segment's u, 11 the next light-pick draw (s_ul's role)
     __shared__ float s_pslot[kPoolDecl ? 12 * 256 : 1];
     __shared__ unsigned long long s_ppend[kPoolDecl ? 4 : 1], s_pdone[kPoolDecl ? 4 : 1];
+    constexpr bool kPoolNee = kPoolDecl && AVR_POOL_NEE && !kImage;
+    __shared__ unsigned long long s_npend[kPoolNee ? 4 : 1], s_ndone[kPoolNee ? 4 : 1];
     __shared__ unsigned char s_plist[kPoolDecl ? 4 * 256 : 1];   // a serving wave's requester list
     if constexpr (kPoolDecl) {
         if (threadIdx.x < 4) s_ppend[threadIdx.x] = s_pdone[threadIdx.x] = 0;
+        if constexpr (kPoolNee)
+            if (threadIdx.x < 4) s_npend[threadIdx.x] = s_ndone[threadIdx.x] = 0;
     }
     float *const ul_slot = kPoolDecl ? s_pslot + 11 * 256 : s_ul;
     // the host routes GridMedium majorant grids of more than 4096 cells to the wavefront kernels
@@ -2271,6 +2280,124 @@ __global__ void __launch_bounds__(256, kGray ? (kMed == 1 ? 3 : AVR_PATHS_WAVES_
         AVR_SEC(0)
         opaque_consts();
         // =================== batched event handlers (each runs once per batch) ===========
+        if constexpr (kPoolNee) {
+            // SampleLd toward a delta light (integrators.cpp:1282-1338), pooled across the block's
+            // waves like the phase requests: slot words 0-2 po, 3-5 wo, 6-9 lambda, 11 the drawn-
+            // ahead light pick in; 0-2 the shadow ray's d, 3-6 seqA / seqB, 7 the light or -1 out
+            constexpr auto WG = __HIP_MEMORY_SCOPE_WORKGROUP;
+            const int wv = threadIdx.x >> 6, tid = threadIdx.x;
+            const uint64_t pub = __ballot(ev == EV_SCATTER);
+            if (pub) {
+                if (ev == EV_SCATTER) {
+                    s_pslot[tid] = po.x;
+                    s_pslot[256 + tid] = po.y;
+                    s_pslot[512 + tid] = po.z;
+                    s_pslot[768 + tid] = -pd.x;
+                    s_pslot[1024 + tid] = -pd.y;
+                    s_pslot[1280 + tid] = -pd.z;
+                    s_pslot[1536 + tid] = lam.v0;
+                    s_pslot[1792 + tid] = lam.v1;
+                    s_pslot[2048 + tid] = lam.v2;
+                    s_pslot[2304 + tid] = lam.v3;
+                    smp.z.dimension += 3;                // the light pick (drawn ahead) and uLight
+                    L = L + Spec::c(0.f);                // L += SampleLd(...) == 0 unless a shadow ray spawns
+                    ev = EV_NEE_WAIT;
+                }
+                if (lane == __ffsll((long long)pub) - 1) __hip_atomic_fetch_or(&s_npend[wv], pub, __ATOMIC_RELEASE, WG);
+            }
+            if (__ballot(ev == EV_NEE_WAIT)) {
+                int total = 0;
+                _Pragma("unroll") for (int k = 0; k < 4; ++k)
+                    total += __popcll(__hip_atomic_load(&s_npend[k], __ATOMIC_RELAXED, WG));
+                const uint64_t tracking = __ballot((mode == M_MEDIUM || mode == M_SHADOW) && ev == EV_NONE);
+                if (total >= AVR_POOL_MIN || (total > 0 && tracking == 0)) {
+                    uint64_t take[4];
+                    _Pragma("unroll") for (int k = 0; k < 4; ++k) {
+                        unsigned long long tk = 0;
+                        if (lane == 0) tk = __hip_atomic_exchange(&s_npend[k], 0ull, __ATOMIC_ACQ_REL, WG);
+                        take[k] = __shfl(tk, 0);
+                    }
+                    const int c0 = __popcll(take[0]), c1 = __popcll(take[1]), c2 = __popcll(take[2]);
+                    const int n = c0 + c1 + c2 + __popcll(take[3]);
+                    unsigned char *lst = s_plist + wv * 256;
+                    const uint64_t lt = lane == 0 ? 0ull : ((~0ull) >> (64 - lane));
+                    if ((take[0] >> lane) & 1ull) lst[__popcll(take[0] & lt)] = (unsigned char)lane;
+                    if ((take[1] >> lane) & 1ull) lst[c0 + __popcll(take[1] & lt)] = (unsigned char)(64 + lane);
+                    if ((take[2] >> lane) & 1ull) lst[c0 + c1 + __popcll(take[2] & lt)] = (unsigned char)(128 + lane);
+                    if ((take[3] >> lane) & 1ull) lst[c0 + c1 + c2 + __popcll(take[3] & lt)] = (unsigned char)(192 + lane);
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                    for (int c = 0; c < n; c += 64) {
+                        const int r = c + lane;
+                        if (r < n) {
+                            const int R = lst[r];
+                            const V3 rpo = {s_pslot[R], s_pslot[256 + R], s_pslot[512 + R]};
+                            const V3 wo = {s_pslot[768 + R], s_pslot[1024 + R], s_pslot[1280 + R]};
+                            const Spec rlam = {s_pslot[1536 + R], s_pslot[1792 + R], s_pslot[2048 + R], s_pslot[2304 + R]};
+                            const float ul = ul_slot[R];
+                            int out = -1;
+                            V3 d{};
+                            uint64_t sa = 0, sb = 0;
+                            if (P.lights.n > 0) {
+                                float pmf = 0.f;
+                                const int idx = light_pick<kImage>(P.lights, ul, &pmf);
+                                if (idx >= 0) {
+                                    const DevLight &lt = P.lights.list[idx];
+                                    if (lt.type == 0) {
+                                        const V3 wi = {lt.w[0], lt.w[1], lt.w[2]};
+                                        const Spec Ls = sample_table(light_table(idx), lambda_index(rlam)) * lt.scale;
+                                        const float fval = hg_eval_c(dot(wo, wi), m.hg);
+                                        if (Ls.nonzero() && fval != 0) {
+                                            s_ls[R] = to4(Ls);
+                                            s_fhat[R] = fval;
+                                            const V3 pOut = rpo + wi * (2 * P.lights.scene_radius);
+                                            d = pOut - rpo;
+                                            sa = hash_3u32(f2u(rpo.x), f2u(rpo.y), f2u(rpo.z));
+                                            sb = hash_3u32(f2u(d.x), f2u(d.y), f2u(d.z));
+                                            out = idx;
+                                        }
+                                    }
+                                }
+                            }
+                            s_pslot[R] = d.x;
+                            s_pslot[256 + R] = d.y;
+                            s_pslot[512 + R] = d.z;
+                            s_pslot[768 + R] = __uint_as_float((uint32_t)sa);
+                            s_pslot[1024 + R] = __uint_as_float((uint32_t)(sa >> 32));
+                            s_pslot[1280 + R] = __uint_as_float((uint32_t)sb);
+                            s_pslot[1536 + R] = __uint_as_float((uint32_t)(sb >> 32));
+                            s_pslot[1792 + R] = __int_as_float(out);
+                        }
+                    }
+                    if (lane == 0) {
+                        _Pragma("unroll") for (int k = 0; k < 4; ++k)
+                            if (take[k]) __hip_atomic_fetch_or(&s_ndone[k], take[k], __ATOMIC_RELEASE, WG);
+                    }
+                }
+                const uint64_t dn = __shfl(lane == 0 ? __hip_atomic_load(&s_ndone[wv], __ATOMIC_ACQUIRE, WG) : 0ull, 0);
+                const bool fin = ev == EV_NEE_WAIT && ((dn >> lane) & 1ull);
+                const uint64_t finMask = __ballot(fin);
+                if (finMask) {
+                    if (lane == 0) __hip_atomic_fetch_and(&s_ndone[wv], ~finMask, __ATOMIC_RELAXED, WG);
+                    if (fin) {
+                        const int idx = __float_as_int(s_pslot[1792 + tid]);
+                        ev = EV_PHASE;                       // unless a shadow ray is spawned
+                        if (idx >= 0) {
+                            light = idx;
+                            T_ray = sr_l = sr_u = sconst<S>(1.f);
+                            seqA = ((uint64_t)__float_as_uint(s_pslot[1024 + tid]) << 32) | __float_as_uint(s_pslot[768 + tid]);
+                            seqB = ((uint64_t)__float_as_uint(s_pslot[1536 + tid]) << 32) | __float_as_uint(s_pslot[1280 + tid]);
+                            sd = {s_pslot[tid], s_pslot[256 + tid], s_pslot[512 + tid]};
+                            segPending = true;
+                            mode = M_SHADOW;
+                            ev = EV_NONE;
+                            AVR_COUNT(nShadow, 4);
+                        }
+                    }
+                }
+            }
+        } else
         if (__ballot(ev == EV_SCATTER)) {
             if (ev == EV_SCATTER) {
                 // SampleLd: light pick (BVH infinite-light branch) + shadow-ray spawn (1282-1338)
@@ -2750,7 +2877,7 @@ __global__ void __launch_bounds__(256, kGray ? (kMed == 1 ? 3 : AVR_PATHS_WAVES_
             AVR_SEC(3)
             const bool busy = (mode == M_MEDIUM || mode == M_SHADOW) && ev == EV_NONE;
             const uint64_t busyNow = __ballot(busy);
-            const uint64_t service = __ballot(mode != M_DONE && !busy && (!kPool || ev != EV_PHASE_WAIT));
+            const uint64_t service = __ballot(mode != M_DONE && !busy && (!kPool || (ev != EV_PHASE_WAIT && ev != EV_NEE_WAIT)));
             if (busyNow == 0 || __popcll(service) >= P.refill_min) break;
             ++nIter;
             nActive += __popcll(busyNow);
