@@ -3,6 +3,8 @@
 # builds whose samples are wrong but statistically the same work): the ZSobol pass-table reads
 # of the cooperative draws (-DAVR_MEASURE_NO_PTAB) and the NEE spawn's two MurmurHash64A
 # (-DAVR_MEASURE_CHEAP_HASH), against the in-tree build, alternating
+# build first (CPU): python -m acceleratedvolrenderer_amd.build noptab -DAVR_MEASURE_NO_PTAB
+#                   python -m acceleratedvolrenderer_amd.build cheaphash -DAVR_MEASURE_CHEAP_HASH
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp

@@ -2,6 +2,8 @@
 # round-5 pass m: how the phase handler's cycles split between its cooperative ZSobol draws and
 # the per-lane rest (section profiles prof / profsplit), and an upper bound for cheapening the
 # per-lane rest (-DAVR_MEASURE_CHEAP_PHASE: hardware transcendentals + multiply-xor seeds)
+# build first (CPU): python tools/section_profile.py --build; python tools/section_profile.py --build --variant profsplit
+#   --define=-DAVR_SEC_SPLIT_PHASE; python -m acceleratedvolrenderer_amd.build cheapphase -DAVR_MEASURE_CHEAP_PHASE
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 O=$GRAFT_REPO_ROOT/gpurun_out/r05/m

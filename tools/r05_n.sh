@@ -2,6 +2,8 @@
 # round-5 pass n: phase requests pooled across a block's waves (-DAVR_POOL_PHASE=1, variants
 # pool32 / pool16 = AVR_POOL_MIN): replay parity of the variant (the GPU parity suite and the
 # driver-configuration full-size replay through AVR_LIB), then A/B bench lines against in-tree
+# build first (CPU): python -m acceleratedvolrenderer_amd.build pool32 -DAVR_POOL_PHASE=1 -DAVR_POOL_MIN=32 (pool16: 16;
+#   poolboth32: also -DAVR_POOL_NEE=1)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 O=$GRAFT_REPO_ROOT/gpurun_out/r05/n
