@@ -1888,11 +1888,12 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
                             for (int k = 0; k < 6; ++k) same = same && key[k] == c->zs_akey[k];
                             if (!same) {
                                 hipLaunchKernelGGL(avr::k_zsobol_pass_table,
-                                                   dim3(blocks_for((long long)c->film.width * c->film.height * c->zs_pdims,
+                                                   dim3(blocks_for((long long)c->film.width * c->film.height * (c->zs_pdims / 2),
                                                                    256, 256 * 64)),
                                                    dim3(256), 0, c->stream, zs, c->film.width, c->film.height, c->zs_pdims,
                                                    plo + 2, (base >> (plo + 2)) << (plo + 2), c->d_zs_atab,
-                                                   (const uint64_t *)nullptr);
+                                                   (const uint64_t *)nullptr, avr::fastdiv_make((uint32_t)(c->zs_pdims / 2)),
+                                                   avr::fastdiv_make((uint32_t)c->film.width));
                                 HIP_TRY(hipGetLastError());
                                 for (int k = 0; k < 6; ++k) c->zs_akey[k] = key[k];
                             }
@@ -1901,10 +1902,11 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
                     }
                     if (c->d_zs_ptab) {
                         hipLaunchKernelGGL(avr::k_zsobol_pass_table,
-                                           dim3(blocks_for((long long)c->film.width * c->film.height * c->zs_pdims, 256,
+                                           dim3(blocks_for((long long)c->film.width * c->film.height * (c->zs_pdims / 2), 256,
                                                            256 * 64)),
                                            dim3(256), 0, c->stream, zs, c->film.width, c->film.height, c->zs_pdims, plo,
-                                           base, c->d_zs_ptab, atab);
+                                           base, c->d_zs_ptab, atab, avr::fastdiv_make((uint32_t)(c->zs_pdims / 2)),
+                                           avr::fastdiv_make((uint32_t)c->film.width));
                         HIP_TRY(hipGetLastError());
                         p.zs.ptab = c->d_zs_ptab;
                         p.zs.pdims = c->zs_pdims;
@@ -2259,6 +2261,12 @@ int avr_last_pass_samples(avr_context *c, float *L, float *lambda, float *pdf, l
         // k_paths' records (L) and its camera stage's wavelengths and pdfs, as k_film read them
         HIP_TRY(hipMemcpy(L, c->ps.rec, n * sizeof(float4), hipMemcpyDeviceToHost));
         HIP_TRY(hipMemcpy(lambda, c->ps.cam2, n * sizeof(float4), hipMemcpyDeviceToHost));
+        if (AVR_FILM_PDF && AVR_CAM_CANON_LDS) {   // k_film evaluates them: recompute for the accessor
+            avr::DevFilm f = c->film;
+            hipLaunchKernelGGL(avr::k_lambda_pdfs, dim3(blocks_for(n)), dim3(256), 0, c->stream, f, c->ps.cam2, c->ps.cam4, n);
+            HIP_TRY(hipGetLastError());
+            HIP_TRY(hipStreamSynchronize(c->stream));
+        }
         HIP_TRY(hipMemcpy(pdf, c->ps.cam4, n * sizeof(float4), hipMemcpyDeviceToHost));
         if (!c->h_pix_slot.empty()) {   // slot order -> pixel order
             const long long np = (long long)c->film.width * c->film.height;

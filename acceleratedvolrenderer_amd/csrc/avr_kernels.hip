@@ -1212,6 +1212,13 @@ __device__ __forceinline__ float u32_to_unit_exp(uint32_t v) { return (float)(v 
 #ifndef AVR_CAM_WAVES
 #define AVR_CAM_WAVES 1   // minimum waves per SIMD asked of k_paths_camera (1: the compiler's choice)
 #endif
+// The wavelength pdfs evaluated by k_film from the wavelengths (the same canonical function on the
+// same floats, so the same bits) instead of by the camera stage and carried in cam4: 16 B less
+// written and read per sample, and the four f64 cosh move from the VALU-bound camera stage to
+// the HBM-bound film kernel (1: on)
+#ifndef AVR_FILM_PDF
+#define AVR_FILM_PDF 1
+#endif
 template <int kSmp, bool kFast>
 __global__ void __launch_bounds__(256, AVR_CAM_WAVES) k_paths_camera(Params P) {
     __shared__ float s_filt[kFiltLds];
@@ -1320,8 +1327,10 @@ __global__ void __launch_bounds__(256, AVR_CAM_WAVES) k_paths_camera(Params P) {
 #else
 #if AVR_CAM_CANON_LDS
         const Spec lam = kFast ? film_sample_lambda_fast(P.film, ulam) : film_sample_lambda(P.film, ulam, s_canon);
+#if !AVR_FILM_PDF
         const Spec pdf = {film_lambda_pdf(P.film, lam.v0, s_canon), film_lambda_pdf(P.film, lam.v1, s_canon),
                           film_lambda_pdf(P.film, lam.v2, s_canon), film_lambda_pdf(P.film, lam.v3, s_canon)};
+#endif
 #else
         const Spec lam = kFast ? film_sample_lambda_fast(P.film, ulam) : film_sample_lambda(P.film, ulam);
         const Spec pdf = {film_lambda_pdf(P.film, lam.v0), film_lambda_pdf(P.film, lam.v1),
@@ -1389,7 +1398,9 @@ __global__ void __launch_bounds__(256, AVR_CAM_WAVES) k_paths_camera(Params P) {
         P.ps.cam1[id] = make_float4(ray.d.x, ray.d.y, ray.d.z, (kSmp != 0 && AVR_UL_IN_CAM1) ? ulight : fweight);
         P.ps.cam2[id] = to4(lam);
         P.ps.cam3[id] = make_uint4((uint32_t)seqA, (uint32_t)(seqA >> 32), (uint32_t)seqB, (uint32_t)(seqB >> 32));
+#if !AVR_FILM_PDF || !AVR_CAM_CANON_LDS
         P.ps.cam4[id] = to4(pdf);
+#endif
         P.ps.camw[id] = fweight;
         if constexpr (kSmp == 0)
             P.ps.cam5[id] = make_uint4((uint32_t)smp.rng.state, (uint32_t)(smp.rng.state >> 32), (uint32_t)smp.rng.inc,
@@ -3152,12 +3163,14 @@ __global__ void __launch_bounds__(256, kGray ? (kMed == 1 ? 3 : AVR_PATHS_WAVES_
 // One sample of the pass: L, the wavelengths, their pdfs and CameraSample::filterWeight —
 // after k_paths: L from its record, the rest from its camera stage (k_paths_camera); after the
 // wavefront kernels: their SoA (pdfs recomputed with the sampling function's pdf)
-__device__ __forceinline__ void film_load_sample(const Params &P, size_t id, Spec *L, Spec *lam, Spec *pdf, float *w) {
+__device__ __forceinline__ void film_load_sample(const Params &P, size_t id, Spec *L, Spec *lam, Spec *pdf, float *w,
+                                                 const double *canon_tabs) {
     *w = 1.f;
     if (P.rec_mode) {
         *L = spec4(P.ps.rec[id]);
         *lam = spec4(P.ps.cam2[id]);
-        *pdf = spec4(P.ps.cam4[id]);
+        // with AVR_FILM_PDF the pdfs are evaluated from the wavelengths after the loads (film_pdfs)
+        if (!(AVR_FILM_PDF && AVR_CAM_CANON_LDS)) *pdf = spec4(P.ps.cam4[id]);
         if (P.film.filter_type != 0) *w = P.ps.camw[id];
     } else {
         *L = spec4(P.ps.L[id]);
@@ -3165,6 +3178,23 @@ __device__ __forceinline__ void film_load_sample(const Params &P, size_t id, Spe
         *pdf = {film_lambda_pdf(P.film, lam->v0), film_lambda_pdf(P.film, lam->v1), film_lambda_pdf(P.film, lam->v2),
                 film_lambda_pdf(P.film, lam->v3)};
         if (P.film.filter_type != 0) *w = P.ps.weight[id];
+    }
+}
+// the camera stage's wavelength pdfs (film_lambda_pdf: the same canonical function of the same
+// floats, so the same bits) when k_film evaluates them (AVR_FILM_PDF with k_paths' records)
+__device__ __forceinline__ void film_pdfs(const Params &P, const Spec &lam, Spec *pdf, const double *canon_tabs) {
+    if (AVR_FILM_PDF && AVR_CAM_CANON_LDS && P.rec_mode)
+        *pdf = {film_lambda_pdf(P.film, lam.v0, canon_tabs), film_lambda_pdf(P.film, lam.v1, canon_tabs),
+                film_lambda_pdf(P.film, lam.v2, canon_tabs), film_lambda_pdf(P.film, lam.v3, canon_tabs)};
+}
+// The pass's wavelength pdfs into cam4 for the host accessor (avr_last_pass_samples) when the
+// camera stage leaves them to k_film (AVR_FILM_PDF): the same function of the same wavelengths
+__global__ void __launch_bounds__(256) k_lambda_pdfs(DevFilm film, const float4 *__restrict__ lam, float4 *__restrict__ pdf,
+                                                     long long n) {
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+        const float4 l = lam[i];
+        pdf[i] = make_float4(film_lambda_pdf(film, l.x), film_lambda_pdf(film, l.y), film_lambda_pdf(film, l.z),
+                             film_lambda_pdf(film, l.w));
     }
 }
 // The X, Y, Z matching tables interleaved per wavelength ({X, Y, Z, 0}, staged in LDS by
@@ -3215,6 +3245,10 @@ __global__ void __launch_bounds__(256) k_film(Params P) {
     __shared__ float4 s_xyz[kNTable];
     for (int i = threadIdx.x; i < kNTable; i += blockDim.x)
         s_xyz[i] = make_float4(P.film.xyz[i], P.film.xyz[kNTable + i], P.film.xyz[2 * kNTable + i], 0.f);
+    __shared__ double s_canon[AVR_FILM_PDF ? canon::kCanonTabDoubles : 1];   // the pdfs' cosh tables
+    if constexpr (AVR_FILM_PDF)
+        for (int i = threadIdx.x; i < canon::kCanonTabDoubles; i += blockDim.x)
+            s_canon[i] = i < 128 ? canon::kLogInvC[i] : (i < 256 ? canon::kLogC[i - 128] : canon::kExp2J64[i - 256]);
     __syncthreads();
     const int npix = P.pass_pixels;
     const int nb = kBuckets ? P.film.nbuckets : 0;
@@ -3265,13 +3299,15 @@ __global__ void __launch_bounds__(256) k_film(Params P) {
             Spec L[kFilmBatch], lam[kFilmBatch], pdf[kFilmBatch];
             float w[kFilmBatch];
             _Pragma("unroll") for (int k = 0; k < kFilmBatch; ++k)
-                film_load_sample(P, (size_t)(s + k) * npix + slot, &L[k], &lam[k], &pdf[k], &w[k]);
+                film_load_sample(P, (size_t)(s + k) * npix + slot, &L[k], &lam[k], &pdf[k], &w[k], s_canon);
+            _Pragma("unroll") for (int k = 0; k < kFilmBatch; ++k) film_pdfs(P, lam[k], &pdf[k], s_canon);
             _Pragma("unroll") for (int k = 0; k < kFilmBatch; ++k) add(L[k], lam[k], pdf[k], w[k]);
         }
         for (; s < P.pass_samples; ++s) {
             Spec L, lam, pdf;
             float w;
-            film_load_sample(P, (size_t)s * npix + slot, &L, &lam, &pdf, &w);
+            film_load_sample(P, (size_t)s * npix + slot, &L, &lam, &pdf, &w, s_canon);
+            film_pdfs(P, lam, &pdf, s_canon);
             add(L, lam, pdf, w);
         }
         if (ldsBuckets)
@@ -3548,27 +3584,39 @@ __global__ void __launch_bounds__(256) k_zsobol_table(smp::ZSobolParams zp, int 
 // from its level-A entry by zsobol_pass_entry_from (one MixBits instead of ~5).
 __global__ void __launch_bounds__(256) k_zsobol_pass_table(smp::ZSobolParams zp, int width, int height, int pdims,
                                                            int plo, long long base, uint64_t *__restrict__ table,
-                                                           const uint64_t *__restrict__ atab) {
-    // 32-bit indices (the host checks width * height * pdims < 2^31): 64-bit divisions by a
-    // run-time divisor are ~100 instructions each, more than the entry's own digits
-    const uint32_t n = (uint32_t)width * (uint32_t)height * (uint32_t)pdims;
+                                                           const uint64_t *__restrict__ atab, FastDiv div_pairs,
+                                                           FastDiv div_width) {
+    // one thread per PAIR of dimensions of a pixel's row (pdims is even, avr_set_sampler_pass_table):
+    // 16-B loads and stores, and the pixel / Morton index arithmetic once per two entries;
+    // 32-bit indices (the host checks width * height * pdims < 2^31) split by multiply-shift
+    const uint32_t half = (uint32_t)pdims >> 1;
+    const uint32_t n = (uint32_t)width * (uint32_t)height * half;
     const bool wide = smp::zsobol_wide(zp);
     for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
-        const uint32_t pix = k / (uint32_t)pdims;
-        const int d = (int)(k - pix * (uint32_t)pdims);
-        const uint32_t py = pix / (uint32_t)width;
-        const uint32_t pm = (uint32_t)smp::encode_morton2(pix - py * (uint32_t)width, py);
+        const int pix = fdiv((int)k, div_pairs);
+        const int d = 2 * (int)(k - (uint32_t)pix * half);
+        const int py = fdiv(pix, div_width);
+        const uint32_t pm = (uint32_t)smp::encode_morton2((uint32_t)(pix - py * width), (uint32_t)py);
         const uint64_t m = ((uint64_t)pm << zp.log2spp) | (uint64_t)base;
         const size_t row = (size_t)pm * pdims + d;
+        ulonglong2 e;
         if (atab) {
-            const uint64_t eA = atab[row];
-            table[row] = wide ? smp::zsobol_pass_entry_from<uint64_t>(m, (uint32_t)d, zp, plo, eA)
-                              : smp::zsobol_pass_entry_from<uint32_t>((uint32_t)m, (uint32_t)d, zp, plo, eA);
-            continue;
+            const ulonglong2 eA = *reinterpret_cast<const ulonglong2 *>(atab + row);
+            e.x = wide ? smp::zsobol_pass_entry_from<uint64_t>(m, (uint32_t)d, zp, plo, eA.x)
+                       : smp::zsobol_pass_entry_from<uint32_t>((uint32_t)m, (uint32_t)d, zp, plo, eA.x);
+            e.y = wide ? smp::zsobol_pass_entry_from<uint64_t>(m, (uint32_t)d + 1, zp, plo, eA.y)
+                       : smp::zsobol_pass_entry_from<uint32_t>((uint32_t)m, (uint32_t)d + 1, zp, plo, eA.y);
+        } else {
+            auto up_of = [&](int dd) -> uint32_t {
+                return (zp.upper && dd < zp.dmax) ? zp.upper[(size_t)pm * zp.dmax + dd] : smp::zsobol_upper(pm, (uint32_t)dd, zp);
+            };
+            const uint32_t u0 = up_of(d), u1 = up_of(d + 1);
+            e.x = wide ? smp::zsobol_pass_entry<uint64_t>(m, (uint32_t)d, zp, plo, u0)
+                       : smp::zsobol_pass_entry<uint32_t>((uint32_t)m, (uint32_t)d, zp, plo, u0);
+            e.y = wide ? smp::zsobol_pass_entry<uint64_t>(m, (uint32_t)d + 1, zp, plo, u1)
+                       : smp::zsobol_pass_entry<uint32_t>((uint32_t)m, (uint32_t)d + 1, zp, plo, u1);
         }
-        const uint32_t up = (zp.upper && d < zp.dmax) ? zp.upper[(size_t)pm * zp.dmax + d] : smp::zsobol_upper(pm, (uint32_t)d, zp);
-        table[row] = wide ? smp::zsobol_pass_entry<uint64_t>(m, (uint32_t)d, zp, plo, up)
-                                             : smp::zsobol_pass_entry<uint32_t>((uint32_t)m, (uint32_t)d, zp, plo, up);
+        *reinterpret_cast<ulonglong2 *>(table + row) = e;
     }
 }
 

@@ -56,9 +56,10 @@ ZSOBOL_TABLE_BYTES_PER_DRAW = 4
 ZSOBOL_PASS_BYTES_PER_DRAW = 8   # the per-pass table's entries (avr_set_sampler_pass_table)
 ZSOBOL_DRAWS_PER_PHASE = 5
 ZSOBOL_CAMERA_DRAWS = 6
-# the camera stage writes cam0, cam1, cam2, cam3, cam4 (5 x 16 B), the 4-B filter weight and, for
-# the independent sampler, cam5 (16 B PCG32 state)
-BYTES_CAMERA_WRITE = {"zsobol": 84, "independent": 100}
+# the camera stage writes cam0, cam1, cam2, cam3 (4 x 16 B), the 4-B filter weight and, for the
+# independent sampler, cam5 (16 B PCG32 state); the wavelength pdfs (cam4 until round 5) are
+# evaluated by k_film from the wavelengths (AVR_FILM_PDF)
+BYTES_CAMERA_WRITE = {"zsobol": 68, "independent": 84}
 RGB_CPU_MAX_RES = 512   # the rgb-explosion CPU baseline copies its 3 grids to the host (6 GiB at 512^3)
 
 
@@ -133,7 +134,7 @@ def roofline_block(agg, launches, sampler, medium, emissive, zsobol_table, pass_
 
 
 def camera_bytes(samples, sampler, zsobol_table=True, pass_dims=0, pixels=0, launches=1):
-    """The camera stage's algorithmic bytes for `samples` samples: its records (88 / 100 B per
+    """The camera stage's algorithmic bytes for `samples` samples: its records (68 / 84 B per
     sample) + the ZSobol table entries (6 draws per quad of 4 samples of one pixel) + with the
     pass table, its per-pass build (an 8-B entry written and a 4-B pixel-table entry read per
     pixel and dimension, once per launch)."""

@@ -62,14 +62,14 @@ def test_lookup_bytes_by_medium():
 
 
 def test_camera_bytes():
-    assert bench.camera_bytes(4, "zsobol") == 4 * 84 + 6 * 4
-    assert bench.camera_bytes(4, "zsobol", zsobol_table=False) == 4 * 84
-    assert bench.camera_bytes(4, "independent") == 400
+    assert bench.camera_bytes(4, "zsobol") == 4 * 68 + 6 * 4
+    assert bench.camera_bytes(4, "zsobol", zsobol_table=False) == 4 * 68
+    assert bench.camera_bytes(4, "independent") == 4 * 84
     # the per-pass ZSobol table: 8-B entries per draw, and its build (8 B written + 4 B of the
     # pixel table read per pixel and dimension) once per launch
-    assert bench.camera_bytes(4, "zsobol", pass_dims=64, pixels=2, launches=1) == 4 * 84 + 6 * 8 + 2 * 64 * 12
+    assert bench.camera_bytes(4, "zsobol", pass_dims=64, pixels=2, launches=1) == 4 * 68 + 6 * 8 + 2 * 64 * 12
     assert bench.camera_bytes(8, "zsobol", zsobol_table=False, pass_dims=16, pixels=2, launches=2) == \
-        8 * 84 + 12 * 8 + 2 * 2 * 16 * 8
+        8 * 68 + 12 * 8 + 2 * 2 * 16 * 8
     agg = {"medium_lookups": 0, "shadow_lookups": 0, "medium_items_in": 0, "medium_items_out": 1000,
            "medium_dda_steps": 0}
     assert bench.kpaths_bytes(agg, "zsobol", pass_table=True)[2]["zsobol_table_reads"] == 40 * 1000
