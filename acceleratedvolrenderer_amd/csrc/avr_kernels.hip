@@ -3240,7 +3240,10 @@ constexpr int kFilmBatch = AVR_FILM_BATCH;
 inline size_t film_lds_bytes(int nb) { return nb > 0 && nb <= kFilmLdsBuckets ? 2 * (size_t)nb * 256 * sizeof(double) : 0; }
 // kBuckets: a SpectralFilm (P.film.nbuckets > 0); RGBFilm's instantiation has no bucket code
 template <bool kBuckets>
-__global__ void __launch_bounds__(256) k_film(Params P) {
+#ifndef AVR_FILM_WAVES
+#define AVR_FILM_WAVES 1   // minimum waves per SIMD asked of k_film (1: the compiler's choice)
+#endif
+__global__ void __launch_bounds__(256, AVR_FILM_WAVES) k_film(Params P) {
     extern __shared__ double s_bk[];   // [sum | weight][bucket][thread]: film_lds_bytes(nb)
     __shared__ float4 s_xyz[kNTable];
     for (int i = threadIdx.x; i < kNTable; i += blockDim.x)
