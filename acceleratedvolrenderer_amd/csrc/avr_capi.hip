@@ -159,6 +159,8 @@ struct avr_context {
     // for every k_paths pass: the digits its sample indices share; zs_pdims 0 = no table
     uint64_t *d_zs_ptab = nullptr;
     size_t zs_ptab_cap = 0;   // entries allocated
+    uint64_t *d_zs_ctab = nullptr;   // the camera stage's compact copy (6 entries per pixel)
+    size_t zs_ctab_cap = 0;
     int zs_pdims = 96;
     // Level-A pass table (the same table for plo + 2, shared by four consecutive passes);
     // zs_akey names the build it holds (rebuilt when any field changes), zs_two_level 0 = off
@@ -765,6 +767,7 @@ int avr_context_destroy(avr_context *c) {
     for (auto &b : c->d_light_img) if (b) (void)hipFree(b), b = nullptr;
     if (c->d_zs_table) (void)hipFree(c->d_zs_table);
     if (c->d_zs_ptab) (void)hipFree(c->d_zs_ptab);
+    if (c->d_zs_ctab) (void)hipFree(c->d_zs_ctab);
     if (c->d_zs_atab) (void)hipFree(c->d_zs_atab);
     if (c->d_image) (void)hipFree(c->d_image);
     if (c->d_reference) (void)hipFree(c->d_reference);
@@ -1893,7 +1896,7 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
                                                    dim3(256), 0, c->stream, zs, c->film.width, c->film.height, c->zs_pdims,
                                                    plo + 2, (base >> (plo + 2)) << (plo + 2), c->d_zs_atab,
                                                    (const uint64_t *)nullptr, avr::fastdiv_make((uint32_t)(c->zs_pdims / 2)),
-                                                   avr::fastdiv_make((uint32_t)c->film.width));
+                                                   avr::fastdiv_make((uint32_t)c->film.width), (uint64_t *)nullptr);
                                 HIP_TRY(hipGetLastError());
                                 for (int k = 0; k < 6; ++k) c->zs_akey[k] = key[k];
                             }
@@ -1901,14 +1904,30 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
                         }
                     }
                     if (c->d_zs_ptab) {
+                        // the camera stage's six entries per pixel (dimensions 0, 1, 6..9) also as a
+                        // compact scanline-ordered copy (48 B per pixel), when the table holds them
+                        const size_t need_c = c->zs_pdims >= 10 ? 6 * (size_t)P : 0;
+                        if (need_c > c->zs_ctab_cap) {
+                            if (c->d_zs_ctab) (void)hipFree(c->d_zs_ctab);
+                            c->d_zs_ctab = nullptr;
+                            c->zs_ctab_cap = 0;
+                            if (hipMalloc((void **)&c->d_zs_ctab, need_c * sizeof(uint64_t)) != hipSuccess) {
+                                (void)hipGetLastError();
+                                c->d_zs_ctab = nullptr;   // no room: the camera reads the rows
+                            } else {
+                                c->zs_ctab_cap = need_c;
+                            }
+                        }
+                        uint64_t *ctab = need_c ? c->d_zs_ctab : nullptr;
                         hipLaunchKernelGGL(avr::k_zsobol_pass_table,
                                            dim3(blocks_for((long long)c->film.width * c->film.height * (c->zs_pdims / 2), 256,
                                                            256 * 64)),
                                            dim3(256), 0, c->stream, zs, c->film.width, c->film.height, c->zs_pdims, plo,
                                            base, c->d_zs_ptab, atab, avr::fastdiv_make((uint32_t)(c->zs_pdims / 2)),
-                                           avr::fastdiv_make((uint32_t)c->film.width));
+                                           avr::fastdiv_make((uint32_t)c->film.width), ctab);
                         HIP_TRY(hipGetLastError());
                         p.zs.ptab = c->d_zs_ptab;
+                        p.zs.ctab = ctab;
                         p.zs.pdims = c->zs_pdims;
                         p.zs.plo = plo;
                     }

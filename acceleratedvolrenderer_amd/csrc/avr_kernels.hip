@@ -1099,7 +1099,9 @@ __device__ __forceinline__ void zsobol_index_quad_pair(M morton, const smp::ZSob
     if (i < iTop) {
         const int shift = 2 * i - pw;
         const M higher = shift + 2 >= kBits ? M(0) : M(morton >> (shift + 2));
-        p = smp::mix_perm24<M>((M)(higher ^ (M)(0x55555555u * (q < 2 ? dA : dB))));
+        // (the quad's lanes mix digits pw and pw + 1, whose prefixes straddle 2^32 for wide indices:
+        // one 64-bit sequence for all instead of both branches of the narrow fast path)
+        p = smp::mix_perm24<M, false>((M)(higher ^ (M)(0x55555555u * (q < 2 ? dA : dB))));
     }
     const uint32_t pA0 = quad_bcast<0>(p), pA1 = quad_bcast<1>(p), pB0 = quad_bcast<2>(p), pB1 = quad_bcast<3>(p);
     auto assemble = [&](uint64_t e, uint32_t d, uint32_t p0, uint32_t p1) -> M {
@@ -1271,8 +1273,11 @@ __global__ void __launch_bounds__(256, AVR_CAM_WAVES) k_paths_camera(Params P) {
                 const uint32_t pmk = PathSampler<kSmp>::kW == 2
                                          ? (uint32_t)((((uint64_t)smp.z.hi << 32) | smp.z.morton) >> P.zs.log2spp)
                                          : smp.z.morton >> P.zs.log2spp;
-                const ulonglong2 *row = reinterpret_cast<const ulonglong2 *>(P.zs.ptab + (size_t)pmk * (size_t)P.zs.pdims);
-                const ulonglong2 r01 = row[0], r67 = row[3], r89 = row[4];
+                // the pixel's compact copy (48 B, pixels consecutive along the wave) when built,
+                // else its pass-table row
+                const ulonglong2 *row = P.zs.ctab ? reinterpret_cast<const ulonglong2 *>(P.zs.ctab + 6 * (size_t)pix)
+                                                  : reinterpret_cast<const ulonglong2 *>(P.zs.ptab + (size_t)pmk * (size_t)P.zs.pdims);
+                const ulonglong2 r01 = row[0], r67 = row[P.zs.ctab ? 1 : 3], r89 = row[P.zs.ctab ? 2 : 4];
                 pe0 = r01.x; pe1 = r01.y; pe6 = r67.x; pe7 = r67.y; pe8 = r89.x; pe9 = r89.y;
                 pe_ok = true;
             }
@@ -3588,7 +3593,7 @@ __global__ void __launch_bounds__(256) k_zsobol_table(smp::ZSobolParams zp, int 
 __global__ void __launch_bounds__(256) k_zsobol_pass_table(smp::ZSobolParams zp, int width, int height, int pdims,
                                                            int plo, long long base, uint64_t *__restrict__ table,
                                                            const uint64_t *__restrict__ atab, FastDiv div_pairs,
-                                                           FastDiv div_width) {
+                                                           FastDiv div_width, uint64_t *__restrict__ ctab) {
     // one thread per PAIR of dimensions of a pixel's row (pdims is even, avr_set_sampler_pass_table):
     // 16-B loads and stores, and the pixel / Morton index arithmetic once per two entries;
     // 32-bit indices (the host checks width * height * pdims < 2^31) split by multiply-shift
@@ -3620,6 +3625,9 @@ __global__ void __launch_bounds__(256) k_zsobol_pass_table(smp::ZSobolParams zp,
                        : smp::zsobol_pass_entry<uint32_t>((uint32_t)m, (uint32_t)d + 1, zp, plo, u1);
         }
         *reinterpret_cast<ulonglong2 *>(table + row) = e;
+        // the camera stage's pairs (0, 1), (6, 7), (8, 9) also into its compact per-pixel copy
+        if (ctab && (d == 0 || d == 6 || d == 8))
+            *reinterpret_cast<ulonglong2 *>(ctab + 6 * (size_t)pix + (d == 0 ? 0 : d - 4)) = e;
     }
 }
 

@@ -110,6 +110,10 @@ struct ZSobolParams {
     // pass's above their low `plo` bits (the host builds it per pass; null = not used)
     const uint64_t *ptab;
     int pdims, plo;
+    // Optional compact copy of the pass table's entries the camera stage reads (dimensions 0, 1
+    // and 6..9, in that order, 48 B per pixel in scanline order) so its loads stream instead of
+    // gathering 48 B from each pixel's row (null = read the rows)
+    const uint64_t *ctab;
 };
 
 // Morton(pixel) << log2(spp) | sampleIndex fits 32 bits (nBase4Digits <= 16: e.g. 1024 spp
@@ -118,11 +122,13 @@ AVR_HD bool zsobol_wide(const ZSobolParams &zp) { return zp.nBase4Digits > 16; }
 
 // (MixBits(x) >> 24) % 24 (util/hash.h:84-92) with the 40-bit quotient split into 32-bit
 // pieces: 2^32 = 16 (mod 24). M = 32-bit: x zero-extended, so v ^= v >> 31 is done in 32 bits.
-template <typename M>
+template <typename M, bool kNarrow = true>
 AVR_HD uint32_t mix_perm24(M x) {
     // a 64-bit prefix below 2^32 mixes exactly as its 32-bit value (x >> 31 < 2 either way): the
     // sample digits of indices up to 34 bits (e.g. 4096 spp at 720p) keep the 32-bit multiplies
-    if (sizeof(M) == 8 && ((uint64_t)x >> 32) == 0) return mix_perm24<uint32_t>((uint32_t)x);
+    // (kNarrow false: always the 64-bit sequence — for lanes of one wave that would split between
+    // the two, where the branch runs both)
+    if (kNarrow && sizeof(M) == 8 && ((uint64_t)x >> 32) == 0) return mix_perm24<uint32_t>((uint32_t)x);
     uint64_t v = sizeof(M) == 4 ? (uint64_t)(uint32_t)(x ^ (x >> 31)) : ((uint64_t)x ^ ((uint64_t)x >> 31));
     v *= 0x7fb5d329728ea185ull;
     v ^= v >> 27;
@@ -391,6 +397,7 @@ inline ZSobolParams zsobol_params(int spp, int width, int height, int seed) {
     zp.ptab = nullptr;
     zp.pdims = 0;
     zp.plo = 0;
+    zp.ctab = nullptr;
     return zp;
 }
 
