@@ -1817,13 +1817,14 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
                 HIP_TRY(dalloc(&c->d_advance, 2 * (size_t)S));
                 c->advance_cap = S;
             }
-            hipLaunchKernelGGL(avr::k_advance, dim3((S + 255) / 256), dim3(256), 0, c->stream, c->d_advance,
-                               (long long)base, S);
-            HIP_TRY(hipGetLastError());
+            if (c->sampler_kind == 0) {   // read by the IndependentSampler's camera stage only
+                hipLaunchKernelGGL(avr::k_advance, dim3((S + 255) / 256), dim3(256), 0, c->stream, c->d_advance,
+                                   (long long)base, S);
+                HIP_TRY(hipGetLastError());
+            }
             p.advance = c->d_advance;
             walk_schedule(c, c->refill_min, c->dda_budget, &p.refill_min, &p.dda_budget);   // defaults: measured optima
-            p.heads = c->d_heads;
-            HIP_TRY(hipMemsetAsync(c->d_heads, 0, 8 * sizeof(int), c->stream));
+            p.heads = c->d_heads;   // zeroed by the camera stage (k_paths_camera), which runs first
             // the camera stage: one lane per sample (k_paths_camera)
             {
                 const int sv = c->sampler_kind == 0 ? 0 : (avr::smp::zsobol_wide(p.zs) ? 2 : 1);

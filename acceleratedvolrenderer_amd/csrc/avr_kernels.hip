@@ -1231,6 +1231,9 @@ __global__ void __launch_bounds__(256, AVR_CAM_WAVES) k_paths_camera(Params P) {
     __shared__ uint64_t s_cdh[kCamDimHash];
     if constexpr (kSmp != 0)
         if (threadIdx.x < kCamDimHash) s_cdh[threadIdx.x] = smp::hash_2u32(threadIdx.x, (uint32_t)P.zs.seed);
+    // the pass's per-XCD work counters of k_paths, zeroed here (stream order: after the previous
+    // pass's k_paths, before this pass's) instead of by a separate fill
+    if (blockIdx.x == 0 && threadIdx.x < 8) P.heads[threadIdx.x] = 0;
     const bool ftab_lds = stage_filter(P, s_filt);   // (its barrier covers s_canon and s_cdh)
     const int npix = P.pass_pixels;
     const long long n = (long long)npix * P.pass_samples;
