@@ -346,7 +346,8 @@ int avr_set_sampler_table(avr_context *ctx, int dims);
  * level-A table it is derived from), rows = Morton(width - 1, height - 1) + 1 — 1.64 M rows at
  * 720p, 1.26 GB per table at 96 dimensions, up to ~4x the pixel count for non-square films —
  * allocated lazily by the first render, only with >= 8 GiB of HBM to spare (else the pixel
- * table serves every draw), next to max_paths' records. */
+ * table serves every draw), next to max_paths' records; with dims >= 10 also a 48-B per-pixel
+ * copy of the camera stage's six entries (44 MB at 720p). */
 int avr_set_sampler_pass_table(avr_context *ctx, int dims);
 
 /* Render sample indices [spp_begin, spp_end) of every pixel (the avr_set_sampler sampler,
