@@ -51,6 +51,9 @@ int fail(int code, const std::string &msg) {
 #ifndef AVR_ZS_TWO_LEVEL
 #define AVR_ZS_TWO_LEVEL 1   // build the ZSobol pass table from a level-A table shared by 4 passes
 #endif
+#ifndef AVR_ZS_PACK
+#define AVR_ZS_PACK 0   // 1: pass-table entries carry the next digit's 4 candidate permutations (zsobol_pass_pack; measured slower: profiles/r05_ab_pass_pack.json)
+#endif
 
 template <typename T>
 hipError_t dalloc(T **p, size_t n) { return hipMalloc((void **)p, std::max<size_t>(n, 1) * sizeof(T)); }
@@ -161,6 +164,7 @@ struct avr_context {
     size_t zs_ptab_cap = 0;   // entries allocated
     uint64_t *d_zs_ctab = nullptr;   // the camera stage's compact copy (6 entries per pixel)
     size_t zs_ctab_cap = 0;
+    int zs_pack = AVR_ZS_PACK;        // pack the next digit's permutations into pass entries
     int zs_pdims = 96;
     // Level-A pass table (the same table for plo + 2, shared by four consecutive passes);
     // zs_akey names the build it holds (rebuilt when any field changes), zs_two_level 0 = off
@@ -1920,15 +1924,24 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
                             }
                         }
                         uint64_t *ctab = need_c ? c->d_zs_ctab : nullptr;
+                        // the permutations of the digit under the perm-fixed one, packed into the
+                        // entries when their fixed prefix fits 36 bits (zsobol_pass_pack)
+                        avr::smp::ZSobolParams zsd = zs;
+                        {
+                            const int pw = zs.log2spp & 1, iTop = (plo + pw - 1) >> 1;
+                            const int prefix_bits = 2 * zs.nBase4Digits - pw - plo;
+                            zsd.pperm4 = (c->zs_pack && iTop - 1 >= pw && prefix_bits <= 36) ? 1 : 0;
+                        }
                         hipLaunchKernelGGL(avr::k_zsobol_pass_table,
                                            dim3(blocks_for((long long)c->film.width * c->film.height * (c->zs_pdims / 2), 256,
                                                            256 * 64)),
-                                           dim3(256), 0, c->stream, zs, c->film.width, c->film.height, c->zs_pdims, plo,
+                                           dim3(256), 0, c->stream, zsd, c->film.width, c->film.height, c->zs_pdims, plo,
                                            base, c->d_zs_ptab, atab, avr::fastdiv_make((uint32_t)(c->zs_pdims / 2)),
                                            avr::fastdiv_make((uint32_t)c->film.width), ctab);
                         HIP_TRY(hipGetLastError());
                         p.zs.ptab = c->d_zs_ptab;
                         p.zs.ctab = ctab;
+                        p.zs.pperm4 = zsd.pperm4;
                         p.zs.pdims = c->zs_pdims;
                         p.zs.plo = plo;
                     }

@@ -1105,7 +1105,7 @@ __device__ __forceinline__ void zsobol_index_quad_pair(M morton, const smp::ZSob
     }
     const uint32_t pA0 = quad_bcast<0>(p), pA1 = quad_bcast<1>(p), pB0 = quad_bcast<2>(p), pB1 = quad_bcast<3>(p);
     auto assemble = [&](uint64_t e, uint32_t d, uint32_t p0, uint32_t p1) -> M {
-        M idx = (M)((e & 0x00ffffffffffffffull) << plo);
+        M idx = (M)((e & smp::pass_prefix_mask(zp)) << plo);
         if (iTop >= pw) {
             const int sh = 2 * iTop - pw;
             idx |= (M)smp::zperm((uint32_t)(e >> 56), (uint32_t)(morton >> sh) & 3u) << sh;
@@ -1153,7 +1153,7 @@ __device__ __forceinline__ void zsobol_draw_quad(smp::ZSobol &z, const smp::ZSob
         const uint64_t e = pe_ok ? pe : zp.ptab[(size_t)pm * (size_t)zp.pdims + z.dimension];
         const int iTop = (zp.plo + pw - 1) >> 1;
         const uint32_t perm = (uint32_t)(e >> 56);
-        const uint64_t fx = (e & 0x00ffffffffffffffull) << zp.plo;
+        const uint64_t fx = (e & smp::pass_prefix_mask(zp)) << zp.plo;
         if constexpr (kW == 2) {
             const uint64_t m = ((uint64_t)z.hi << 32) | z.morton;
             uint64_t idx = fx | zsobol_lower_quad<uint64_t>(m, z.dimension, zp, pw, iTop - 1);
@@ -3626,6 +3626,12 @@ __global__ void __launch_bounds__(256) k_zsobol_pass_table(smp::ZSobolParams zp,
                        : smp::zsobol_pass_entry<uint32_t>((uint32_t)m, (uint32_t)d, zp, plo, u0);
             e.y = wide ? smp::zsobol_pass_entry<uint64_t>(m, (uint32_t)d + 1, zp, plo, u1)
                        : smp::zsobol_pass_entry<uint32_t>((uint32_t)m, (uint32_t)d + 1, zp, plo, u1);
+        }
+        if (zp.pperm4) {
+            e.x = wide ? smp::zsobol_pass_pack<uint64_t>(m, (uint32_t)d, zp, plo, e.x)
+                       : smp::zsobol_pass_pack<uint32_t>((uint32_t)m, (uint32_t)d, zp, plo, e.x);
+            e.y = wide ? smp::zsobol_pass_pack<uint64_t>(m, (uint32_t)d + 1, zp, plo, e.y)
+                       : smp::zsobol_pass_pack<uint32_t>((uint32_t)m, (uint32_t)d + 1, zp, plo, e.y);
         }
         *reinterpret_cast<ulonglong2 *>(table + row) = e;
         // the camera stage's pairs (0, 1), (6, 7), (8, 9) also into its compact per-pixel copy

@@ -114,7 +114,15 @@ struct ZSobolParams {
     // and 6..9, in that order, 48 B per pixel in scanline order) so its loads stream instead of
     // gathering 48 B from each pixel's row (null = read the rows)
     const uint64_t *ctab;
+    // 1: the pass table's entries also carry, in bits 36..55, the permutations of the digit
+    // under the perm-fixed one for each of the 4 values of that digit (5 bits each; the host sets
+    // it when the fixed prefix fits 36 bits), so a draw mixes one digit fewer (zsobol_pass_pack)
+    int pperm4;
 };
+// the fixed-prefix bits of a pass-table entry (below the packed permutations when pperm4)
+AVR_HD uint64_t pass_prefix_mask(const ZSobolParams &zp) {
+    return zp.pperm4 ? 0x0000000fffffffffull : 0x00ffffffffffffffull;
+}
 
 // Morton(pixel) << log2(spp) | sampleIndex fits 32 bits (nBase4Digits <= 16: e.g. 1024 spp
 // at 1080p); beyond it (4096 spp at 720p ...) the index and the digit prefixes are 64-bit.
@@ -255,6 +263,26 @@ AVR_HD uint64_t zsobol_pass_entry_from(M morton, uint32_t dimension, const ZSobo
     return (fixed >> plo) | ((uint64_t)perm << 56);
 }
 
+// A pass entry with the permutations of the digit under its perm-fixed digit iTop packed in
+// bits 36..55 (ZSobolParams::pperm4): that digit's permutation hashes the bits above it, which
+// are the pass's fixed bits and digit iTop's value — one of 4 — so the 4 candidates are
+// tabulated per (pixel, dimension, pass) instead of mixed per draw. `morton`: any sample of
+// the pass; the entry's prefix must fit 36 bits (the host checks).
+template <typename M>
+AVR_HD uint64_t zsobol_pass_pack(M morton, uint32_t dimension, const ZSobolParams &zp, int plo, uint64_t e) {
+    const int pw = zp.log2spp & 1;
+    const int iTop = (plo + pw - 1) >> 1;
+    if (iTop - 1 < pw) return e;
+    constexpr int kBits = 8 * (int)sizeof(M);
+    const int shTop = 2 * iTop - pw;   // the bits above digit iTop - 1 start here
+    const M above = shTop + 2 >= kBits ? M(0) : M((morton >> (shTop + 2)) << 2);
+    const M dmix = (M)(0x55555555u * dimension);
+    uint64_t packed = 0;
+    _Pragma("unroll") for (uint32_t v = 0; v < 4; ++v)
+        packed |= (uint64_t)mix_perm24<M>((M)((above | (M)v) ^ dmix)) << (5 * v);
+    return (e & 0xff00000fffffffffull) | (packed << 36);
+}
+
 // GetSampleIndex of (morton, dimension) from the sample's pass entry e: the varying digits
 // computed, the perm-fixed digit from e's permutation, the rest from e; an odd log2(spp)'s
 // final base-2 digit as zsobol_lower. Bit-identical to zsobol_index without tables.
@@ -263,12 +291,16 @@ AVR_HD M zsobol_index_pass(M morton, uint32_t dimension, const ZSobolParams &zp,
     const int pw = zp.log2spp & 1, plo = zp.plo;
     const uint32_t dmix = 0x55555555u * dimension;
     constexpr int kBits = 8 * (int)sizeof(M);
-    M idx = (M)((e & 0x00ffffffffffffffull) << plo);
+    M idx = (M)((e & pass_prefix_mask(zp)) << plo);
     const uint32_t perm = (uint32_t)(e >> 56);
-    for (int i = (plo + pw - 1) >> 1; i >= pw; --i) {   // digits with shift < plo
+    const int iTop = (plo + pw - 1) >> 1;
+    for (int i = iTop; i >= pw; --i) {   // digits with shift < plo
         const int shift = 2 * i - pw;
         uint32_t p = perm;
-        if (shift + 2 < plo) {
+        if (zp.pperm4 && i == iTop - 1) {
+            // packed by the table build: indexed by the value of the digit above (bits shift + 2..)
+            p = (uint32_t)(e >> (36 + 5 * ((uint32_t)(morton >> (shift + 2)) & 3u))) & 31u;
+        } else if (shift + 2 < plo) {
             const M higher = shift + 2 >= kBits ? M(0) : M(morton >> (shift + 2));
             p = mix_perm24<M>((M)(higher ^ (M)dmix));
         }
@@ -398,6 +430,7 @@ inline ZSobolParams zsobol_params(int spp, int width, int height, int seed) {
     zp.pdims = 0;
     zp.plo = 0;
     zp.ctab = nullptr;
+    zp.pperm4 = 0;
     return zp;
 }
 
