@@ -51,9 +51,6 @@ int fail(int code, const std::string &msg) {
 #ifndef AVR_ZS_TWO_LEVEL
 #define AVR_ZS_TWO_LEVEL 1   // build the ZSobol pass table from a level-A table shared by 4 passes
 #endif
-#ifndef AVR_ZS_PACK
-#define AVR_ZS_PACK 0   // 1: pass-table entries carry the next digit's 4 candidate permutations (zsobol_pass_pack; measured slower: profiles/r05_ab_pass_pack.json)
-#endif
 
 template <typename T>
 hipError_t dalloc(T **p, size_t n) { return hipMalloc((void **)p, std::max<size_t>(n, 1) * sizeof(T)); }

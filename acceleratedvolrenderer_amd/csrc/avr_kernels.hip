@@ -3627,7 +3627,7 @@ __global__ void __launch_bounds__(256) k_zsobol_pass_table(smp::ZSobolParams zp,
             e.y = wide ? smp::zsobol_pass_entry<uint64_t>(m, (uint32_t)d + 1, zp, plo, u1)
                        : smp::zsobol_pass_entry<uint32_t>((uint32_t)m, (uint32_t)d + 1, zp, plo, u1);
         }
-        if (zp.pperm4) {
+        if (AVR_ZS_PACK && zp.pperm4) {
             e.x = wide ? smp::zsobol_pass_pack<uint64_t>(m, (uint32_t)d, zp, plo, e.x)
                        : smp::zsobol_pass_pack<uint32_t>((uint32_t)m, (uint32_t)d, zp, plo, e.x);
             e.y = wide ? smp::zsobol_pass_pack<uint64_t>(m, (uint32_t)d + 1, zp, plo, e.y)

@@ -119,9 +119,15 @@ struct ZSobolParams {
     // it when the fixed prefix fits 36 bits), so a draw mixes one digit fewer (zsobol_pass_pack)
     int pperm4;
 };
+// Packed permutations in pass-table entries (zsobol_pass_pack): compiled in only with
+// AVR_ZS_PACK 1 (measured slower: profiles/r05_ab_pass_pack.json), so the default draws carry
+// no check for them
+#ifndef AVR_ZS_PACK
+#define AVR_ZS_PACK 0
+#endif
 // the fixed-prefix bits of a pass-table entry (below the packed permutations when pperm4)
 AVR_HD uint64_t pass_prefix_mask(const ZSobolParams &zp) {
-    return zp.pperm4 ? 0x0000000fffffffffull : 0x00ffffffffffffffull;
+    return (AVR_ZS_PACK && zp.pperm4) ? 0x0000000fffffffffull : 0x00ffffffffffffffull;
 }
 
 // Morton(pixel) << log2(spp) | sampleIndex fits 32 bits (nBase4Digits <= 16: e.g. 1024 spp
@@ -297,7 +303,7 @@ AVR_HD M zsobol_index_pass(M morton, uint32_t dimension, const ZSobolParams &zp,
     for (int i = iTop; i >= pw; --i) {   // digits with shift < plo
         const int shift = 2 * i - pw;
         uint32_t p = perm;
-        if (zp.pperm4 && i == iTop - 1) {
+        if (AVR_ZS_PACK && zp.pperm4 && i == iTop - 1) {
             // packed by the table build: indexed by the value of the digit above (bits shift + 2..)
             p = (uint32_t)(e >> (36 + 5 * ((uint32_t)(morton >> (shift + 2)) & 3u))) & 31u;
         } else if (shift + 2 < plo) {

@@ -17,7 +17,7 @@ def hdr(tmp_path_factory):
     d = tmp_path_factory.mktemp("smp")
     src = d / "shim.cpp"
     src.write_text(
-        "#define AVR_HD inline\n"
+        "#define AVR_HD inline\n#define AVR_ZS_PACK 1\n"
         f'#include "{ROOT}/acceleratedvolrenderer_amd/csrc/avr_sampling.h"\n'
         "using namespace avr::smp;\n"
         'extern "C" {\n'
