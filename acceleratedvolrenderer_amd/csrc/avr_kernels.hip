@@ -1089,7 +1089,13 @@ __device__ __forceinline__ uint32_t zsobol_lower_quad(M morton, uint32_t dimensi
 // of its four lanes busy). Same bits as zsobol_index_pass / zsobol_index.
 template <typename M>
 __device__ __forceinline__ void zsobol_index_quad_pair(M morton, const smp::ZSobolParams &zp, uint32_t dA, uint64_t eA,
-                                                       uint32_t dB, uint64_t eB, M *ia, M *ib) {
+                                                       uint32_t dB, uint64_t eB, M *ia, M *ib,
+                                                       const uint8_t *zpt = nullptr) {
+    // zpt: the 24 permutations as bytes (4 x 2 bits, smp::zperm's table) staged in LDS — one
+    // byte read and a bit-field extract per digit instead of selecting among three 64-bit words
+    auto zp_ = [&](uint32_t p, uint32_t digit) -> uint32_t {
+        return zpt ? ((uint32_t)zpt[p] >> (2 * digit)) & 3u : smp::zperm(p, digit);
+    };
     constexpr int kBits = 8 * (int)sizeof(M);
     const int pw = zp.log2spp & 1, plo = zp.plo;
     const int iTop = (plo + pw - 1) >> 1;   // the perm-fixed digit (when >= pw); digits below it vary
@@ -1108,10 +1114,10 @@ __device__ __forceinline__ void zsobol_index_quad_pair(M morton, const smp::ZSob
         M idx = (M)((e & smp::pass_prefix_mask(zp)) << plo);
         if (iTop >= pw) {
             const int sh = 2 * iTop - pw;
-            idx |= (M)smp::zperm((uint32_t)(e >> 56), (uint32_t)(morton >> sh) & 3u) << sh;
+            idx |= (M)zp_((uint32_t)(e >> 56), (uint32_t)(morton >> sh) & 3u) << sh;
         }
-        if (pw < iTop) idx |= (M)smp::zperm(p0, (uint32_t)(morton >> pw) & 3u) << pw;
-        if (pw + 1 < iTop) idx |= (M)smp::zperm(p1, (uint32_t)(morton >> (pw + 2)) & 3u) << (pw + 2);
+        if (pw < iTop) idx |= (M)zp_(p0, (uint32_t)(morton >> pw) & 3u) << pw;
+        if (pw + 1 < iTop) idx |= (M)zp_(p1, (uint32_t)(morton >> (pw + 2)) & 3u) << (pw + 2);
         if (pw) {   // the final base-2 digit (as zsobol_lower)
             const M x = (M)(morton >> 1) ^ (M)(0x55555555u * d);
             uint64_t v = (uint64_t)x;
@@ -1229,6 +1235,11 @@ __global__ void __launch_bounds__(256, AVR_CAM_WAVES) k_paths_camera(Params P) {
         for (int i = threadIdx.x; i < canon::kCanonTabDoubles; i += blockDim.x)
             s_canon[i] = i < 128 ? canon::kLogInvC[i] : (i < 256 ? canon::kLogC[i - 128] : canon::kExp2J64[i - 256]);
     __shared__ uint64_t s_cdh[kCamDimHash];
+    __shared__ uint8_t s_zpt[24];   // smp::zperm's 24 permutations, one byte each
+    if (threadIdx.x < 24) {
+        const uint64_t w = threadIdx.x < 8 ? smp::kZPermW0 : (threadIdx.x < 16 ? smp::kZPermW1 : smp::kZPermW2);
+        s_zpt[threadIdx.x] = (uint8_t)(w >> ((threadIdx.x & 7) * 8));
+    }
     if constexpr (kSmp != 0)
         if (threadIdx.x < kCamDimHash) s_cdh[threadIdx.x] = smp::hash_2u32(threadIdx.x, (uint32_t)P.zs.seed);
     // the pass's per-XCD work counters of k_paths, zeroed here (stream order: after the previous
@@ -1313,9 +1324,9 @@ __global__ void __launch_bounds__(256, AVR_CAM_WAVES) k_paths_camera(Params P) {
                 const M m = PathSampler<kSmp>::kW == 2 ? (M)(((uint64_t)smp.z.hi << 32) | smp.z.morton) : (M)smp.z.morton;
                 const uint64_t *dh = AVR_CAM_DIM_HASH ? s_cdh : nullptr;
                 M i0, i1, i6, i7, i8, i9;
-                zsobol_index_quad_pair<M>(m, P.zs, 0, pe0, 1, pe1, &i0, &i1);
-                zsobol_index_quad_pair<M>(m, P.zs, 6, pe6, 7, pe7, &i6, &i7);
-                zsobol_index_quad_pair<M>(m, P.zs, 8, pe8, 9, pe9, &i8, &i9);
+                zsobol_index_quad_pair<M>(m, P.zs, 0, pe0, 1, pe1, &i0, &i1, s_zpt);
+                zsobol_index_quad_pair<M>(m, P.zs, 6, pe6, 7, pe7, &i6, &i7, s_zpt);
+                zsobol_index_quad_pair<M>(m, P.zs, 8, pe8, 9, pe9, &i8, &i9, s_zpt);
                 float dummy;
                 zsobol_finish<M>(i0, 1, P.zs, false, &pu[0], &dummy, dh);
                 zsobol_finish<M>(i1, 3, P.zs, true, &pu[1], &pu[2], dh);
