@@ -937,7 +937,7 @@ __device__ __forceinline__ void coop_draws(smp::ZSobol &z, const smp::ZSobolPara
 template <int kW, int N, int K>
 __device__ __forceinline__ int coop_draws_lds(smp::ZSobol &z, const smp::ZSobolParams &zp, bool req, const int (&off)[N],
                                               const bool (&two)[N], const int (&slot)[N], int adv, float *s_res,
-                                              uint3 *s_st, const uint64_t *dhash = nullptr) {
+                                              uint3 *s_st, const uint64_t *dhash = nullptr, const uint8_t *zpt = nullptr) {
     const uint64_t mask = __ballot(req);
     const int lane = lane_id();
     const int rank = __popcll(mask & ((1ull << lane) - 1ull));
@@ -963,7 +963,7 @@ __device__ __forceinline__ int coop_draws_lds(smp::ZSobol &z, const smp::ZSobolP
             q.hi = st.y;
             q.dimension = 0;
             float v0, v1;
-            q.template draw_at<kW>(zp, st.z + (uint32_t)o, tw, &v0, &v1, dhash, dhash ? kDimHash : 0);
+            q.template draw_at<kW>(zp, st.z + (uint32_t)o, tw, &v0, &v1, dhash, dhash ? kDimHash : 0, zpt);
             s_res[r * K + sl] = v0;
             if (tw) s_res[r * K + sl + 1] = v1;
         }
@@ -2154,6 +2154,13 @@ __global__ void __launch_bounds__(256, kGray ? (kMed == 1 ? 3 : AVR_PATHS_WAVES_
     __shared__ uint64_t s_dh[kSmp != 0 ? kDimHash : 1];
     if constexpr (kSmp != 0)
         for (int i = threadIdx.x; i < kDimHash; i += blockDim.x) s_dh[i] = smp::hash_2u32((uint32_t)i, (uint32_t)P.zs.seed);
+    // ZSobol: smp::zperm's 24 permutations as bytes (the cooperative draws' digit permutations)
+    __shared__ uint8_t s_zpt[kSmp != 0 ? 24 : 1];
+    if constexpr (kSmp != 0)
+        if (threadIdx.x < 24) {
+            const uint64_t w = threadIdx.x < 8 ? smp::kZPermW0 : (threadIdx.x < 16 ? smp::kZPermW1 : smp::kZPermW2);
+            s_zpt[threadIdx.x] = (uint8_t)(w >> ((threadIdx.x & 7) * 8));
+        }
     // ZSobol: each lane's next light-pick draw (SampleLd's 1D, integrators.cpp:1302), evaluated
     // ahead with the previous bounce's cooperative phase draws (or by the camera stage)
     __shared__ float s_ul[(kSmp != 0 && !kPoolDecl) ? 256 : 1];
@@ -2685,7 +2692,8 @@ __global__ void __launch_bounds__(256, kGray ? (kMed == 1 ? 3 : AVR_PATHS_WAVES_
                 constexpr int slot[5] = {0, 2, 3, 4, 5};
                 float *sres = s_res + (threadIdx.x & ~63u) * 6;
                 const int rk = coop_draws_lds<PathSampler<kSmp>::kW, 5, 6>(smp.z, P.zs, ev == EV_PHASE, off, two, slot, 5, sres,
-                                                                          s_zst + (threadIdx.x & ~63u), AVR_DIM_HASH ? s_dh : nullptr);
+                                                                          s_zst + (threadIdx.x & ~63u), AVR_DIM_HASH ? s_dh : nullptr,
+                                                                          s_zpt);
                 qr = sres + rk * 6;
                 if (ev == EV_PHASE) s_ul[threadIdx.x] = qr[5];
             } else if constexpr (kUlAhead) {

@@ -154,6 +154,11 @@ AVR_HD uint32_t zperm(uint32_t p, uint32_t digit) {
     const uint64_t w = p < 8 ? kZPermW0 : (p < 16 ? kZPermW1 : kZPermW2);
     return (uint32_t)(w >> ((p & 7) * 8 + 2 * digit)) & 3u;
 }
+// zperm from the 24 permutations staged as bytes (zpt[p] = byte p of kZPermW0..2, e.g. in LDS),
+// or from the 64-bit words when zpt is null
+AVR_HD uint32_t zperm_t(const uint8_t *zpt, uint32_t p, uint32_t digit) {
+    return zpt ? ((uint32_t)zpt[p] >> (2 * digit)) & 3u : zperm(p, digit);
+}
 
 // ZSobolSampler::GetSampleIndex (samplers.h:296-355), digits i in [iLo, iHi] (most
 // significant first) of the current dimension. M is uint32_t when the whole index fits 32
@@ -293,7 +298,7 @@ AVR_HD uint64_t zsobol_pass_pack(M morton, uint32_t dimension, const ZSobolParam
 // computed, the perm-fixed digit from e's permutation, the rest from e; an odd log2(spp)'s
 // final base-2 digit as zsobol_lower. Bit-identical to zsobol_index without tables.
 template <typename M>
-AVR_HD M zsobol_index_pass(M morton, uint32_t dimension, const ZSobolParams &zp, uint64_t e) {
+AVR_HD M zsobol_index_pass(M morton, uint32_t dimension, const ZSobolParams &zp, uint64_t e, const uint8_t *zpt = nullptr) {
     const int pw = zp.log2spp & 1, plo = zp.plo;
     const uint32_t dmix = 0x55555555u * dimension;
     constexpr int kBits = 8 * (int)sizeof(M);
@@ -310,7 +315,7 @@ AVR_HD M zsobol_index_pass(M morton, uint32_t dimension, const ZSobolParams &zp,
             const M higher = shift + 2 >= kBits ? M(0) : M(morton >> (shift + 2));
             p = mix_perm24<M>((M)(higher ^ (M)dmix));
         }
-        idx |= (M)zperm(p, (uint32_t)(morton >> shift) & 3u) << shift;
+        idx |= (M)zperm_t(zpt, p, (uint32_t)(morton >> shift) & 3u) << shift;
     }
     if (pw) {
         const uint32_t digit = (uint32_t)morton & 1u;
@@ -329,7 +334,7 @@ AVR_HD M zsobol_index_pass(M morton, uint32_t dimension, const ZSobolParams &zp,
 // GetSampleIndex of (morton, dimension): from the pass table, else the upper digits from the
 // pixel table when present
 template <typename M>
-AVR_HD M zsobol_index(M morton, uint32_t dimension, const ZSobolParams &zp) {
+AVR_HD M zsobol_index(M morton, uint32_t dimension, const ZSobolParams &zp, const uint8_t *zpt = nullptr) {
     if (zp.ptab && (int)dimension < zp.pdims) {
         const uint32_t pm = (uint32_t)(morton >> zp.log2spp);
 #if defined(AVR_MEASURE_NO_PTAB) && defined(AVR_KPATHS_TU)
@@ -338,7 +343,7 @@ AVR_HD M zsobol_index(M morton, uint32_t dimension, const ZSobolParams &zp) {
         const uint64_t fake = ((uint64_t)pm * 0x9E3779B97F4A7C15ull) ^ ((uint64_t)dimension << 40);
         return zsobol_index_pass<M>(morton, dimension, zp, fake);
 #else
-        return zsobol_index_pass<M>(morton, dimension, zp, zp.ptab[(size_t)pm * (size_t)zp.pdims + dimension]);
+        return zsobol_index_pass<M>(morton, dimension, zp, zp.ptab[(size_t)pm * (size_t)zp.pdims + dimension], zpt);
 #endif
     }
     uint32_t up;
@@ -373,13 +378,13 @@ struct ZSobol {
     // bits; the caller guarantees !zsobol_wide), 2 = 64-bit (the caller guarantees zsobol_wide).
     // The fixed widths let a kernel instantiation carry one code path only.
     template <int kW = 0>
-    AVR_HD void index(const ZSobolParams &zp, uint32_t *alo, uint32_t *ahi) const {
+    AVR_HD void index(const ZSobolParams &zp, uint32_t *alo, uint32_t *ahi, const uint8_t *zpt = nullptr) const {
         if (kW == 2 || (kW == 0 && zsobol_wide(zp))) {
-            const uint64_t a = zsobol_index<uint64_t>(((uint64_t)hi << 32) | morton, dimension, zp);
+            const uint64_t a = zsobol_index<uint64_t>(((uint64_t)hi << 32) | morton, dimension, zp, zpt);
             *alo = (uint32_t)a;
             *ahi = (uint32_t)(a >> 32);
         } else {
-            *alo = zsobol_index<uint32_t>(morton, dimension, zp);
+            *alo = zsobol_index<uint32_t>(morton, dimension, zp, zpt);
             *ahi = 0;
         }
     }
@@ -406,11 +411,11 @@ struct ZSobol {
     // `dhash`: optional table of Hash(d, seed) for d < dhash_n (the draw's scramble seeds)
     template <int kW = 0>
     AVR_HD void draw_at(const ZSobolParams &zp, uint32_t dim, bool two, float *u0, float *u1,
-                        const uint64_t *dhash = nullptr, uint32_t dhash_n = 0) const {
+                        const uint64_t *dhash = nullptr, uint32_t dhash_n = 0, const uint8_t *zpt = nullptr) const {
         ZSobol s = *this;
         s.dimension = dim;
         uint32_t a, ah;
-        s.index<kW>(zp, &a, &ah);
+        s.index<kW>(zp, &a, &ah, zpt);
         const uint32_t hd = dim + (two ? 2u : 1u);
         const uint64_t h = hd < dhash_n ? dhash[hd] : hash_2u32(hd, (uint32_t)zp.seed);
         *u0 = u32_to_unit(fast_owen(sobol_bits(a, 0), (uint32_t)h));
