@@ -1,5 +1,5 @@
 #!/bin/bash
-# round-5 pass z (run twice: the camera stage, then also k_paths' cooperative draws): the's digit permutations from a 24-byte LDS table (one byte read +
+# round-5 pass z (reused for each small change of this kind against variants/prevlib): the's digit permutations from a 24-byte LDS table (one byte read +
 # bit-field extract) instead of selecting among three 64-bit words; GPU parity, then A/B against
 # the previous build (variants/prevlib)
 set -o pipefail
