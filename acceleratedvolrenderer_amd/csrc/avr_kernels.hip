@@ -2154,9 +2154,11 @@ __global__ void __launch_bounds__(256, kGray ? (kMed == 1 ? 3 : AVR_PATHS_WAVES_
     __shared__ uint64_t s_dh[kSmp != 0 ? kDimHash : 1];
     if constexpr (kSmp != 0)
         for (int i = threadIdx.x; i < kDimHash; i += blockDim.x) s_dh[i] = smp::hash_2u32((uint32_t)i, (uint32_t)P.zs.seed);
-    // ZSobol: smp::zperm's 24 permutations as bytes (the cooperative draws' digit permutations)
-    __shared__ uint8_t s_zpt[kSmp != 0 ? 24 : 1];
-    if constexpr (kSmp != 0)
+    // ZSobol: smp::zperm's 24 permutations as bytes (the cooperative draws' digit permutations;
+    // not for NanoVDB, whose kernel measured 2.4 % slower with them: profiles/r05_ab_zperm_lds.json)
+    constexpr bool kZpt = kSmp != 0 && !kVdb;
+    __shared__ uint8_t s_zpt[kZpt ? 24 : 1];
+    if constexpr (kZpt)
         if (threadIdx.x < 24) {
             const uint64_t w = threadIdx.x < 8 ? smp::kZPermW0 : (threadIdx.x < 16 ? smp::kZPermW1 : smp::kZPermW2);
             s_zpt[threadIdx.x] = (uint8_t)(w >> ((threadIdx.x & 7) * 8));
@@ -2693,7 +2695,7 @@ __global__ void __launch_bounds__(256, kGray ? (kMed == 1 ? 3 : AVR_PATHS_WAVES_
                 float *sres = s_res + (threadIdx.x & ~63u) * 6;
                 const int rk = coop_draws_lds<PathSampler<kSmp>::kW, 5, 6>(smp.z, P.zs, ev == EV_PHASE, off, two, slot, 5, sres,
                                                                           s_zst + (threadIdx.x & ~63u), AVR_DIM_HASH ? s_dh : nullptr,
-                                                                          s_zpt);
+                                                                          kZpt ? s_zpt : nullptr);
                 qr = sres + rk * 6;
                 if (ev == EV_PHASE) s_ul[threadIdx.x] = qr[5];
             } else if constexpr (kUlAhead) {
