@@ -77,6 +77,14 @@ def hdr(tmp_path_factory):
         "      if (zt.pperm4) e = zsobol_pass_pack<unsigned>((unsigned)mb, d, zt, plo, e);\n"
         "      pass[i] = zsobol_index_pass<unsigned>((unsigned)ms, d, zt, e); } }\n"
         "  return packed; }\n"
+        "int zperm_bytes_check() {\n"
+        "  unsigned char t[24]; const unsigned long long W[3] = {kZPermW0, kZPermW1, kZPermW2};\n"
+        "  for (int p = 0; p < 24; ++p) t[p] = (unsigned char)(W[p >> 3] >> ((p & 7) * 8));\n"
+        "  int bad = 0; for (unsigned p = 0; p < 24; ++p) for (unsigned d = 0; d < 4; ++d)\n"
+        "    bad += zperm_t(t, p, d) != zperm(p, d) || zperm_t(nullptr, p, d) != zperm(p, d);\n"
+        "  for (unsigned p = 0; p < 24; ++p) { unsigned m = 0; for (unsigned d = 0; d < 4; ++d) m |= 1u << zperm(p, d);\n"
+        "    bad += m != 15u; }\n"
+        "  return bad; }\n"
         "int zs_pass_from(int spp, int rx, int ry, int n, const int *q) {\n"
         "  ZSobolParams zp = zsobol_params(spp, rx, ry, 0); int bad = 0;\n"
         "  for (int i = 0; i < n; ++i) {\n"
@@ -261,3 +269,9 @@ def test_filter_guided_weighted_sample_identical(hdr, r, sigma):
     F = ctypes.POINTER(ctypes.c_float)
     hdr.fs_check.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_float, ctypes.c_float, F, ctypes.c_int, F]
     assert hdr.fs_check(n, n, r, r, f.ctypes.data_as(F), len(u), u.ctypes.data_as(F)) == 0
+
+
+def test_zperm_byte_table(hdr):
+    """The 24-byte permutation table the camera stage and k_paths stage in LDS (zperm_t) gives
+    zperm's digit for every permutation and digit, and every entry is a permutation of 0..3."""
+    assert hdr.zperm_bytes_check() == 0
