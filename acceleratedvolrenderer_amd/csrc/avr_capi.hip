@@ -161,7 +161,6 @@ struct avr_context {
     size_t zs_ptab_cap = 0;   // entries allocated
     uint64_t *d_zs_ctab = nullptr;   // the camera stage's compact copy (6 entries per pixel)
     size_t zs_ctab_cap = 0;
-    int zs_pack = AVR_ZS_PACK;        // pack the next digit's permutations into pass entries
     int zs_pdims = 96;
     // Level-A pass table (the same table for plo + 2, shared by four consecutive passes);
     // zs_akey names the build it holds (rebuilt when any field changes), zs_two_level 0 = off
@@ -1921,14 +1920,7 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
                             }
                         }
                         uint64_t *ctab = need_c ? c->d_zs_ctab : nullptr;
-                        // the permutations of the digit under the perm-fixed one, packed into the
-                        // entries when their fixed prefix fits 36 bits (zsobol_pass_pack)
-                        avr::smp::ZSobolParams zsd = zs;
-                        {
-                            const int pw = zs.log2spp & 1, iTop = (plo + pw - 1) >> 1;
-                            const int prefix_bits = 2 * zs.nBase4Digits - pw - plo;
-                            zsd.pperm4 = (c->zs_pack && iTop - 1 >= pw && prefix_bits <= 36) ? 1 : 0;
-                        }
+                        const avr::smp::ZSobolParams zsd = zs;
                         hipLaunchKernelGGL(avr::k_zsobol_pass_table,
                                            dim3(blocks_for((long long)c->film.width * c->film.height * (c->zs_pdims / 2), 256,
                                                            256 * 64)),
@@ -1938,7 +1930,6 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
                         HIP_TRY(hipGetLastError());
                         p.zs.ptab = c->d_zs_ptab;
                         p.zs.ctab = ctab;
-                        p.zs.pperm4 = zsd.pperm4;
                         p.zs.pdims = c->zs_pdims;
                         p.zs.plo = plo;
                     }
@@ -2288,10 +2279,10 @@ int avr_last_pass_samples(avr_context *c, float *L, float *lambda, float *pdf, l
     if (n > 0 && c->last_persistent && c->last_order_gen != c->order_gen)
         return fail(AVR_ERR_STATE, "the pixel order changed since the last render (its records are in the old order)");
     if (n > 0 && c->last_persistent) {
-        // k_paths' records (L) and its camera stage's wavelengths and pdfs, as k_film read them
+        // k_paths' records (L), its camera stage's wavelengths and their pdfs as k_film evaluates them
         HIP_TRY(hipMemcpy(L, c->ps.rec, n * sizeof(float4), hipMemcpyDeviceToHost));
         HIP_TRY(hipMemcpy(lambda, c->ps.cam2, n * sizeof(float4), hipMemcpyDeviceToHost));
-        if (AVR_FILM_PDF && AVR_CAM_CANON_LDS) {   // k_film evaluates them: recompute for the accessor
+        {
             avr::DevFilm f = c->film;
             hipLaunchKernelGGL(avr::k_lambda_pdfs, dim3(blocks_for(n)), dim3(256), 0, c->stream, f, c->ps.cam2, c->ps.cam4, n);
             HIP_TRY(hipGetLastError());

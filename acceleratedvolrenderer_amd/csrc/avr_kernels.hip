@@ -253,9 +253,6 @@ struct ShadowSoA {
 // [2] items out k_medium (survivors + shadow pushes), [3] lookups k_shadow, [4] items k_shadow,
 // [5] DDA steps k_medium, [6] DDA steps k_shadow; k_paths: [6] loop iterations (per wave),
 // [7] sum over iterations of active lanes (SIMD utilisation = [7] / (64 * [6]))
-#ifndef AVR_UL_IN_CAM1
-#define AVR_UL_IN_CAM1 1   // ZSobol's first light-pick draw in cam1.w (0: a separate 4-B array, round 4)
-#endif
 constexpr int kNumStats = 10;   // 0-6 wavefront/shared work counters, 8-9 k_paths wave loop
 
 struct Params {
@@ -351,14 +348,7 @@ __device__ __forceinline__ bool fat_issue(const float4 *__restrict__ fat, int nx
     if (ix < -1 || ix >= nx || iy < -1 || iy >= ny || iz < -1 || iz >= nz) return false;
     dx = psx - (float)ix, dy = psy - (float)iy, dz = psz - (float)iz;
     const size_t e = (((size_t)(iz + 1) * (ny + 1) + (iy + 1)) * (nx + 1) + (ix + 1)) * 2;
-#if AVR_NT_FETCH
-    typedef float v4f __attribute__((ext_vector_type(4)));
-    const v4f va = __builtin_nontemporal_load(reinterpret_cast<const v4f *>(fat + e)),
-              vb = __builtin_nontemporal_load(reinterpret_cast<const v4f *>(fat + e + 1));
-    a = make_float4(va.x, va.y, va.z, va.w), b = make_float4(vb.x, vb.y, vb.z, vb.w);
-#else
     a = fat[e], b = fat[e + 1];
-#endif
     return true;
 }
 __device__ __forceinline__ float fat_lerp(float4 a, float4 b, float dx, float dy, float dz) {
@@ -880,60 +870,13 @@ __device__ __forceinline__ void camera_sample(const Params &P, Smp &smp, int px,
 // Cooperative ZSobol draws in k_paths' service rounds. Each lane with `req` needs N draws at
 // its dimension + off[j] (a 2D draw where two[j]); the wave's N * popc(req) draws are spread
 // over all 64 lanes — busy lanes included, which wait through the handler anyway — so a
-// round evaluates the sampler ceil(N * popc / 64) times instead of N times, and each
-// requester pulls its results back with ds_bpermute. Results are bit-identical to the
-// sequential get1d / get2d calls (ZSobol::draw_at: a pure function of sample and dimension);
-// the requesters' dimension then advances by `adv`. s_st: this wave's 64 LDS entries.
+// round evaluates the sampler ceil(N * popc / 64) times instead of N times. The lane that
+// evaluates draw j of requester rank r writes it to s_res[r * K + slot[j]] (a 2D draw's second
+// value after it), so no requester holds N results in VGPRs through the evaluation loop;
+// returns the calling lane's rank (its record is s_res + rank * K). Results are bit-identical
+// to the sequential get1d / get2d calls (ZSobol::draw_at: a pure function of sample and
+// dimension); the requesters' dimension then advances by `adv`. s_st: this wave's 64 LDS entries.
 constexpr int kDimHash = 128;   // Hash(d, seed) of the first dimensions, staged in LDS by k_paths (paths deeper than ~15 bounces hash per draw)
-template <int kW, int N>
-__device__ __forceinline__ void coop_draws(smp::ZSobol &z, const smp::ZSobolParams &zp, bool req, const int (&off)[N],
-                                           const bool (&two)[N], int adv, float (&r0)[N], float (&r1)[N], uint3 *s_st,
-                                           const uint64_t *dhash = nullptr) {
-    const uint64_t mask = __ballot(req);
-    const int lane = lane_id();
-    const int rank = __popcll(mask & ((1ull << lane) - 1ull));
-    if (req) s_st[rank] = make_uint3(z.morton, z.hi, z.dimension);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    _Pragma("unroll") for (int j = 0; j < N; ++j) r0[j] = r1[j] = 0.f;
-    const int total = __popcll(mask) * N;
-    for (int c = 0; c < total; c += 64) {
-        const int t = c + lane;
-        float v0 = 0.f, v1 = 0.f;
-        if (t < total) {
-            const int r = t / N, j = t - r * N;
-            int o = off[0];
-            bool tw = two[0];
-            _Pragma("unroll") for (int jj = 1; jj < N; ++jj) {
-                o = j == jj ? off[jj] : o;
-                tw = j == jj ? two[jj] : tw;
-            }
-            const uint3 st = s_st[r];
-            smp::ZSobol q;
-            q.morton = st.x;
-            q.hi = st.y;
-            q.dimension = 0;
-            q.template draw_at<kW>(zp, st.z + (uint32_t)o, tw, &v0, &v1, dhash, dhash ? kDimHash : 0);
-        }
-        _Pragma("unroll") for (int j = 0; j < N; ++j) {
-            const int src = rank * N + j - c;
-            const bool mine = req && src >= 0 && src < 64;
-            const float a0 = __shfl(v0, src & 63);
-            if (mine) r0[j] = a0;
-            if (two[j]) {
-                const float a1 = __shfl(v1, src & 63);
-                if (mine) r1[j] = a1;
-            }
-        }
-    }
-    if (req) z.dimension += (uint32_t)adv;
-}
-
-// coop_draws with the results in LDS instead of registers: the lane that evaluates draw j of
-// requester rank r writes it to s_res[r * K + slot[j]] (a 2D draw's second value after it), so
-// no requester holds N results in VGPRs through the evaluation loop and no result travels by
-// ds_bpermute; returns the calling lane's rank (its record is s_res + rank * K).
 template <int kW, int N, int K>
 __device__ __forceinline__ int coop_draws_lds(smp::ZSobol &z, const smp::ZSobolParams &zp, bool req, const int (&off)[N],
                                               const bool (&two)[N], const int (&slot)[N], int adv, float *s_res,
@@ -1207,33 +1150,20 @@ __device__ __forceinline__ void zsobol_draw_quad(smp::ZSobol &z, const smp::ZSob
 // 64 B per new path instead of running this per service round with most lanes idle, and
 // k_film reads the wavelengths, pdfs and filter weight instead of re-deriving them.
 // kSmp: 0 IndependentSampler, 2 / 3 ZSobolSampler with 32- / 64-bit indices.
-#ifndef AVR_CAM_EXPERIMENT
-#define AVR_CAM_EXPERIMENT 0
-#endif
-__device__ __forceinline__ float u32_to_unit_exp(uint32_t v) { return (float)(v >> 8) * 0x1p-24f; }
-#ifndef AVR_CAM_DIM_HASH
-#define AVR_CAM_DIM_HASH 1    // the camera stage's ZSobol draws read Hash(dimension, seed) from LDS
-#endif
-#ifndef AVR_CAM_CANON_LDS
-#define AVR_CAM_CANON_LDS 1   // the camera stage's wavelength math reads the canonical tables from LDS
-#endif
+// The camera stage's ZSobol draws read Hash(dimension, seed) and its wavelength math the
+// canonical tables from LDS. The wavelength pdfs are evaluated by k_film from the wavelengths
+// (the same canonical function on the same floats, so the same bits) instead of being carried
+// from here: 16 B less written and read per sample, and the four f64 cosh move from this
+// VALU-bound stage to the HBM-bound film kernel.
 #ifndef AVR_CAM_WAVES
 #define AVR_CAM_WAVES 1   // minimum waves per SIMD asked of k_paths_camera (1: the compiler's choice)
-#endif
-// The wavelength pdfs evaluated by k_film from the wavelengths (the same canonical function on the
-// same floats, so the same bits) instead of by the camera stage and carried in cam4: 16 B less
-// written and read per sample, and the four f64 cosh move from the VALU-bound camera stage to
-// the HBM-bound film kernel (1: on)
-#ifndef AVR_FILM_PDF
-#define AVR_FILM_PDF 1
 #endif
 template <int kSmp, bool kFast>
 __global__ void __launch_bounds__(256, AVR_CAM_WAVES) k_paths_camera(Params P) {
     __shared__ float s_filt[kFiltLds];
     __shared__ double s_canon[canon::kCanonTabDoubles];
-    if constexpr (AVR_CAM_CANON_LDS)   // (fast mode too: the pdfs stay canonical)
-        for (int i = threadIdx.x; i < canon::kCanonTabDoubles; i += blockDim.x)
-            s_canon[i] = i < 128 ? canon::kLogInvC[i] : (i < 256 ? canon::kLogC[i - 128] : canon::kExp2J64[i - 256]);
+    for (int i = threadIdx.x; i < canon::kCanonTabDoubles; i += blockDim.x)   // (fast mode too: k_film's pdfs stay canonical)
+        s_canon[i] = i < 128 ? canon::kLogInvC[i] : (i < 256 ? canon::kLogC[i - 128] : canon::kExp2J64[i - 256]);
     __shared__ uint64_t s_cdh[kCamDimHash];
     __shared__ uint8_t s_zpt[24];   // smp::zperm's 24 permutations, one byte each
     if (threadIdx.x < 24) {
@@ -1299,15 +1229,10 @@ __global__ void __launch_bounds__(256, AVR_CAM_WAVES) k_paths_camera(Params P) {
         // the sampler's draws: a ZSobol quad shares its digit permutations
         // pe: the draw's preloaded pass-table entry (used when pe_ok)
         auto get1 = [&](uint64_t pe) -> float {
-#if AVR_CAM_EXPERIMENT == 2   // measurement only: no sampler work (breaks replay)
-            static_assert(kSmp >= 0, "");
-            if constexpr (kSmp != 0) return u32_to_unit_exp((uint32_t)(id * 2654435761u + smp.z.dimension++ * 40503u));
-#endif
             if constexpr (kSmp != 0) {
                 if (quad) {
                     float a, b;
-                    zsobol_draw_quad<PathSampler<kSmp>::kW>(smp.z, P.zs, false, &a, &b, AVR_CAM_DIM_HASH ? s_cdh : nullptr,
-                                                            pe, pe_ok);
+                    zsobol_draw_quad<PathSampler<kSmp>::kW>(smp.z, P.zs, false, &a, &b, s_cdh, pe, pe_ok);
                     return a;
                 }
             }
@@ -1317,12 +1242,11 @@ __global__ void __launch_bounds__(256, AVR_CAM_WAVES) k_paths_camera(Params P) {
         // of indices (zsobol_index_quad_pair), each pair one round of MixBits for the quad
         [[maybe_unused]] float pu[7] = {};   // ulam, fu0, fu1, h0, h1, u, ulight
         bool paired = false;
-#if AVR_CAM_EXPERIMENT != 2
         if constexpr (kSmp != 0) {
             if (pe_ok && ((P.zs.plo + (P.zs.log2spp & 1) - 1) >> 1) - (P.zs.log2spp & 1) <= 2) {
                 using M = typename std::conditional<PathSampler<kSmp>::kW == 2, uint64_t, uint32_t>::type;
                 const M m = PathSampler<kSmp>::kW == 2 ? (M)(((uint64_t)smp.z.hi << 32) | smp.z.morton) : (M)smp.z.morton;
-                const uint64_t *dh = AVR_CAM_DIM_HASH ? s_cdh : nullptr;
+                const uint64_t *dh = s_cdh;
                 M i0, i1, i6, i7, i8, i9;
                 zsobol_index_quad_pair<M>(m, P.zs, 0, pe0, 1, pe1, &i0, &i1, s_zpt);
                 zsobol_index_quad_pair<M>(m, P.zs, 6, pe6, 7, pe7, &i6, &i7, s_zpt);
@@ -1338,53 +1262,25 @@ __global__ void __launch_bounds__(256, AVR_CAM_WAVES) k_paths_camera(Params P) {
                 paired = true;
             }
         }
-#endif
         const float ulam = paired ? pu[0] : get1(pe0);
-#if AVR_CAM_EXPERIMENT == 1   // measurement only: wavelengths without transcendentals (breaks replay)
-        const Spec lam = {360 + 470 * ulam, 360 + 470 * (1 - ulam), 400 + 400 * ulam, 600 - 200 * ulam};
-        const Spec pdf = Spec::c(1.f / 470);
-#else
-#if AVR_CAM_CANON_LDS
         const Spec lam = kFast ? film_sample_lambda_fast(P.film, ulam) : film_sample_lambda(P.film, ulam, s_canon);
-#if !AVR_FILM_PDF
-        const Spec pdf = {film_lambda_pdf(P.film, lam.v0, s_canon), film_lambda_pdf(P.film, lam.v1, s_canon),
-                          film_lambda_pdf(P.film, lam.v2, s_canon), film_lambda_pdf(P.film, lam.v3, s_canon)};
-#endif
-#else
-        const Spec lam = kFast ? film_sample_lambda_fast(P.film, ulam) : film_sample_lambda(P.film, ulam);
-        const Spec pdf = {film_lambda_pdf(P.film, lam.v0), film_lambda_pdf(P.film, lam.v1),
-                          film_lambda_pdf(P.film, lam.v2), film_lambda_pdf(P.film, lam.v3)};
-#endif
-#endif
         float pFilmX, pFilmY, fweight;
         if constexpr (kSmp != 0) {
             float fu0, fu1;
-#if AVR_CAM_EXPERIMENT == 2
-            fu0 = get1(0);
-            fu1 = get1(0);
-#else
             if (paired) {
                 fu0 = pu[1];
                 fu1 = pu[2];
             } else if (quad) {
-                zsobol_draw_quad<PathSampler<kSmp>::kW>(smp.z, P.zs, true, &fu0, &fu1, AVR_CAM_DIM_HASH ? s_cdh : nullptr,
-                                                        pe1, pe_ok);
+                zsobol_draw_quad<PathSampler<kSmp>::kW>(smp.z, P.zs, true, &fu0, &fu1, s_cdh, pe1, pe_ok);
             } else {
                 smp.get2d(P, &fu0, &fu1);
             }
-#endif
-#if AVR_CAM_EXPERIMENT == 3   // measurement only: no filter-table sampling (breaks replay)
-            pFilmX = (float)px + fu0;
-            pFilmY = (float)py + fu1;
-            fweight = 1.f;
-#else
             if (ftab_lds) {
                 const smp::FilterTables ft = filter_lds_tables(P.film.gauss, s_filt);
                 camera_filter(P, px, py, fu0, fu1, &pFilmX, &pFilmY, &fweight, &ft);
             } else {
                 camera_filter(P, px, py, fu0, fu1, &pFilmX, &pFilmY, &fweight, nullptr);
             }
-#endif
             if (!paired) smp.z.dimension += 3;   // time (1D) and lens (2D): drawn by pbrt, unused by pinholes
         } else {
             if (ftab_lds) {
@@ -1414,18 +1310,13 @@ __global__ void __launch_bounds__(256, AVR_CAM_WAVES) k_paths_camera(Params P) {
         const float ulight = kSmp != 0 ? (paired ? pu[6] : get1(pe9)) : 0.f;
         P.ps.cam0[id] = make_float4(o.x, o.y, o.z, u);
         // ZSobol: the first light pick rides in cam1.w (k_paths' refill reads 4 x 16 B, no 4-B gather)
-        P.ps.cam1[id] = make_float4(ray.d.x, ray.d.y, ray.d.z, (kSmp != 0 && AVR_UL_IN_CAM1) ? ulight : fweight);
+        P.ps.cam1[id] = make_float4(ray.d.x, ray.d.y, ray.d.z, kSmp != 0 ? ulight : fweight);
         P.ps.cam2[id] = to4(lam);
         P.ps.cam3[id] = make_uint4((uint32_t)seqA, (uint32_t)(seqA >> 32), (uint32_t)seqB, (uint32_t)(seqB >> 32));
-#if !AVR_FILM_PDF || !AVR_CAM_CANON_LDS
-        P.ps.cam4[id] = to4(pdf);
-#endif
         P.ps.camw[id] = fweight;
         if constexpr (kSmp == 0)
             P.ps.cam5[id] = make_uint4((uint32_t)smp.rng.state, (uint32_t)(smp.rng.state >> 32), (uint32_t)smp.rng.inc,
                                        (uint32_t)(smp.rng.inc >> 32));
-        else if constexpr (!AVR_UL_IN_CAM1)
-            reinterpret_cast<float *>(P.ps.cam5)[id] = ulight;
     }
 }
 #endif
@@ -1947,27 +1838,6 @@ __global__ void __launch_bounds__(256) k_bin_scatter(const int *__restrict__ que
 #ifndef AVR_PATHS_WAVES_GRAY
 #define AVR_PATHS_WAVES_GRAY 4   // <= 128 VGPRs: with the k_paths units' -disable-machine-licm and the host-computed constants, 126 (ZSobol-64 GridMedium) / 127 (NanoVDB) and no scratch (tools/kres.py on the -Rpass-analysis log)
 #endif
-#ifndef AVR_COOP_SPEC
-#define AVR_COOP_SPEC 1
-#endif
-#ifndef AVR_DIM_HASH
-#define AVR_DIM_HASH 1   // the cooperative draws read Hash(d, seed) from the LDS table
-#endif
-#ifndef AVR_NEE_AHEAD
-#define AVR_NEE_AHEAD 1
-#endif
-#ifndef AVR_REJECT_BY_EXP
-#define AVR_REJECT_BY_EXP 1   // replay's fast reject from T_maj's FastExp factor instead of v_log_f32 + v_rcp_f32
-#endif
-#ifndef AVR_COOP_LDS
-#define AVR_COOP_LDS 1
-#endif
-#ifndef AVR_WAVE_COUNTERS
-#define AVR_WAVE_COUNTERS 1
-#endif
-#ifndef AVR_OPAQUE_CONSTS
-#define AVR_OPAQUE_CONSTS 0
-#endif
 #ifndef AVR_PATHS_WAVES_SPEC
 #define AVR_PATHS_WAVES_SPEC 2   // 4-wavelength state: ~220 VGPRs without scratch
 #endif
@@ -1975,24 +1845,9 @@ __global__ void __launch_bounds__(256) k_bin_scatter(const int *__restrict__ que
 // enough lanes of its wave need service, so each event handler runs once per batch
 // instead of once per tracking iteration (SQ_INSTS_VALU showed the per-iteration union
 // of all branches, ~8k wave-instructions, dominating an eager state machine).
-enum : int { EV_NONE = 0, EV_SCATTER = 1, EV_SHADOW_DONE = 2, EV_PHASE = 3, EV_ESCAPE = 4, EV_END = 5, EV_PHASE_WAIT = 6,
-              EV_NEE_WAIT = 7 };
-// Phase requests pooled across the block's four waves (variant, -DAVR_POOL_PHASE=1): a lane that
-// needs phase sampling publishes its sampler state and wo to a per-thread LDS slot and parks
-// (EV_PHASE_WAIT); a wave serves every request pending in the block once at least
-// AVR_POOL_MIN are pending (or none of its own lanes is tracking), evaluating the draws and the
-// phase sample for all of them at once, and flags them done; each owner picks its results up.
-// No barrier: the waves meet only through LDS atomics on the pending / done masks.
-#ifndef AVR_POOL_PHASE
-#define AVR_POOL_PHASE 0
-#endif
-#ifndef AVR_POOL_MIN
-#define AVR_POOL_MIN 32
-#endif
-// ... and the NEE spawns toward delta lights the same way (-DAVR_POOL_NEE=1, with AVR_POOL_PHASE)
-#ifndef AVR_POOL_NEE
-#define AVR_POOL_NEE 0
-#endif
+// (Phase requests and NEE spawns pooled across the block's four waves through LDS were measured
+// 4-18 % slower and removed: DESIGN §6, profiles/r05_ab_pooled_handlers.json.)
+enum : int { EV_NONE = 0, EV_SCATTER = 1, EV_SHADOW_DONE = 2, EV_PHASE = 3, EV_ESCAPE = 4, EV_END = 5 };
 
 // Spectral-state type of k_paths: Spec (4 wavelengths) in general; float for a GRAY medium
 // (sigma_a and sigma_s tables constant over 360..830 nm, decided on the host). In a gray
@@ -2135,15 +1990,13 @@ __global__ void __launch_bounds__(256, kGray ? (kMed == 1 ? 3 : AVR_PATHS_WAVES_
     __shared__ float s_maj[kVdb ? 1 : 4096];
     // (a gray medium's sigma_a / sigma_s are one value each: the kernel takes them as scalars)
     constexpr int kSigTabs = kGray ? 0 : 2;
-    // pooled phase requests: two LDS light tables instead of four (the slots below need the room)
-    constexpr bool kPoolDecl = kSmp != 0 && (kGray || AVR_COOP_SPEC) && AVR_NEE_AHEAD && AVR_COOP_LDS && AVR_POOL_PHASE;
-    constexpr int kLdsLights = kPoolDecl ? 2 : 4;
+    constexpr int kLdsLights = 4;
     __shared__ float s_tab[(kSigTabs + kLdsLights) * kNTable];
     // ImageInfiniteLight shadow rays (non-delta NEE): the sampled (u, v), p_l and the phase
     // value per lane, parked here while the lane traces its shadow ray (off the VGPR budget)
     __shared__ float4 s_img[kImage ? 256 : 1];
-    // ZSobol: the requesters' sampler state for the cooperative draws (coop_draws), 64 per wave
-    __shared__ uint3 s_zst[(kSmp != 0 && !kPoolDecl) ? 256 : 1];
+    // ZSobol: the requesters' sampler state for the cooperative draws (coop_draws_lds), 64 per wave
+    __shared__ uint3 s_zst[kSmp != 0 ? 256 : 1];
     // NEE toward a delta light: the light's spectrum at the path's wavelengths and the phase
     // value f_hat, computed when the shadow ray is spawned and read back when it finishes
     // (SampleLd evaluates them once, integrators.cpp:1311-1331)
@@ -2165,43 +2018,14 @@ __global__ void __launch_bounds__(256, kGray ? (kMed == 1 ? 3 : AVR_PATHS_WAVES_
         }
     // ZSobol: each lane's next light-pick draw (SampleLd's 1D, integrators.cpp:1302), evaluated
     // ahead with the previous bounce's cooperative phase draws (or by the camera stage)
-    __shared__ float s_ul[(kSmp != 0 && !kPoolDecl) ? 256 : 1];
-    // pooled phase requests, word-major (slot word k of thread t at s_pslot[k * 256 + t]):
-    // 0-2 sampler state (morton, hi, dimension) then wi, 3-5 wo then [3] phPdf [4-7] seqA / seqB,
-    // 6-9 the draws u0 u1 h0 h1, 10 the next segment's u, 11 the next light-pick draw (s_ul's role)
-    __shared__ float s_pslot[kPoolDecl ? 12 * 256 : 1];
-    __shared__ unsigned long long s_ppend[kPoolDecl ? 4 : 1], s_pdone[kPoolDecl ? 4 : 1];
-    constexpr bool kPoolNee = kPoolDecl && AVR_POOL_NEE && !kImage;
-    __shared__ unsigned long long s_npend[kPoolNee ? 4 : 1], s_ndone[kPoolNee ? 4 : 1];
-    __shared__ unsigned char s_plist[kPoolDecl ? 4 * 256 : 1];   // a serving wave's requester list
-    if constexpr (kPoolDecl) {
-        if (threadIdx.x < 4) s_ppend[threadIdx.x] = s_pdone[threadIdx.x] = 0;
-        if constexpr (kPoolNee)
-            if (threadIdx.x < 4) s_npend[threadIdx.x] = s_ndone[threadIdx.x] = 0;
-    }
-    float *const ul_slot = kPoolDecl ? s_pslot + 11 * 256 : s_ul;
+    __shared__ float s_ul[kSmp != 0 ? 256 : 1];
     // the host routes GridMedium majorant grids of more than 4096 cells to the wavefront kernels
     if constexpr (!kVdb) stage_majorant(P.med, s_maj);
-#ifndef AVR_VDB_MAJ_LDS
     const float *__restrict__ majp = kVdb ? P.med.majorant : s_maj;
-#endif
     // NanoVDB: the majorant's coarse occupancy level (one bit per cell pair, 16 KiB at 64^3;
     // 33 + 16 KiB per block keeps three blocks of 256 lanes per CU)
     __shared__ unsigned s_occ[kVdb ? kOccWords : 1];
     const bool useOcc = kVdb && P.med.occ != nullptr;
-#ifdef AVR_VDB_MAJ_LDS
-    // measurement variant (tools/vdb_maj_lds.py): a NanoVDB majorant of at most 4096 cells (a
-    // non-pbrt resolution, avr_set_majorant_res 16; the variant assumes it) read from LDS — staged
-    // in the occupancy level's 16 KiB, unused without it — instead of through L2: the same walk,
-    // only the majorant's memory path differs
-    float *const s_vmaj = reinterpret_cast<float *>(s_occ);
-    if constexpr (kVdb) {
-        for (int i = threadIdx.x; i < 4096; i += blockDim.x)
-            s_vmaj[i] = i < P.med.mres[0] * P.med.mres[1] * P.med.mres[2] + 1 ? P.med.majorant[i] : 0.f;
-        __syncthreads();
-    }
-    const float *__restrict__ majp = kVdb ? s_vmaj : s_maj;
-#endif
     if (useOcc) {
         const int nw = (P.med.mres[0] * P.med.mres[1] * P.med.mres[2] + 63) >> 6;
         for (int i = threadIdx.x; i < nw; i += blockDim.x) s_occ[i] = P.med.occ[i];
@@ -2220,30 +2044,14 @@ __global__ void __launch_bounds__(256, kGray ? (kMed == 1 ? 3 : AVR_PATHS_WAVES_
     auto light_table = [&](int k) -> const float * {
         return k < kLdsLights ? s_tab + (kSigTabs + k) * kNTable : P.lights.list[k].L;
     };
-#if AVR_OPAQUE_CONSTS
-    // a local copy whose loop-invariant scalars (grid and majorant resolutions, g, bounds) are
-    // passed through an empty asm at the top of the loops (opaque_consts): the compiler then
-    // re-derives float(n), 1 + g^2, bmax - bmin, ... from the scalar registers where they are
-    // used instead of hoisting ~20 derived copies into VGPRs for the kernel's lifetime
-    DevMedium m = P.med;
-    auto opaque_consts = [&]() {
-        asm volatile("" : "+s"(m.nx), "+s"(m.ny), "+s"(m.nz), "+s"(m.mres[0]), "+s"(m.mres[1]), "+s"(m.mres[2]));
-        asm volatile("" : "+s"(m.g), "+s"(m.bmin[0]), "+s"(m.bmin[1]), "+s"(m.bmin[2]), "+s"(m.bmax[0]),
-                     "+s"(m.bmax[1]), "+s"(m.bmax[2]));
-    };
-#else
     const DevMedium &m = P.med;
-    auto opaque_consts = [&]() {};
-#endif
     const int npix = P.pass_pixels;
     const long long N = (long long)npix * P.pass_samples;
     const int lane = lane_id();
     const int xcc = xcc_id();
-    // work counters: per lane in 32 bits (a lane traces at most a few thousand segments per
-    // launch), the wave-loop counters wave-uniform (scalar registers)
-#if AVR_WAVE_COUNTERS
     // work counters off the VGPR budget: per wave in LDS, one ds_add by the first active lane
-    // of each event batch (wave_count); DDA steps as a wave-uniform (scalar) sum of ballots
+    // of each event batch (wave_count); DDA steps as a wave-uniform (scalar) sum of ballots;
+    // the wave-loop counters wave-uniform (scalar registers)
     __shared__ unsigned s_cnt[4][6];
     if (threadIdx.x < 24) (&s_cnt[0][0])[threadIdx.x] = 0;
     __syncthreads();
@@ -2254,10 +2062,6 @@ __global__ void __launch_bounds__(256, kGray ? (kMed == 1 ? 3 : AVR_PATHS_WAVES_
     };
     unsigned long long nStepsW = 0;
 #define AVR_COUNT(var, k) wave_count(k)
-#else
-    uint32_t nLookup = 0, nSteps = 0, nPaths = 0, nShadow = 0, nShadowLookup = 0, nPhase = 0;
-#define AVR_COUNT(var, k) ++var
-#endif
     unsigned long long nIter = 0, nActive = 0;
 
     int mode = M_FETCH, ev = EV_NONE;
@@ -2272,16 +2076,10 @@ __global__ void __launch_bounds__(256, kGray ? (kMed == 1 ? 3 : AVR_PATHS_WAVES_
         sig_s = P.med.gray_sigma_s;
     }
     constexpr bool kZSobol = kSmp != 0;   // kSmp: 0 Independent, 2 / 3 ZSobol with 32 / 64-bit index
-    // cooperative ZSobol draws (coop_draws) in the phase handler and the refill; the
-    // 4-wavelength instantiations may opt out (AVR_COOP_SPEC=0: per-lane draws as pbrt does)
-    constexpr bool kCoop = kZSobol && (kGray || AVR_COOP_SPEC);
-    // the next light-pick draw evaluated ahead with the phase draws (s_ul)
-    constexpr bool kUlAhead = kCoop && AVR_NEE_AHEAD;
-    // ... with the cooperative draws' results in LDS (coop_draws_lds)
-    constexpr bool kCoopLds = kUlAhead && AVR_COOP_LDS;
-    __shared__ float s_res[(kCoopLds && !kPoolDecl) ? 256 * 6 : 1];
-    constexpr bool kPool = kPoolDecl;
-    static_assert(!kPool || kCoopLds, "pooled phase requests build on the LDS cooperative draws");
+    // ZSobol: the phase handler's draws evaluated cooperatively by the whole wave with their
+    // results in LDS (coop_draws_lds), including the next light-pick draw (s_ul)
+    constexpr bool kCoopLds = kZSobol;
+    __shared__ float s_res[kCoopLds ? 256 * 6 : 1];
     PathSampler<kSmp> smp{};
     int depth = 0;
     V3 po{}, pd{};         // segment origin (== the path vertex) and the path's ray direction
@@ -2317,133 +2115,14 @@ __global__ void __launch_bounds__(256, kGray ? (kMed == 1 ? 3 : AVR_PATHS_WAVES_
 #endif
     while (true) {
         AVR_SEC(0)
-        opaque_consts();
         // =================== batched event handlers (each runs once per batch) ===========
-        if constexpr (kPoolNee) {
-            // SampleLd toward a delta light (integrators.cpp:1282-1338), pooled across the block's
-            // waves like the phase requests: slot words 0-2 po, 3-5 wo, 6-9 lambda, 11 the drawn-
-            // ahead light pick in; 0-2 the shadow ray's d, 3-6 seqA / seqB, 7 the light or -1 out
-            constexpr auto WG = __HIP_MEMORY_SCOPE_WORKGROUP;
-            const int wv = threadIdx.x >> 6, tid = threadIdx.x;
-            const uint64_t pub = __ballot(ev == EV_SCATTER);
-            if (pub) {
-                if (ev == EV_SCATTER) {
-                    s_pslot[tid] = po.x;
-                    s_pslot[256 + tid] = po.y;
-                    s_pslot[512 + tid] = po.z;
-                    s_pslot[768 + tid] = -pd.x;
-                    s_pslot[1024 + tid] = -pd.y;
-                    s_pslot[1280 + tid] = -pd.z;
-                    s_pslot[1536 + tid] = lam.v0;
-                    s_pslot[1792 + tid] = lam.v1;
-                    s_pslot[2048 + tid] = lam.v2;
-                    s_pslot[2304 + tid] = lam.v3;
-                    smp.z.dimension += 3;                // the light pick (drawn ahead) and uLight
-                    L = L + Spec::c(0.f);                // L += SampleLd(...) == 0 unless a shadow ray spawns
-                    ev = EV_NEE_WAIT;
-                }
-                if (lane == __ffsll((long long)pub) - 1) __hip_atomic_fetch_or(&s_npend[wv], pub, __ATOMIC_RELEASE, WG);
-            }
-            if (__ballot(ev == EV_NEE_WAIT)) {
-                int total = 0;
-                _Pragma("unroll") for (int k = 0; k < 4; ++k)
-                    total += __popcll(__hip_atomic_load(&s_npend[k], __ATOMIC_RELAXED, WG));
-                const uint64_t tracking = __ballot((mode == M_MEDIUM || mode == M_SHADOW) && ev == EV_NONE);
-                if (total >= AVR_POOL_MIN || (total > 0 && tracking == 0)) {
-                    uint64_t take[4];
-                    _Pragma("unroll") for (int k = 0; k < 4; ++k) {
-                        unsigned long long tk = 0;
-                        if (lane == 0) tk = __hip_atomic_exchange(&s_npend[k], 0ull, __ATOMIC_ACQ_REL, WG);
-                        take[k] = __shfl(tk, 0);
-                    }
-                    const int c0 = __popcll(take[0]), c1 = __popcll(take[1]), c2 = __popcll(take[2]);
-                    const int n = c0 + c1 + c2 + __popcll(take[3]);
-                    unsigned char *lst = s_plist + wv * 256;
-                    const uint64_t lt = lane == 0 ? 0ull : ((~0ull) >> (64 - lane));
-                    if ((take[0] >> lane) & 1ull) lst[__popcll(take[0] & lt)] = (unsigned char)lane;
-                    if ((take[1] >> lane) & 1ull) lst[c0 + __popcll(take[1] & lt)] = (unsigned char)(64 + lane);
-                    if ((take[2] >> lane) & 1ull) lst[c0 + c1 + __popcll(take[2] & lt)] = (unsigned char)(128 + lane);
-                    if ((take[3] >> lane) & 1ull) lst[c0 + c1 + c2 + __popcll(take[3] & lt)] = (unsigned char)(192 + lane);
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                    __builtin_amdgcn_wave_barrier();
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                    for (int c = 0; c < n; c += 64) {
-                        const int r = c + lane;
-                        if (r < n) {
-                            const int R = lst[r];
-                            const V3 rpo = {s_pslot[R], s_pslot[256 + R], s_pslot[512 + R]};
-                            const V3 wo = {s_pslot[768 + R], s_pslot[1024 + R], s_pslot[1280 + R]};
-                            const Spec rlam = {s_pslot[1536 + R], s_pslot[1792 + R], s_pslot[2048 + R], s_pslot[2304 + R]};
-                            const float ul = ul_slot[R];
-                            int out = -1;
-                            V3 d{};
-                            uint64_t sa = 0, sb = 0;
-                            if (P.lights.n > 0) {
-                                float pmf = 0.f;
-                                const int idx = light_pick<kImage>(P.lights, ul, &pmf);
-                                if (idx >= 0) {
-                                    const DevLight &lt = P.lights.list[idx];
-                                    if (lt.type == 0) {
-                                        const V3 wi = {lt.w[0], lt.w[1], lt.w[2]};
-                                        const Spec Ls = sample_table(light_table(idx), lambda_index(rlam)) * lt.scale;
-                                        const float fval = hg_eval_c(dot(wo, wi), m.hg);
-                                        if (Ls.nonzero() && fval != 0) {
-                                            s_ls[R] = to4(Ls);
-                                            s_fhat[R] = fval;
-                                            const V3 pOut = rpo + wi * (2 * P.lights.scene_radius);
-                                            d = pOut - rpo;
-                                            sa = hash_3u32(f2u(rpo.x), f2u(rpo.y), f2u(rpo.z));
-                                            sb = hash_3u32(f2u(d.x), f2u(d.y), f2u(d.z));
-                                            out = idx;
-                                        }
-                                    }
-                                }
-                            }
-                            s_pslot[R] = d.x;
-                            s_pslot[256 + R] = d.y;
-                            s_pslot[512 + R] = d.z;
-                            s_pslot[768 + R] = __uint_as_float((uint32_t)sa);
-                            s_pslot[1024 + R] = __uint_as_float((uint32_t)(sa >> 32));
-                            s_pslot[1280 + R] = __uint_as_float((uint32_t)sb);
-                            s_pslot[1536 + R] = __uint_as_float((uint32_t)(sb >> 32));
-                            s_pslot[1792 + R] = __int_as_float(out);
-                        }
-                    }
-                    if (lane == 0) {
-                        _Pragma("unroll") for (int k = 0; k < 4; ++k)
-                            if (take[k]) __hip_atomic_fetch_or(&s_ndone[k], take[k], __ATOMIC_RELEASE, WG);
-                    }
-                }
-                const uint64_t dn = __shfl(lane == 0 ? __hip_atomic_load(&s_ndone[wv], __ATOMIC_ACQUIRE, WG) : 0ull, 0);
-                const bool fin = ev == EV_NEE_WAIT && ((dn >> lane) & 1ull);
-                const uint64_t finMask = __ballot(fin);
-                if (finMask) {
-                    if (lane == 0) __hip_atomic_fetch_and(&s_ndone[wv], ~finMask, __ATOMIC_RELAXED, WG);
-                    if (fin) {
-                        const int idx = __float_as_int(s_pslot[1792 + tid]);
-                        ev = EV_PHASE;                       // unless a shadow ray is spawned
-                        if (idx >= 0) {
-                            light = idx;
-                            T_ray = sr_l = sr_u = sconst<S>(1.f);
-                            seqA = ((uint64_t)__float_as_uint(s_pslot[1024 + tid]) << 32) | __float_as_uint(s_pslot[768 + tid]);
-                            seqB = ((uint64_t)__float_as_uint(s_pslot[1536 + tid]) << 32) | __float_as_uint(s_pslot[1280 + tid]);
-                            sd = {s_pslot[tid], s_pslot[256 + tid], s_pslot[512 + tid]};
-                            segPending = true;
-                            mode = M_SHADOW;
-                            ev = EV_NONE;
-                            AVR_COUNT(nShadow, 4);
-                        }
-                    }
-                }
-            }
-        } else
         if (__ballot(ev == EV_SCATTER)) {
             if (ev == EV_SCATTER) {
                 // SampleLd: light pick (BVH infinite-light branch) + shadow-ray spawn (1282-1338)
                 const V3 wo = -pd;
                 float ul;
-                if constexpr (kUlAhead) {
-                    ul = ul_slot[threadIdx.x];   // drawn ahead (same sampler dimension)
+                if constexpr (kZSobol) {
+                    ul = s_ul[threadIdx.x];   // drawn ahead (same sampler dimension)
                     smp.z.dimension += 1;
                 } else {
                     ul = smp.get1d(P);
@@ -2500,15 +2179,8 @@ __global__ void __launch_bounds__(256, kGray ? (kMed == 1 ? 3 : AVR_PATHS_WAVES_
                                 light = idx;
                                 T_ray = sr_l = sr_u = sconst<S>(1.f);
                                 // shadow-ray RNG (integrators.cpp:1338); u is its first draw
-#ifdef AVR_MEASURE_CHEAP_HASH
-                                // measurement only (other shadow-ray streams, statistically the
-                                // same work): a multiply-xor instead of the two MurmurHash64A
-                                seqA = ((uint64_t)f2u(po.x) * 0x9E3779B97F4A7C15ull) ^ f2u(po.y) ^ ((uint64_t)f2u(po.z) << 29);
-                                seqB = ((uint64_t)f2u(d.x) * 0xC2B2AE3D27D4EB4Full) ^ f2u(d.y) ^ ((uint64_t)f2u(d.z) << 29);
-#else
                                 seqA = hash_3u32(f2u(po.x), f2u(po.y), f2u(po.z));
                                 seqB = hash_3u32(f2u(d.x), f2u(d.y), f2u(d.z));
-#endif
                                 sd = d;
                                 segPending = true;
                                 mode = M_SHADOW;
@@ -2560,132 +2232,10 @@ __global__ void __launch_bounds__(256, kGray ? (kMed == 1 ? 3 : AVR_PATHS_WAVES_
             }
         }
         AVR_SEC(6)
-        if constexpr (kPool) {
-            constexpr auto WG = __HIP_MEMORY_SCOPE_WORKGROUP;
-            const int wv = threadIdx.x >> 6, tid = threadIdx.x;
-            // (1) publish: the sampler state and wo of every lane that needs phase sampling
-            const uint64_t pub = __ballot(ev == EV_PHASE);
-            if (pub) {
-                if (ev == EV_PHASE) {
-                    AVR_COUNT(nPhase, 2);
-                    s_pslot[tid] = __uint_as_float(smp.z.morton);
-                    s_pslot[256 + tid] = __uint_as_float(smp.z.hi);
-                    s_pslot[512 + tid] = __uint_as_float(smp.z.dimension);
-                    s_pslot[768 + tid] = -pd.x;
-                    s_pslot[1024 + tid] = -pd.y;
-                    s_pslot[1280 + tid] = -pd.z;
-                    smp.z.dimension += 5;
-                    ev = EV_PHASE_WAIT;
-                }
-                if (lane == __ffsll((long long)pub) - 1) __hip_atomic_fetch_or(&s_ppend[wv], pub, __ATOMIC_RELEASE, WG);
-            }
-            // (2) serve every pending request of the block once enough are pending, or when none
-            // of this wave's lanes is tracking (nothing else to run)
-            if (__ballot(ev == EV_PHASE_WAIT)) {
-                int total = 0;
-                _Pragma("unroll") for (int k = 0; k < 4; ++k)
-                    total += __popcll(__hip_atomic_load(&s_ppend[k], __ATOMIC_RELAXED, WG));
-                const uint64_t tracking = __ballot((mode == M_MEDIUM || mode == M_SHADOW) && ev == EV_NONE);
-                if (total >= AVR_POOL_MIN || (total > 0 && tracking == 0)) {
-                    uint64_t take[4];
-                    _Pragma("unroll") for (int k = 0; k < 4; ++k) {
-                        unsigned long long tk = 0;
-                        if (lane == 0) tk = __hip_atomic_exchange(&s_ppend[k], 0ull, __ATOMIC_ACQ_REL, WG);
-                        take[k] = __shfl(tk, 0);
-                    }
-                    const int c0 = __popcll(take[0]), c1 = __popcll(take[1]), c2 = __popcll(take[2]);
-                    const int n = c0 + c1 + c2 + __popcll(take[3]);
-                    unsigned char *lst = s_plist + wv * 256;
-                    const uint64_t lt = lane == 0 ? 0ull : ((~0ull) >> (64 - lane));
-                    if ((take[0] >> lane) & 1ull) lst[__popcll(take[0] & lt)] = (unsigned char)lane;
-                    if ((take[1] >> lane) & 1ull) lst[c0 + __popcll(take[1] & lt)] = (unsigned char)(64 + lane);
-                    if ((take[2] >> lane) & 1ull) lst[c0 + c1 + __popcll(take[2] & lt)] = (unsigned char)(128 + lane);
-                    if ((take[3] >> lane) & 1ull) lst[c0 + c1 + c2 + __popcll(take[3] & lt)] = (unsigned char)(192 + lane);
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                    __builtin_amdgcn_wave_barrier();
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                    // the five draws of every requester (phase 2D at +0, h0 h1 u at +2..4, the next
-                    // light pick at +5), spread over the wave as coop_draws_lds does for one wave
-                    for (int c = 0; c < 5 * n; c += 64) {
-                        const int t5 = c + lane;
-                        if (t5 < 5 * n) {
-                            const int r = t5 / 5, j = t5 - r * 5;
-                            const int R = lst[r];
-                            smp::ZSobol q;
-                            q.morton = __float_as_uint(s_pslot[R]);
-                            q.hi = __float_as_uint(s_pslot[256 + R]);
-                            q.dimension = 0;
-                            const uint32_t d0 = __float_as_uint(s_pslot[512 + R]);
-                            const int o = j == 0 ? 0 : j + 1;   // dimension offsets 0, 2, 3, 4, 5
-                            const int w = 6 + o;                // slot words 6-7, 8, 9, 10, 11
-                            float v0, v1;
-                            q.template draw_at<PathSampler<kSmp>::kW>(P.zs, d0 + (uint32_t)o, j == 0, &v0, &v1,
-                                                                        AVR_DIM_HASH ? s_dh : nullptr, AVR_DIM_HASH ? kDimHash : 0);
-                            s_pslot[w * 256 + R] = v0;
-                            if (j == 0) s_pslot[(w + 1) * 256 + R] = v1;
-                        }
-                    }
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                    __builtin_amdgcn_wave_barrier();
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                    // phase-function sampling (integrators.cpp:1046-1061) and the next segment's
-                    // RNG seeds, one lane per requester
-                    for (int c = 0; c < n; c += 64) {
-                        const int r = c + lane;
-                        if (r < n) {
-                            const int R = lst[r];
-                            const V3 wo = {s_pslot[768 + R], s_pslot[1024 + R], s_pslot[1280 + R]};
-                            const float up0 = s_pslot[1536 + R], up1 = s_pslot[1792 + R];
-                            const float h0 = s_pslot[2048 + R], h1 = s_pslot[2304 + R];
-                            float phPdf;
-                            const V3 wi = hg_sample_c<kFast>(wo, m.hg, up0, up1, &phPdf);
-                            const uint64_t a = hash_u32(f2u(h0)), b = hash_u32(f2u(h1));
-                            s_pslot[R] = wi.x;
-                            s_pslot[256 + R] = wi.y;
-                            s_pslot[512 + R] = wi.z;
-                            s_pslot[768 + R] = phPdf;
-                            s_pslot[1024 + R] = __uint_as_float((uint32_t)a);
-                            s_pslot[1280 + R] = __uint_as_float((uint32_t)(a >> 32));
-                            s_pslot[1536 + R] = __uint_as_float((uint32_t)b);
-                            s_pslot[1792 + R] = __uint_as_float((uint32_t)(b >> 32));
-                        }
-                    }
-                    if (lane == 0) {
-                        _Pragma("unroll") for (int k = 0; k < 4; ++k)
-                            if (take[k]) __hip_atomic_fetch_or(&s_pdone[k], take[k], __ATOMIC_RELEASE, WG);
-                    }
-                }
-                // (3) pick up this wave's finished requests (served here or by another wave)
-                const uint64_t dn = __shfl(lane == 0 ? __hip_atomic_load(&s_pdone[wv], __ATOMIC_ACQUIRE, WG) : 0ull, 0);
-                const bool fin = ev == EV_PHASE_WAIT && ((dn >> lane) & 1ull);
-                const uint64_t finMask = __ballot(fin);
-                if (finMask) {
-                    if (lane == 0) __hip_atomic_fetch_and(&s_pdone[wv], ~finMask, __ATOMIC_RELAXED, WG);
-                    if (fin) {
-                        const float phPdf = s_pslot[768 + tid];
-                        if (phPdf == 0) {
-                            ev = EV_END;
-                        } else {
-                            beta = beta * unit_quot(phPdf);
-                            r_l = r_u / phPdf;
-                            pd = {s_pslot[tid], s_pslot[256 + tid], s_pslot[512 + tid]};
-                            seqA = ((uint64_t)__float_as_uint(s_pslot[1280 + tid]) << 32) | __float_as_uint(s_pslot[1024 + tid]);
-                            seqB = ((uint64_t)__float_as_uint(s_pslot[1792 + tid]) << 32) | __float_as_uint(s_pslot[1536 + tid]);
-                            u = s_pslot[2560 + tid];
-                            sd = pd;
-                            segPending = true;
-                            mode = M_MEDIUM;
-                            ev = EV_NONE;
-                        }
-                    }
-                }
-            }
-        } else
         if (__ballot(ev == EV_PHASE)) {
             // ZSobol: the phase 2D draw and the next segment's three 1D draws of every lane in
             // EV_PHASE, evaluated cooperatively by the whole wave
             // (and, at offset 5, the next bounce's light-pick draw, parked in s_ul)
-            float q0[5], q1[5];
             [[maybe_unused]] const float *qr = nullptr;   // this lane's results in s_res (kCoopLds)
             if constexpr (kCoopLds) {
                 // [u0, u1] phase 2D, [h0, h1, u] the next segment, [ul] the next light pick
@@ -2694,30 +2244,11 @@ __global__ void __launch_bounds__(256, kGray ? (kMed == 1 ? 3 : AVR_PATHS_WAVES_
                 constexpr int slot[5] = {0, 2, 3, 4, 5};
                 float *sres = s_res + (threadIdx.x & ~63u) * 6;
                 const int rk = coop_draws_lds<PathSampler<kSmp>::kW, 5, 6>(smp.z, P.zs, ev == EV_PHASE, off, two, slot, 5, sres,
-                                                                          s_zst + (threadIdx.x & ~63u), AVR_DIM_HASH ? s_dh : nullptr,
+                                                                          s_zst + (threadIdx.x & ~63u), s_dh,
                                                                           kZpt ? s_zpt : nullptr);
                 qr = sres + rk * 6;
                 if (ev == EV_PHASE) s_ul[threadIdx.x] = qr[5];
-            } else if constexpr (kUlAhead) {
-                constexpr int off[5] = {0, 2, 3, 4, 5};
-                constexpr bool two[5] = {true, false, false, false, false};
-                coop_draws<PathSampler<kSmp>::kW, 5>(smp.z, P.zs, ev == EV_PHASE, off, two, 5, q0, q1,
-                                                     s_zst + (threadIdx.x & ~63u), AVR_DIM_HASH ? s_dh : nullptr);
-                if (ev == EV_PHASE) s_ul[threadIdx.x] = q0[4];
-            } else if constexpr (kCoop) {
-                constexpr int off[4] = {0, 2, 3, 4};
-                constexpr bool two[4] = {true, false, false, false};
-                float r0[4], r1[4];
-                coop_draws<PathSampler<kSmp>::kW, 4>(smp.z, P.zs, ev == EV_PHASE, off, two, 5, r0, r1,
-                                                     s_zst + (threadIdx.x & ~63u), AVR_DIM_HASH ? s_dh : nullptr);
-                _Pragma("unroll") for (int j = 0; j < 4; ++j) {
-                    q0[j] = r0[j];
-                    q1[j] = r1[j];
-                }
             }
-#ifdef AVR_SEC_SPLIT_PHASE
-            AVR_SEC(7)   // profiling variant: section 6 = the cooperative draws only, the rest of the phase handler into 7
-#endif
             if (ev == EV_PHASE) {
                 // phase-function sampling (integrators.cpp:1046-1061), then the next segment
                 AVR_COUNT(nPhase, 2);
@@ -2725,36 +2256,22 @@ __global__ void __launch_bounds__(256, kGray ? (kMed == 1 ? 3 : AVR_PATHS_WAVES_
                 if constexpr (kCoopLds) {
                     up0 = qr[0];
                     up1 = qr[1];
-                } else if constexpr (kCoop) {
-                    up0 = q0[0];
-                    up1 = q1[0];
                 } else {
                     smp.get2d(P, &up0, &up1);
                 }
                 float phPdf;
-#ifdef AVR_MEASURE_CHEAP_PHASE
-                // measurement only (other directions, statistically the same work): the hardware
-                // transcendentals of fast mode and multiply-xor seeds instead of two MurmurHash64A
-                const V3 wi = hg_sample_c<true>(-pd, m.hg, up0, up1, &phPdf);
-#else
                 const V3 wi = hg_sample_c<kFast>(-pd, m.hg, up0, up1, &phPdf);
-#endif
                 if (phPdf == 0) {
                     ev = EV_END;
                 } else {
                     beta = beta * unit_quot(phPdf);
                     r_l = r_u / phPdf;
                     pd = wi;
-                    const float h0 = kCoopLds ? qr[2] : (kCoop ? q0[1] : smp.get1d(P));
-                    const float h1 = kCoopLds ? qr[3] : (kCoop ? q0[2] : smp.get1d(P));
-#ifdef AVR_MEASURE_CHEAP_PHASE
-                    seqA = (uint64_t)f2u(h0) * 0x9E3779B97F4A7C15ull;
-                    seqB = (uint64_t)f2u(h1) * 0xC2B2AE3D27D4EB4Full;
-#else
+                    const float h0 = kCoopLds ? qr[2] : smp.get1d(P);
+                    const float h1 = kCoopLds ? qr[3] : smp.get1d(P);
                     seqA = hash_u32(f2u(h0));
                     seqB = hash_u32(f2u(h1));
-#endif
-                    u = kCoopLds ? qr[4] : (kCoop ? q0[3] : smp.get1d(P));
+                    u = kCoopLds ? qr[4] : smp.get1d(P);
                     sd = pd;
                     segPending = true;
                     mode = M_MEDIUM;
@@ -2849,7 +2366,7 @@ __global__ void __launch_bounds__(256, kGray ? (kMed == 1 ? 3 : AVR_PATHS_WAVES_
                     [[maybe_unused]] float ul5 = 0.f;
                     [[maybe_unused]] uint4 c5{};
                     if constexpr (!kZSobol) c5 = P.ps.cam5[gn];
-                    else if constexpr (kUlAhead) ul5 = AVR_UL_IN_CAM1 ? c1.w : reinterpret_cast<const float *>(P.ps.cam5)[gn];
+                    else ul5 = c1.w;
                     g = gn;
                     if constexpr (kZSobol) {
                         // the sample's ZSobol state past the camera draws and the first segment's three
@@ -2858,7 +2375,7 @@ __global__ void __launch_bounds__(256, kGray ? (kMed == 1 ? 3 : AVR_PATHS_WAVES_
                         const int slot = g % npix, sIdx = g / npix;
                         const int pix = P.pix_order ? P.pix_order[slot] : slot;
                         smp.start(P, pix % P.film.width, pix / P.film.width, P.sample_base + sIdx);
-                        if constexpr (kUlAhead) ul_slot[threadIdx.x] = ul5;
+                        s_ul[threadIdx.x] = ul5;
                         smp.z.dimension = 9;
                     } else {
                         smp.rng.state = ((uint64_t)c5.y << 32) | c5.x;
@@ -2903,13 +2420,7 @@ __global__ void __launch_bounds__(256, kGray ? (kMed == 1 ? 3 : AVR_PATHS_WAVES_
                 segPending = false;
             }
         }
-#ifdef AVR_BLOCK_SYNC
-        // measurement variant: the block's four waves meet at a barrier once per iteration (the
-        // cost of lockstep iterations, the precondition for pooling event handlers across waves)
-        if (!__syncthreads_or(mode != M_DONE)) break;
-#else
         if (__ballot(mode != M_DONE) == 0) break;
-#endif
 
         // =================== tracking: advance every busy lane collision by collision ======
         // until a batch of lanes needs service (events or refill) or none is busy.
@@ -2917,7 +2428,7 @@ __global__ void __launch_bounds__(256, kGray ? (kMed == 1 ? 3 : AVR_PATHS_WAVES_
             AVR_SEC(3)
             const bool busy = (mode == M_MEDIUM || mode == M_SHADOW) && ev == EV_NONE;
             const uint64_t busyNow = __ballot(busy);
-            const uint64_t service = __ballot(mode != M_DONE && !busy && (!kPool || (ev != EV_PHASE_WAIT && ev != EV_NEE_WAIT)));
+            const uint64_t service = __ballot(mode != M_DONE && !busy);
             if (busyNow == 0 || __popcll(service) >= P.refill_min) break;
             ++nIter;
             nActive += __popcll(busyNow);
@@ -2943,11 +2454,7 @@ __global__ void __launch_bounds__(256, kGray ? (kMed == 1 ? 3 : AVR_PATHS_WAVES_
                     if (!ddal_next(it, majp, maj_sy, maj_sz, maj_n, &s0, &s1, &mv)) {
                         walk = 2;
                     } else {
-#if AVR_WAVE_COUNTERS
                         stepped = true;
-#else
-                        ++nSteps;
-#endif
                         // zero-majorant cell: T_maj *= FastExp(-0 * dt); for a gray medium that
                         // factor is exactly 1, so the multiply is skipped
                         const S sigma_maj = sig_t * mv;
@@ -2967,18 +2474,15 @@ __global__ void __launch_bounds__(256, kGray ? (kMed == 1 ? 3 : AVR_PATHS_WAVES_
                         }
                     }
                 }
-#if AVR_WAVE_COUNTERS
                 nStepsW += __popcll(__ballot(stepped));
-#endif
                 // unconditional (all busy lanes): in flight during the candidate test below
                 if (kVdb && useOcc) ddal_prefetch_occ(it, majp, s_occ, maj_n);
                 else ddal_prefetch(it, majp);
                 if (walk == 0 && !needNext) {
                     // Fast reject: the candidate t = tMin - log(1-u)/sigma_maj is decided against
-                    // segMax from the hardware log2 (v_log_f32, ~1 ulp) when it lies outside an
-                    // error margin bounding |tFast - t| (relative terms for the log and the add,
-                    // an absolute one for log2 near 1); accepted and ambiguous candidates stay
-                    // "pending" and are decided exactly, once per wave, after the walk.
+                    // segMax from T_maj's own FastExp factor when 1-u lies outside an error margin
+                    // (below); accepted and ambiguous candidates stay "pending" and are decided
+                    // exactly, once per wave, after the walk.
                     const float sm0 = st0 * mv;
                     bool pending;
                     float dt = segMax - tMin;
@@ -2988,7 +2492,7 @@ __global__ void __launch_bounds__(256, kGray ? (kMed == 1 ? 3 : AVR_PATHS_WAVES_
                     if constexpr (kFast) {
                         // fast mode: the hardware candidate is the candidate (decided once)
                         pending = tMin + m_exp_dist<true>(u, sm0) < segMax;
-                    } else if constexpr (AVR_REJECT_BY_EXP) {
+                    } else {
                         // t = tMin + (-log(1-u) / sm0) >= segMax  <=>  1-u <= exp(-sm0 (segMax - tMin))
                         // in real arithmetic; FastExp(-A) (relative error < 1.2e-4 for A < 40, the
                         // rounding of A = sm0 * dt and of pbrt's log / division / add all inside
@@ -2996,12 +2500,6 @@ __global__ void __launch_bounds__(256, kGray ? (kMed == 1 ? 3 : AVR_PATHS_WAVES_
                         // transcendental of its own — the factor is T_maj's anyway
                         const float A = sm0 * dt;
                         pending = !(A < 40.f && (1 - u) <= sv0(fac) * (1 - 1e-3f - 5e-7f * A));
-                    } else {
-                        const float rs = __builtin_amdgcn_rcpf(sm0);
-                        const float eFast = -__builtin_amdgcn_logf(1 - u) * (kLn2 * rs);
-                        const float tFast = tMin + eFast;
-                        const float margin = 1e-5f * eFast + 4.8e-7f * __builtin_fabsf(segMax) + 1e-6f * rs + 1e-30f;
-                        pending = !(tFast > segMax + margin);
                     }
                     if (pending) {
                         walk = 1;
@@ -3161,20 +2659,11 @@ __global__ void __launch_bounds__(256, kGray ? (kMed == 1 ? 3 : AVR_PATHS_WAVES_
 #ifdef AVR_PROBE_STATS
     probe.flush(P.stats);
 #endif
-#if AVR_WAVE_COUNTERS
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     if (lane < 5 && wcnt[lane]) atomicAdd(P.stats + lane, (unsigned long long)wcnt[lane]);
     if (lane == 0 && nStepsW) atomicAdd(P.stats + 5, nStepsW);
-#else
-    flush_stat(P.stats, 0, nLookup);
-    flush_stat(P.stats, 1, nPaths);
-    flush_stat(P.stats, 2, nPhase);
-    flush_stat(P.stats, 3, nShadowLookup);
-    flush_stat(P.stats, 4, nShadow);
-    flush_stat(P.stats, 5, nSteps);
-#endif
 #undef AVR_COUNT
     if (lane == 0) {   // wave-uniform counters: one add per wave
         if (nIter) atomicAdd(P.stats + 8, nIter);
@@ -3198,8 +2687,7 @@ __device__ __forceinline__ void film_load_sample(const Params &P, size_t id, Spe
     if (P.rec_mode) {
         *L = spec4(P.ps.rec[id]);
         *lam = spec4(P.ps.cam2[id]);
-        // with AVR_FILM_PDF the pdfs are evaluated from the wavelengths after the loads (film_pdfs)
-        if (!(AVR_FILM_PDF && AVR_CAM_CANON_LDS)) *pdf = spec4(P.ps.cam4[id]);
+        // the pdfs are evaluated from the wavelengths after the loads (film_pdfs)
         if (P.film.filter_type != 0) *w = P.ps.camw[id];
     } else {
         *L = spec4(P.ps.L[id]);
@@ -3210,20 +2698,25 @@ __device__ __forceinline__ void film_load_sample(const Params &P, size_t id, Spe
     }
 }
 // the camera stage's wavelength pdfs (film_lambda_pdf: the same canonical function of the same
-// floats, so the same bits) when k_film evaluates them (AVR_FILM_PDF with k_paths' records)
+// floats, so the same bits) when k_film evaluates them (k_paths' records)
 __device__ __forceinline__ void film_pdfs(const Params &P, const Spec &lam, Spec *pdf, const double *canon_tabs) {
-    if (AVR_FILM_PDF && AVR_CAM_CANON_LDS && P.rec_mode)
+    if (P.rec_mode)
         *pdf = {film_lambda_pdf(P.film, lam.v0, canon_tabs), film_lambda_pdf(P.film, lam.v1, canon_tabs),
                 film_lambda_pdf(P.film, lam.v2, canon_tabs), film_lambda_pdf(P.film, lam.v3, canon_tabs)};
 }
-// The pass's wavelength pdfs into cam4 for the host accessor (avr_last_pass_samples) when the
-// camera stage leaves them to k_film (AVR_FILM_PDF): the same function of the same wavelengths
+// The pass's wavelength pdfs into cam4 for the host accessor (avr_last_pass_samples): k_film's
+// own evaluation (film_pdfs: the same overload over the same LDS-staged canonical tables), so
+// the accessor returns exactly the pdfs the film divided by
 __global__ void __launch_bounds__(256) k_lambda_pdfs(DevFilm film, const float4 *__restrict__ lam, float4 *__restrict__ pdf,
                                                      long long n) {
+    __shared__ double s_canon[canon::kCanonTabDoubles];
+    for (int i = threadIdx.x; i < canon::kCanonTabDoubles; i += blockDim.x)
+        s_canon[i] = i < 128 ? canon::kLogInvC[i] : (i < 256 ? canon::kLogC[i - 128] : canon::kExp2J64[i - 256]);
+    __syncthreads();
     for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
         const float4 l = lam[i];
-        pdf[i] = make_float4(film_lambda_pdf(film, l.x), film_lambda_pdf(film, l.y), film_lambda_pdf(film, l.z),
-                             film_lambda_pdf(film, l.w));
+        pdf[i] = make_float4(film_lambda_pdf(film, l.x, s_canon), film_lambda_pdf(film, l.y, s_canon),
+                             film_lambda_pdf(film, l.z, s_canon), film_lambda_pdf(film, l.w, s_canon));
     }
 }
 // The X, Y, Z matching tables interleaved per wavelength ({X, Y, Z, 0}, staged in LDS by
@@ -3277,10 +2770,9 @@ __global__ void __launch_bounds__(256, AVR_FILM_WAVES) k_film(Params P) {
     __shared__ float4 s_xyz[kNTable];
     for (int i = threadIdx.x; i < kNTable; i += blockDim.x)
         s_xyz[i] = make_float4(P.film.xyz[i], P.film.xyz[kNTable + i], P.film.xyz[2 * kNTable + i], 0.f);
-    __shared__ double s_canon[AVR_FILM_PDF ? canon::kCanonTabDoubles : 1];   // the pdfs' cosh tables
-    if constexpr (AVR_FILM_PDF)
-        for (int i = threadIdx.x; i < canon::kCanonTabDoubles; i += blockDim.x)
-            s_canon[i] = i < 128 ? canon::kLogInvC[i] : (i < 256 ? canon::kLogC[i - 128] : canon::kExp2J64[i - 256]);
+    __shared__ double s_canon[canon::kCanonTabDoubles];   // the pdfs' cosh tables
+    for (int i = threadIdx.x; i < canon::kCanonTabDoubles; i += blockDim.x)
+        s_canon[i] = i < 128 ? canon::kLogInvC[i] : (i < 256 ? canon::kLogC[i - 128] : canon::kExp2J64[i - 256]);
     __syncthreads();
     const int npix = P.pass_pixels;
     const int nb = kBuckets ? P.film.nbuckets : 0;
@@ -3647,12 +3139,6 @@ __global__ void __launch_bounds__(256) k_zsobol_pass_table(smp::ZSobolParams zp,
                        : smp::zsobol_pass_entry<uint32_t>((uint32_t)m, (uint32_t)d, zp, plo, u0);
             e.y = wide ? smp::zsobol_pass_entry<uint64_t>(m, (uint32_t)d + 1, zp, plo, u1)
                        : smp::zsobol_pass_entry<uint32_t>((uint32_t)m, (uint32_t)d + 1, zp, plo, u1);
-        }
-        if (AVR_ZS_PACK && zp.pperm4) {
-            e.x = wide ? smp::zsobol_pass_pack<uint64_t>(m, (uint32_t)d, zp, plo, e.x)
-                       : smp::zsobol_pass_pack<uint32_t>((uint32_t)m, (uint32_t)d, zp, plo, e.x);
-            e.y = wide ? smp::zsobol_pass_pack<uint64_t>(m, (uint32_t)d + 1, zp, plo, e.y)
-                       : smp::zsobol_pass_pack<uint32_t>((uint32_t)m, (uint32_t)d + 1, zp, plo, e.y);
         }
         *reinterpret_cast<ulonglong2 *>(table + row) = e;
         // the camera stage's pairs (0, 1), (6, 7), (8, 9) also into its compact per-pixel copy

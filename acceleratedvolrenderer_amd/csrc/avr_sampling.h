@@ -114,21 +114,9 @@ struct ZSobolParams {
     // and 6..9, in that order, 48 B per pixel in scanline order) so its loads stream instead of
     // gathering 48 B from each pixel's row (null = read the rows)
     const uint64_t *ctab;
-    // 1: the pass table's entries also carry, in bits 36..55, the permutations of the digit
-    // under the perm-fixed one for each of the 4 values of that digit (5 bits each; the host sets
-    // it when the fixed prefix fits 36 bits), so a draw mixes one digit fewer (zsobol_pass_pack)
-    int pperm4;
 };
-// Packed permutations in pass-table entries (zsobol_pass_pack): compiled in only with
-// AVR_ZS_PACK 1 (measured slower: profiles/r05_ab_pass_pack.json), so the default draws carry
-// no check for them
-#ifndef AVR_ZS_PACK
-#define AVR_ZS_PACK 0
-#endif
-// the fixed-prefix bits of a pass-table entry (below the packed permutations when pperm4)
-AVR_HD uint64_t pass_prefix_mask(const ZSobolParams &zp) {
-    return (AVR_ZS_PACK && zp.pperm4) ? 0x0000000fffffffffull : 0x00ffffffffffffffull;
-}
+// the fixed-prefix bits of a pass-table entry (below its perm-fixed digit's permutation)
+AVR_HD uint64_t pass_prefix_mask(const ZSobolParams &) { return 0x00ffffffffffffffull; }
 
 // Morton(pixel) << log2(spp) | sampleIndex fits 32 bits (nBase4Digits <= 16: e.g. 1024 spp
 // at 1080p); beyond it (4096 spp at 720p ...) the index and the digit prefixes are 64-bit.
@@ -274,26 +262,6 @@ AVR_HD uint64_t zsobol_pass_entry_from(M morton, uint32_t dimension, const ZSobo
     return (fixed >> plo) | ((uint64_t)perm << 56);
 }
 
-// A pass entry with the permutations of the digit under its perm-fixed digit iTop packed in
-// bits 36..55 (ZSobolParams::pperm4): that digit's permutation hashes the bits above it, which
-// are the pass's fixed bits and digit iTop's value — one of 4 — so the 4 candidates are
-// tabulated per (pixel, dimension, pass) instead of mixed per draw. `morton`: any sample of
-// the pass; the entry's prefix must fit 36 bits (the host checks).
-template <typename M>
-AVR_HD uint64_t zsobol_pass_pack(M morton, uint32_t dimension, const ZSobolParams &zp, int plo, uint64_t e) {
-    const int pw = zp.log2spp & 1;
-    const int iTop = (plo + pw - 1) >> 1;
-    if (iTop - 1 < pw) return e;
-    constexpr int kBits = 8 * (int)sizeof(M);
-    const int shTop = 2 * iTop - pw;   // the bits above digit iTop - 1 start here
-    const M above = shTop + 2 >= kBits ? M(0) : M((morton >> (shTop + 2)) << 2);
-    const M dmix = (M)(0x55555555u * dimension);
-    uint64_t packed = 0;
-    _Pragma("unroll") for (uint32_t v = 0; v < 4; ++v)
-        packed |= (uint64_t)mix_perm24<M>((M)((above | (M)v) ^ dmix)) << (5 * v);
-    return (e & 0xff00000fffffffffull) | (packed << 36);
-}
-
 // GetSampleIndex of (morton, dimension) from the sample's pass entry e: the varying digits
 // computed, the perm-fixed digit from e's permutation, the rest from e; an odd log2(spp)'s
 // final base-2 digit as zsobol_lower. Bit-identical to zsobol_index without tables.
@@ -308,10 +276,7 @@ AVR_HD M zsobol_index_pass(M morton, uint32_t dimension, const ZSobolParams &zp,
     for (int i = iTop; i >= pw; --i) {   // digits with shift < plo
         const int shift = 2 * i - pw;
         uint32_t p = perm;
-        if (AVR_ZS_PACK && zp.pperm4 && i == iTop - 1) {
-            // packed by the table build: indexed by the value of the digit above (bits shift + 2..)
-            p = (uint32_t)(e >> (36 + 5 * ((uint32_t)(morton >> (shift + 2)) & 3u))) & 31u;
-        } else if (shift + 2 < plo) {
+        if (shift + 2 < plo) {
             const M higher = shift + 2 >= kBits ? M(0) : M(morton >> (shift + 2));
             p = mix_perm24<M>((M)(higher ^ (M)dmix));
         }
@@ -337,14 +302,7 @@ template <typename M>
 AVR_HD M zsobol_index(M morton, uint32_t dimension, const ZSobolParams &zp, const uint8_t *zpt = nullptr) {
     if (zp.ptab && (int)dimension < zp.pdims) {
         const uint32_t pm = (uint32_t)(morton >> zp.log2spp);
-#if defined(AVR_MEASURE_NO_PTAB) && defined(AVR_KPATHS_TU)
-        // measurement only (wrong samples, statistically the same work): the pass-table entry
-        // from registers instead of its HBM / L2 read — the read's latency cost in k_paths
-        const uint64_t fake = ((uint64_t)pm * 0x9E3779B97F4A7C15ull) ^ ((uint64_t)dimension << 40);
-        return zsobol_index_pass<M>(morton, dimension, zp, fake);
-#else
         return zsobol_index_pass<M>(morton, dimension, zp, zp.ptab[(size_t)pm * (size_t)zp.pdims + dimension], zpt);
-#endif
     }
     uint32_t up;
     const uint32_t pm = (uint32_t)(morton >> zp.log2spp);
@@ -441,7 +399,6 @@ inline ZSobolParams zsobol_params(int spp, int width, int height, int seed) {
     zp.pdims = 0;
     zp.plo = 0;
     zp.ctab = nullptr;
-    zp.pperm4 = 0;
     return zp;
 }
 

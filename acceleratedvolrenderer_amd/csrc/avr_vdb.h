@@ -21,9 +21,6 @@
 #ifndef AVR_HD
 #define AVR_HD __host__ __device__ __forceinline__
 #endif
-#ifndef AVR_NT_FETCH
-#define AVR_NT_FETCH 0   // non-temporal density fetches (measured)
-#endif
 
 namespace avr {
 namespace vdb {
@@ -186,15 +183,7 @@ AVR_HD float sample_trilinear(const Apron &g, float x, float y, float z) {
             v000 = v001 = v010 = v011 = v100 = v101 = v110 = v111 = g.consts[-s - 1];
         } else if (g.fat) {
             const float *f = g.fat + ((long long)s * 512 + ((rx & 7) << 6) + ((ry & 7) << 3) + (rz & 7)) * 8;
-#if defined(__HIP_DEVICE_COMPILE__) && AVR_NT_FETCH
-            // streaming (non-temporal) loads: the gathered taps are rarely reused, so they should
-            // not evict the 64^3 majorant every DDA step reads from L2
-            typedef float v4f __attribute__((ext_vector_type(4)));
-            const v4f lo = __builtin_nontemporal_load(reinterpret_cast<const v4f *>(f)),
-                      hi = __builtin_nontemporal_load(reinterpret_cast<const v4f *>(f + 4));
-            v000 = lo.x; v001 = lo.y; v010 = lo.z; v011 = lo.w;
-            v100 = hi.x; v101 = hi.y; v110 = hi.z; v111 = hi.w;
-#elif defined(__HIP_DEVICE_COMPILE__)
+#if defined(__HIP_DEVICE_COMPILE__)
             const float4 lo = *reinterpret_cast<const float4 *>(f), hi = *reinterpret_cast<const float4 *>(f + 4);
             v000 = lo.x; v001 = lo.y; v010 = lo.z; v011 = lo.w;
             v100 = hi.x; v101 = hi.y; v110 = hi.z; v111 = hi.w;

@@ -1970,8 +1970,10 @@ void *oracle_vdb_create(int nLeaves, const int *leafOrigin, const float *leafVal
         for (int a = 0; a < 3; ++a) g->tileBox.push_back(tileOrigin[3 * t + a]);
         g->tileBox.push_back(tileSize[t]);
         g->tileValue.push_back(tileValue[t]);
-        if (tileSize[t] == 8) {
-            const int *o = tileOrigin + 3 * t;
+        const int *o = tileOrigin + 3 * t;
+        // the hash lookup keys a voxel by (x >> 3, y >> 3, z >> 3): only an 8-aligned 8^3 tile
+        // covers exactly its key's block; any other tile goes to the box search
+        if (tileSize[t] == 8 && ((o[0] | o[1] | o[2]) & 7) == 0) {
             g->tile8[VdbTree::Key(o[0], o[1], o[2])] = tileValue[t];
         } else {
             g->bigTiles.push_back(t);

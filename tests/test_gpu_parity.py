@@ -50,8 +50,9 @@ def _integrator(scene, **kw):
 
 
 def _compare_samples(integ, ref, first, ns):
-    """Per-sample replay: GPU L / lambda / filter weight of the last pass vs
-    oracle_pixel_sample. A sample counts as exact when all three are bit-identical."""
+    """Per-sample replay: GPU L / lambda / lambda pdfs / filter weight of the last pass vs
+    oracle_pixel_sample. A sample counts as exact when all four are bit-identical (the pdfs are
+    the ones k_film divides by: avr_last_pass_samples evaluates them with k_film's overload)."""
     f = integ.scene.film
     npix = f.width * f.height
     _, _, L, lam, pdf = integ.ctx.last_pass_samples(npix, ns)
@@ -67,6 +68,8 @@ def _compare_samples(integ, ref, first, ns):
             total += 1
             if (np.array_equal(L[g].view(np.uint32), Lo.view(np.uint32))
                     and np.array_equal(lam[g].view(np.uint32), lo.view(np.uint32))
+                    and np.array_equal(np.asarray(pdf[g], np.float32).view(np.uint32),
+                                       np.asarray(po, np.float32).view(np.uint32))
                     and np.float32(wts[g]).view(np.uint32) == np.float32(wo).view(np.uint32)):
                 exact += 1
             worst = max(worst, float(np.max(np.abs(lam[g] - lo))))

@@ -17,7 +17,7 @@ def hdr(tmp_path_factory):
     d = tmp_path_factory.mktemp("smp")
     src = d / "shim.cpp"
     src.write_text(
-        "#define AVR_HD inline\n#define AVR_ZS_PACK 1\n"
+        "#define AVR_HD inline\n"
         f'#include "{ROOT}/acceleratedvolrenderer_amd/csrc/avr_sampling.h"\n'
         "using namespace avr::smp;\n"
         'extern "C" {\n'
@@ -55,28 +55,6 @@ def hdr(tmp_path_factory):
         "      pass[i] = zsobol_index_pass<unsigned long long>(ms, d, zt, zsobol_pass_entry<unsigned long long>(mb, d, zp, plo, up)); }\n"
         "    else { full[i] = zsobol_index<unsigned>((unsigned)ms, d, zp);\n"
         "      pass[i] = zsobol_index_pass<unsigned>((unsigned)ms, d, zt, zsobol_pass_entry<unsigned>((unsigned)mb, d, zp, plo, up)); } } }\n"
-        "int zs_pass_packed(int spp, int rx, int ry, int n, const int *q, unsigned long long *full,\n"
-        "                   unsigned long long *pass) {\n"
-        "  ZSobolParams zp = zsobol_params(spp, rx, ry, 0); int packed = 0;\n"
-        "  for (int i = 0; i < n; ++i) {\n"
-        "    const int *r = q + 6 * i; int base = r[4], S = r[5], plo = 0;\n"
-        "    while ((base >> plo) != ((base + S - 1) >> plo)) ++plo;\n"
-        "    unsigned pm = (unsigned)encode_morton2(r[0], r[1]); unsigned d = (unsigned)r[3];\n"
-        "    unsigned long long mb = ((unsigned long long)pm << zp.log2spp) | (unsigned)base;\n"
-        "    unsigned long long ms = ((unsigned long long)pm << zp.log2spp) | (unsigned)r[2];\n"
-        "    unsigned up = zsobol_upper(pm, d, zp);\n"
-        "    const int pw = zp.log2spp & 1, iTop = (plo + pw - 1) >> 1;\n"
-        "    ZSobolParams zt = zp; zt.plo = plo;\n"
-        "    zt.pperm4 = (iTop - 1 >= pw && 2 * zp.nBase4Digits - pw - plo <= 36) ? 1 : 0; packed += zt.pperm4;\n"
-        "    if (zsobol_wide(zp)) { full[i] = zsobol_index<unsigned long long>(ms, d, zp);\n"
-        "      unsigned long long e = zsobol_pass_entry<unsigned long long>(mb, d, zp, plo, up);\n"
-        "      if (zt.pperm4) e = zsobol_pass_pack<unsigned long long>(mb, d, zt, plo, e);\n"
-        "      pass[i] = zsobol_index_pass<unsigned long long>(ms, d, zt, e); }\n"
-        "    else { full[i] = zsobol_index<unsigned>((unsigned)ms, d, zp);\n"
-        "      unsigned long long e = zsobol_pass_entry<unsigned>((unsigned)mb, d, zp, plo, up);\n"
-        "      if (zt.pperm4) e = zsobol_pass_pack<unsigned>((unsigned)mb, d, zt, plo, e);\n"
-        "      pass[i] = zsobol_index_pass<unsigned>((unsigned)ms, d, zt, e); } }\n"
-        "  return packed; }\n"
         "int zperm_bytes_check() {\n"
         "  unsigned char t[24]; const unsigned long long W[3] = {kZPermW0, kZPermW1, kZPermW2};\n"
         "  for (int p = 0; p < 24; ++p) t[p] = (unsigned char)(W[p >> 3] >> ((p & 7) * 8));\n"
@@ -200,14 +178,6 @@ def test_zsobol_pass_table(hdr, spp, rx, ry):
     assert np.array_equal(full, pas)
     # the two-level build: the entry for plo from the one for plo + 2 (built once per 4 passes)
     assert hdr.zs_pass_from(spp, rx, ry, n, q.ctypes.data_as(ctypes.POINTER(ctypes.c_int))) == 0
-    # entries with the next digit's 4 candidate permutations packed (zsobol_pass_pack, pperm4):
-    # the same index for every sample, and packing applies wherever two or more digits vary
-    pk = np.zeros(n, np.uint64)
-    packed = hdr.zs_pass_packed(spp, rx, ry, n, q.ctypes.data_as(ctypes.POINTER(ctypes.c_int)), full.ctypes.data_as(U),
-                                pk.ctypes.data_as(U))
-    assert np.array_equal(full, pk)
-    if spp >= 256:
-        assert packed > n // 10
 
 
 def _pc1d_cdf(f, lo, hi):

@@ -319,3 +319,21 @@ def test_oracle_vdb_white_furnace():
     run = binding.OracleRun(scene, max_depth=1000, seed=0)
     Ls = np.array([run.pixel_sample(px, py, s)[0] for px in range(12) for py in range(12) for s in range(4)])
     assert np.all(Ls == 1.0)
+
+
+def test_oracle_tree_unaligned_tile():
+    """The oracle's tree takes tiles as given (oracle_vdb_create): an 8^3 tile whose origin is
+    not 8-aligned covers exactly its own box, not the hash block its origin falls in."""
+    from types import SimpleNamespace
+    g = SimpleNamespace(leaf_origins=np.zeros((0, 3), np.int32), leaf_values=np.zeros((0, 8, 8, 8), np.float32),
+                        tile_origins=np.array([[3, -5, 12], [16, 16, 16]], np.int32), tile_sizes=np.array([8, 8], np.int32),
+                        tile_values=np.array([0.5, 0.75], np.float32), background=np.float32(0.125),
+                        index_bbox=np.array([3, -5, 12, 23, 23, 23], np.int32), index_to_world=np.eye(4)[:3],
+                        world_to_index=np.eye(3))
+    tree = binding.VdbTree(g)
+    for x in range(-2, 28):
+        for y in range(-8, 26, 3):
+            for z in range(8, 26, 2):
+                inside = [3 <= x < 11 and -5 <= y < 3 and 12 <= z < 20, 16 <= x < 24 and 16 <= y < 24 and 16 <= z < 24]
+                want = 0.5 if inside[0] else (0.75 if inside[1] else 0.125)
+                assert tree.value(x, y, z) == np.float32(want), (x, y, z)

@@ -39,9 +39,7 @@ def main():
     p.add_argument("--pixelsamples", type=int, default=16384, help="sampler pixelsamples (bench.py --steps 20: 16384)")
     p.add_argument("--pass-size", type=int, default=64, help="sample indices per pass (bench.py: 64)")
     p.add_argument("--variant", default="prof", help="variants/<name> (e.g. profsplit)")
-    p.add_argument("--define", action="append", default=[],
-                   help="extra -D for --build (-DAVR_SEC_SPLIT_PHASE: section 'phase sampling' = its cooperative draws only, "
-                        "the rest of the phase handler counted under 'escape+end')")
+    p.add_argument("--define", action="append", default=[], help="extra -D for --build")
     a = p.parse_args()
     if a.build:
         return build(a.variant, a.define)
