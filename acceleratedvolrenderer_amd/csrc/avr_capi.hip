@@ -97,7 +97,8 @@ struct avr_context {
     int kernel_mode = 0;      // 0: persistent k_paths (default), 1: wavefront k_medium/k_shadow
     bool last_persistent = false;   // which organisation the last avr_render ran
     bool last_fast = false;         // ... and whether k_paths ran in fast mode
-    int *d_heads = nullptr;   // 8 per-XCD work counters of k_paths
+    int *d_heads = nullptr;   // 8 per-XCD work counters of k_paths + the pass generation
+    int pass_gen = 0;         // k_paths passes enqueued (the camera stage stamps it into d_heads[8])
     // k_paths' pixel order (avr_set_pixel_order): slot -> pixel and pixel -> slot, and the
     // host copy of the latter (to return the last pass in pixel order); empty = scanline
     int *d_pix_order = nullptr, *d_pix_slot = nullptr;
@@ -644,7 +645,7 @@ int avr_context_create(int device, long long max_paths, avr_context **out) {
         delete c;
         return fail(AVR_ERR_HIP, "context allocation failed");
     }
-    if (dalloc(&c->d_heads, 8) != hipSuccess ||
+    if (dalloc(&c->d_heads, 9) != hipSuccess || hipMemset(c->d_heads, 0xff, 9 * sizeof(int)) != hipSuccess ||
         hipMemset(c->d_stats, 0, sizeof(unsigned long long) * (avr::kNumStats + 8)) != hipSuccess) {
         delete c;
         return fail(AVR_ERR_HIP, "context allocation failed");
@@ -1692,6 +1693,10 @@ static int fold_stats(avr_context *c) {
     c->stats.shadow_dda_steps = h[6];
     c->stats.loop_iterations = h[8];
     c->stats.active_lane_iterations = h[9];
+    if (h[7]) {
+        HIP_TRY(hipMemset(c->d_stats + 7, 0, sizeof(unsigned long long)));
+        return fail(AVR_ERR_STATE, "k_paths launched without its pass's camera stage (work heads not reset): pass not rendered");
+    }
     return AVR_OK;
 }
 
@@ -1824,7 +1829,11 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
             }
             p.advance = c->d_advance;
             walk_schedule(c, c->refill_min, c->dda_budget, &p.refill_min, &p.dda_budget);   // defaults: measured optima
-            p.heads = c->d_heads;   // zeroed by the camera stage (k_paths_camera), which runs first
+            // zeroed by the camera stage (k_paths_camera), which must run first on this stream: it
+            // stamps pass_gen into heads[8], and a k_paths launched without it renders nothing and
+            // makes the stats readback fail (stats[7])
+            p.heads = c->d_heads;
+            p.pass_gen = ++c->pass_gen & 0x7fffffff;
             // the camera stage: one lane per sample (k_paths_camera)
             {
                 const int sv = c->sampler_kind == 0 ? 0 : (avr::smp::zsobol_wide(p.zs) ? 2 : 1);

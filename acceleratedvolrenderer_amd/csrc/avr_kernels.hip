@@ -273,7 +273,9 @@ struct Params {
     int *count_out;
     int *shadow_count;
     unsigned long long *stats;
-    int *heads;                       // k_paths: 8 per-XCD work counters (zeroed per pass)
+    int *heads;                       // k_paths: 8 per-XCD work counters (zeroed per pass by the
+                                      //   camera stage) + [8] the pass generation it last zeroed them for
+    int pass_gen;                     // this pass's generation (k_paths runs only after its camera stage)
     const uint64_t *advance;          // k_paths: per pass sample s, {A, H}: Advance(sIdx*65536) ==
                                       //   state' = A*state + inc*H (PCG32 advance is linear in inc)
     int sampler_kind;                 // 0 IndependentSampler, 1 ZSobolSampler (kernels templated on it)
@@ -1174,7 +1176,7 @@ __global__ void __launch_bounds__(256, AVR_CAM_WAVES) k_paths_camera(Params P) {
         if (threadIdx.x < kCamDimHash) s_cdh[threadIdx.x] = smp::hash_2u32(threadIdx.x, (uint32_t)P.zs.seed);
     // the pass's per-XCD work counters of k_paths, zeroed here (stream order: after the previous
     // pass's k_paths, before this pass's) instead of by a separate fill
-    if (blockIdx.x == 0 && threadIdx.x < 8) P.heads[threadIdx.x] = 0;
+    if (blockIdx.x == 0 && threadIdx.x < 9) P.heads[threadIdx.x] = threadIdx.x < 8 ? 0 : P.pass_gen;
     const bool ftab_lds = stage_filter(P, s_filt);   // (its barrier covers s_canon and s_cdh)
     const int npix = P.pass_pixels;
     const long long n = (long long)npix * P.pass_samples;
@@ -1984,6 +1986,13 @@ __global__ void __launch_bounds__(256, kGray ? (kMed == 1 ? 3 : AVR_PATHS_WAVES_
     // HomogeneousMajorantIterator segment over a 1^3 majorant of 1.0; properties from sample_point
     constexpr bool kVdb = kMed == 3, kRgb = kMed == 4, kAnalytic = kMed == 1;
     static_assert(!(kRgb && kGray), "RGB grids carry per-voxel spectra");
+    // the work heads are valid only after this pass's camera stage zeroed them (it stamps the
+    // pass generation): otherwise render nothing and flag stats[7], which the host reports
+    if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(P.heads + 8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) !=
+        P.pass_gen) {
+        if (threadIdx.x == 0) atomicAdd(P.stats + 7, 1ull);
+        return;
+    }
     using S = typename std::conditional<kGray, float, Spec>::type;
     // LDS: majorant grid (16 KiB at pbrt's 16^3) + the 471-entry spectral tables the path
     // samples at path start, NEE and escape (sigma_a, sigma_s, up to 4 light spectra).

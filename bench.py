@@ -13,9 +13,11 @@ child, acceleratedvolrenderer_amd/launch.py); under a launcher WORLD_SIZE must e
 
 Prints ONE JSON line (rank 0) with
   * roofline: k_paths (the fused delta-tracking / ratio-tracking / density-fetch kernel),
-    algorithmic bytes per launch / its HIP-event time on the context stream, against the
-    HBM peak; `traffic` and the `limiter` block come from rocprofv3 PMC passes that this
-    script runs as child processes on the same configuration (N=1, --pmc auto);
+    algorithmic HBM bytes per launch / its HIP-event time on the context stream, against the
+    HBM peak; `traffic` (memory-side reads priced by request size + WRITE_SIZE) and the
+    `limiter` block come from rocprofv3 PMC passes that this script runs as child processes
+    on the same configuration (N=1, --pmc auto); the fast-mode and NanoVDB legs carry the
+    same roofline block (NanoVDB's 64^3 majorant reads, served by L2, reported apart);
   * cpu_baseline: the oracle restatement (`port`) on a bounded sample of the same
     workload, on every host core this process may use (affinity and cgroup quota).
 """
@@ -38,7 +40,8 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 HBM_ACHIEVABLE_GBPS = 6300.0   # MI355X_MICROARCH.md: ~6.3 TB/s achievable streaming
-HBM_REQUEST_BYTES = 64  # gfx950 memory-side read request (FETCH_SIZE = TCC_EA0_RDREQ x 64 B)
+HBM_REQUEST_BYTES = 128  # gfx950 memory-side read request of a 32-B random gather (TCC_EA0_RDREQ_128B:
+                         # profiles/r06_fetch_size_calibration.json)
 VALU_SIMDS = 1024       # 256 CUs x 4 SIMDs; a wave64 VALU op issues in 2 cycles (MI355X_MICROARCH.md)
 # SURVEY.md §8d algorithmic bytes: 32 B per trilinear lookup (8 taps x 4 B) and 132 B per
 # work item read / written (ray 24, tMax 4, lambda+pdf 32, beta/r_u/r_l 48, RNG 16, pixel/depth 8).
@@ -78,25 +81,32 @@ def lookup_bytes(medium, emissive=False, rgb_fields=2):
 # NanoVDB's apron layout reads one 4-B slot index per grid lookup before the 32-B stencil entry:
 # a cost of this implementation's sparse layout, not a §8(d) algorithmic byte
 VDB_SLOT_BYTES = 4
-# §8(d): "4 B per majorant DDA step (counted as 0 HBM if LDS-staged; report it separately)"
+# §8(d): "4 B per majorant DDA step (counted as 0 HBM if LDS-staged; report it separately)": the
+# 16^3 majorants are in LDS; NanoVDB's 64^3 one (1 MiB) is read through L2 — reported apart
+# (`l2_majorant`), never in an HBM fraction
 BYTES_PER_MAJORANT_STEP = 4
+# where `traffic` comes from: the memory-side reads by request size (TCC_EA0_RDREQ_32B/64B/128B)
+# + WRITE_SIZE; FETCH_SIZE tallies 128-B requests at 64 B on gfx950 (MI355X_MICROARCH.md §HBM)
+# and its x2 rule holds only for all-128-B streaming — calibrated on k_density_fetch over known
+# byte counts in profiles/r06_fetch_size_calibration.json (tools/fetch_calibrate.py)
+FETCH_CALIBRATION = "profiles/r06_fetch_size_calibration.json"
 
 
 def kpaths_bytes(agg, sampler, medium="grid", emissive=False, zsobol_table=True, pass_table=False,
                  majorant_in_lds=True):
-    """k_paths' bytes over the stats `agg` (counters summed over its launches), split as SURVEY
-    §8(d) prices them. Algorithmic: 32 B per trilinear lookup (delta + ratio tracking), 4 B per
-    majorant DDA step where the majorant is NOT staged in LDS (NanoVDB's 64^3 grid, read through
-    L2; 0 for the LDS-staged 16^3 grids), and the per-work-item state k_paths moves through HBM —
-    its 16-B sample record and the camera record it reads per path (68 B ZSobol / 80 B
-    independent). Implementation (reported apart, not in `frac`): the ZSobol table entries of the
-    phase draws (they replace register arithmetic pbrt does in samplers.h:225-330) and NanoVDB's
-    4-B apron slot per lookup. Returns (algorithmic total, parts, implementation parts)."""
+    """k_paths' HBM bytes over the stats `agg` (counters summed over its launches), split as SURVEY
+    §8(d) prices them. Algorithmic: 32 B per trilinear lookup (delta + ratio tracking) and the
+    per-work-item state k_paths moves through HBM — its 16-B sample record and the camera record
+    it reads per path (BYTES_CAMERA_RECORD_READ: 64 B ZSobol / 80 B independent). Implementation
+    (reported apart, not in `frac`): the ZSobol table entries of the phase draws (they replace
+    register arithmetic pbrt does in samplers.h:225-330), NanoVDB's 4-B apron slot per lookup and
+    — where the majorant is NOT staged in LDS (NanoVDB's 64^3 grid, 1 MiB, served by the XCD's L2)
+    — §8(d)'s 4 B per majorant DDA step (`l2_majorant_steps`: L2, not HBM, bytes).
+    Returns (algorithmic total, parts, implementation parts)."""
     # delta tracking evaluates emission (Le grid / temperature) at its lookups; shadow rays never
     lk = agg["medium_lookups"] * lookup_bytes(medium, emissive) + agg["shadow_lookups"] * lookup_bytes(medium, False)
     parts = {
         "density_lookups": lk,
-        "majorant_steps": 0 if majorant_in_lds else BYTES_PER_MAJORANT_STEP * agg["medium_dda_steps"],
         "sample_records_written": BYTES_PER_SAMPLE_RECORD * agg["medium_items_in"],
         "camera_records_read": BYTES_CAMERA_RECORD_READ[sampler] * agg["medium_items_in"],
     }
@@ -106,19 +116,22 @@ def kpaths_bytes(agg, sampler, medium="grid", emissive=False, zsobol_table=True,
                                if sampler == "zsobol" and (zsobol_table or pass_table) else 0),
         "vdb_slot_reads": (VDB_SLOT_BYTES * (agg["medium_lookups"] * (2 if emissive else 1) + agg["shadow_lookups"])
                            if medium == "nanovdb" else 0),
+        "l2_majorant_steps": 0 if majorant_in_lds else BYTES_PER_MAJORANT_STEP * agg["medium_dda_steps"],
     }
     return sum(parts.values()), parts, impl
 
 
 def roofline_block(agg, launches, sampler, medium, emissive, zsobol_table, pass_table):
-    """The §8(d) numbers of one k_paths configuration from its stats: per-launch algorithmic bytes
-    over the average HIP-event launch time, and the density-fetch share the north star prices
-    (`density_fetch`: lookup bytes only)."""
+    """The §8(d) numbers of one k_paths configuration from its stats: per-launch algorithmic HBM
+    bytes over the average HIP-event launch time, and the density-fetch share the north star
+    prices (`density_fetch`: lookup bytes only); NanoVDB's L2-served majorant reads apart
+    (`l2_majorant`)."""
     alg, parts, impl = kpaths_bytes(agg, sampler, medium, emissive, zsobol_table, pass_table,
                                     majorant_in_lds=medium != "nanovdb")
     ms = agg["ms_medium"] / launches
     s = ms / 1e3
     lk = parts["density_lookups"] / launches
+    l2m = impl["l2_majorant_steps"] / launches
     return {
         "achieved": round(alg / launches / s / 1e9, 2) if s > 0 else 0.0,
         "peak": HBM_PEAK_GBPS, "unit": "GB/s",
@@ -130,12 +143,17 @@ def roofline_block(agg, launches, sampler, medium, emissive, zsobol_table, pass_
         "density_fetch": {"bytes_per_launch": lk, "GBps": round(lk / s / 1e9, 2) if s > 0 else 0.0,
                           "frac": round(lk / s / 1e9 / HBM_PEAK_GBPS, 5) if s > 0 else 0.0,
                           "basis": "32 B per trilinear lookup (SURVEY §8d) x lookups per launch / avg launch time"},
+        "l2_majorant": ({"bytes_per_launch": l2m, "GBps": round(l2m / s / 1e9, 2) if s > 0 else 0.0,
+                         "basis": "4 B per majorant DDA step (SURVEY §8d, reported separately): the 64^3 majorant "
+                                  "(1 MiB) is served by the XCD's L2, not HBM; not in `frac`"} if l2m else None),
+        "lookups_per_launch": (agg["medium_lookups"] + agg["shadow_lookups"]) / launches,
+        "samples_per_launch": agg["medium_items_in"] / launches,
     }
 
 
 def camera_bytes(samples, sampler, zsobol_table=True, pass_dims=0, pixels=0, launches=1):
-    """The camera stage's algorithmic bytes for `samples` samples: its records (68 / 84 B per
-    sample) + the ZSobol table entries (6 draws per quad of 4 samples of one pixel) + with the
+    """The camera stage's algorithmic bytes for `samples` samples: its records
+    (BYTES_CAMERA_WRITE: 68 / 84 B per sample) + the ZSobol table entries (6 draws per quad of 4 samples of one pixel) + with the
     pass table, its per-pass build (an 8-B entry written and a 4-B pixel-table entry read per
     pixel and dimension, once per launch)."""
     b = BYTES_CAMERA_WRITE[sampler] * samples
@@ -163,7 +181,9 @@ def kernel_targs(name):
 
 
 # rocprofv3 passes (one run each; at most 8 SQ, 4 TCC (FETCH_SIZE 3, WRITE_SIZE 2), 2 GRBM)
-PMC_PASSES = (("fetch", ("FETCH_SIZE",)), ("write", ("WRITE_SIZE",)), ("tcc", ("TCC_HIT_sum", "TCC_MISS_sum")),
+RDREQ_SIZES = ("TCC_EA0_RDREQ_sum", "TCC_EA0_RDREQ_32B_sum", "TCC_EA0_RDREQ_64B_sum", "TCC_EA0_RDREQ_128B_sum")
+PMC_PASSES = (("size", RDREQ_SIZES), ("fetch", ("FETCH_SIZE",)), ("write", ("WRITE_SIZE",)),
+              ("tcc", ("TCC_HIT_sum", "TCC_MISS_sum")),
               ("sq", ("SQ_INSTS_VALU", "SQ_WAVE_CYCLES", "SQ_ACTIVE_INST_ANY", "SQ_WAIT_INST_ANY", "SQ_WAIT_ANY",
                       "SQ_WAVES", "GRBM_GUI_ACTIVE")))
 
@@ -178,7 +198,7 @@ def parse(argv=None):
     p.add_argument("--height", type=int, default=720)
     p.add_argument("--spp-per-step", type=int, default=64,
                    help="sample indices per pass (one step); 64 x 720p = 59M samples: k_paths' 16-B records and the "
-                        "camera stage's 100 B per sample, 6.8 GB)")
+                        "camera stage's 68 B per sample (ZSobol), 4.9 GB")
     p.add_argument("--max-paths", type=int, default=0)
     p.add_argument("--pixelsamples", type=int, default=0,
                    help="sampler pixelsamples (0: the smallest power of two >= 256 holding every timed sample index "
@@ -222,6 +242,9 @@ def parse(argv=None):
                         "writes the synthetic cloud's tree to a temporary .nvdb and reads it back")
     p.add_argument("--fast-leg", type=int, default=1,
                    help="after the replay measurement, time the same steps in fast mode (reported as fast_mode)")
+    p.add_argument("--fast-majorant-res", type=int, default=0,
+                   help="the fast leg's majorant resolution (0: tuned on the device among 1..16, outside the timed "
+                        "region); a fixed value skips the probe renders (e.g. for a kernel-stats run)")
     p.add_argument("--scene", default="cloud", choices=["cloud", "uniform", "explosion", "rgb-explosion"],
                    help="cloud: the metric workload (S-cloud); uniform: BASELINE C2's uniform cube (orthographic, "
                         "use --res 256 --width 512 --height 512); explosion: C5's emissive NanoVDB stand-in with a "
@@ -357,7 +380,17 @@ def pmc_child_argv(args, pixelsamples):
 CAMERA_RE = r"\bk_paths_camera<|k_paths_cameraI"
 
 
-def pmc_passes(args, pixelsamples, kernel_re=r"\bk_paths<|\dk_pathsI", timeout_s=240, side=None):
+def traffic_bytes(ctr):
+    """HBM bytes of one launch from its counters: the memory-side reads by request size (32 R32 +
+    64 R64 + 128 R128) + WRITE_SIZE; None without the size pass. FETCH_SIZE would tally the 128-B
+    requests at 64 B (FETCH_CALIBRATION)."""
+    if not all(k in ctr for k in RDREQ_SIZES[1:]) or "WRITE_SIZE" not in ctr:
+        return None
+    rd = 32 * ctr["TCC_EA0_RDREQ_32B_sum"] + 64 * ctr["TCC_EA0_RDREQ_64B_sum"] + 128 * ctr["TCC_EA0_RDREQ_128B_sum"]
+    return rd + ctr["WRITE_SIZE"] * 1024
+
+
+def pmc_passes(args, pixelsamples, kernel_re=r"\bk_paths<|\dk_pathsI", timeout_s=240, side=None, passes=PMC_PASSES):
     """rocprofv3 counter passes of this same bench configuration, one child process per
     pass (--pmc only: no tracing in the same run), each killed after timeout_s. The child
     renders with the parent's RESOLVED pixelsamples (so the same k_paths instantiation and
@@ -374,7 +407,7 @@ def pmc_passes(args, pixelsamples, kernel_re=r"\bk_paths<|\dk_pathsI", timeout_s
     names = set()
     tmp = tempfile.mkdtemp(prefix="avr_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
     try:
-        for name, counters in PMC_PASSES:
+        for name, counters in passes:
             d = os.path.join(tmp, name)
             cmd = [exe, "--pmc", *counters, "-d", d, "-o", "run", "--output-format", "csv", "--"] + child
             log(f"pmc pass {name}: {' '.join(counters)}")
@@ -699,7 +732,11 @@ def main():
     if args.mode == "replay" and args.fast_leg and args.kernel == "persistent":
         integ.ctx.set_render_mode("fast")
         cands = (1, 2, 4, 8, 16) + ((32, 64) if vdb is not None else ())
-        fres, fms = integ.tune_majorant(candidates=cands, probe=(0, 4))
+        if args.fast_majorant_res > 0:
+            fres, fms = (args.fast_majorant_res,) * 3, {}
+            integ.ctx.set_majorant_res(fres)
+        else:
+            fres, fms = integ.tune_majorant(candidates=cands, probe=(0, 4))
         if world > 1:   # every rank renders with rank 0's choice
             t = torch.tensor(list(fres), dtype=torch.int64, device=f"cuda:{dev}")
             dist.broadcast(t, src=0)
@@ -709,6 +746,7 @@ def main():
         for k in range(args.warmup):
             step(k)
         integ.ctx.film_clear()
+        integ.ctx.reset_stats()   # waits for the warmup; the fast leg's own counters and kernel times
         integ.ctx.sync()
         torch.cuda.synchronize()
         if world > 1:
@@ -730,8 +768,14 @@ def main():
             t = torch.tensor([ef], dtype=torch.float64, device=f"cuda:{dev}")
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             ef = float(t.item())
+        fagg = integ.ctx.stats()
+        fast_kernel = integ.ctx.last_kernel()
+        flaunches = max(1, fagg["medium_launches"])
         fast_line = {"value": round(samples / ef / 1e6, 4), "unit": "Msamples/s", "ms_per_step": round(1e3 * ef / args.steps, 3),
                      "majorant_res": list(fres), "majorant_probe_ms": {str(k): round(v, 4) for k, v in fms.items()},
+                     "instantiation": fast_kernel,
+                     "roofline": roofline_block(fagg, flaunches, args.sampler, "nanovdb" if vdb is not None else "grid", False,
+                                                args.zsobol_table > 0, args.zsobol_pass_table > 0),
                      "parity": "statistical (hardware log/exp/sin/cos, tuned majorant): tests/test_gpu_fast.py"}
         log(f"fast mode: {fast_line['value']} Msamples/s (majorant {fres})")
     # roofline of the dominant kernel: algorithmic bytes / summed device time of its launches
@@ -820,7 +864,7 @@ def main():
         # HBM traffic and the VALU limiter from rocprofv3 counter passes of this same
         # configuration (child processes; the guide's gfx950 rule: FETCH_SIZE x2 + WRITE_SIZE)
         traffic, limiter, pmc_note, cache = None, None, "pmc off", None
-        traffic_raw = None
+        traffic_raw = traffic_x2 = None
         want_pmc = args.pmc == "on" or (args.pmc == "auto" and world == 1)
         pmc_kernel = None
         if want_pmc:
@@ -840,13 +884,19 @@ def main():
             else:
                 pmc_note = (f"rocprofv3 --pmc child passes of this configuration (bench.py pmc_passes, pixelsamples "
                             f"{spp_total}, same instantiation)")
+                tb = traffic_bytes(ctr)
+                if tb is not None:
+                    traffic = round(tb / 1e9, 4)
                 if "FETCH_SIZE" in ctr and "WRITE_SIZE" in ctr:
-                    traffic = round((2 * ctr["FETCH_SIZE"] + ctr["WRITE_SIZE"]) * 1024 / 1e9, 4)
                     traffic_raw = round((ctr["FETCH_SIZE"] + ctr["WRITE_SIZE"]) * 1024 / 1e9, 4)
+                    traffic_x2 = round((2 * ctr["FETCH_SIZE"] + ctr["WRITE_SIZE"]) * 1024 / 1e9, 4)
                 lookups_pl = (agg["medium_lookups"] + (agg["shadow_lookups"] if persistent else 0)) / launches
+                rd = (tb - ctr["WRITE_SIZE"] * 1024) if tb is not None else None
                 cache = {
-                    "fetch_bytes_per_lookup": (round(2 * ctr["FETCH_SIZE"] * 1024 / lookups_pl, 2)
-                                               if "FETCH_SIZE" in ctr and lookups_pl else None),
+                    "read_bytes_per_lookup": round(rd / lookups_pl, 2) if rd is not None and lookups_pl else None,
+                    "read_requests_by_size": ({"32B": ctr["TCC_EA0_RDREQ_32B_sum"], "64B": ctr["TCC_EA0_RDREQ_64B_sum"],
+                                               "128B": ctr["TCC_EA0_RDREQ_128B_sum"], "all": ctr.get("TCC_EA0_RDREQ_sum")}
+                                              if tb is not None else None),
                     "tcc_hit_rate": (round(ctr["TCC_HIT_sum"] / (ctr["TCC_HIT_sum"] + ctr["TCC_MISS_sum"]), 4)
                                      if ctr.get("TCC_HIT_sum") is not None and ctr.get("TCC_MISS_sum") else None),
                 }
@@ -881,9 +931,29 @@ def main():
                         "wave_cycle_split": {"issuing": round(cam_ctr["SQ_ACTIVE_INST_ANY"] / cwc, 4),
                                              "dependency/issue stall": round(cam_ctr["SQ_WAIT_INST_ANY"] / cwc, 4),
                                              "s_waitcnt (memory/LDS)": round(cam_ctr["SQ_WAIT_ANY"] / cwc, 4)},
-                        "hbm_traffic_GB": (round((2 * cam_ctr["FETCH_SIZE"] + cam_ctr["WRITE_SIZE"]) * 1024 / 1e9, 4)
-                                           if "FETCH_SIZE" in cam_ctr and "WRITE_SIZE" in cam_ctr else None),
+                        "hbm_traffic_GB": (round(traffic_bytes(cam_ctr) / 1e9, 4) if traffic_bytes(cam_ctr) is not None
+                                           else None),
                     }
+        if want_pmc and fast_line is not None and persistent:
+            # the fast leg's HBM traffic: the same counter passes (request sizes, WRITE_SIZE, FETCH_SIZE)
+            # of the fast configuration at its majorant resolution
+            import copy
+            fargs = copy.copy(args)
+            fargs.mode, fargs.majorant_res, fargs.fast_leg = "fast", fast_line["majorant_res"][0], 0
+            fctr, ferr, fnames = pmc_passes(fargs, spp_total, passes=tuple(x for x in PMC_PASSES
+                                                                           if x[0] in ("size", "write", "fetch")))
+            if fctr is not None and {kernel_targs(nm) for nm in fnames} != {kernel_targs(fast_line["instantiation"])}:
+                fctr, ferr = None, f"pmc child profiled {sorted(fnames)}, the fast leg launched {fast_line['instantiation']}"
+            frb = fast_line["roofline"]
+            ftb = traffic_bytes(fctr) if fctr is not None else None
+            frb["traffic"] = round(ftb / 1e9, 4) if ftb is not None else None
+            frb["traffic_over_algorithmic"] = round(ftb / frb["bytes_per_launch"], 3) if ftb and frb["bytes_per_launch"] else None
+            frb["traffic_fetch_x2_rule"] = (round((2 * fctr["FETCH_SIZE"] + fctr["WRITE_SIZE"]) * 1024 / 1e9, 4)
+                                            if fctr is not None and "FETCH_SIZE" in fctr and "WRITE_SIZE" in fctr else None)
+            frb["traffic_source"] = (f"rocprofv3 --pmc child passes of the fast configuration (majorant "
+                                     f"{fast_line['majorant_res'][0]}^3), {FETCH_CALIBRATION}" if ftb is not None else ferr)
+            if ferr:
+                log(f"fast-mode pmc: {ferr}")
         out = {
             "metric": "Msamples/s (whole node) on synthetic S-cloud-1024 720p (disney-cloud stand-in)",
             "value": round(value, 4),
@@ -921,13 +991,17 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBPS, 5),
                 "traffic": traffic,
                 "traffic_source": pmc_note,
-                # counter bytes over §8(d) bytes: > 1 is over-fetch (whole lines per 32-B gather,
-                # ZSobol tables, NanoVDB slots). FETCH_SIZE is doubled per MI355X_MICROARCH.md's
-                # gfx950 rule, calibrated there on 16-B/lane streaming reads; for 32-B random
-                # gathers the factor is uncalibrated, so traffic_fetch_raw keeps the undoubled reads
+                # counter bytes over §8(d) bytes: > 1 is over-fetch (a whole 64- or 128-B request per
+                # 32-B gather, ZSobol tables, NanoVDB slots). `traffic` prices the memory-side reads
+                # by request size (traffic_bytes); FETCH_SIZE undoubled / doubled (the guide's x2
+                # rule for streaming reads) are kept for comparison: FETCH_CALIBRATION measures
+                # which holds for this kernel's 32-B gathers
                 "traffic_over_algorithmic": (round(traffic * 1e9 / (med_bytes / launches), 3)
                                              if traffic and med_bytes else None),
+                "traffic_basis": (f"TCC_EA0_RDREQ 32B/64B/128B request sizes x bytes + WRITE_SIZE, per launch "
+                                  f"(calibration: {FETCH_CALIBRATION})" if traffic is not None else None),
                 "traffic_fetch_raw": traffic_raw,
+                "traffic_fetch_x2_rule": traffic_x2,
                 "bytes_per_launch": med_bytes / launches,
                 "bytes_parts_per_launch": ({k: v / launches for k, v in bytes_parts.items()} if bytes_parts else None),
                 "implementation_bytes_per_launch": ({k: v / launches for k, v in impl_parts.items()}
@@ -937,8 +1011,8 @@ def main():
                 "avg_launch_ms": avg_launch_ms,
                 "launches": launches,
                 # the ceiling of this access pattern: a random 32-B fat-entry gather moves one whole
-                # memory-side request (64 B) per lookup, so at the achievable 6.3 TB/s at most half of
-                # the bytes are the lookup's own
+                # 128-B memory-side request per lookup (FETCH_CALIBRATION), so at the achievable
+                # 6.3 TB/s at most a quarter of the bytes are the lookup's own
                 "attainable": {"random_gather_GBps": HBM_ACHIEVABLE_GBPS * BYTES_PER_LOOKUP / HBM_REQUEST_BYTES,
                                "basis": f"{HBM_ACHIEVABLE_GBPS:.0f} GB/s achievable x {BYTES_PER_LOOKUP} B used per "
                                         f"{HBM_REQUEST_BYTES}-B request",

@@ -20,7 +20,7 @@ def test_kpaths_bytes_follow_the_per_unit_figures():
     assert parts["density_lookups"] == 32 * (1813622114 + 652134642)
     assert parts["sample_records_written"] == 16 * 1179648000
     assert parts["camera_records_read"] == 64 * 1179648000   # round 4: 68 (the light pick apart)
-    assert parts["majorant_steps"] == 0          # the 16^3 majorant is staged in LDS
+    assert impl["l2_majorant_steps"] == 0        # the 16^3 majorant is staged in LDS
     assert (tot + 4 * 1179648000) / 20 / 1e9 == pytest.approx(8.90, abs=0.01)
     # phase events read 5 ZSobol table entries of 4 B each: implementation bytes, not in the total
     agg["medium_items_out"] = 1000
@@ -28,10 +28,39 @@ def test_kpaths_bytes_follow_the_per_unit_figures():
     assert impl["zsobol_table_reads"] == 20 * 1000 and t2 == tot
     assert bench.kpaths_bytes(agg, "zsobol", zsobol_table=False)[2]["zsobol_table_reads"] == 0
     assert bench.kpaths_bytes(agg, "independent")[1]["camera_records_read"] == 80 * 1179648000
-    # NanoVDB: 4 B per majorant step read through L2, the 4-B apron slot apart
-    _, pv, iv = bench.kpaths_bytes(agg, "zsobol", "nanovdb", majorant_in_lds=False)
-    assert pv["majorant_steps"] == 4 * 19127199408
+    # NanoVDB: 4 B per majorant step read through L2 (reported separately, not HBM
+    # bytes, so not in the total) and the 4-B apron slot apart
+    tv, pv, iv = bench.kpaths_bytes(agg, "zsobol", "nanovdb", majorant_in_lds=False)
+    assert iv["l2_majorant_steps"] == 4 * 19127199408 and "majorant_steps" not in pv
+    assert tv == tot
     assert iv["vdb_slot_reads"] == 4 * (1813622114 + 652134642)
+
+
+def test_nanovdb_frac_excludes_the_l2_majorant():
+    """BENCH_r05's NanoVDB leg priced on lookups + records only = 7.66 GB per
+    launch over 35.9 ms = 0.027 of 8 TB/s; its 16.4 GB of majorant reads per launch (L2) apart."""
+    # per launch (4 launches): lookups 2938699472 B / 32, records 943718400 / 16, camera 3774873600 / 64
+    L = 4
+    agg = {"medium_lookups": L * 2938699472 // 32, "shadow_lookups": 0, "medium_items_in": L * 58982400,
+           "medium_items_out": 0, "medium_dda_steps": L * 16403993540 // 4, "ms_medium": L * 35.89823055267334}
+    rb = bench.roofline_block(agg, L, "zsobol", "nanovdb", False, True, True)
+    assert rb["bytes_per_launch"] / 1e9 == pytest.approx(7.657, abs=0.001)
+    assert rb["frac"] == pytest.approx(0.027, abs=0.0005)
+    assert rb["l2_majorant"]["bytes_per_launch"] == pytest.approx(16403993540)
+    assert bench.roofline_block(agg, L, "zsobol", "grid", False, True, True)["l2_majorant"] is None
+
+
+def test_traffic_prices_reads_by_request_size():
+    ctr = {"TCC_EA0_RDREQ_sum": 60, "TCC_EA0_RDREQ_32B_sum": 10, "TCC_EA0_RDREQ_64B_sum": 20,
+           "TCC_EA0_RDREQ_128B_sum": 30, "WRITE_SIZE": 2.0, "FETCH_SIZE": 5.0}
+    assert bench.traffic_bytes(ctr) == 32 * 10 + 64 * 20 + 128 * 30 + 2048
+    assert bench.traffic_bytes({"FETCH_SIZE": 5.0, "WRITE_SIZE": 1.0}) is None
+    names = [c for _, cs in bench.PMC_PASSES for c in cs]
+    assert all(c in names for c in bench.RDREQ_SIZES)
+    for _, cs in bench.PMC_PASSES:   # TCC block: at most 4 counters a pass (FETCH_SIZE costs 3)
+        tcc = sum(3 if c == "FETCH_SIZE" else (2 if c == "WRITE_SIZE" else 1) for c in cs
+                  if c.startswith("TCC") or c in ("FETCH_SIZE", "WRITE_SIZE"))
+        assert tcc <= 4
 
 
 def test_roofline_block_reproduces_the_r04_recomputation(monkeypatch):
