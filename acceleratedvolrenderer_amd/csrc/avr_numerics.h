@@ -69,6 +69,17 @@ AVR_HD float fast_exp(float x) {
     bits |= (uint32_t)(exponent + 127) << 23;
     return u2f(bits);
 }
+// fast_exp(x) for x in (-40, 0]: x log2(e) > -57.8, so the exponent stays inside [-58, 0] and
+// neither range check can fire — the same bits without them (the walk's reject factor, whose
+// caller only uses it when A = -x < 40)
+AVR_HD float fast_exp_m40(float x) {
+    float xp = x * 1.442695041f;
+    float fxp = __builtin_floorf(xp), f = xp - fxp;
+    int i = (int)fxp;
+    float twoToF = __builtin_fmaf(f, __builtin_fmaf(f, __builtin_fmaf(f, 0.0781455737f, 0.226173572f), 0.695556856f), 1.f);
+    uint32_t bits = f2u(twoToF);
+    return u2f(bits + ((uint32_t)i << 23));
+}
 
 // ---------------------------------------------------------------------------
 // MurmurHash64A specialised to the byte lengths the path hashes (4, 12 bytes)
@@ -171,17 +182,10 @@ AVR_HD Spec fast_exp(Spec a) { return {fast_exp(a.v0), fast_exp(a.v1), fast_exp(
 // variants, MSVC, CUDA); the oracle's "canonical" mode restates the same sequences, so a
 // device sample replays the oracle's bit for bit. Used once per path (wavelengths), per
 // scatter (phase direction) and per accepted free-flight candidate (log).
-#ifndef AVR_FLOAT_LIBM
 AVR_HD float cr_log(float x) { return canon::log_f(x); }
 AVR_HD float cr_atanh(float x) { return canon::atanh_f(x); }
 AVR_HD float cr_cosh(float x) { return canon::cosh_f(x); }
 AVR_HD void cr_sincos(float x, float *s, float *c) { canon::sincos_f(x, s, c); }
-#else   // measurement-only build (cost of the canonical convention); breaks replay parity
-AVR_HD float cr_log(float x) { return logf(x); }
-AVR_HD float cr_atanh(float x) { return atanhf(x); }
-AVR_HD float cr_cosh(float x) { return coshf(x); }
-AVR_HD void cr_sincos(float x, float *s, float *c) { *s = sinf(x); *c = cosf(x); }
-#endif
 
 // "fast" render mode (avr_set_render_mode 1; SURVEY §7: replay / fast): the hardware
 // transcendentals (v_log_f32, v_exp_f32, v_sin/cos_f32 — about 1 ulp) replace the canonical
