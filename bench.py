@@ -456,6 +456,42 @@ def pmc_passes(args, pixelsamples, kernel_re=r"\bk_paths<|\dk_pathsI", timeout_s
         shutil.rmtree(tmp, ignore_errors=True)
 
 
+def broadcast_choice(vals, world, device):
+    """Rank 0's choice on every rank (the tuned walk schedule and majorant resolutions), so that
+    every rank renders the same k_paths schedule and majorant segments; `vals` a tuple of ints."""
+    if world <= 1:
+        return tuple(int(v) for v in vals)
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([int(v) for v in vals], dtype=torch.int64, device=device)
+    dist.broadcast(t, src=0)
+    return tuple(int(v) for v in t.tolist())
+
+
+def reduce_step_film(buf, world):
+    """The multi-GPU path's one exchange, inside the timed region: SUM-reduce of the packed fp64
+    film (avr_film_export_device layout) to rank 0 (RCCL over xGMI; gloo in the CPU tests)."""
+    if world > 1:
+        import torch.distributed as dist
+        dist.reduce(buf, dst=0, op=dist.ReduceOp.SUM)
+
+
+def max_over_ranks(seconds, world, device):
+    """The slowest rank's time (the driver's clock covers the whole world)."""
+    if world <= 1:
+        return seconds
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([seconds], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def step_base(warm_bases, timed_bases, rank, warmup, k):
+    """This rank's first sample index of step k (the warmup steps first, then the timed ones)."""
+    return warm_bases[rank][k] if k < warmup else timed_bases[rank][k - warmup]
+
+
 def timed_steps(integ, bases, S, maxdepth, world, buf):
     """Render the sample ranges [b, b + S) for b in bases back to back on the context stream,
     then export the film (and SUM-reduce it over the world), bracketed by barrier + sync;
@@ -471,19 +507,13 @@ def timed_steps(integ, bases, S, maxdepth, world, buf):
     for b in bases:
         integ.ctx.render(b, b + S, 0, maxdepth)
     integ.ctx.film_export_device(buf.data_ptr())
-    if world > 1:
-        dist.reduce(buf, dst=0, op=dist.ReduceOp.SUM)
+    reduce_step_film(buf, world)
     integ.ctx.sync()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    el = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device=buf.device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
-    return el
+    return max_over_ranks(time.perf_counter() - t0, world, buf.device)
 
 
 def nanovdb_leg(args, density, dev, world, rank, S, warm_bases, timed_bases, spp_total, buf):
@@ -653,10 +683,7 @@ def main():
         rc = (0, 12, 16, 24, 32, 40)
         dc = (0, 16, 24, 28, 32, 40) if fine else (0, 8, 10, 12, 16, 24)
         (r_best, d_best), wms = integ.ctx.tune_walk(rc, dc, 0, 8, 0, maxdepth)
-        if world > 1:   # every rank renders with rank 0's choice
-            t = torch.tensor([r_best, d_best], dtype=torch.int64, device=f"cuda:{dev}")
-            dist.broadcast(t, src=0)
-            r_best, d_best = (int(v) for v in t.tolist())
+        r_best, d_best = broadcast_choice((r_best, d_best), world, f"cuda:{dev}")   # rank 0's, on every rank
         integ.ctx.set_refill_min(r_best)
         integ.ctx.set_dda_budget(d_best)
         walk_tuned = {"refill_min": r_best, "dda_budget": d_best, "refill_candidates": list(rc), "dda_candidates": list(dc),
@@ -671,16 +698,14 @@ def main():
         cands = (1, 2, 4, 8, 16) + ((32, 64) if vdb is not None else ())
         maj_res, tune_ms = integ.tune_majorant(candidates=cands, probe=(0, 4))
         if world > 1:   # every rank renders with rank 0's choice
-            t = torch.tensor(list(maj_res), dtype=torch.int64, device=f"cuda:{dev}")
-            dist.broadcast(t, src=0)
-            maj_res = tuple(int(v) for v in t.tolist())
+            maj_res = broadcast_choice(maj_res, world, f"cuda:{dev}")
             integ.ctx.set_majorant_res(maj_res)
         log(f"tuned majorant {maj_res} (probe ms {tune_ms})")
         args.majorant_res = maj_res[0]   # the counter passes (child processes) render the same majorant
 
     def step(k):
         # asynchronous on the context stream: steps queue back to back
-        base = warm_bases[rank][k] if k < args.warmup else timed_bases[rank][k - args.warmup]
+        base = step_base(warm_bases, timed_bases, rank, args.warmup, k)
         integ.ctx.render(base, base + S, 0, maxdepth)
 
     log(f"scene uploaded; pixelsamples {spp_total}; warmup")
@@ -703,8 +728,7 @@ def main():
     buf = torch.empty(film_buffer_size(npix, getattr(scene.film, "nbuckets", 0)), dtype=torch.float64,
                       device=f"cuda:{dev}")
     integ.ctx.film_export_device(buf.data_ptr())
-    if world > 1:
-        dist.reduce(buf, dst=0, op=dist.ReduceOp.SUM)
+    reduce_step_film(buf, world)
     integ.ctx.sync()
     torch.cuda.synchronize()
     if world > 1:
@@ -714,10 +738,7 @@ def main():
     agg = integ.ctx.stats()   # device counters + per-launch HIP-event times of the timed steps
     # the k_paths instantiation the timed steps ran (before the fast-mode leg launches another)
     timed_kernel = integ.ctx.last_kernel() if agg.get("loop_iterations") else "k_medium"
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{dev}")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = max_over_ranks(elapsed, world, f"cuda:{dev}")
     if args.pmc_child:
         integ.close()
         return
@@ -738,9 +759,7 @@ def main():
         else:
             fres, fms = integ.tune_majorant(candidates=cands, probe=(0, 4))
         if world > 1:   # every rank renders with rank 0's choice
-            t = torch.tensor(list(fres), dtype=torch.int64, device=f"cuda:{dev}")
-            dist.broadcast(t, src=0)
-            fres = tuple(int(v) for v in t.tolist())
+            fres = broadcast_choice(fres, world, f"cuda:{dev}")
             integ.ctx.set_majorant_res(fres)
         integ.ctx.film_clear()
         for k in range(args.warmup):
@@ -756,18 +775,13 @@ def main():
         for k in range(args.warmup, args.warmup + args.steps):
             step(k)
         integ.ctx.film_export_device(buf.data_ptr())
-        if world > 1:
-            dist.reduce(buf, dst=0, op=dist.ReduceOp.SUM)
+        reduce_step_film(buf, world)
         integ.ctx.sync()
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
-        ef = time.perf_counter() - tf
-        if world > 1:
-            t = torch.tensor([ef], dtype=torch.float64, device=f"cuda:{dev}")
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            ef = float(t.item())
+        ef = max_over_ranks(time.perf_counter() - tf, world, f"cuda:{dev}")
         fagg = integ.ctx.stats()
         fast_kernel = integ.ctx.last_kernel()
         flaunches = max(1, fagg["medium_launches"])
