@@ -1864,6 +1864,23 @@ __global__ void __launch_bounds__(256) k_bin_scatter(const int *__restrict__ que
 // 4-18 % slower and removed: DESIGN §6, profiles/r05_ab_pooled_handlers.json.)
 enum : int { EV_NONE = 0, EV_SCATTER = 1, EV_SHADOW_DONE = 2, EV_PHASE = 3, EV_ESCAPE = 4, EV_END = 5 };
 
+// k_paths' kernel arguments re-read where they are used: each event handler and the collision
+// block take the Params through the kernarg segment pointer passed through an empty asm, so
+// the compiler reloads the fields they use with scalar loads right there instead of keeping
+// them live in SGPRs across the kernel's loops. At k_paths' SGPR limit those long-lived values
+// were spilled to VGPR lanes (180 SGPR spills, 1095 v_readlane VALU instructions in the
+// headline instantiation, 771 of them in the tracking loop); reloaded, the kernel has 2
+// v_readlane, 8572 instead of 9829 instructions and 107 instead of 126 VGPRs (+3.7 % grid,
+// +1.6 % NanoVDB, profiles/r06_ab_walk.json). The segment pointer, not the by-value
+// argument's address: taking that would make the compiler copy the argument to scratch.
+// Only for kernels whose (first and only) argument is a Params by value, as k_paths'.
+__device__ __forceinline__ const Params &fresh_params() {
+    typedef const __attribute__((address_space(4))) Params *KP;
+    KP p = (KP)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(p));
+    return *(const Params *)p;
+}
+
 // Spectral-state type of k_paths: Spec (4 wavelengths) in general; float for a GRAY medium
 // (sigma_a and sigma_s tables constant over 360..830 nm, decided on the host). In a gray
 // medium beta, r_u, r_l, T_maj and the shadow ratios have four equal components at every
@@ -1994,7 +2011,8 @@ struct ProbeStats {
 // escapes); a separate instantiation so the other kernels keep their register budget.
 // kFast: the "fast" render mode (hardware transcendentals, statistical parity); replay otherwise.
 template <bool kEmissive, bool kGray, int kSmp, int kMed, bool kImage, bool kFast>
-__global__ void __launch_bounds__(256, kGray ? (kMed == 1 ? 3 : AVR_PATHS_WAVES_GRAY) : AVR_PATHS_WAVES_SPEC) k_paths(Params P) {
+__global__ void __launch_bounds__(256, kGray ? (kMed == 1 ? 3 : AVR_PATHS_WAVES_GRAY) : AVR_PATHS_WAVES_SPEC) k_paths(Params Pk) {
+    const Params &P = Pk;
     // kMed 1: HomogeneousMedium or CloudMedium — dda_init gives their single
     // HomogeneousMajorantIterator segment over a 1^3 majorant of 1.0; properties from sample_point
     constexpr bool kVdb = kMed == 3, kRgb = kMed == 4, kAnalytic = kMed == 1;
@@ -2119,12 +2137,12 @@ __global__ void __launch_bounds__(256, kGray ? (kMed == 1 ? 3 : AVR_PATHS_WAVES_
     int light = 0;
     S T_ray{}, sr_l{}, sr_u{};
 
-    auto seg_start = [&](V3 o, V3 d, float tMax) {
+    auto seg_start = [&](const DevMedium &md, V3 o, V3 d, float tMax) {
         // SampleT_maj prologue (media.h:744-749): normalise, medium-space ray, clip, DDA
         tMax *= length(d);
         d = normalize(d);
         sd = d;
-        ddal_init(it, m, Ray{o, d}, tMax, majp);
+        ddal_init(it, md, Ray{o, d}, tMax, majp);
         T_maj = sconst<S>(1.f);
         needNext = true;
     };
@@ -2140,6 +2158,8 @@ __global__ void __launch_bounds__(256, kGray ? (kMed == 1 ? 3 : AVR_PATHS_WAVES_
         AVR_SEC(0)
         // =================== batched event handlers (each runs once per batch) ===========
         if (__ballot(ev == EV_SCATTER)) {
+            [[maybe_unused]] const Params &P = fresh_params();
+            [[maybe_unused]] const DevMedium &m = P.med;
             if (ev == EV_SCATTER) {
                 // SampleLd: light pick (BVH infinite-light branch) + shadow-ray spawn (1282-1338)
                 const V3 wo = -pd;
@@ -2217,6 +2237,8 @@ __global__ void __launch_bounds__(256, kGray ? (kMed == 1 ? 3 : AVR_PATHS_WAVES_
         }
         AVR_SEC(5)
         if (__ballot(ev == EV_SHADOW_DONE)) {
+            [[maybe_unused]] const Params &P = fresh_params();
+            [[maybe_unused]] const DevMedium &m = P.med;
             if (ev == EV_SHADOW_DONE) {
                 // finish SampleLd (1379-1398); SampleT_maj returned 1 if the callback stopped
                 const S Tm = shadowStopped ? sconst<S>(1.f) : T_maj;
@@ -2256,6 +2278,8 @@ __global__ void __launch_bounds__(256, kGray ? (kMed == 1 ? 3 : AVR_PATHS_WAVES_
         }
         AVR_SEC(6)
         if (__ballot(ev == EV_PHASE)) {
+            [[maybe_unused]] const Params &P = fresh_params();
+            [[maybe_unused]] const DevMedium &m = P.med;
             // ZSobol: the phase 2D draw and the next segment's three 1D draws of every lane in
             // EV_PHASE, evaluated cooperatively by the whole wave
             // (and, at offset 5, the next bounce's light-pick draw, parked in s_ul)
@@ -2304,6 +2328,8 @@ __global__ void __launch_bounds__(256, kGray ? (kMed == 1 ? 3 : AVR_PATHS_WAVES_
         }
         AVR_SEC(7)
         if (__ballot(ev == EV_ESCAPE)) {
+            [[maybe_unused]] const Params &P = fresh_params();
+            [[maybe_unused]] const DevMedium &m = P.med;
             if (ev == EV_ESCAPE) {
                 // escaped (integrators.cpp:1078-1107)
                 if constexpr (kGray) {
@@ -2340,6 +2366,8 @@ __global__ void __launch_bounds__(256, kGray ? (kMed == 1 ? 3 : AVR_PATHS_WAVES_
             }
         }
         if (__ballot(ev == EV_END)) {
+            [[maybe_unused]] const Params &P = fresh_params();
+            [[maybe_unused]] const DevMedium &m = P.med;
             if (ev == EV_END) {
                 // the per-sample record: L (k_film takes the rest from the camera stage)
                 P.ps.rec[g] = to4(L);
@@ -2353,6 +2381,8 @@ __global__ void __launch_bounds__(256, kGray ? (kMed == 1 ? 3 : AVR_PATHS_WAVES_
         const uint64_t needMask = __ballot(mode == M_FETCH);
         const uint64_t busyMask = __ballot(mode == M_MEDIUM || mode == M_SHADOW);
         if (needMask && (busyMask == 0 || __popcll(needMask) >= P.refill_min)) {
+            [[maybe_unused]] const Params &P = fresh_params();
+            [[maybe_unused]] const DevMedium &m = P.med;
             const int cnt = __popcll(needMask);
             const int leader = __ffsll((long long)needMask) - 1;
             long long base = 0;
@@ -2434,12 +2464,14 @@ __global__ void __launch_bounds__(256, kGray ? (kMed == 1 ? 3 : AVR_PATHS_WAVES_
         // continuation and the camera ray: RNG(seqA, seqB), then SampleT_maj's prologue
         // (medium-space ray, clip, DDA setup) once per batch for every lane that needs one
         if (__ballot(segPending)) {
+            [[maybe_unused]] const Params &P = fresh_params();
+            [[maybe_unused]] const DevMedium &m = P.med;
             if (segPending) {
                 rng.set_sequence(seqA, seqB);
                 if (mode == M_SHADOW) u = rng.uniform();
                 float tMax = mode == M_SHADOW ? 1 - kShadowEpsilon : kInf;
                 if (m.boundary) tMax = fminf_(tMax, interface_exit(m, po, sd));
-                seg_start(po, sd, tMax);
+                seg_start(m, po, sd, tMax);
                 segPending = false;
             }
         }
@@ -2572,6 +2604,7 @@ __global__ void __launch_bounds__(256, kGray ? (kMed == 1 ? 3 : AVR_PATHS_WAVES_
                 continue;
             }
             // ---- collision: density fetch for every lane that reached one ----
+            const DevMedium &m = fresh_params().med;   // the medium's fields re-read here (s_load)
             const S sigma_maj = sig_t * mv;
             T_maj = T_maj * sexpm<kFast>(-(sigma_maj * (t - tMin)));
             const V3 pc = po + sd * t;
