@@ -29,11 +29,14 @@ KP_UNITS = [(m, f) for f in (0, 1) for m in (0, 1, 3, 4)]
 # so a device sample replays the CPU oracle's sample.
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC",
          "-I" + os.path.join(ROOT, "include")]
-# k_paths units only: no MachineLICM. The persistent kernel's main loop would otherwise keep
-# ~40 hoisted loop invariants (f32 literals for VOP3 operands, float(n), 1 + g^2, ...) in VGPRs
-# for its whole lifetime; without the hoisting it fits 4 waves/SIMD (128 VGPRs, DESIGN §6:
-# 1926 -> 2029 Msamples/s at the driver's command).
-KP_FLAGS = ["-mllvm", "-disable-machine-licm"]
+# k_paths units' extra flags. Rounds 4-5 built them without MachineLICM (-mllvm
+# -disable-machine-licm): the hoisted invariants did not fit 4 waves/SIMD next to the kernel
+# arguments spilled to VGPR lanes. Since k_paths reloads its kernel arguments where it uses them
+# (fresh_params, round 6: 126 -> 107 VGPRs), the hoisting fits (128 VGPRs, no scratch) and wins
+# +0.6 % (profiles/r06_ab_walk.json). `python -m acceleratedvolrenderer_amd.build <variant>
+# --no-licm` builds the old way.
+KP_FLAGS = []
+NO_LICM = ["-mllvm", "-disable-machine-licm"]
 # RCCL for avr_film_reduce_rccl (in-process multi-GPU film reduce)
 LIBS = ["-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"]
 
@@ -68,9 +71,10 @@ def _compile(args):
     return obj
 
 
-def build(force=False, verbose=False, jobs=None, variant=None, defines=()):
+def build(force=False, verbose=False, jobs=None, variant=None, defines=(), kp_flags=None):
     """Build the library. `variant` + `defines` (e.g. ["-DAVR_PATHS_WAVES_GRAY=4"]) build an
-    experiment copy into variants/<variant>/libavr_hip.so instead (load it with AVR_LIB)."""
+    experiment copy into variants/<variant>/libavr_hip.so instead (load it with AVR_LIB);
+    `kp_flags` replaces the k_paths units' KP_FLAGS in such a copy."""
     out, objdir = OUT, OBJDIR
     if variant:
         out = os.path.join(ROOT, "variants", variant, "libavr_hip.so")
@@ -82,7 +86,8 @@ def build(force=False, verbose=False, jobs=None, variant=None, defines=()):
     units = [(SRC, os.path.join(objdir, "avr_capi.o"), ["-DAVR_KP_SPLIT"] + defines, verbose)]
     for med, fast in KP_UNITS:
         units.append((KPATHS, os.path.join(objdir, f"avr_kpaths_m{med}_f{fast}.o"),
-                      KP_FLAGS + [f"-DAVR_KP_MED={med}", f"-DAVR_KP_FAST={fast}"] + defines, verbose))
+                      (KP_FLAGS if kp_flags is None else list(kp_flags)) + [f"-DAVR_KP_MED={med}", f"-DAVR_KP_FAST={fast}"]
+                      + defines, verbose))
     jobs = jobs or max(1, min(len(units), int(os.environ.get("MAX_JOBS", os.cpu_count() or 4))))
     with ThreadPoolExecutor(jobs) as ex:
         objs = list(ex.map(_compile, units))
@@ -98,7 +103,8 @@ def build(force=False, verbose=False, jobs=None, variant=None, defines=()):
 
 if __name__ == "__main__":
     import sys
-    if len(sys.argv) > 1:   # python -m acceleratedvolrenderer_amd.build <variant> -DNAME=VALUE ...
-        print(build(verbose=True, variant=sys.argv[1], defines=sys.argv[2:]))
+    if len(sys.argv) > 1:   # python -m acceleratedvolrenderer_amd.build <variant> [--no-licm] -DNAME=VALUE ...
+        print(build(verbose=True, variant=sys.argv[1], defines=[a for a in sys.argv[2:] if a != "--no-licm"],
+                    kp_flags=NO_LICM if "--no-licm" in sys.argv[2:] else None))
     else:
         print(build(force=True, verbose=True))

@@ -9,6 +9,8 @@ import sys
 from collections import Counter
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from acceleratedvolrenderer_amd import build as B  # noqa: E402
 
 
 def main():
@@ -21,7 +23,7 @@ def main():
     fast = next((d.split("=")[1] for d in defs if d.startswith("-DAVR_KP_FAST=")), "0")
     defs = [d for d in defs if not d.startswith(("-DAVR_KP_MED=", "-DAVR_KP_FAST="))]
     subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
-                           "-fPIC", "-I" + os.path.join(ROOT, "include"), "-mllvm", "-disable-machine-licm",   # build.py KP_FLAGS
+                           "-fPIC", "-I" + os.path.join(ROOT, "include"), *B.KP_FLAGS,   # the k_paths units' flags
                            f"-DAVR_KP_MED={med}", f"-DAVR_KP_FAST={fast}",
                            *defs, "--save-temps", "-c", os.path.join(ROOT, "acceleratedvolrenderer_amd", "csrc", "avr_kpaths.hip"),
                            "-o", os.path.join(out, "kp.o")], cwd=out, stderr=subprocess.DEVNULL)
