@@ -295,6 +295,24 @@ struct Params {
     FastDiv div_width;                // by film.width
 };
 
+// Kernel arguments re-read where they are used: k_paths' event handlers and collision block and
+// the camera stage's sample loop take the Params through the kernarg segment pointer passed
+// through an empty asm, so the compiler reloads the fields they use with scalar loads right
+// there instead of keeping them live in SGPRs across the kernels' loops. At the SGPR limit those
+// long-lived values were spilled to VGPR lanes: in k_paths' headline instantiation 180 SGPR
+// spills and 1095 v_readlane VALU instructions (771 in the tracking loop); reloaded, it has 2
+// v_readlane, 8572 instead of 9829 instructions and 107 instead of 126 VGPRs (+3.7 % grid,
+// +1.6 % NanoVDB, profiles/r06_ab_walk.json); in the camera stage 858 v_readlane and 175
+// v_writelane go. The segment pointer, not the by-value argument's address: taking that would
+// make the compiler copy the argument to scratch. Only for kernels whose (first and only)
+// argument is a Params by value (k_paths, k_paths_camera).
+__device__ __forceinline__ const Params &fresh_params() {
+    typedef const __attribute__((address_space(4))) Params *KP;
+    KP p = (KP)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(p));
+    return *(const Params *)p;
+}
+
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 
 // Wave-aggregated queue push: one atomic per wave, lane offset from the ballot prefix.
@@ -1161,7 +1179,8 @@ __device__ __forceinline__ void zsobol_draw_quad(smp::ZSobol &z, const smp::ZSob
 #define AVR_CAM_WAVES 1   // minimum waves per SIMD asked of k_paths_camera (1: the compiler's choice)
 #endif
 template <int kSmp, bool kFast>
-__global__ void __launch_bounds__(256, AVR_CAM_WAVES) k_paths_camera(Params P) {
+__global__ void __launch_bounds__(256, AVR_CAM_WAVES) k_paths_camera(Params Pk) {
+    const Params &P = Pk;
     __shared__ float s_filt[kFiltLds];
     __shared__ double s_canon[canon::kCanonTabDoubles];
     for (int i = threadIdx.x; i < canon::kCanonTabDoubles; i += blockDim.x)   // (fast mode too: k_film's pdfs stay canonical)
@@ -1186,6 +1205,9 @@ __global__ void __launch_bounds__(256, AVR_CAM_WAVES) k_paths_camera(Params P) {
     const bool quad = kSmp != 0 && P.cam_quad;
     // (n < 2^31: the host bounds a pass by max_paths; 32-bit index arithmetic, FastDiv splits)
     for (uint32_t tu = blockIdx.x * blockDim.x + threadIdx.x; tu < (uint32_t)n; tu += gridDim.x * blockDim.x) {
+        // the kernel arguments re-read per sample with scalar loads (fresh_params) instead of
+        // living across the loop in SGPRs that spill to VGPR lanes
+        const Params &P = fresh_params();
         const int t = (int)tu;
         int slot, s;
         if (quad) {
@@ -1864,22 +1886,6 @@ __global__ void __launch_bounds__(256) k_bin_scatter(const int *__restrict__ que
 // 4-18 % slower and removed: DESIGN §6, profiles/r05_ab_pooled_handlers.json.)
 enum : int { EV_NONE = 0, EV_SCATTER = 1, EV_SHADOW_DONE = 2, EV_PHASE = 3, EV_ESCAPE = 4, EV_END = 5 };
 
-// k_paths' kernel arguments re-read where they are used: each event handler and the collision
-// block take the Params through the kernarg segment pointer passed through an empty asm, so
-// the compiler reloads the fields they use with scalar loads right there instead of keeping
-// them live in SGPRs across the kernel's loops. At k_paths' SGPR limit those long-lived values
-// were spilled to VGPR lanes (180 SGPR spills, 1095 v_readlane VALU instructions in the
-// headline instantiation, 771 of them in the tracking loop); reloaded, the kernel has 2
-// v_readlane, 8572 instead of 9829 instructions and 107 instead of 126 VGPRs (+3.7 % grid,
-// +1.6 % NanoVDB, profiles/r06_ab_walk.json). The segment pointer, not the by-value
-// argument's address: taking that would make the compiler copy the argument to scratch.
-// Only for kernels whose (first and only) argument is a Params by value, as k_paths'.
-__device__ __forceinline__ const Params &fresh_params() {
-    typedef const __attribute__((address_space(4))) Params *KP;
-    KP p = (KP)__builtin_amdgcn_kernarg_segment_ptr();
-    asm volatile("" : "+s"(p));
-    return *(const Params *)p;
-}
 
 // Spectral-state type of k_paths: Spec (4 wavelengths) in general; float for a GRAY medium
 // (sigma_a and sigma_s tables constant over 360..830 nm, decided on the host). In a gray
