@@ -18,7 +18,7 @@ KPATHS = os.path.join(CSRC, "avr_kpaths.hip")
 DEPS = [os.path.join(CSRC, f) for f in (
     "avr_capi.hip", "avr_kernels.hip", "avr_kpaths.hip", "avr_kpaths_list.h", "avr_numerics.h", "avr_canon.h",
     "avr_sampling.h", "avr_vdb.h", "avr_envmap.h", "avr_flip.h", "avr_graph.hip", "avr_graph_capi.hip",
-    "avr_graph_host.h", "avr_boundary.h", "avr_fastdiv.h")] + [os.path.join(ROOT, "include", "avr.h")]
+    "avr_graph_host.h", "avr_boundary.h", "avr_fastdiv.h", "avr_image_kernels.h")] + [os.path.join(ROOT, "include", "avr.h")]
 OUT = os.path.join(HERE, "libavr_hip.so")
 OBJDIR = os.path.join(ROOT, "build", "obj")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")

@@ -1943,8 +1943,11 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
                         p.zs.plo = plo;
                     }
                 }
-                hipLaunchKernelGGL(kcam[c->render_mode ? 1 : 0][sv], dim3(blocks_for(n0, 256, 256 * 8)), dim3(256), 0,
-                                   c->stream, p);
+                // 16384 blocks (64 per CU, ~14 samples per thread at the bench's pass): the measured optimum
+                // between one round of resident blocks and one sample per thread
+                // (profiles/r06_ab_camera_grid.json)
+                const int cgrid = blocks_for(n0, 256, 256 * 64);
+                hipLaunchKernelGGL(kcam[c->render_mode ? 1 : 0][sv], dim3(cgrid), dim3(256), 0, c->stream, p);
                 HIP_TRY(hipGetLastError());
                 EV_MARK(ec1);
                 c->timed.push_back({ec, ec1, &avr_stats::ms_camera, false});

@@ -952,20 +952,24 @@ __device__ __forceinline__ const float *stage_majorant(const DevMedium &m, float
     return lds;
 }
 
-// GaussianFilter's FilterSampler tables (pbrt's default radius 1.5: 48 x 48 function + CDFs,
-// ~19 KB, their 6.3 KB of search guides and 9.2 KB of cell weights) staged in LDS when they fit, so the camera
-// sample's two guided searches run on LDS. Returns (after a block barrier) whether they were
-// staged; filter_lds_tables then describes the copy. The descriptor is built in registers from
-// the kernel arguments, not read back from LDS: its pointers then stay LDS-typed (ds_read, not
-// flat loads) and the first table read does not wait for a descriptor read.
-constexpr int kFiltLds = 8704;
+// GaussianFilter's FilterSampler tables (pbrt's default radius 1.5: the 48 x 48 CDFs, ~9.6 KB,
+// their 6.3 KB of search guides and 9.2 KB of cell weights) staged in LDS when they fit, so the
+// camera sample's two guided searches run on LDS. The function table f (another 9.2 KB) stays in
+// global memory: with the cell weights it is read only for a cell whose weight entry is NaN.
+// 25.6 KB instead of 34.8 lets five camera blocks share a CU's LDS instead of four (with the
+// 16384-block grid: camera stage 2.71 -> 2.41 ms, profiles/r06_ab_camera_grid.json). Returns
+// (after a block barrier) whether they were staged; filter_lds_tables then describes the copy.
+// The descriptor is built in registers from the kernel arguments, not read back from LDS: its
+// pointers then stay LDS-typed (ds_read, not flat loads) and the first table read does not wait
+// for a descriptor read.
+constexpr int kFiltLds = 6400;
 __device__ __forceinline__ bool stage_filter(const Params &P, float *s_filt) {
     bool staged = false;
     if (P.film.filter_type != 0) {
         const smp::FilterTables &g = P.film.gauss;
-        const int nf = smp::filter_blob_floats(g.nx, g.ny);
+        const int nf = smp::filter_blob_floats(g.nx, g.ny) - g.nx * g.ny;   // the blob after f
         if (g.guide && g.wt && nf <= kFiltLds) {
-            const float *base = g.f;
+            const float *base = g.f + g.nx * g.ny;
             for (int i = threadIdx.x; i < nf; i += blockDim.x) s_filt[i] = base[i];
             staged = true;
         }
@@ -974,13 +978,13 @@ __device__ __forceinline__ bool stage_filter(const Params &P, float *s_filt) {
     return staged;
 }
 __device__ __forceinline__ smp::FilterTables filter_lds_tables(const smp::FilterTables &g, const float *s_filt) {
-    smp::FilterTables t = g;
-    t.f = s_filt;
-    t.ccdf = s_filt + g.nx * g.ny;
+    smp::FilterTables t = g;   // (t.f stays g.f, in global memory)
+    t.ccdf = s_filt;
     t.cint = t.ccdf + g.ny * (g.nx + 1);
     t.mcdf = t.cint + g.ny;
-    t.guide = reinterpret_cast<const uint8_t *>(s_filt + smp::filter_table_floats(g.nx, g.ny));
-    t.wt = s_filt + smp::filter_table_floats(g.nx, g.ny) + smp::filter_guide_floats(g.ny);
+    const int tabs = smp::filter_table_floats(g.nx, g.ny) - g.nx * g.ny;
+    t.guide = reinterpret_cast<const uint8_t *>(s_filt + tabs);
+    t.wt = s_filt + tabs + smp::filter_guide_floats(g.ny);
     return t;
 }
 
@@ -3222,100 +3226,6 @@ __global__ void __launch_bounds__(256) k_zsobol_pass_table(smp::ZSobolParams zp,
     }
 }
 
-// RGBFilm::GetImage on the device (film.cpp:533-565): GetPixelRGB (film.h:258-274; rgbSum and
-// weightSum rounded to float, divided, outputRGBFromSensorRGB applied as Mul's
-// ((0 + m0 r) + m1 g) + m2 b; no splats) and, for the fp16 image, the 65504 clamp and the
-// round-to-nearest-even half conversion.
-struct Mat3 { float m[9]; };
-__global__ void __launch_bounds__(256) k_film_image(DevFilm F, Mat3 M, int fp16, float *__restrict__ out) {
-    const int np = F.width * F.height;
-    for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < np; p += gridDim.x * blockDim.x) {
-        float r = (float)F.rgb_sum[3 * p], g = (float)F.rgb_sum[3 * p + 1], b = (float)F.rgb_sum[3 * p + 2];
-        const float w = (float)F.w_sum[p];
-        if (w != 0) { r /= w; g /= w; b /= w; }
-        float o[3];
-        for (int i = 0; i < 3; ++i) o[i] = (M.m[3 * i] * r + M.m[3 * i + 1] * g) + M.m[3 * i + 2] * b;
-        if (fp16) {
-            const float mx = fmaxf_(o[0], fmaxf_(o[1], o[2]));
-            for (int i = 0; i < 3; ++i) {
-                if (mx > 65504.f && o[i] > 65504.f) o[i] = 65504.f;
-                o[i] = (float)(_Float16)o[i];   // IEEE round-to-nearest-even
-            }
-        }
-        out[3 * p] = o[0];
-        out[3 * p + 1] = o[1];
-        out[3 * p + 2] = o[2];
-    }
-}
-
-// Image::ME / MAE / MSE / MRSE terms (util/image.cpp:543-678) summed in f64: per thread over a
-// grid-strided pixel range, then a fixed-order tree per block (deterministic for a fixed
-// grid); k_metric_final adds the block partials in order. Slots per channel c: [c] for
-// MAE/MSE/MRSE; ME: [c] absolute, [3 + c] positive, [6 + c] negative. Infinite terms skipped.
-constexpr int kMetricSlots = 9;
-__global__ void __launch_bounds__(256) k_metric(const float *__restrict__ img, const float *__restrict__ ref, int np,
-                                                int metric, double *__restrict__ partial) {
-    double acc[kMetricSlots];
-    for (int k = 0; k < kMetricSlots; ++k) acc[k] = 0;
-    for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < np; p += gridDim.x * blockDim.x) {
-        for (int c = 0; c < 3; ++c) {
-            const double v = img[3 * p + c], vr = ref[3 * p + c];
-            const double d = v - vr;
-            double t;
-            if (metric == 0) t = d * d;
-            else if (metric == 1) t = d < 0 ? -d : d;
-            else if (metric == 2) { const double q = vr + 0.01; t = (d * d) / (q * q); }
-            else t = d;
-            if (__builtin_isinf(t)) continue;
-            if (metric == 3) {
-                acc[c] += d < 0 ? -d : d;
-                if (d > 0) acc[3 + c] += d;
-                else acc[6 + c] += d;
-            } else {
-                acc[c] += t;
-            }
-        }
-    }
-    __shared__ double red[256];
-    for (int k = 0; k < kMetricSlots; ++k) {
-        red[threadIdx.x] = acc[k];
-        __syncthreads();
-        for (int s = blockDim.x / 2; s > 0; s >>= 1) {
-            if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
-            __syncthreads();
-        }
-        if (threadIdx.x == 0) partial[blockIdx.x * kMetricSlots + k] = red[0];
-        __syncthreads();
-    }
-}
-__global__ void k_metric_final(const double *__restrict__ partial, int nblocks, double *__restrict__ out) {
-    const int k = threadIdx.x;
-    if (k >= kMetricSlots) return;
-    double s = 0;
-    for (int b = 0; b < nblocks; ++b) s += partial[b * kMetricSlots + k];
-    out[k] = s;
-}
-
-// FLIP (src/ext/flip/flip.cpp:941-984) — k_flip_prep: both images to YCxCz, w = the achromatic
-// channel (Y + 16) / 116 the feature detectors read; k_flip_error: per pixel, the CSF
-// convolution of both images (taps in the reference's row-major order, borders replicated),
-// Lab + Hunt, HyAB colour difference, edge / point detector responses, error = cdiff^(1-fdiff).
-__global__ void __launch_bounds__(256) k_flip_prep(const float *__restrict__ test, const float *__restrict__ ref, int n,
-                                                   flip::F4 *__restrict__ ycT, flip::F4 *__restrict__ ycR) {
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        ycT[i] = flip::prep_pixel(test[3 * i], test[3 * i + 1], test[3 * i + 2]);
-        ycR[i] = flip::prep_pixel(ref[3 * i], ref[3 * i + 1], ref[3 * i + 2]);
-    }
-}
-__global__ void __launch_bounds__(256) k_flip_error(const flip::F4 *__restrict__ ycT, const flip::F4 *__restrict__ ycR,
-                                                    int w, int h, const float *__restrict__ sf, int rs,
-                                                    const float *__restrict__ ef, const float *__restrict__ pf, int rd,
-                                                    float cmax, float *__restrict__ out) {
-    const int n = w * h;
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
-        out[i] = flip::error_at(ycT, ycR, w, h, i % w, i / w, sf, rs, ef, pf, rd, cmax);
-}
-
 __global__ void __launch_bounds__(256) k_cloud(float *out, int n, long long first, long long count, float density,
                                                float wispiness, float frequency) {
     for (long long k = blockIdx.x * (long long)blockDim.x + threadIdx.x; k < count; k += (long long)gridDim.x * blockDim.x) {
@@ -3353,3 +3263,7 @@ __global__ void __launch_bounds__(256) k_rgb_explosion(float4 *sa, float4 *ss, f
 
 #endif  // AVR_KPATHS_TU
 }  // namespace avr
+
+#ifndef AVR_KPATHS_TU
+#include "avr_image_kernels.h"   // the film image, image metrics and FLIP kernels
+#endif

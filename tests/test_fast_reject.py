@@ -1,4 +1,4 @@
-"""k_paths' replay fast reject (csrc/avr_kernels.hip, AVR_REJECT_BY_EXP): inside the
+"""k_paths' replay fast reject (csrc/avr_kernels.hip, the DDA walk's candidate test): inside the
 DDA walk a free-flight candidate t = tMin + SampleExponential(u, sm0) (sampling.h:222-225,
 media.h:770-777) is rejected WITHOUT evaluating the canonical log when
 
