@@ -96,6 +96,7 @@ SIGNATURES = {
     "avr_density_fetch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_longlong, c_float_p, c_float_p]),
     "avr_set_ray_binning": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "avr_set_majorant_occupancy": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "avr_set_pass_table_ahead": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "avr_set_majorant_res": (ctypes.c_int, [ctypes.c_void_p, c_int_p]),
     "avr_medium_boundary_sphere": (ctypes.c_int, [ctypes.c_void_p, c_float_p, ctypes.c_float]),
     "avr_medium_boundary_convex": (ctypes.c_int, [ctypes.c_void_p, c_float_p, ctypes.c_int]),
@@ -304,6 +305,9 @@ class Context:
 
     def set_majorant_occupancy(self, on):
         _check(self.lib.avr_set_majorant_occupancy(self.h, 1 if on else 0))
+
+    def set_pass_table_ahead(self, on):
+        _check(self.lib.avr_set_pass_table_ahead(self.h, 1 if on else 0))
 
     def record_lookups(self, d_points, cap, d_count):
         """Trace the wavefront kernels' density fetches into device buffers (0 / None stops)."""

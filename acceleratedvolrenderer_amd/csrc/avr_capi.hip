@@ -158,11 +158,20 @@ struct avr_context {
     int zs_key[3] = {-1, -1, -1};
     // ZSobol pass table (zsobol_pass_entry per Morton(pixel) x dimension < zs_pdims), rebuilt
     // for every k_paths pass: the digits its sample indices share; zs_pdims 0 = no table
-    uint64_t *d_zs_ptab = nullptr;
-    size_t zs_ptab_cap = 0;   // entries allocated
-    uint64_t *d_zs_ctab = nullptr;   // the camera stage's compact copy (6 entries per pixel)
-    size_t zs_ctab_cap = 0;
+    // Two buffers: a pass reads one while the next pass's table is built ahead into the other
+    // (ptab_spec) on the low-priority side stream tstream
+    uint64_t *d_zs_ptab[2] = {};
+    size_t zs_ptab_cap[2] = {};   // entries allocated
+    uint64_t *d_zs_ctab[2] = {};  // the camera stage's compact copy (6 entries per pixel)
+    size_t zs_ctab_cap[2] = {};
     int zs_pdims = 96;
+    int tab_buf = 1;              // the buffer the last pass read
+    int ptab_spec = 1;            // avr_set_pass_table_ahead
+    bool spec_valid = false;      // tstream holds (or is building) the table for spec_key
+    long long spec_key[8] = {};
+    int spec_buf = 0;
+    hipStream_t tstream = nullptr;
+    hipEvent_t ev_cam = nullptr, ev_tab = nullptr;
     // Level-A pass table (the same table for plo + 2, shared by four consecutive passes);
     // zs_akey names the build it holds (rebuilt when any field changes), zs_two_level 0 = off
     uint64_t *d_zs_atab = nullptr;
@@ -621,7 +630,8 @@ const char *avr_last_error(void) { return g_err.c_str(); }
 #define AVR_QUIESCE(c)                                                                              \
     do {                                                                                            \
         if ((c) && (c)->stream) {                                                                   \
-            const hipError_t qe_ = hipStreamSynchronize((c)->stream);                               \
+            hipError_t qe_ = hipStreamSynchronize((c)->stream);                                     \
+            if (qe_ == hipSuccess && (c)->tstream) qe_ = hipStreamSynchronize((c)->tstream);        \
             if (qe_ != hipSuccess) return fail(AVR_ERR_HIP, std::string("stream: ") + hipGetErrorString(qe_)); \
         }                                                                                           \
     } while (0)
@@ -637,8 +647,16 @@ int avr_context_create(int device, long long max_paths, avr_context **out) {
     auto *c = new avr_context();
     c->device = device;
     if (max_paths > 0) c->max_paths = max_paths, c->max_paths_set = true;
-    hipError_t e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
-    if (e != hipSuccess) { delete c; return fail(AVR_ERR_HIP, hipGetErrorString(e)); }
+    // the path stream at the greatest priority, the side stream (ptab_spec's tables built
+    // ahead) at the least, so the dispatcher serves the side stream's blocks only from CUs the
+    // path kernels leave free
+    int prLeast = 0, prGreatest = 0;
+    hipError_t e = hipDeviceGetStreamPriorityRange(&prLeast, &prGreatest);
+    if (e == hipSuccess) e = hipStreamCreateWithPriority(&c->own_stream, hipStreamNonBlocking, prGreatest);
+    if (e == hipSuccess) e = hipStreamCreateWithPriority(&c->tstream, hipStreamNonBlocking, prLeast);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_cam, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_tab, hipEventDisableTiming);
+    if (e != hipSuccess) { (void)avr_context_destroy(c); return fail(AVR_ERR_HIP, hipGetErrorString(e)); }
     c->stream = c->own_stream;
     if (dalloc(&c->d_counts, 4) != hipSuccess || dalloc(&c->d_stats, avr::kNumStats + 8) != hipSuccess ||
         hipHostMalloc((void **)&c->h_count, sizeof(int) * 4) != hipSuccess) {
@@ -723,6 +741,14 @@ int avr_set_ray_binning(avr_context *c, int on) {
     return AVR_OK;
 }
 
+int avr_set_pass_table_ahead(avr_context *c, int on) {
+    AVR_QUIESCE(c);
+    if (!c || (on != 0 && on != 1)) return fail(AVR_ERR_ARG, "pass table ahead must be 0 or 1");
+    c->ptab_spec = on;
+    c->spec_valid = false;   // (the side stream is idle after the quiesce)
+    return AVR_OK;
+}
+
 int avr_set_majorant_occupancy(avr_context *c, int on) {
     AVR_QUIESCE(c);
     if (!c || (on != 0 && on != 1)) return fail(AVR_ERR_ARG, "majorant occupancy must be 0 or 1");
@@ -745,6 +771,7 @@ int avr_context_destroy(avr_context *c) {
     if (!c) return AVR_OK;
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
+    if (c->tstream) (void)hipStreamSynchronize(c->tstream);
     release_comms(c);
     free_paths(c);
     free_records(c);
@@ -767,8 +794,10 @@ int avr_context_destroy(avr_context *c) {
     free_rgb(c);
     for (auto &b : c->d_light_img) if (b) (void)hipFree(b), b = nullptr;
     if (c->d_zs_table) (void)hipFree(c->d_zs_table);
-    if (c->d_zs_ptab) (void)hipFree(c->d_zs_ptab);
-    if (c->d_zs_ctab) (void)hipFree(c->d_zs_ctab);
+    for (int b = 0; b < 2; ++b) {
+        if (c->d_zs_ptab[b]) (void)hipFree(c->d_zs_ptab[b]);
+        if (c->d_zs_ctab[b]) (void)hipFree(c->d_zs_ctab[b]);
+    }
     if (c->d_zs_atab) (void)hipFree(c->d_zs_atab);
     if (c->d_image) (void)hipFree(c->d_image);
     if (c->d_reference) (void)hipFree(c->d_reference);
@@ -780,6 +809,9 @@ int avr_context_destroy(avr_context *c) {
     if (c->h_count) (void)hipHostFree(c->h_count);
     for (auto e : c->evpool) (void)hipEventDestroy(e);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+    if (c->tstream) (void)hipStreamDestroy(c->tstream);
+    if (c->ev_cam) (void)hipEventDestroy(c->ev_cam);
+    if (c->ev_tab) (void)hipEventDestroy(c->ev_tab);
     delete c;
     return AVR_OK;
 }
@@ -1700,6 +1732,102 @@ static int fold_stats(avr_context *c) {
     return AVR_OK;
 }
 
+// The ZSobol pass table of sample indices [base, base + S): its entries hold the digits above
+// the lowest plo bits, where the pass's indices differ
+static int pass_plo(long long base, int S) {
+    int plo = 0;
+    while ((base >> plo) != ((base + S - 1) >> plo)) ++plo;
+    return plo;
+}
+constexpr int kPtabKey = 8;
+// what a built table depends on (a table built ahead is used only when the pass's key equals it)
+static void ptab_key(const avr_context *c, const avr::smp::ZSobolParams &zs, long long base, int plo, long long *key) {
+    const long long k[kPtabKey] = {base, plo, (long long)zs.log2spp, (long long)zs.seed,
+                                   (long long)c->film.width * 65536 + c->film.height, c->zs_pdims,
+                                   (long long)(uintptr_t)zs.upper, zs.dmax};
+    for (int i = 0; i < kPtabKey; ++i) key[i] = k[i];
+}
+// Build the pass table (and the camera stage's compact copy) of [base, base + S) into buffer buf
+// on stream s, with its level-A table when the two-level build applies. No room for a buffer:
+// d_zs_ptab[buf] stays null (the pixel table / every digit per call serve the pass).
+static int ptab_build(avr_context *c, hipStream_t s, const avr::smp::ZSobolParams &zs, long long base, int plo, int buf) {
+    const long long P = (long long)c->film.width * c->film.height;
+    const size_t prow = (size_t)avr::smp::encode_morton2((uint32_t)c->film.width - 1, (uint32_t)c->film.height - 1) + 1;
+    const size_t need_e = prow * (size_t)c->zs_pdims;
+    // the same headroom policy as the fat / bricked density copies: allocate only with >= 8 GiB
+    // of HBM to spare
+    auto fits = [](size_t bytes) {
+        size_t freeB = 0, totalB = 0;
+        return hipMemGetInfo(&freeB, &totalB) == hipSuccess && bytes + (8ull << 30) < freeB;
+    };
+    if (need_e > c->zs_ptab_cap[buf]) {
+        if (c->d_zs_ptab[buf]) (void)hipFree(c->d_zs_ptab[buf]);
+        c->d_zs_ptab[buf] = nullptr;
+        c->zs_ptab_cap[buf] = 0;
+        if (!fits(need_e * sizeof(uint64_t)) ||
+            hipMalloc((void **)&c->d_zs_ptab[buf], need_e * sizeof(uint64_t)) != hipSuccess) {
+            (void)hipGetLastError();
+            c->d_zs_ptab[buf] = nullptr;
+            return AVR_OK;
+        }
+        c->zs_ptab_cap[buf] = need_e;
+    }
+    // two-level build: the plo + 2 table is shared by the four passes whose indices agree above
+    // plo + 2 bits; each pass then derives its own from it
+    const uint64_t *atab = nullptr;
+    if (c->zs_two_level && plo + 2 <= zs.log2spp) {
+        if (need_e > c->zs_atab_cap) {
+            if (c->d_zs_atab) (void)hipFree(c->d_zs_atab);
+            c->d_zs_atab = nullptr;
+            c->zs_atab_cap = 0;
+            for (long long &k : c->zs_akey) k = -1;
+            if (!fits(need_e * sizeof(uint64_t)) ||
+                hipMalloc((void **)&c->d_zs_atab, need_e * sizeof(uint64_t)) != hipSuccess) {
+                (void)hipGetLastError();
+                c->d_zs_atab = nullptr;   // no room: one-level build
+            } else {
+                c->zs_atab_cap = need_e;
+            }
+        }
+        if (c->d_zs_atab) {
+            const long long key[6] = {base >> (plo + 2), plo, (long long)zs.log2spp, zs.seed,
+                                      (long long)c->film.width * 65536 + c->film.height, c->zs_pdims};
+            bool same = true;
+            for (int k = 0; k < 6; ++k) same = same && key[k] == c->zs_akey[k];
+            if (!same) {
+                hipLaunchKernelGGL(avr::k_zsobol_pass_table,
+                                   dim3(blocks_for(P * (c->zs_pdims / 2), 256, 256 * 64)), dim3(256), 0, s, zs,
+                                   c->film.width, c->film.height, c->zs_pdims, plo + 2, (base >> (plo + 2)) << (plo + 2),
+                                   c->d_zs_atab, (const uint64_t *)nullptr, avr::fastdiv_make((uint32_t)(c->zs_pdims / 2)),
+                                   avr::fastdiv_make((uint32_t)c->film.width), (uint64_t *)nullptr);
+                HIP_TRY(hipGetLastError());
+                for (int k = 0; k < 6; ++k) c->zs_akey[k] = key[k];
+            }
+            atab = c->d_zs_atab;
+        }
+    }
+    // the camera stage's six entries per pixel (dimensions 0, 1, 6..9) also as a compact
+    // scanline-ordered copy (48 B per pixel), when the table holds them
+    const size_t need_c = c->zs_pdims >= 10 ? 6 * (size_t)P : 0;
+    if (need_c > c->zs_ctab_cap[buf]) {
+        if (c->d_zs_ctab[buf]) (void)hipFree(c->d_zs_ctab[buf]);
+        c->d_zs_ctab[buf] = nullptr;
+        c->zs_ctab_cap[buf] = 0;
+        if (hipMalloc((void **)&c->d_zs_ctab[buf], need_c * sizeof(uint64_t)) != hipSuccess) {
+            (void)hipGetLastError();
+            c->d_zs_ctab[buf] = nullptr;   // no room: the camera reads the rows
+        } else {
+            c->zs_ctab_cap[buf] = need_c;
+        }
+    }
+    uint64_t *ctab = need_c ? c->d_zs_ctab[buf] : nullptr;
+    hipLaunchKernelGGL(avr::k_zsobol_pass_table, dim3(blocks_for(P * (c->zs_pdims / 2), 256, 256 * 64)), dim3(256), 0, s,
+                       zs, c->film.width, c->film.height, c->zs_pdims, plo, base, c->d_zs_ptab[buf], atab,
+                       avr::fastdiv_make((uint32_t)(c->zs_pdims / 2)), avr::fastdiv_make((uint32_t)c->film.width), ctab);
+    HIP_TRY(hipGetLastError());
+    return AVR_OK;
+}
+
 // next free pool event (folds first when the pool is full)
 static int next_event(avr_context *c, int *idx) {
     if (c->ev_used >= 512) {
@@ -1750,6 +1878,9 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
         // the log2(spp)/2 sample digits plus one load instead of all nBase4Digits
         const int key[3] = {c->sampler_spp, c->film.width, c->film.height};
         if (c->zs_key[0] != key[0] || c->zs_key[1] != key[1] || c->zs_key[2] != key[2]) {
+            // a table built ahead reads the pixel table: let it finish, and drop it
+            if (c->tstream) HIP_TRY(hipStreamSynchronize(c->tstream));
+            c->spec_valid = false;
             if (c->d_zs_table) (void)hipFree(c->d_zs_table);
             c->d_zs_table = nullptr;
             for (int k = 0; k < 3; ++k) c->zs_key[k] = key[k];
@@ -1792,6 +1923,8 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
     EV_MARK(evStart);
     for (long long base = spp_begin; base < spp_end; base += Smax) {
         const int S = (int)std::min<long long>(Smax, spp_end - base);
+        bool spec_next = false;   // build the next pass's ZSobol table ahead (ptab_spec)
+        avr::smp::ZSobolParams spec_zs{};
         avr::Params p{};
         p.med = c->med;
         p.lights = c->lights;
@@ -1856,91 +1989,34 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
                     // indices [base, base + S) share (those above their lowest differing bits),
                     // for the first zs_pdims dimensions; the camera stage and k_paths then
                     // evaluate only the digits below (two MixBits at 64 indices per pass)
-                    int plo = 0;
-                    while ((base >> plo) != ((base + S - 1) >> plo)) ++plo;
-                    const size_t need_e = (size_t)prow * (size_t)c->zs_pdims;
-                    // the same headroom policy as the fat / bricked density copies: allocate only
-                    // with >= 8 GiB of HBM to spare (else the pixel table serves every draw)
-                    auto fits = [](size_t bytes) {
-                        size_t freeB = 0, totalB = 0;
-                        return hipMemGetInfo(&freeB, &totalB) == hipSuccess && bytes + (8ull << 30) < freeB;
-                    };
-                    if (need_e > c->zs_ptab_cap) {
-                        if (c->d_zs_ptab) (void)hipFree(c->d_zs_ptab);
-                        c->d_zs_ptab = nullptr;
-                        c->zs_ptab_cap = 0;
-                        if (!fits(need_e * sizeof(uint64_t)) ||
-                            hipMalloc((void **)&c->d_zs_ptab, need_e * sizeof(uint64_t)) != hipSuccess) {
-                            (void)hipGetLastError();
-                            c->d_zs_ptab = nullptr;   // no room: the pixel table / every digit per call
-                        } else {
-                            c->zs_ptab_cap = need_e;
-                        }
+                    const int plo = pass_plo(base, S);
+                    long long key[kPtabKey];
+                    ptab_key(c, zs, base, plo, key);
+                    int buf = -1;
+                    if (c->spec_valid) {
+                        // the table the previous pass built ahead on the side stream (ptab_build's
+                        // caller below): this stream waits for it, whether it is used or not, so
+                        // no build of this pass overlaps it
+                        HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_tab, 0));
+                        bool same = true;
+                        for (int k = 0; k < kPtabKey; ++k) same = same && key[k] == c->spec_key[k];
+                        if (same) buf = c->spec_buf;
+                        c->spec_valid = false;
                     }
-                    // two-level build: the plo + 2 table is shared by the four passes whose
-                    // indices agree above plo + 2 bits; each pass then derives its own from it
-                    const uint64_t *atab = nullptr;
-                    if (c->d_zs_ptab && c->zs_two_level && plo + 2 <= zs.log2spp) {
-                        if (need_e > c->zs_atab_cap) {
-                            if (c->d_zs_atab) (void)hipFree(c->d_zs_atab);
-                            c->d_zs_atab = nullptr;
-                            c->zs_atab_cap = 0;
-                            for (long long &k : c->zs_akey) k = -1;
-                            if (!fits(need_e * sizeof(uint64_t)) ||
-                                hipMalloc((void **)&c->d_zs_atab, need_e * sizeof(uint64_t)) != hipSuccess) {
-                                (void)hipGetLastError();
-                                c->d_zs_atab = nullptr;   // no room: one-level build
-                            } else {
-                                c->zs_atab_cap = need_e;
-                            }
-                        }
-                        if (c->d_zs_atab) {
-                            const long long key[6] = {base >> (plo + 2), plo, (long long)zs.log2spp, zs.seed,
-                                                      (long long)c->film.width * 65536 + c->film.height, c->zs_pdims};
-                            bool same = true;
-                            for (int k = 0; k < 6; ++k) same = same && key[k] == c->zs_akey[k];
-                            if (!same) {
-                                hipLaunchKernelGGL(avr::k_zsobol_pass_table,
-                                                   dim3(blocks_for((long long)c->film.width * c->film.height * (c->zs_pdims / 2),
-                                                                   256, 256 * 64)),
-                                                   dim3(256), 0, c->stream, zs, c->film.width, c->film.height, c->zs_pdims,
-                                                   plo + 2, (base >> (plo + 2)) << (plo + 2), c->d_zs_atab,
-                                                   (const uint64_t *)nullptr, avr::fastdiv_make((uint32_t)(c->zs_pdims / 2)),
-                                                   avr::fastdiv_make((uint32_t)c->film.width), (uint64_t *)nullptr);
-                                HIP_TRY(hipGetLastError());
-                                for (int k = 0; k < 6; ++k) c->zs_akey[k] = key[k];
-                            }
-                            atab = c->d_zs_atab;
-                        }
+                    if (buf < 0) {
+                        buf = 1 - c->tab_buf;
+                        int rc2 = ptab_build(c, c->stream, zs, base, plo, buf);
+                        if (rc2) return rc2;
+                        if (!c->d_zs_ptab[buf]) buf = -1;
                     }
-                    if (c->d_zs_ptab) {
-                        // the camera stage's six entries per pixel (dimensions 0, 1, 6..9) also as a
-                        // compact scanline-ordered copy (48 B per pixel), when the table holds them
-                        const size_t need_c = c->zs_pdims >= 10 ? 6 * (size_t)P : 0;
-                        if (need_c > c->zs_ctab_cap) {
-                            if (c->d_zs_ctab) (void)hipFree(c->d_zs_ctab);
-                            c->d_zs_ctab = nullptr;
-                            c->zs_ctab_cap = 0;
-                            if (hipMalloc((void **)&c->d_zs_ctab, need_c * sizeof(uint64_t)) != hipSuccess) {
-                                (void)hipGetLastError();
-                                c->d_zs_ctab = nullptr;   // no room: the camera reads the rows
-                            } else {
-                                c->zs_ctab_cap = need_c;
-                            }
-                        }
-                        uint64_t *ctab = need_c ? c->d_zs_ctab : nullptr;
-                        const avr::smp::ZSobolParams zsd = zs;
-                        hipLaunchKernelGGL(avr::k_zsobol_pass_table,
-                                           dim3(blocks_for((long long)c->film.width * c->film.height * (c->zs_pdims / 2), 256,
-                                                           256 * 64)),
-                                           dim3(256), 0, c->stream, zsd, c->film.width, c->film.height, c->zs_pdims, plo,
-                                           base, c->d_zs_ptab, atab, avr::fastdiv_make((uint32_t)(c->zs_pdims / 2)),
-                                           avr::fastdiv_make((uint32_t)c->film.width), ctab);
-                        HIP_TRY(hipGetLastError());
-                        p.zs.ptab = c->d_zs_ptab;
-                        p.zs.ctab = ctab;
+                    if (buf >= 0) {
+                        c->tab_buf = buf;
+                        p.zs.ptab = c->d_zs_ptab[buf];
+                        p.zs.ctab = c->zs_pdims >= 10 ? c->d_zs_ctab[buf] : nullptr;
                         p.zs.pdims = c->zs_pdims;
                         p.zs.plo = plo;
+                        spec_next = c->ptab_spec != 0;
+                        spec_zs = zs;
                     }
                 }
                 // 16384 blocks (64 per CU, ~14 samples per thread at the bench's pass): the measured optimum
@@ -1951,6 +2027,7 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
                 HIP_TRY(hipGetLastError());
                 EV_MARK(ec1);
                 c->timed.push_back({ec, ec1, &avr_stats::ms_camera, false});
+                if (spec_next) HIP_TRY(hipEventRecord(c->ev_cam, c->stream));
             }
             EV_MARK(e0);
             // gray medium: sigma_a and sigma_s tables constant over all 471 wavelengths
@@ -1979,6 +2056,27 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
             EV_MARK(e2);
             c->timed.push_back({e0, e1, &avr_stats::ms_medium, true});
             c->timed.push_back({e1, e2, &avr_stats::ms_film, false});
+            if (spec_next) {
+                // the NEXT pass's table (sample indices [base + S, base + 2S): the next loop
+                // iteration's, or the next avr_render call's when the caller walks the indices in
+                // order) built ahead into the other buffer on the low-priority side stream: it
+                // waits for this pass's camera stage (the last reader of that buffer, k_paths of
+                // the previous pass, is then done too) and is dispatched as k_paths' blocks retire
+                // in its drain, instead of in front of the next camera stage. A pass whose key
+                // differs builds its own table (and this one is discarded).
+                const long long nb = base + S;
+                const int nplo = pass_plo(nb, S);
+                HIP_TRY(hipStreamWaitEvent(c->tstream, c->ev_cam, 0));
+                const int tb = 1 - c->tab_buf;
+                // (not timed: events around it would measure its wait for the drain too)
+                { int rc2 = ptab_build(c, c->tstream, spec_zs, nb, nplo, tb); if (rc2) return rc2; }
+                HIP_TRY(hipEventRecord(c->ev_tab, c->tstream));
+                if (c->d_zs_ptab[tb]) {
+                    ptab_key(c, spec_zs, nb, nplo, c->spec_key);
+                    c->spec_buf = tb;
+                    c->spec_valid = true;
+                }
+            }
             c->last_base = (int)base;
             c->last_S = S;
             c->last_order_gen = c->order_gen;

@@ -100,6 +100,14 @@ int avr_set_ray_binning(avr_context *ctx, int on);
  * Results unchanged (no reference counterpart: a DDAMajorantIterator, media.h:141-214, memory
  * schedule only). */
 int avr_set_majorant_occupancy(avr_context *ctx, int on);
+/* ZSobolSampler passes of the persistent kernel: 1 (default) = after launching a pass, build the
+ * NEXT pass's ZSobol pass table (sample indices [base + S, base + 2S)) into a second buffer on a
+ * low-priority side stream, where the dispatcher serves it as the pass's k_paths blocks retire;
+ * the next pass (in the same avr_render call, or the next call when the caller walks the sample
+ * indices in order, as pbrt's pass loop does) then skips its own build. A pass whose indices
+ * differ builds its table as before. 0 = build every table in front of its camera stage.
+ * Results unchanged (a schedule of ZSobolSampler::GetSampleIndex's digits, samplers.h:225-330). */
+int avr_set_pass_table_ahead(avr_context *ctx, int on);
 /* k_paths: refill a wave's idle lanes with new samples once at least `lanes` (1..64)
  * are idle (or none is busy); larger values batch the per-event handlers across lanes.
  * 0 = default (the measured optima in both render modes: 32; 16 for a non-emissive

@@ -369,3 +369,42 @@ def test_film_nan_inf_guard_with_overflowing_radiance(kernel):
     assert frac == 1.0
     assert np.array_equal(w, w_o) and np.array_equal(rgb, rgb_o, equal_nan=True)
     integ.close()
+
+
+def test_pass_tables_built_ahead_change_nothing():
+    """avr_set_pass_table_ahead: the next pass's ZSobol pass table built on the side stream while
+    this pass runs. Films bit-identical with it on and off for per-pass calls in order (every
+    pass after the first uses the table built ahead), out of order and pbrt's doubling waves
+    (the keys differ: those passes build in front of their camera stage), and one call of six
+    passes (max_paths), which also equals the in-order per-pass calls."""
+    from acceleratedvolrenderer_amd import VolPathIntegrator, scenes
+    from oracle import binding
+    dens = binding.cloud_grid(24)
+    W, H, S = 40, 24, 8
+
+    def run(ahead, seq, max_paths=0):
+        scene = scenes.s_cloud(dens, width=W, height=H, sampler="zsobol", spp=64, filter="gaussian")
+        integ = VolPathIntegrator(scene, maxdepth=scenes.CLOUD_MAXDEPTH, spp=64, seed=0, device=0,
+                                  max_paths=max_paths)
+        integ.ctx.set_pass_table_ahead(ahead)
+        integ.ctx.film_clear()
+        for b, e in seq:
+            integ.ctx.render(b, e, 0, scenes.CLOUD_MAXDEPTH)
+        out = integ.film_sums()
+        integ.close()
+        return out
+
+    def same(a, b):
+        return np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+
+    in_order = [(k * S, (k + 1) * S) for k in range(6)]
+    seqs = [in_order, [(16, 24), (0, 8), (8, 16), (32, 40), (24, 32)], [(0, 1), (1, 2), (2, 4), (4, 8), (8, 16), (16, 32)]]
+    per_pass = []
+    for seq in seqs:
+        a, b = run(1, seq), run(0, seq)
+        assert same(a, b), seq
+        assert a[1].sum() > 0
+        per_pass.append(a)
+    one_a, one_b = run(1, [(0, 6 * S)], max_paths=S * W * H), run(0, [(0, 6 * S)], max_paths=S * W * H)
+    assert same(one_a, one_b)
+    assert same(one_a, per_pass[0])
