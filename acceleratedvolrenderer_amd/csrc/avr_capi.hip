@@ -172,6 +172,7 @@ struct avr_context {
     int spec_buf = 0;
     hipStream_t tstream = nullptr;
     hipEvent_t ev_cam = nullptr, ev_tab = nullptr;
+    long long prev_call_begin = -1;   // avr_render's previous spp_begin (the call stride)
     // Level-A pass table (the same table for plo + 2, shared by four consecutive passes);
     // zs_akey names the build it holds (rebuilt when any field changes), zs_two_level 0 = off
     uint64_t *d_zs_atab = nullptr;
@@ -1921,6 +1922,11 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
     int rc = persistent ? ensure_records(c, need) : ensure_paths(c, need);
     if (rc) return rc;
     EV_MARK(evStart);
+    // the stride between consecutive calls' first sample indices (S for pbrt's pass loop and the
+    // one-GPU bench, N x S for a rank of an N-GPU sample shard): where the pass after this call's
+    // last one is expected to start, for the pass table built ahead
+    const long long call_stride = (c->prev_call_begin >= 0 && spp_begin > c->prev_call_begin) ? spp_begin - c->prev_call_begin : 0;
+    c->prev_call_begin = spp_begin;
     for (long long base = spp_begin; base < spp_end; base += Smax) {
         const int S = (int)std::min<long long>(Smax, spp_end - base);
         bool spec_next = false;   // build the next pass's ZSobol table ahead (ptab_spec)
@@ -2064,7 +2070,7 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
                 // the previous pass, is then done too) and is dispatched as k_paths' blocks retire
                 // in its drain, instead of in front of the next camera stage. A pass whose key
                 // differs builds its own table (and this one is discarded).
-                const long long nb = base + S;
+                const long long nb = (base + Smax < spp_end || call_stride == 0) ? base + S : spp_begin + call_stride;
                 const int nplo = pass_plo(nb, S);
                 HIP_TRY(hipStreamWaitEvent(c->tstream, c->ev_cam, 0));
                 const int tb = 1 - c->tab_buf;

@@ -103,9 +103,9 @@ int avr_set_majorant_occupancy(avr_context *ctx, int on);
 /* ZSobolSampler passes of the persistent kernel: 1 (default) = after launching a pass, build the
  * NEXT pass's ZSobol pass table (sample indices [base + S, base + 2S)) into a second buffer on a
  * low-priority side stream, where the dispatcher serves it as the pass's k_paths blocks retire;
- * the next pass (in the same avr_render call, or the next call when the caller walks the sample
- * indices in order, as pbrt's pass loop does) then skips its own build. A pass whose indices
- * differ builds its table as before. 0 = build every table in front of its camera stage.
+ * the next pass (in the same avr_render call, or the next call when the caller's calls advance
+ * by a fixed stride: pbrt's pass loop, a rank of a sample shard) then skips its own build. A
+ * pass whose indices differ builds its table as before. 0 = build every table in front of its camera stage.
  * Results unchanged (a schedule of ZSobolSampler::GetSampleIndex's digits, samplers.h:225-330). */
 int avr_set_pass_table_ahead(avr_context *ctx, int on);
 /* k_paths: refill a wave's idle lanes with new samples once at least `lanes` (1..64)

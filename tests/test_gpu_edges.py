@@ -376,7 +376,8 @@ def test_pass_tables_built_ahead_change_nothing():
     this pass runs. Films bit-identical with it on and off for per-pass calls in order (every
     pass after the first uses the table built ahead), out of order and pbrt's doubling waves
     (the keys differ: those passes build in front of their camera stage), and one call of six
-    passes (max_paths), which also equals the in-order per-pass calls."""
+    passes (max_paths), which also equals the in-order per-pass calls; calls with a stride of 2
+    passes (a rank of a sample shard: the table ahead follows the stride)."""
     from acceleratedvolrenderer_amd import VolPathIntegrator, scenes
     from oracle import binding
     dens = binding.cloud_grid(24)
@@ -398,7 +399,9 @@ def test_pass_tables_built_ahead_change_nothing():
         return np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
 
     in_order = [(k * S, (k + 1) * S) for k in range(6)]
-    seqs = [in_order, [(16, 24), (0, 8), (8, 16), (32, 40), (24, 32)], [(0, 1), (1, 2), (2, 4), (4, 8), (8, 16), (16, 32)]]
+    strided = [(k * 2 * S, k * 2 * S + S) for k in range(4)]   # a rank of a 2-way sample shard
+    seqs = [in_order, [(16, 24), (0, 8), (8, 16), (32, 40), (24, 32)], [(0, 1), (1, 2), (2, 4), (4, 8), (8, 16), (16, 32)],
+            strided]
     per_pass = []
     for seq in seqs:
         a, b = run(1, seq), run(0, seq)
