@@ -179,7 +179,7 @@ struct avr_context {
     size_t zs_atab_cap = 0;
     long long zs_akey[6] = {-1, -1, -1, -1, -1, -1};
     int zs_two_level = AVR_ZS_TWO_LEVEL;
-    int refill_min = 0;       // 0: the default (32 lanes; 12 for a non-emissive NanoVDB walk, 16 for RGB grids)
+    int refill_min = 0;       // 0: the default (32 lanes; 20 for a non-emissive NanoVDB walk, 16 for RGB grids)
     int dda_budget = 0;       // 0: by majorant resolution (12 cells up to 16^3, 32 for NanoVDB's 64^3)
     int grid_layout = 1;
     bool gray = false;        // sigma_a and sigma_s constant over 360..830 nm      // 1: build the fat (footprint) copy when memory allows, 0: linear only
@@ -1235,7 +1235,8 @@ static void walk_schedule(const avr_context *c, int refill, int dda, int *r_eff,
     const int mres = std::max(c->med.mres[0], std::max(c->med.mres[1], c->med.mres[2]));
     const bool vdbWalk = c->med.type == 3 && !c->med.emissive && mres > 16;
     const bool rgbWalk = c->med.type == 4;
-    *r_eff = refill > 0 ? refill : (vdbWalk || rgbWalk ? 16 : 32);
+    // measured optima (profiles/r06_walk_sweep.json for the round-6 kernels: NanoVDB 20 / 28)
+    *r_eff = refill > 0 ? refill : (vdbWalk ? 20 : (rgbWalk ? 16 : 32));
     *d_eff = dda > 0 ? dda : (vdbWalk ? 28 : (rgbWalk || mres > 16 ? 32 : 10));
 }
 

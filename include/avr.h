@@ -110,9 +110,9 @@ int avr_set_majorant_occupancy(avr_context *ctx, int on);
 int avr_set_pass_table_ahead(avr_context *ctx, int on);
 /* k_paths: refill a wave's idle lanes with new samples once at least `lanes` (1..64)
  * are idle (or none is busy); larger values batch the per-event handlers across lanes.
- * 0 = default (the measured optima in both render modes: 32; 16 for a non-emissive
- * NanoVDB medium at pbrt's 64^3 majorant, whose longer DDA walks favour smaller batches,
- * and for an RGBGridMedium). */
+ * 0 = default (the measured optima in both render modes: 32; 20 for a non-emissive
+ * NanoVDB medium at pbrt's 64^3 majorant, whose longer DDA walks favour smaller batches;
+ * 16 for an RGBGridMedium). */
 int avr_set_refill_min(avr_context *ctx, int lanes);
 /* k_paths: majorant-grid cells a lane may cross per tracking iteration before yielding to
  * the wave (0 = default: 10 for majorant grids up to 16^3, 32 for finer ones and for
