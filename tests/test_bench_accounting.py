@@ -136,16 +136,17 @@ def _trace_avg_ms(rows, inst):
     return sum(keep) / len(keep), len(keep)
 
 
-def test_r06_line_fracs_reproduce_from_the_committed_kernel_trace():
+@pytest.mark.parametrize("tag", ["final", "end"])
+def test_r06_line_fracs_reproduce_from_the_committed_kernel_trace(tag):
     """VERDICT r5 item 1's Done: the grid, NanoVDB and fast `frac` of the round-6 line
-    (profiles/r06_bench_line_final.json) from its per-launch algorithmic bytes over the kernel's
-    average duration in the committed rocprofv3 trace of the same command
-    (profiles/r06_kernel_trace_final.csv, tools/final_pass.sh `stats`) — separate runs, so within
+    (profiles/r06_bench_line_{final,end}.json: mid-round and end of round) from its per-launch
+    algorithmic bytes over the kernel's average duration in the committed rocprofv3 trace of the
+    same command (profiles/r06_kernel_trace_{final,end}.csv, tools/final_pass.sh `stats`) — separate runs, so within
     2 % — and `traffic_over_algorithmic` as the calibrated counter bytes over those bytes."""
     import csv
     import json
-    line = json.load(open(os.path.join(ROOT, "profiles", "r06_bench_line_final.json")))
-    rows = list(csv.DictReader(open(os.path.join(ROOT, "profiles", "r06_kernel_trace_final.csv"))))
+    line = json.load(open(os.path.join(ROOT, "profiles", f"r06_bench_line_{tag}.json")))
+    rows = list(csv.DictReader(open(os.path.join(ROOT, "profiles", f"r06_kernel_trace_{tag}.csv"))))
     legs = [(line["roofline"]["instantiation"], line["roofline"]),
             (line["nanovdb"]["instantiation"], line["nanovdb"]["roofline"]),
             (line["fast_mode"]["instantiation"], line["fast_mode"]["roofline"])]
