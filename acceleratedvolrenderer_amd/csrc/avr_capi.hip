@@ -179,7 +179,7 @@ struct avr_context {
     size_t zs_atab_cap = 0;
     long long zs_akey[6] = {-1, -1, -1, -1, -1, -1};
     int zs_two_level = AVR_ZS_TWO_LEVEL;
-    int refill_min = 0;       // 0: the default (32 lanes; 20 for a non-emissive NanoVDB walk, 16 for RGB grids)
+    int refill_min = 0;       // 0: the default (32 lanes; 20 for a non-emissive NanoVDB walk, 16 for RGB grids, 48 for a <= 2^3 GridMedium majorant)
     int dda_budget = 0;       // 0: by majorant resolution (12 cells up to 16^3, 32 for NanoVDB's 64^3)
     int grid_layout = 1;
     bool gray = false;        // sigma_a and sigma_s constant over 360..830 nm      // 1: build the fat (footprint) copy when memory allows, 0: linear only
@@ -1227,16 +1227,20 @@ int avr_tune_majorant(avr_context *c, const int *candidates, int n, int spp_begi
 // k_paths' effective walk schedule for requested (refill lanes, DDA cells), 0 = the defaults —
 // measured optima: refill at 32 idle lanes and 10 DDA cells per iteration for 16^3
 // majorants, 32 cells for finer ones; a non-emissive NanoVDB medium (pbrt's 64^3 majorant: ~4x the
-// DDA steps of the grid) refills at 16 lanes with 28 cells (S-cloud-1024: 1239 -> 1352
-// Msamples/s at 12 / 28 in round 3, 1435 -> 1464 at 16 / 28 in round 5,
-// profiles/r05_refill_dda_sweep.json); an RGBGridMedium (8 sigmoid taps x 4 wavelengths per
+// DDA steps of the grid) refills at 20 lanes with 28 cells (S-cloud-1024: 1239 -> 1352
+// Msamples/s at 12 / 28 in round 3, 1435 -> 1464 at 16 / 28 in round 5, 1619 -> 1638 at 20 / 28
+// in round 6, profiles/r06_walk_sweep.json); an RGBGridMedium (8 sigmoid taps x 4 wavelengths per
 // lookup, 2 waves / SIMD) at 16 lanes with 32 cells (C5's RGB explosion: 1770 -> 2094 Msamples/s)
 static void walk_schedule(const avr_context *c, int refill, int dda, int *r_eff, int *d_eff) {
     const int mres = std::max(c->med.mres[0], std::max(c->med.mres[1], c->med.mres[2]));
     const bool vdbWalk = c->med.type == 3 && !c->med.emissive && mres > 16;
     const bool rgbWalk = c->med.type == 4;
-    // measured optima (profiles/r06_walk_sweep.json for the round-6 kernels: NanoVDB 20 / 28)
-    *r_eff = refill > 0 ? refill : (vdbWalk ? 20 : (rgbWalk ? 16 : 32));
+    // a GridMedium majorant of at most 2 cells per axis (fast mode's tuned 1^3): walks of one
+    // or two cells, so the event handlers dominate and larger batches win
+    const bool coarse = c->med.type == 0 && mres <= 2;
+    // measured optima (profiles/r06_walk_sweep.json for the round-6 kernels: NanoVDB 20 / 28,
+    // coarse 48)
+    *r_eff = refill > 0 ? refill : (vdbWalk ? 20 : (rgbWalk ? 16 : (coarse ? 48 : 32)));
     *d_eff = dda > 0 ? dda : (vdbWalk ? 28 : (rgbWalk || mres > 16 ? 32 : 10));
 }
 

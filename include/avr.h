@@ -112,7 +112,8 @@ int avr_set_pass_table_ahead(avr_context *ctx, int on);
  * are idle (or none is busy); larger values batch the per-event handlers across lanes.
  * 0 = default (the measured optima in both render modes: 32; 20 for a non-emissive
  * NanoVDB medium at pbrt's 64^3 majorant, whose longer DDA walks favour smaller batches;
- * 16 for an RGBGridMedium). */
+ * 16 for an RGBGridMedium; 48 for a GridMedium majorant of at most 2 cells per axis, e.g.
+ * fast mode's tuned 1^3, whose one-cell walks leave the handlers dominant). */
 int avr_set_refill_min(avr_context *ctx, int lanes);
 /* k_paths: majorant-grid cells a lane may cross per tracking iteration before yielding to
  * the wave (0 = default: 10 for majorant grids up to 16^3, 32 for finer ones and for

@@ -31,6 +31,7 @@ def main():
     p.add_argument("--rounds", type=int, default=2)
     p.add_argument("--pixelsamples", type=int, default=16384)
     p.add_argument("--majorant-res", type=int, default=0, help="r^3 majorant instead of pbrt's (0)")
+    p.add_argument("--mode", default="replay", choices=["replay", "fast"], help="render mode (fast: the bench's fast leg)")
     a = p.parse_args()
     import torch
     from acceleratedvolrenderer_amd import VolPathIntegrator, scenes, capi
@@ -49,7 +50,7 @@ def main():
     else:
         scene = scenes.s_cloud(density, sampler="zsobol", spp=a.pixelsamples, filter="gaussian")
     S = 64
-    integ = VolPathIntegrator(scene, maxdepth=scenes.CLOUD_MAXDEPTH, spp=S, seed=0, device=0)
+    integ = VolPathIntegrator(scene, maxdepth=scenes.CLOUD_MAXDEPTH, spp=S, seed=0, device=0, mode=a.mode)
     if a.majorant_res:
         integ.ctx.set_majorant_res((a.majorant_res,) * 3)
     npix = scene.film.width * scene.film.height
@@ -82,7 +83,7 @@ def main():
              "step_ms": round(v[1] / v[2], 4), "Msamples_s": round(npix * S / (v[1] / v[2] / 1e3) / 1e6, 2)}
             for c, v in acc.items()]
     integ.close()
-    print(json.dumps({"medium": a.medium, "res": n, "majorant_res": a.majorant_res or None, "lib": os.environ.get("AVR_LIB"), "pixelsamples": a.pixelsamples, "steps_per_round": a.steps,
+    print(json.dumps({"medium": a.medium, "mode": a.mode, "res": n, "majorant_res": a.majorant_res or None, "lib": os.environ.get("AVR_LIB"), "pixelsamples": a.pixelsamples, "steps_per_round": a.steps,
                       "rounds": a.rounds, "rows": rows}))
 
 
