@@ -99,6 +99,9 @@ def test_camera_bytes():
     assert bench.camera_bytes(4, "zsobol", pass_dims=64, pixels=2, launches=1) == 4 * 68 + 6 * 8 + 2 * 64 * 12
     assert bench.camera_bytes(8, "zsobol", zsobol_table=False, pass_dims=16, pixels=2, launches=2) == \
         8 * 68 + 12 * 8 + 2 * 2 * 16 * 8
+    # the pass table built ahead on the side stream (avr_set_pass_table_ahead): the camera
+    # stage's interval is the camera kernel alone, so its bytes leave the build out
+    assert bench.camera_bytes(4, "zsobol", pass_dims=64, pixels=2, launches=0) == 4 * 68 + 6 * 8
     agg = {"medium_lookups": 0, "shadow_lookups": 0, "medium_items_in": 0, "medium_items_out": 1000,
            "medium_dda_steps": 0}
     assert bench.kpaths_bytes(agg, "zsobol", pass_table=True)[2]["zsobol_table_reads"] == 40 * 1000
