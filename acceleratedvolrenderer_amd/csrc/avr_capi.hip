@@ -1756,7 +1756,8 @@ static void ptab_key(const avr_context *c, const avr::smp::ZSobolParams &zs, lon
 // Build the pass table (and the camera stage's compact copy) of [base, base + S) into buffer buf
 // on stream s, with its level-A table when the two-level build applies. No room for a buffer:
 // d_zs_ptab[buf] stays null (the pixel table / every digit per call serve the pass).
-static int ptab_build(avr_context *c, hipStream_t s, const avr::smp::ZSobolParams &zs, long long base, int plo, int buf) {
+static int ptab_build(avr_context *c, hipStream_t s, const avr::smp::ZSobolParams &zs, long long base, int plo, int buf,
+                      bool two_level) {
     const long long P = (long long)c->film.width * c->film.height;
     const size_t prow = (size_t)avr::smp::encode_morton2((uint32_t)c->film.width - 1, (uint32_t)c->film.height - 1) + 1;
     const size_t need_e = prow * (size_t)c->zs_pdims;
@@ -1779,9 +1780,10 @@ static int ptab_build(avr_context *c, hipStream_t s, const avr::smp::ZSobolParam
         c->zs_ptab_cap[buf] = need_e;
     }
     // two-level build: the plo + 2 table is shared by the four passes whose indices agree above
-    // plo + 2 bits; each pass then derives its own from it
+    // plo + 2 bits; each pass then derives its own from it (not when the caller's passes stride
+    // past each other's group: a sample shard's rank would rebuild it for every pass)
     const uint64_t *atab = nullptr;
-    if (c->zs_two_level && plo + 2 <= zs.log2spp) {
+    if (two_level && c->zs_two_level && plo + 2 <= zs.log2spp) {
         if (need_e > c->zs_atab_cap) {
             if (c->d_zs_atab) (void)hipFree(c->d_zs_atab);
             c->d_zs_atab = nullptr;
@@ -2016,7 +2018,7 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
                     }
                     if (buf < 0) {
                         buf = 1 - c->tab_buf;
-                        int rc2 = ptab_build(c, c->stream, zs, base, plo, buf);
+                        int rc2 = ptab_build(c, c->stream, zs, base, plo, buf, call_stride == 0 || call_stride == S);
                         if (rc2) return rc2;
                         if (!c->d_zs_ptab[buf]) buf = -1;
                     }
@@ -2075,12 +2077,13 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
                 // the previous pass, is then done too) and is dispatched as k_paths' blocks retire
                 // in its drain, instead of in front of the next camera stage. A pass whose key
                 // differs builds its own table (and this one is discarded).
-                const long long nb = (base + Smax < spp_end || call_stride == 0) ? base + S : spp_begin + call_stride;
+                const bool in_call = base + Smax < spp_end || call_stride == 0;
+                const long long nb = in_call ? base + S : spp_begin + call_stride;
                 const int nplo = pass_plo(nb, S);
                 HIP_TRY(hipStreamWaitEvent(c->tstream, c->ev_cam, 0));
                 const int tb = 1 - c->tab_buf;
                 // (not timed: events around it would measure its wait for the drain too)
-                { int rc2 = ptab_build(c, c->tstream, spec_zs, nb, nplo, tb); if (rc2) return rc2; }
+                { int rc2 = ptab_build(c, c->tstream, spec_zs, nb, nplo, tb, in_call || call_stride == S); if (rc2) return rc2; }
                 HIP_TRY(hipEventRecord(c->ev_tab, c->tstream));
                 if (c->d_zs_ptab[tb]) {
                     ptab_key(c, spec_zs, nb, nplo, c->spec_key);
