@@ -61,9 +61,12 @@ def sample_plan(world, steps, warmup, spp_per_step, base_spp=256, pixelsamples=0
     samplers.h:252-254, so disjoint index ranges are disjoint paths).
 
     Returns (pixelsamples, warm, timed): warm[r] / timed[r] are rank r's first sample index of
-    each warmup / timed step. The timed steps of all ranks cover [0, steps * world * S) once
-    — no (pixel, index) pair is rendered twice, so the reduced film is one render at
-    pixelsamples spp. pixelsamples is the smallest power of two >= steps * max(world,
+    each warmup / timed step. Rank r's timed steps are the consecutive block [r * steps * S,
+    (r + 1) * steps * S) (rank-major: each rank walks its indices in order, as pbrt's pass loop
+    does, so its ZSobol pass tables are built one pass ahead and share their level-A table —
+    an interleaved plan measured 0.2 ms per step slower, profiles/r06_pass_stride_probe.json).
+    The timed steps of all ranks cover [0, steps * world * S) once — no (pixel, index) pair is
+    rendered twice, so the reduced film is one render at pixelsamples spp. pixelsamples is the smallest power of two >= steps * max(world,
     plan_world) * S and >= base_spp (BASELINE config C3: 256), unless given: sized for the
     largest world (8 GPUs) at EVERY world size, so the N = 1, 2, 4 and 8 lines of one command
     run the same ZSobol instantiation with the same number of sample digits per draw
@@ -83,6 +86,6 @@ def sample_plan(world, steps, warmup, spp_per_step, base_spp=256, pixelsamples=0
             P *= 2
     if P < need or P % S:
         raise ValueError(f"pixelsamples {P} cannot hold {steps} steps x {world} ranks x {S} distinct sample indices")
-    timed = [[(k * world + r) * S for k in range(steps)] for r in range(world)]
-    warm = [[((k * world + r) * S) % P for k in range(warmup)] for r in range(world)]
+    timed = [[(r * steps + k) * S for k in range(steps)] for r in range(world)]
+    warm = [[((r * steps + k) * S) % P for k in range(warmup)] for r in range(world)]
     return P, warm, timed
