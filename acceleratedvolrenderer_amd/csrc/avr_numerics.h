@@ -127,7 +127,9 @@ struct Pcg32 {
         uint32_t rot = (uint32_t)(old >> 59u);
         return (xorshifted >> rot) | (xorshifted << ((~rot + 1u) & 31));
     }
-    AVR_HD float uniform() { return fminf_(kOneMinusEpsilon, (float)next_u32() * 0x1p-32f); }
+    // std::min(OneMinusEpsilon, v * 2^-32) (rng.h:128-130): the product is never NaN, so the
+    // hardware minimum (one v_min_f32 instead of a compare and a select) gives the same value
+    AVR_HD float uniform() { return __builtin_fminf(kOneMinusEpsilon, (float)next_u32() * 0x1p-32f); }
     AVR_HD void advance(uint64_t delta) {
         uint64_t curMult = 0x5851f42d4c957f2dULL, curPlus = inc, accMult = 1u, accPlus = 0u;
         while (delta > 0) {

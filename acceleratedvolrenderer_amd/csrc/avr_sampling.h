@@ -89,8 +89,8 @@ AVR_HD uint32_t fast_owen(uint32_t v, uint32_t seed) {   // lowdiscrepancy.h:220
     return bitrev32(v);
 }
 AVR_HD float u32_to_unit(uint32_t v) {   // min(v * 2^-32, OneMinusEpsilon)
-    const float f = (float)v * 0x1p-32f;
-    return f < 0x1.fffffep-1f ? f : 0x1.fffffep-1f;
+    // (never NaN: the hardware minimum, one v_min_f32, gives the select's value)
+    return __builtin_fminf((float)v * 0x1p-32f, 0x1.fffffep-1f);
 }
 
 // The 24 permutations of a base-4 digit in ZSobolSampler::GetSampleIndex's table order,
