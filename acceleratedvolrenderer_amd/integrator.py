@@ -110,11 +110,12 @@ class VolPathIntegrator:
         """Integrator::Create-style factory from a pbrt ParameterDictionary-like dict."""
         return cls(scene, device=device, **cls.create_params(name, params, maxdepth_override), **kw)
 
-    def tune_majorant(self, candidates=(1, 2, 4, 8, 16), probe=(0, 16)):
+    def tune_majorant(self, candidates=(1, 2, 4, 8, 16), probe=(0, 64)):
         """The fast mode's tuned majorant: time one probe render of sample
         indices [probe[0], probe[1]) per candidate majorant resolution (r^3) on the device and
-        keep the fastest (16 indices: with 4 the launch's drain decided for the 720p bench, and
-        it chose 2^3 where 1^3 renders 4 % faster at 64 indices per pass) (avr_tune_majorant; the film is left as it was). Any conservative
+        keep the fastest (64 indices, a full pass at 720p: with 4 or 16 the launch's drain and
+        the camera stage and film, which the majorant does not change, hid the difference, and
+        1^3 and 2^3 swapped between runs — 2^3 renders 4 % slower at 64 indices per pass) (avr_tune_majorant; the film is left as it was). Any conservative
         majorant gives the same estimator in expectation; only pbrt's own resolution (16^3
         grids, 64^3 NanoVDB) replays pbrt's sample streams. Returns (chosen, {r: probe ms})."""
         cands = [(int(r),) * 3 for r in candidates]

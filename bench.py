@@ -703,7 +703,7 @@ def main():
     tune_ms = None
     if args.majorant_res == -1 or (args.majorant_res is None and args.mode == "fast"):
         cands = (1, 2, 4, 8, 16) + ((32, 64) if vdb is not None else ())
-        maj_res, tune_ms = integ.tune_majorant(candidates=cands, probe=(0, 16))
+        maj_res, tune_ms = integ.tune_majorant(candidates=cands, probe=(0, 64))
         if world > 1:   # every rank renders with rank 0's choice
             maj_res = broadcast_choice(maj_res, world, f"cuda:{dev}")
             integ.ctx.set_majorant_res(maj_res)
@@ -764,7 +764,7 @@ def main():
             fres, fms = (args.fast_majorant_res,) * 3, {}
             integ.ctx.set_majorant_res(fres)
         else:
-            fres, fms = integ.tune_majorant(candidates=cands, probe=(0, 16))
+            fres, fms = integ.tune_majorant(candidates=cands, probe=(0, 64))
         if world > 1:   # every rank renders with rank 0's choice
             fres = broadcast_choice(fres, world, f"cuda:{dev}")
             integ.ctx.set_majorant_res(fres)
