@@ -367,7 +367,14 @@ __device__ __forceinline__ bool fat_issue(const float4 *__restrict__ fat, int nx
     int ix = (int)__builtin_floorf(psx), iy = (int)__builtin_floorf(psy), iz = (int)__builtin_floorf(psz);
     if (ix < -1 || ix >= nx || iy < -1 || iy >= ny || iz < -1 || iz >= nz) return false;
     dx = psx - (float)ix, dy = psy - (float)iy, dz = psz - (float)iz;
-    const size_t e = (((size_t)(iz + 1) * (ny + 1) + (iy + 1)) * (nx + 1) + (ix + 1)) * 2;
+    // entry index in 32 bits with 24-bit multiplies when the copy has < 2^31 entries (grids to
+    // 1290^3; the condition is wave-uniform): (iz + 1)(ny + 1) + iy + 1 < 1291^2 < 2^24
+    const uint32_t ex = (uint32_t)nx + 1, ey = (uint32_t)ny + 1;
+    size_t e;
+    if ((uint64_t)ex * ey * ((uint64_t)nz + 1) < (1ull << 31))
+        e = (size_t)(__umul24(__umul24((uint32_t)(iz + 1), ey) + (uint32_t)(iy + 1), ex) + (uint32_t)(ix + 1)) * 2;
+    else
+        e = (((size_t)(iz + 1) * ey + (iy + 1)) * ex + (ix + 1)) * 2;
     a = fat[e], b = fat[e + 1];
     return true;
 }
