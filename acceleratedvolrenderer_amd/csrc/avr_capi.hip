@@ -2063,7 +2063,11 @@ int avr_render(avr_context *c, int spp_begin, int spp_end, int seed, int max_dep
             p.rec_mode = 1;   // k_film reads the records k_paths wrote (in slot order)
             p.pix_slot = c->d_pix_slot;
             p.fast = c->render_mode;
-            hipLaunchKernelGGL((c->film.nbuckets > 0 ? avr::k_film<true> : avr::k_film<false>), dim3(blocks_for(P)), dim3(256), avr::film_lds_bytes(c->film.nbuckets),
+            // fast mode: the wavelength pdfs with the hardware exp (its wavelengths are the hardware log's)
+            using KF = void (*)(avr::Params);
+            static const KF kfilm[2][2] = {{avr::k_film<false, false>, avr::k_film<true, false>},
+                                           {avr::k_film<false, true>, avr::k_film<true, true>}};
+            hipLaunchKernelGGL(kfilm[c->render_mode ? 1 : 0][c->film.nbuckets > 0 ? 1 : 0], dim3(blocks_for(P)), dim3(256), avr::film_lds_bytes(c->film.nbuckets),
                                c->stream, p);
             HIP_TRY(hipGetLastError());
             EV_MARK(e2);
@@ -2408,7 +2412,8 @@ int avr_last_pass_samples(avr_context *c, float *L, float *lambda, float *pdf, l
         HIP_TRY(hipMemcpy(lambda, c->ps.cam2, n * sizeof(float4), hipMemcpyDeviceToHost));
         {
             avr::DevFilm f = c->film;
-            hipLaunchKernelGGL(avr::k_lambda_pdfs, dim3(blocks_for(n)), dim3(256), 0, c->stream, f, c->ps.cam2, c->ps.cam4, n);
+            hipLaunchKernelGGL(avr::k_lambda_pdfs, dim3(blocks_for(n)), dim3(256), 0, c->stream, f, c->ps.cam2, c->ps.cam4, n,
+                               c->last_fast ? 1 : 0);
             HIP_TRY(hipGetLastError());
             HIP_TRY(hipStreamSynchronize(c->stream));
         }

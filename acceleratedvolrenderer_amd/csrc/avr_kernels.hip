@@ -2785,8 +2785,21 @@ __device__ __forceinline__ void film_load_sample(const Params &P, size_t id, Spe
 }
 // the camera stage's wavelength pdfs (film_lambda_pdf: the same canonical function of the same
 // floats, so the same bits) when k_film evaluates them (k_paths' records)
+// fast mode (its wavelengths come from the hardware log already): VisibleWavelengthsPDF
+// (spectrum.h:255-259) with the hardware exp for cosh — about 1 ulp, statistical parity
+__device__ __forceinline__ float film_lambda_pdf_fast(const DevFilm &f, float l) {
+    if (f.nbuckets > 0) return 1 / (f.lmax - f.lmin);
+    if (l < 360 || l > 830) return 0;
+    const float x = 0.0072f * (l - 538);
+    return 0.0039398042f / sqr(0.5f * (__expf(x) + __expf(-x)));
+}
+template <bool kFast = false>
 __device__ __forceinline__ void film_pdfs(const Params &P, const Spec &lam, Spec *pdf, const double *canon_tabs) {
-    if (P.rec_mode)
+    if (!P.rec_mode) return;
+    if constexpr (kFast)
+        *pdf = {film_lambda_pdf_fast(P.film, lam.v0), film_lambda_pdf_fast(P.film, lam.v1),
+                film_lambda_pdf_fast(P.film, lam.v2), film_lambda_pdf_fast(P.film, lam.v3)};
+    else
         *pdf = {film_lambda_pdf(P.film, lam.v0, canon_tabs), film_lambda_pdf(P.film, lam.v1, canon_tabs),
                 film_lambda_pdf(P.film, lam.v2, canon_tabs), film_lambda_pdf(P.film, lam.v3, canon_tabs)};
 }
@@ -2794,15 +2807,17 @@ __device__ __forceinline__ void film_pdfs(const Params &P, const Spec &lam, Spec
 // own evaluation (film_pdfs: the same overload over the same LDS-staged canonical tables), so
 // the accessor returns exactly the pdfs the film divided by
 __global__ void __launch_bounds__(256) k_lambda_pdfs(DevFilm film, const float4 *__restrict__ lam, float4 *__restrict__ pdf,
-                                                     long long n) {
+                                                     long long n, int fast) {
     __shared__ double s_canon[canon::kCanonTabDoubles];
     for (int i = threadIdx.x; i < canon::kCanonTabDoubles; i += blockDim.x)
         s_canon[i] = i < 128 ? canon::kLogInvC[i] : (i < 256 ? canon::kLogC[i - 128] : canon::kExp2J64[i - 256]);
     __syncthreads();
     for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
         const float4 l = lam[i];
-        pdf[i] = make_float4(film_lambda_pdf(film, l.x, s_canon), film_lambda_pdf(film, l.y, s_canon),
-                             film_lambda_pdf(film, l.z, s_canon), film_lambda_pdf(film, l.w, s_canon));
+        pdf[i] = fast ? make_float4(film_lambda_pdf_fast(film, l.x), film_lambda_pdf_fast(film, l.y),
+                                    film_lambda_pdf_fast(film, l.z), film_lambda_pdf_fast(film, l.w))
+                      : make_float4(film_lambda_pdf(film, l.x, s_canon), film_lambda_pdf(film, l.y, s_canon),
+                                    film_lambda_pdf(film, l.z, s_canon), film_lambda_pdf(film, l.w, s_canon));
     }
 }
 // The X, Y, Z matching tables interleaved per wavelength ({X, Y, Z, 0}, staged in LDS by
@@ -2847,7 +2862,7 @@ constexpr int kFilmLdsBuckets = 16;
 constexpr int kFilmBatch = AVR_FILM_BATCH;
 inline size_t film_lds_bytes(int nb) { return nb > 0 && nb <= kFilmLdsBuckets ? 2 * (size_t)nb * 256 * sizeof(double) : 0; }
 // kBuckets: a SpectralFilm (P.film.nbuckets > 0); RGBFilm's instantiation has no bucket code
-template <bool kBuckets>
+template <bool kBuckets, bool kFast = false>
 #ifndef AVR_FILM_WAVES
 #define AVR_FILM_WAVES 1   // minimum waves per SIMD asked of k_film (1: the compiler's choice)
 #endif
@@ -2910,14 +2925,14 @@ __global__ void __launch_bounds__(256, AVR_FILM_WAVES) k_film(Params P) {
             float w[kFilmBatch];
             _Pragma("unroll") for (int k = 0; k < kFilmBatch; ++k)
                 film_load_sample(P, (size_t)(s + k) * npix + slot, &L[k], &lam[k], &pdf[k], &w[k], s_canon);
-            _Pragma("unroll") for (int k = 0; k < kFilmBatch; ++k) film_pdfs(P, lam[k], &pdf[k], s_canon);
+            _Pragma("unroll") for (int k = 0; k < kFilmBatch; ++k) film_pdfs<kFast>(P, lam[k], &pdf[k], s_canon);
             _Pragma("unroll") for (int k = 0; k < kFilmBatch; ++k) add(L[k], lam[k], pdf[k], w[k]);
         }
         for (; s < P.pass_samples; ++s) {
             Spec L, lam, pdf;
             float w;
             film_load_sample(P, (size_t)s * npix + slot, &L, &lam, &pdf, &w, s_canon);
-            film_pdfs(P, lam, &pdf, s_canon);
+            film_pdfs<kFast>(P, lam, &pdf, s_canon);
             add(L, lam, pdf, w);
         }
         if (ldsBuckets)
