@@ -1134,9 +1134,10 @@ int avr_set_majorant_res(avr_context *c, const int res[3]) {
 }
 
 // The probe loop of the device-side tuners (avr_tune_majorant, avr_tune_walk): render
-// [spp_begin, spp_end) once after setup(k) for each k < n — plus one untimed render after
-// setup(0) first (the first render after a scene change builds one-off tables) — timed with
-// HIP events on the context stream; *bestk = the fastest, ms[k] the times when non-null. The
+// [spp_begin, spp_end) after setup(k) for each k < n, twice (k ascending, then descending) —
+// plus one untimed render after setup(0) first (the first render after a scene change builds
+// one-off tables) — timed with HIP events on the context stream; each candidate's time is the
+// faster of its two probes; *bestk = the fastest, ms[k] the times when non-null. The
 // film sums are saved before and restored after (also when a probe fails; the first error is
 // kept); restore() then re-applies the chosen (or, after a failure, the original) setting.
 // prefer >= 0: that candidate (the default schedule) is kept unless the fastest probe beats it
@@ -1159,7 +1160,16 @@ static int probe_loop(avr_context *c, int n, Setup setup, Restore restore, int s
     if (!rc && (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess)) rc = fail(AVR_ERR_HIP, "event");
     float best = -1.f, tPrefer = -1.f;
     *bestk = 0;
-    for (int k = -1; k < n && !rc; ++k) {
+    // the probes render one range over and over: no pass table built ahead on the side stream
+    // (a probe would wait for the previous one's), restored afterwards
+    const int spec0 = c->ptab_spec;
+    c->ptab_spec = 0;
+    c->spec_valid = false;
+    // two rounds over the candidates, the second in reverse order, each candidate's time the
+    // faster of its two probes (one probe each left 1^3 and 2^3 of fast mode to noise)
+    std::vector<float> tmin(n, -1.f);
+    for (int it = -1; it < 2 * n && !rc; ++it) {
+        const int k = it < 0 ? -1 : (it < n ? it : 2 * n - 1 - it);
         if ((rc = setup(k < 0 ? 0 : k))) break;
         if (hipEventRecord(e0, c->stream) != hipSuccess) { rc = fail(AVR_ERR_HIP, "event record"); break; }
         if ((rc = avr_render(c, spp_begin, spp_end, seed, max_depth))) break;
@@ -1169,7 +1179,11 @@ static int probe_loop(avr_context *c, int n, Setup setup, Restore restore, int s
         }
         float t = 0.f;
         (void)hipEventElapsedTime(&t, e0, e1);
-        if (k < 0) continue;
+        if (k >= 0 && (tmin[k] < 0 || t < tmin[k])) tmin[k] = t;
+    }
+    c->ptab_spec = spec0;
+    for (int k = 0; k < n && !rc; ++k) {
+        const float t = tmin[k];
         if (ms) ms[k] = t;
         if ((k == prefer || (same && (*same)[k])) && (tPrefer < 0 || t < tPrefer)) tPrefer = t;
         if (best < 0 || t < best) { best = t; *bestk = k; }

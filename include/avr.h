@@ -269,15 +269,16 @@ int avr_read_majorant(avr_context *ctx, float *out);
  * in expectation (SURVEY §7 "fast": tuned majorant, statistical parity). The persistent
  * kernel keeps grids of up to 4096 cells in LDS; finer grid majorants run the wavefront kernels. */
 int avr_set_majorant_res(avr_context *ctx, const int res[3]);
-/* The "tuned majorant": render the probe sample range [spp_begin, spp_end) once per
- * candidate resolution (n triples in `candidates`), timed with HIP events on the context
- * stream, keep the fastest (chosen[3]; per-candidate times in ms[n] when non-null). The
- * film sums are restored and the work counters reset afterwards. */
+/* The "tuned majorant": render the probe sample range [spp_begin, spp_end) twice per
+ * candidate resolution (n triples in `candidates`; candidates ascending, then descending),
+ * timed with HIP events on the context stream, keep the fastest (chosen[3]; each candidate's
+ * faster probe in ms[n] when non-null). The film sums are restored and the work counters
+ * reset afterwards; no pass table is built ahead during the probes. */
 int avr_tune_majorant(avr_context *ctx, const int *candidates, int n, int spp_begin, int spp_end, int seed,
                       int max_depth, int chosen[3], float *ms);
 /* k_paths' lane schedule chosen on the device for the current scene (replaces fixed
- * per-medium defaults): render the probe sample range once per (refill lanes, DDA cells)
- * candidate pair, refill[i] x dda[j] (0 = the library default for either), timed with HIP
+ * per-medium defaults): render the probe sample range twice per (refill lanes, DDA cells)
+ * candidate pair (the faster probe counts), refill[i] x dda[j] (0 = the library default for either), timed with HIP
  * events on the context stream, and keep the fastest (chosen[2] = {refill, dda}; the nr*nd
  * probe times in ms[i * nd + j] when non-null) — except that the default pair (0, 0), when
  * listed (else the current schedule, when listed), is kept unless the fastest probe beats
