@@ -256,7 +256,7 @@ def parse(argv=None):
     p.add_argument("--nanovdb-leg", type=int, default=1,
                    help="after the headline (S-cloud GridMedium), time the same sample indices over the same cloud as a "
                         "NanoVDBMedium (disney-cloud's medium type; tree built on the device), reported as `nanovdb`")
-    p.add_argument("--nanovdb-steps", type=int, default=4, help="timed steps of the NanoVDB leg (at most --steps)")
+    p.add_argument("--nanovdb-steps", type=int, default=8, help="timed steps of the NanoVDB leg (at most --steps)")
     p.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     return p.parse_args(argv)
 
